@@ -1,0 +1,260 @@
+"""Fused execution of ``TransformerDecoderLM``: one autograd function per parameter unit.
+
+Forward / backward of a decoder layer (reference ``models/gpt.py:108-135`` and the ops
+it calls), as kernel calls on the bf16 compute weights of the parameter store:
+
+  forward                                      backward (dx3 arrives f32)
+  h1  = LN1(x)                 bf16            dz2 = dx3 * act'(z2) -> bf16, db2 += colsum
+  qkv = h1 @ [Wq;Wk;Wv]^T      one GEMM        dW2 += dz2^T u ; dz1 = (dz2 @ W2) * act'(.)  (+db1 colsum)
+  o   = flash_attn(qkv)        causal+pad      dW1 += dz1^T h2 ; dh2 = dz1 @ W1 (f32)
+  x2  = x + o @ Wo^T + bo      epilogue        dx2 = dx3 + LN2'(dh2)      (in place)
+  h2  = LN2(x2)                bf16            dYo = bf16(dx2), dbo += colsum ; dWo += dYo^T o
+  u   = act(h2 @ W1^T + b1)    epilogue        do = dYo @ Wo ; dqkv = flash_attn_bwd
+  x3  = x2 + act(u @ W2^T+b2)  epilogue, z2    dWqkv += dqkv^T h1 ; dh1 = dqkv @ Wqkv (f32)
+                                               dx = dx2 + LN1'(dh1)       (in place)
+
+Weight gradients are accumulated by the GEMM epilogues straight into the store's f32
+gradient views (flat buffer), and each function reports unit boundaries to the store
+(``pre/post_forward``, ``pre/post_backward``) -- that is where DDP launches bucket
+all-reduces and FSDP all-gathers / reduce-scatters, overlapped with this compute.
+Q, K, V weights are adjacent in the flat layout, so ``[Wq; Wk; Wv]`` is a view.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+from typing import Optional
+
+import torch
+
+from ..ops.attention import attention_bwd, attention_fwd
+from ..ops.elementwise import bias_act_bwd
+from ..ops.embedding import embedding_bwd, embedding_fwd
+from ..ops.gemm import ACT_GELU, ACT_RELU, act_code, linear_dgrad, linear_fwd, linear_wgrad
+from ..ops.loss import cross_entropy_fused
+from ..ops.norm import layernorm_bwd, layernorm_fwd
+
+LN_EPS = 1e-5
+
+
+def vocab_ld(vocab: int) -> int:
+    """Row stride of the logits buffer: 64-element aligned (16-B chunks, MFMA tiles)."""
+    return (vocab + 63) // 64 * 64
+
+
+@dataclass
+class LMOutput:
+    loss: torch.Tensor
+    n_valid: torch.Tensor
+    n_correct: Optional[torch.Tensor] = None
+
+
+def _qkv_weight(store, attn):
+    wq, wk, wv = (store.weight(m.weight) for m in (attn.to_q, attn.to_k, attn.to_v))
+    n = wq.shape[0]
+    if (wk.data_ptr() == wq.data_ptr() + wq.numel() * wq.element_size()
+            and wv.data_ptr() == wk.data_ptr() + wk.numel() * wk.element_size()):
+        return wq.as_strided((3 * n, wq.shape[1]), (wq.shape[1], 1))  # adjacent in the flat buffer
+    return torch.cat([wq, wk, wv], 0)
+
+
+def _qkv_grad(store, attn):
+    gq, gk, gv = (store.grad(m.weight) for m in (attn.to_q, attn.to_k, attn.to_v))
+    n = gq.shape[0]
+    if (gk.data_ptr() == gq.data_ptr() + gq.numel() * 4 and gv.data_ptr() == gk.data_ptr() + gk.numel() * 4):
+        return gq.as_strided((3 * n, gq.shape[1]), (gq.shape[1], 1)), None
+    buf = torch.zeros(3 * n, gq.shape[1], device=gq.device, dtype=torch.float32)
+    return buf, (gq, gk, gv)
+
+
+class _EmbedFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, anchor, ids, pos, mod, store):
+        u = mod._unit_id
+        store.pre_forward(u)
+        x = embedding_fwd(ids, pos, store.weight(mod.input_embeddings.weight),
+                          store.weight(mod.position_embeddings.weight))
+        store.post_forward(u)
+        ctx.save_for_backward(ids, pos)
+        ctx.mod, ctx.store = mod, store
+        return x
+
+    @staticmethod
+    def backward(ctx, dx):
+        ids, pos = ctx.saved_tensors
+        mod, store = ctx.mod, ctx.store
+        u = mod._unit_id
+        store.pre_backward(u, need_weights=False)
+        embedding_bwd(dx.contiguous(), ids, pos, store.grad(mod.input_embeddings.weight),
+                      store.grad(mod.position_embeddings.weight))
+        store.post_backward(u)
+        return None, None, None, None, None
+
+
+class _LayerFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, mask, layer, store, N, S, act, training):
+        u = layer._unit_id
+        store.pre_forward(u)
+        attn, fc = layer.attn, layer.fc
+        H, hd = attn.heads, attn.head_dim
+        w = store.weight
+        T, D = x.shape
+        cdt = store.compute_dtype
+        h1, mu1, rs1 = layernorm_fwd(x, w(layer.norm1.weight), w(layer.norm1.bias), LN_EPS, cdt)
+        qkv = linear_fwd(h1, _qkv_weight(store, attn), out_dtype=cdt)
+        o, lse = attention_fwd(qkv, N, S, H, hd, mask, causal=True)
+        x2 = linear_fwd(o, w(attn.to_out.weight), bias=w(attn.to_out.bias), residual=x,
+                        out_dtype=torch.float32)
+        h2, mu2, rs2 = layernorm_fwd(x2, w(layer.norm2.weight), w(layer.norm2.bias), LN_EPS, cdt)
+        F4 = fc.up_proj.weight.shape[0]
+        z1 = torch.empty(T, F4, device=x.device, dtype=cdt) if (training and act == ACT_GELU) else None
+        uact = linear_fwd(h2, w(fc.up_proj.weight), bias=w(fc.up_proj.bias), act=act, aux_out=z1,
+                          out_dtype=cdt)
+        z2 = torch.empty(T, D, device=x.device, dtype=cdt) if training else None
+        x3 = linear_fwd(uact, w(fc.down_proj.weight), bias=w(fc.down_proj.bias), act=act,
+                        residual=x2, aux_out=z2, out_dtype=torch.float32)
+        store.post_forward(u)
+        if training:
+            ctx.save_for_backward(x, h1, mu1, rs1, qkv, o, lse, x2, h2, mu2, rs2,
+                                  z1 if z1 is not None else uact, uact, z2, mask)
+            ctx.layer, ctx.store, ctx.dims, ctx.act = layer, store, (N, S, H, hd), act
+        return x3
+
+    @staticmethod
+    def backward(ctx, dx3):
+        (x, h1, mu1, rs1, qkv, o, lse, x2, h2, mu2, rs2, zup, uact, z2, mask) = ctx.saved_tensors
+        layer, store, act = ctx.layer, ctx.store, ctx.act
+        N, S, H, hd = ctx.dims
+        u = layer._unit_id
+        store.pre_backward(u)
+        attn, fc = layer.attn, layer.fc
+        w, g = store.weight, store.grad
+        cdt = store.compute_dtype
+        dx = dx3.contiguous()  # becomes dx2 then dx (in place)
+        # FFN down projection: x3 = x2 + act(z2), z2 = u W2^T + b2
+        dz2 = bias_act_bwd(dx, z2, act, g(fc.down_proj.bias), out_dtype=cdt)
+        linear_wgrad(dz2, uact, out=g(fc.down_proj.weight))
+        # up projection gradient with act' fused (relu' from its output, gelu' from z1)
+        dz1 = linear_dgrad(dz2, w(fc.down_proj.weight), act_bwd=act, aux_in=zup, out_dtype=cdt,
+                           colsum=g(fc.up_proj.bias))
+        linear_wgrad(dz1, h2, out=g(fc.up_proj.weight))
+        dh2 = linear_dgrad(dz1, w(fc.up_proj.weight), out_dtype=torch.float32)
+        layernorm_bwd(dh2, x2, mu2, rs2, w(layer.norm2.weight), dx, g(layer.norm2.weight),
+                      g(layer.norm2.bias))
+        # attention output projection: x2 = x + o Wo^T + bo
+        dyo = bias_act_bwd(dx, None, 0, g(attn.to_out.bias), out_dtype=cdt)
+        linear_wgrad(dyo, o, out=g(attn.to_out.weight))
+        do = linear_dgrad(dyo, w(attn.to_out.weight), out_dtype=cdt)
+        dqkv = attention_bwd(do, qkv, o, lse, N, S, H, hd, mask, causal=True)
+        gqkv, split = _qkv_grad(store, attn)
+        linear_wgrad(dqkv, h1, out=gqkv)
+        if split is not None:
+            n = split[0].shape[0]
+            for i, gi in enumerate(split):
+                gi.add_(gqkv[i * n:(i + 1) * n])
+        dh1 = linear_dgrad(dqkv, _qkv_weight(store, attn), out_dtype=torch.float32)
+        layernorm_bwd(dh1, x, mu1, rs1, w(layer.norm1.weight), dx, g(layer.norm1.weight),
+                      g(layer.norm1.bias))
+        store.post_backward(u)
+        return dx, None, None, None, None, None, None, None
+
+
+class _HeadFn(torch.autograd.Function):
+    """norm_out -> lm_head -> fused cross-entropy (reference gpt.py:229-231 + main-*.py loss)."""
+
+    @staticmethod
+    def forward(ctx, x, targets, norm, head, store, unit, training, want_correct):
+        store.pre_forward(unit)
+        w = store.weight
+        cdt = store.compute_dtype
+        V = head.weight.shape[0]
+        T = x.shape[0]
+        hf, mu, rs = layernorm_fwd(x, w(norm.weight), w(norm.bias), LN_EPS, cdt)
+        ld = vocab_ld(V) if x.is_cuda else V
+        buf = torch.empty(T, ld, device=x.device, dtype=cdt)
+        linear_fwd(hf, w(head.weight), out=buf[:, :V])
+        loss, n_valid, n_correct = cross_entropy_fused(buf, targets, V, write_grad=training,
+                                                       want_correct=want_correct)
+        store.post_forward(unit)
+        if training:
+            ctx.save_for_backward(x, hf, mu, rs, buf)
+            ctx.mods, ctx.store, ctx.unit, ctx.V = (norm, head), store, unit, V
+        ctx.mark_non_differentiable(n_valid)
+        if n_correct is None:
+            n_correct = torch.zeros((), device=x.device)
+        ctx.mark_non_differentiable(n_correct)
+        return loss, n_valid, n_correct
+
+    @staticmethod
+    def backward(ctx, dloss, _dn, _dc):
+        x, hf, mu, rs, dlogits = ctx.saved_tensors
+        (norm, head), store, unit, V = ctx.mods, ctx.store, ctx.unit, ctx.V
+        store.pre_backward(unit)
+        w, g = store.weight, store.grad
+        dl = dlogits[:, :V]
+        scale = dloss.reshape(()).float().contiguous()
+        linear_wgrad(dl, hf, out=g(head.weight), alpha_t=scale)
+        dhf = linear_dgrad(dl, w(head.weight), out_dtype=torch.float32, alpha_t=scale)
+        dx = torch.zeros_like(x)
+        layernorm_bwd(dhf, x, mu, rs, w(norm.weight), dx, g(norm.weight), g(norm.bias))
+        store.post_backward(unit)
+        return dx, None, None, None, None, None, None, None
+
+
+def head_logits(model, x, store):
+    """Inference head: logits [T, V] (view of a row-padded buffer), no loss."""
+    w = store.weight
+    V = model.lm_head.weight.shape[0]
+    unit = model._head_unit_id
+    store.pre_forward(unit)
+    hf, _, _ = layernorm_fwd(x, w(model.norm_out.weight), w(model.norm_out.bias), LN_EPS,
+                             store.compute_dtype)
+    ld = vocab_ld(V) if x.is_cuda else V
+    buf = torch.empty(x.shape[0], ld, device=x.device, dtype=store.compute_dtype)
+    linear_fwd(hf, w(model.lm_head.weight), out=buf[:, :V])
+    store.post_forward(unit)
+    return buf[:, :V]
+
+
+def ensure_store(model):
+    store = model.param_store
+    if store is None:
+        from ..parallel.store import LocalStore
+
+        dev = next(model.parameters()).device
+        store = LocalStore(model, dev)
+    return store
+
+
+def run_embeddings(model, store, input_ids, position_ids, training):
+    anchor = store.anchor if training else store.anchor.detach()
+    return _EmbedFn.apply(anchor, input_ids.reshape(-1), position_ids.reshape(-1),
+                          model.embeddings, store)
+
+
+def run_layers(model, store, x, mask, N, S, layers, training):
+    act = act_code(model.activation)
+    if model.dropout and training:
+        raise NotImplementedError("dropout > 0 is not supported on the fused path yet")
+    for layer in layers:
+        x = _LayerFn.apply(x, mask, layer, store, N, S, act, training)
+    return x
+
+
+def run_head(model, store, x, targets, training, want_correct):
+    return _HeadFn.apply(x, targets.reshape(-1), model.norm_out, model.lm_head, store,
+                         model._head_unit_id, training, want_correct)
+
+
+def fused_lm_forward(model, input_ids, position_ids, mask=None, targets=None, want_correct=False):
+    store = ensure_store(model)
+    N, S = input_ids.shape
+    training = torch.is_grad_enabled()
+    if mask is not None:
+        mask = mask.to(device=input_ids.device, dtype=torch.bool).contiguous()
+    x = run_embeddings(model, store, input_ids, position_ids, training)
+    x = run_layers(model, store, x, mask, N, S, model.decoder.layers, training)
+    if targets is None:
+        return head_logits(model, x, store).reshape(N, S, -1)
+    loss, n_valid, n_correct = run_head(model, store, x, targets, training, want_correct)
+    return LMOutput(loss, n_valid, n_correct if want_correct else None)

@@ -1,0 +1,153 @@
+"""ctypes binding of ``libdpc_kernels.so`` (the gfx950 kernels in ``ops/csrc``).
+
+Each C launcher takes a pointer to an argument struct plus the raw ``hipStream_t`` of
+the caller's current torch stream, so the kernels are ordered with torch's own work and
+are captured by HIP graphs exactly like torch's kernels.  The structs below mirror the C
+structs field-for-field (standard C layout on both sides).
+
+Loading is strict on a GPU: if the library is missing it is built in-tree with hipcc;
+if that fails the error propagates -- there is no silent fallback to torch ops.
+"""
+from __future__ import annotations
+
+import ctypes
+import threading
+from ctypes import c_float, c_int, c_longlong, c_void_p
+
+import torch
+
+from . import build as _build
+
+P = c_void_p
+LL = c_longlong
+
+
+class GemmArgs(ctypes.Structure):
+    _fields_ = [
+        ("A", P), ("B", P), ("C", P), ("bias", P), ("residual", P), ("aux_in", P),
+        ("aux_out", P), ("alpha_ptr", P), ("colsum", P),
+        ("lda", LL), ("ldb", LL), ("ldc", LL), ("ldr", LL), ("ld_aux_in", LL), ("ld_aux_out", LL),
+        ("M", c_int), ("N", c_int), ("K", c_int),
+        ("alpha", c_float),
+        ("act", c_int), ("act_bwd", c_int), ("out_f32", c_int), ("accumulate", c_int),
+        ("a_kmaj", c_int), ("b_kmaj", c_int),
+    ]
+
+
+class AttnArgs(ctypes.Structure):
+    _fields_ = [
+        ("q", P), ("k", P), ("v", P), ("o", P), ("lse", P), ("pad", P), ("dout", P),
+        ("dq", P), ("dk", P), ("dv", P), ("delta", P),
+        ("ld_qkv", LL), ("ld_o", LL), ("ld_dqkv", LL),
+        ("N", c_int), ("S", c_int), ("H", c_int),
+        ("scale", c_float),
+        ("causal", c_int),
+    ]
+
+
+class LNArgs(ctypes.Structure):
+    _fields_ = [
+        ("x", P), ("gamma", P), ("beta", P), ("y", P), ("mean", P), ("rstd", P),
+        ("dy", P), ("dx", P), ("dgamma", P), ("dbeta", P),
+        ("ldx", LL), ("ldy", LL), ("lddy", LL), ("lddx", LL),
+        ("T", c_int), ("D", c_int),
+        ("eps", c_float),
+        ("y_f32", c_int),
+    ]
+
+
+class EmbArgs(ctypes.Structure):
+    _fields_ = [
+        ("ids", P), ("pos", P), ("tok", P), ("ptab", P), ("out", P), ("dout", P),
+        ("dtok", P), ("dpos", P),
+        ("T", c_int), ("D", c_int), ("V", c_int), ("P", c_int),
+        ("table_bf16", c_int),
+    ]
+
+
+class CEArgs(ctypes.Structure):
+    _fields_ = [
+        ("logits", P), ("dlogits", P), ("targets", P), ("inv_count", P), ("row_loss", P),
+        ("row_correct", P),
+        ("ld", LL),
+        ("T", c_int), ("V", c_int),
+        ("write_grad", c_int), ("ignore_index", c_int),
+    ]
+
+
+class AdamArgs(ctypes.Structure):
+    _fields_ = [
+        ("param", P), ("grad", P), ("exp_avg", P), ("exp_avg_sq", P), ("shadow", P),
+        ("grad_scale_ptr", P),
+        ("n", LL),
+        ("lr", c_float), ("beta1", c_float), ("beta2", c_float), ("eps", c_float),
+        ("weight_decay", c_float), ("bias_correction1", c_float),
+        ("bias_correction2_sqrt", c_float), ("grad_scale", c_float),
+    ]
+
+
+class CastArgs(ctypes.Structure):
+    _fields_ = [("src", P), ("dst", P), ("n", LL)]
+
+
+class BiasActArgs(ctypes.Structure):
+    _fields_ = [
+        ("dy", P), ("z", P), ("dz", P), ("db", P),
+        ("lddy", LL), ("ldz", LL), ("lddz", LL),
+        ("T", c_int), ("N", c_int),
+        ("act", c_int),
+    ]
+
+
+_FUNCS = {
+    "dpc_gemm": GemmArgs,
+    "dpc_attn_fwd": AttnArgs,
+    "dpc_attn_bwd": AttnArgs,
+    "dpc_layernorm_fwd": LNArgs,
+    "dpc_layernorm_bwd": LNArgs,
+    "dpc_embedding_fwd": EmbArgs,
+    "dpc_embedding_bwd": EmbArgs,
+    "dpc_cross_entropy": CEArgs,
+    "dpc_adamw": AdamArgs,
+    "dpc_cast_f32_bf16": CastArgs,
+    "dpc_bias_act_bwd": BiasActArgs,
+}
+
+_lock = threading.Lock()
+_lib = None
+
+
+def lib() -> ctypes.CDLL:
+    """Load (building if needed) the kernel library. Raises if it cannot be had."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    with _lock:
+        if _lib is None:
+            if _build.needs_build():
+                _build.build()
+            handle = ctypes.CDLL(str(_build.LIB_PATH), mode=ctypes.RTLD_GLOBAL)
+            for name, st in _FUNCS.items():
+                fn = getattr(handle, name)
+                fn.argtypes = [ctypes.POINTER(st), c_void_p]
+                fn.restype = c_int
+            _lib = handle
+    return _lib
+
+
+def is_loaded() -> bool:
+    return _lib is not None
+
+
+def stream_ptr(device: torch.device | None = None) -> int:
+    return torch.cuda.current_stream(device).cuda_stream
+
+
+def call(name: str, args: ctypes.Structure, device: torch.device | None = None) -> None:
+    rc = getattr(lib(), name)(ctypes.byref(args), stream_ptr(device))
+    if rc != 0:
+        raise RuntimeError(f"{name} launch failed: hipError {rc}")
+
+
+def ptr(t: torch.Tensor | None) -> int | None:
+    return None if t is None else t.data_ptr()

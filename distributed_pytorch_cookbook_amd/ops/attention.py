@@ -1,0 +1,180 @@
+"""Causal self-attention core (softmax(q k^T * scale + masks) v) on the fused QKV buffer.
+
+Semantics follow ``/root/reference/models/gpt.py:68-105``: causal mask (key j > query i
+is excluded), optional key-padding mask (``True`` = padded key, excluded), softmax in
+f32, output heads merged back to ``[T, H*hd]``.  One deliberate difference: a query row
+whose every key is masked yields 0 here (the reference's finfo.min / -1e9 arithmetic
+yields an ill-defined average); such rows only occur for all-padding sequences.
+
+HIP path (bf16, head_dim 64): ``dpc_attn_fwd`` / ``dpc_attn_bwd`` flash kernels
+(``csrc/attention.hip``) -- O(S) memory, f32 log-sum-exp saved for the backward.
+head_dim 32 (the reference default config) is zero-padded to 64 on the way in.
+CPU / fp32 path: the same math with torch ops (test oracle).
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+
+from . import _lib
+
+HD_KERNEL = 64
+
+
+def _use_hip(t: torch.Tensor) -> bool:
+    return t.is_cuda and t.dtype == torch.bfloat16
+
+
+def split_qkv(qkv: torch.Tensor, heads: int, head_dim: int):
+    """Views q, k, v [T, H*hd] out of the fused [T, 3*H*hd] projection."""
+    hd = heads * head_dim
+    return qkv[:, :hd], qkv[:, hd:2 * hd], qkv[:, 2 * hd:]
+
+
+def attention_ref(qkv, N, S, heads, head_dim, pad_mask=None, causal=True, scale=None):
+    """Reference math; returns (o [T, H*hd] in qkv.dtype, lse [N*H, S] f32)."""
+    scale = 1.0 / math.sqrt(head_dim) if scale is None else scale
+    q, k, v = split_qkv(qkv, heads, head_dim)
+    q = q.float().reshape(N, S, heads, head_dim).transpose(1, 2)
+    k = k.float().reshape(N, S, heads, head_dim).transpose(1, 2)
+    v = v.float().reshape(N, S, heads, head_dim).transpose(1, 2)
+    s = (q @ k.transpose(-1, -2)) * scale
+    allowed = torch.ones(S, S, dtype=torch.bool, device=qkv.device)
+    if causal:
+        allowed = torch.tril(allowed)
+    allowed = allowed.expand(N, 1, S, S)
+    if pad_mask is not None:
+        allowed = allowed & ~pad_mask.bool()[:, None, None, :]
+    s = s.masked_fill(~allowed, float("-inf"))
+    m = s.amax(-1, keepdim=True)
+    m = torch.where(torch.isfinite(m), m, torch.zeros_like(m))
+    e = torch.exp(s - m)
+    l = e.sum(-1, keepdim=True)
+    p = torch.where(l > 0, e / l.clamp_min(1e-30), torch.zeros_like(e))
+    o = (p @ v).transpose(1, 2).reshape(N * S, heads * head_dim)
+    lse = torch.where(l > 0, m + torch.log(l.clamp_min(1e-30)), torch.full_like(l, float("inf")))
+    return o.to(qkv.dtype), lse.reshape(N * heads, S)
+
+
+def _pad_heads(x: torch.Tensor, T: int, heads: int, head_dim: int) -> torch.Tensor:
+    """[T, H*hd] (strided view ok) -> contiguous [T, H*64] with zero padding."""
+    out = torch.zeros(T, heads, HD_KERNEL, device=x.device, dtype=x.dtype)
+    out[:, :, :head_dim] = x.reshape(T, heads, head_dim)
+    return out.reshape(T, heads * HD_KERNEL)
+
+
+def attention_fwd(qkv: torch.Tensor, N: int, S: int, heads: int, head_dim: int,
+                  pad_mask: torch.Tensor | None = None, causal: bool = True,
+                  out: torch.Tensor | None = None):
+    """qkv [T = N*S, 3*H*hd] -> (o [T, H*hd], lse [N*H, S] f32)."""
+    T = N * S
+    if not _use_hip(qkv):
+        o, lse = attention_ref(qkv, N, S, heads, head_dim, pad_mask, causal)
+        if out is not None:
+            out.copy_(o)
+            o = out
+        return o, lse
+    scale = 1.0 / math.sqrt(head_dim)
+    if head_dim != HD_KERNEL:
+        if head_dim > HD_KERNEL:
+            raise NotImplementedError(f"attention kernel supports head_dim <= {HD_KERNEL}")
+        q, k, v = split_qkv(qkv, heads, head_dim)
+        qkv_p = torch.cat([_pad_heads(t, T, heads, head_dim) for t in (q, k, v)], dim=1)
+        o_p, lse = _attn_fwd_hip(qkv_p, N, S, heads, pad_mask, causal, scale, None)
+        o = o_p.reshape(T, heads, HD_KERNEL)[:, :, :head_dim].reshape(T, heads * head_dim)
+        if out is not None:
+            out.copy_(o)
+            o = out
+        return o.contiguous() if out is None else o, lse
+    return _attn_fwd_hip(qkv, N, S, heads, pad_mask, causal, scale, out)
+
+
+def _check(t, T, cols, name):
+    if t.shape[0] != T or t.stride(1) != 1 or t.dtype != torch.bfloat16:
+        raise ValueError(f"attention: bad {name} {tuple(t.shape)} {t.stride()} {t.dtype}")
+    if t.data_ptr() % 16 or t.stride(0) % 8 or t.shape[1] < cols:
+        raise ValueError(f"attention: {name} must be 16-B aligned with row stride % 8 == 0")
+
+
+def _attn_fwd_hip(qkv, N, S, heads, pad_mask, causal, scale, out):
+    T = N * S
+    hd = heads * HD_KERNEL
+    _check(qkv, T, 3 * hd, "qkv")
+    if out is None:
+        out = torch.empty(T, hd, device=qkv.device, dtype=torch.bfloat16)
+    _check(out, T, hd, "out")
+    lse = torch.empty(N * heads, S, device=qkv.device, dtype=torch.float32)
+    pad = None
+    if pad_mask is not None:
+        pad = pad_mask.to(torch.uint8).contiguous()
+        assert pad.shape == (N, S)
+    q, k, v = split_qkv(qkv, heads, HD_KERNEL)
+    args = _lib.AttnArgs(
+        q=q.data_ptr(), k=k.data_ptr(), v=v.data_ptr(), o=out.data_ptr(), lse=lse.data_ptr(),
+        pad=_lib.ptr(pad), ld_qkv=qkv.stride(0), ld_o=out.stride(0), ld_dqkv=0,
+        N=N, S=S, H=heads, scale=float(scale), causal=int(causal),
+    )
+    _lib.call("dpc_attn_fwd", args, qkv.device)
+    return out, lse
+
+
+def attention_bwd(dout: torch.Tensor, qkv: torch.Tensor, o: torch.Tensor, lse: torch.Tensor,
+                  N: int, S: int, heads: int, head_dim: int,
+                  pad_mask: torch.Tensor | None = None, causal: bool = True,
+                  dqkv: torch.Tensor | None = None) -> torch.Tensor:
+    """Gradient w.r.t. the fused qkv buffer: returns dqkv [T, 3*H*hd] (qkv dtype)."""
+    T = N * S
+    if not _use_hip(qkv):
+        with torch.enable_grad():
+            x = qkv.detach().float().requires_grad_(True)
+            o_ref, _ = attention_ref(x, N, S, heads, head_dim, pad_mask, causal)
+            (g,) = torch.autograd.grad(o_ref, x, dout.float())
+        if dqkv is not None:
+            dqkv.copy_(g)
+            return dqkv
+        return g.to(qkv.dtype)
+    scale = 1.0 / math.sqrt(head_dim)
+    if head_dim != HD_KERNEL:
+        q, k, v = split_qkv(qkv, heads, head_dim)
+        qkv_p = torch.cat([_pad_heads(t, T, heads, head_dim) for t in (q, k, v)], dim=1)
+        o_p = _pad_heads(o, T, heads, head_dim)
+        do_p = _pad_heads(dout, T, heads, head_dim)
+        g_p = _attn_bwd_hip(do_p, qkv_p, o_p, lse, N, S, heads, pad_mask, causal, scale, None)
+        g = g_p.reshape(T, 3, heads, HD_KERNEL)[..., :head_dim].reshape(T, 3 * heads * head_dim)
+        if dqkv is not None:
+            dqkv.copy_(g)
+            return dqkv
+        return g.contiguous()
+    return _attn_bwd_hip(dout, qkv, o, lse, N, S, heads, pad_mask, causal, scale, dqkv)
+
+
+def _attn_bwd_hip(dout, qkv, o, lse, N, S, heads, pad_mask, causal, scale, dqkv):
+    T = N * S
+    hd = heads * HD_KERNEL
+    _check(qkv, T, 3 * hd, "qkv")
+    _check(o, T, hd, "o")
+    _check(dout, T, hd, "dout")
+    if o.stride(0) != dout.stride(0):
+        dout = dout.contiguous()
+        o = o.contiguous()
+        if o.stride(0) != dout.stride(0):
+            raise ValueError("attention_bwd: o and dout need equal row strides")
+    if dqkv is None:
+        dqkv = torch.empty(T, 3 * hd, device=qkv.device, dtype=torch.bfloat16)
+    _check(dqkv, T, 3 * hd, "dqkv")
+    delta = torch.empty(N * heads, S, device=qkv.device, dtype=torch.float32)
+    pad = None
+    if pad_mask is not None:
+        pad = pad_mask.to(torch.uint8).contiguous()
+    q, k, v = split_qkv(qkv, heads, HD_KERNEL)
+    dq, dk, dv = split_qkv(dqkv, heads, HD_KERNEL)
+    args = _lib.AttnArgs(
+        q=q.data_ptr(), k=k.data_ptr(), v=v.data_ptr(), o=o.data_ptr(), lse=lse.data_ptr(),
+        pad=_lib.ptr(pad), dout=dout.data_ptr(), dq=dq.data_ptr(), dk=dk.data_ptr(),
+        dv=dv.data_ptr(), delta=delta.data_ptr(),
+        ld_qkv=qkv.stride(0), ld_o=o.stride(0), ld_dqkv=dqkv.stride(0),
+        N=N, S=S, H=heads, scale=float(scale), causal=int(causal),
+    )
+    _lib.call("dpc_attn_bwd", args, qkv.device)
+    return dqkv

@@ -1,0 +1,111 @@
+"""Build the gfx950 kernel library (``libdpc_kernels.so``) in-tree with hipcc.
+
+The kernels are plain HIP C++ with a C ABI (no torch headers, no hipify, no
+``torch.utils.cpp_extension``): every ``csrc/*.hip`` file is compiled for
+``--offload-arch=gfx950`` into an object file and the objects are linked into one
+shared library next to this file.  ``ops/_lib.py`` loads it with ``ctypes`` after
+``import torch`` so the process keeps a single HIP runtime (torch's
+``libamdhip64.so.7``; the library's dependency resolves to the already-loaded
+soname).
+
+Usage::
+
+    python -m distributed_pytorch_cookbook_amd.ops.build [--force] [-j N]
+"""
+from __future__ import annotations
+
+import argparse
+import os
+import shutil
+import subprocess
+import sys
+from concurrent.futures import ThreadPoolExecutor
+from pathlib import Path
+
+HERE = Path(__file__).resolve().parent
+CSRC = HERE / "csrc"
+BUILD_DIR = HERE / "_build"
+LIB_PATH = HERE / "libdpc_kernels.so"
+ARCH = os.environ.get("DPC_OFFLOAD_ARCH", "gfx950")
+
+SOURCES = ["gemm.hip", "attention.hip", "layernorm.hip", "misc.hip"]
+HEADERS = ["common.h"]
+
+# code-object v5 keeps the library loadable by torch's bundled ROCm 7.0 runtime as
+# well as by the 7.2 toolchain in /opt/rocm.
+CFLAGS = [
+    f"--offload-arch={ARCH}",
+    "-O3",
+    "-std=c++17",
+    "-fPIC",
+    "-mcode-object-version=5",
+    "-ffp-contract=fast",
+    "-Wno-unused-result",
+]
+
+
+def hipcc() -> str:
+    for cand in (os.environ.get("HIPCC"), shutil.which("hipcc"), "/opt/rocm/bin/hipcc"):
+        if cand and Path(cand).exists():
+            return cand
+    raise RuntimeError("hipcc not found: cannot build the gfx950 kernel library")
+
+
+def _newest(paths) -> float:
+    return max(p.stat().st_mtime for p in paths)
+
+
+def needs_build() -> bool:
+    if not LIB_PATH.exists():
+        return True
+    srcs = [CSRC / s for s in SOURCES] + [CSRC / h for h in HEADERS]
+    return _newest(srcs) > LIB_PATH.stat().st_mtime
+
+
+def _compile(src: Path, obj: Path, verbose: bool) -> None:
+    cmd = [hipcc(), *CFLAGS, "-c", str(src), "-o", str(obj)]
+    if verbose:
+        print(" ".join(cmd), flush=True)
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"hipcc failed for {src.name}:\n{r.stdout}\n{r.stderr}")
+
+
+def build(force: bool = False, jobs: int = 4, verbose: bool = False) -> Path:
+    if not force and not needs_build():
+        return LIB_PATH
+    BUILD_DIR.mkdir(exist_ok=True)
+    header_mtime = _newest([CSRC / h for h in HEADERS])
+    todo = []
+    objs = []
+    for s in SOURCES:
+        src, obj = CSRC / s, BUILD_DIR / (Path(s).stem + ".o")
+        objs.append(obj)
+        if force or not obj.exists() or obj.stat().st_mtime < max(src.stat().st_mtime, header_mtime):
+            todo.append((src, obj))
+    with ThreadPoolExecutor(max_workers=max(1, jobs)) as ex:
+        list(ex.map(lambda so: _compile(so[0], so[1], verbose), todo))
+    tmp = LIB_PATH.with_suffix(".so.tmp")
+    cmd = [hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", *map(str, objs), "-o", str(tmp)]
+    if verbose:
+        print(" ".join(cmd), flush=True)
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"link failed:\n{r.stdout}\n{r.stderr}")
+    os.replace(tmp, LIB_PATH)
+    return LIB_PATH
+
+
+def main(argv=None) -> int:
+    ap = argparse.ArgumentParser(description=__doc__)
+    ap.add_argument("--force", action="store_true")
+    ap.add_argument("-j", "--jobs", type=int, default=4)
+    ap.add_argument("-v", "--verbose", action="store_true")
+    a = ap.parse_args(argv)
+    path = build(force=a.force, jobs=a.jobs, verbose=a.verbose)
+    print(f"built {path}")
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -1,0 +1,517 @@
+// Flash attention (forward + backward) for gfx950, head_dim 64, bf16 in / bf16 out,
+// f32 online softmax, causal + optional key-padding mask.
+//
+// Replaces the reference's materialised attention (models/gpt.py:75-100: q@k, host-built
+// causal mask copied H2D every layer, masked_fill, fp32 softmax, @v, head merge) with an
+// O(S) kernel that reads q/k/v straight out of the fused QKV projection ([T, 3*H*hd],
+// token-major) and writes the merged-head output [T, H*hd] -- no permute/clone copies.
+//
+// MFMA layout (v_mfma_f32_32x32x16_bf16; C/D: col = lane & 31,
+// row = (r & 3) + 8 (r >> 2) + 4 (lane >> 5)):
+//   forward  S^T = K Q^T   -> the query sits on the lane, so the row max / row sum are
+//            lane-local (+ one xor-32 shuffle) and the O^T = V^T P^T accumulator is
+//            rescaled without any cross-lane traffic.  The S^T accumulator registers are
+//            the B operand of the PV product directly (pairs packed to bf16); V^T comes
+//            from LDS through ds_read_b64_tr_b16 (transposing read).
+//   backward dK/dV kernel: S = Q K^T and dP = dO V^T with the key on the lane (K, V rows
+//            live in registers for the whole sweep over queries); P / dS registers feed
+//            dV^T += dO^T P and dK^T += Q^T dS with dO^T / Q^T via transposing reads.
+//            dQ kernel: S^T, dP^T with the query on the lane, dQ^T += K^T dS^T.
+//            No float atomics: each output is owned by exactly one wave.
+// LDS tiles are [row][64] bf16 (128-B rows) with the 16-B chunk swizzle
+//   chunk ^ (((row >> 1) & 7) ^ (((row >> 1) & 1) << 2))
+// which is conflict free for both the ds_read_b128 row reads and the tr_b16 column reads.
+#include "common.h"
+
+namespace dpc {
+
+struct AttnArgs {
+  const void* q; const void* k; const void* v;  // bf16, row = token (n*S + s), head h at col h*64
+  void* o;                                      // bf16 [T][ld_o]
+  float* lse;                                   // f32 [N*H][S] (natural log of scaled scores)
+  const unsigned char* pad;                     // [N][S], 1 = padded key (masked), optional
+  const void* dout;                             // bwd: dO bf16 [T][ld_o]
+  void* dq; void* dk; void* dv;                 // bwd: bf16 outputs, row stride ld_dqkv
+  float* delta;                                 // bwd: f32 [N*H][S]
+  long long ld_qkv, ld_o, ld_dqkv;
+  int N, S, H;
+  float scale;
+  int causal;
+};
+
+constexpr int HD = 64;
+constexpr int KT = 64;       // keys (or queries) per staged tile
+constexpr int QB = 128;      // rows per workgroup (4 waves x 32)
+constexpr float LOG2E = 1.4426950408889634f;
+
+typedef short4_t __attribute__((address_space(3))) * lds4_t;
+
+__device__ __forceinline__ int aswz(int row) {
+  const int a = (row >> 1) & 7;
+  return a ^ ((a & 1) << 2);
+}
+__device__ __forceinline__ int aoff(int row, int chunk) {  // element offset in a [row][64] tile
+  return row * HD + ((chunk ^ aswz(row)) << 3);
+}
+
+// Stage a 64-row x 64-col bf16 tile (rows r0.., zero beyond `rows`) into LDS.
+__device__ __forceinline__ void tile_load(uint4 (&r)[2], const bf16_t* base, long long ld,
+                                          int row0, int rows) {
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int c = threadIdx.x + i * 256;
+    const int row = c >> 3, ch = c & 7;
+    uint4 v = make_uint4(0, 0, 0, 0);
+    if (row0 + row < rows) v = *reinterpret_cast<const uint4*>(base + (long long)(row0 + row) * ld + ch * 8);
+    r[i] = v;
+  }
+}
+__device__ __forceinline__ void tile_store(const uint4 (&r)[2], bf16_t* lds) {
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int c = threadIdx.x + i * 256;
+    *reinterpret_cast<uint4*>(lds + aoff(c >> 3, c & 7)) = r[i];
+  }
+}
+
+// Row fragment (A or B operand of 32x32x16): lane holds X[row0 + (lane & 31)][16 st + 8 h .. +7]
+__device__ __forceinline__ bf16x8 row_frag(const bf16_t* lds, int row0, int st, int lane) {
+  const int row = row0 + (lane & 31);
+  const int chunk = 2 * st + (lane >> 5);
+  return *reinterpret_cast<const bf16x8*>(lds + aoff(row, chunk));
+}
+
+// Transposed fragment: lane gets X[rows r0 + 16 s + 8 (j >> 2) + 4 h + (j & 3)][col c0 + (lane & 31)]
+// i.e. the permuted k order of an accumulator-as-operand k-step s.
+__device__ __forceinline__ bf16x8 tr_frag(const bf16_t* lds, int r0, int s, int c0, int lane) {
+  const int h = lane >> 5, g2 = (lane >> 4) & 1, i16 = lane & 15, q = i16 >> 2, p = i16 & 3;
+  const int row = r0 + 16 * s + 4 * h + q;
+  const int col = c0 + 16 * g2 + 4 * p;
+  const int chunk = col >> 3, within = col & 7;
+  const bf16_t* a0 = lds + row * HD + (((chunk ^ aswz(row)) << 3) | within);
+  const bf16_t* a1 = lds + (row + 8) * HD + (((chunk ^ aswz(row + 8)) << 3) | within);
+  short4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds4_t)a0);
+  short4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds4_t)a1);
+  typedef short short8_t __attribute__((ext_vector_type(8)));
+  short8_t s8 = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  return __builtin_bit_cast(bf16x8, s8);
+}
+
+// Accumulator registers 8s..8s+7 -> bf16 operand fragment of k-step s.
+__device__ __forceinline__ bf16x8 acc_frag(const floatx16& x, int s) {
+  uint4 u;
+  u.x = pack2bf(x[8 * s + 0], x[8 * s + 1]);
+  u.y = pack2bf(x[8 * s + 2], x[8 * s + 3]);
+  u.z = pack2bf(x[8 * s + 4], x[8 * s + 5]);
+  u.w = pack2bf(x[8 * s + 6], x[8 * s + 7]);
+  return __builtin_bit_cast(bf16x8, u);
+}
+
+__device__ __forceinline__ int acc_row(int r, int lane) { return (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5); }
+
+__device__ __forceinline__ bf16x8 load_row8(const bf16_t* p) {
+  return *reinterpret_cast<const bf16x8*>(p);
+}
+
+#define MFMA32(a, b, c) __builtin_amdgcn_mfma_f32_32x32x16_bf16((a), (b), (c), 0, 0, 0)
+
+// ------------------------------------------------------------------ forward
+__global__ __launch_bounds__(256) void attn_fwd_kernel(AttnArgs p) {
+  __shared__ __attribute__((aligned(16))) bf16_t smem[2 * 2 * KT * HD];  // [stage][K|V]
+  const int S = p.S, H = p.H;
+  const int nqb = (S + QB - 1) / QB;
+  const int qb = nqb - 1 - (int)blockIdx.x;  // heaviest causal blocks first
+  const int bh = blockIdx.y, n = bh / H, h = bh % H;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, hh = lane >> 5;
+  const int q0 = qb * QB + wid * 32;
+  const int q = q0 + (lane & 31);
+  const long long tok0 = (long long)n * S;
+  const bf16_t* Q = static_cast<const bf16_t*>(p.q) + h * HD;
+  const bf16_t* K = static_cast<const bf16_t*>(p.k) + tok0 * p.ld_qkv + h * HD;
+  const bf16_t* V = static_cast<const bf16_t*>(p.v) + tok0 * p.ld_qkv + h * HD;
+
+  bf16x8 qf[4];
+#pragma unroll
+  for (int st = 0; st < 4; ++st) {
+    if (q < S) qf[st] = load_row8(Q + (tok0 + q) * p.ld_qkv + 16 * st + 8 * hh);
+    else qf[st] = bf16x8{};
+  }
+  const float c = p.scale * LOG2E;
+  const int kend = p.causal ? min(S, qb * QB + QB) : S;
+  const int ntiles = (kend + KT - 1) / KT;
+  const unsigned char* pad = p.pad ? p.pad + (long long)n * S : nullptr;
+
+  float m = -INFINITY, l = 0.f;
+  floatx16 o[2];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) { o[0][i] = 0.f; o[1][i] = 0.f; }
+
+  uint4 rk[2], rv[2];
+  tile_load(rk, K, p.ld_qkv, 0, S);
+  tile_load(rv, V, p.ld_qkv, 0, S);
+  tile_store(rk, smem);
+  tile_store(rv, smem + KT * HD);
+  __syncthreads();
+
+  for (int t = 0; t < ntiles; ++t) {
+    const int cur = t & 1;
+    const bool more = t + 1 < ntiles;
+    if (more) {
+      tile_load(rk, K, p.ld_qkv, (t + 1) * KT, S);
+      tile_load(rv, V, p.ld_qkv, (t + 1) * KT, S);
+    }
+    const bf16_t* lk = smem + cur * 2 * KT * HD;
+    const bf16_t* lv = lk + KT * HD;
+    const int kt0 = t * KT;
+    const bool active = !(p.causal && kt0 > q0 + 31);  // wave-uniform
+    if (active) {
+      floatx16 s[2];
+#pragma unroll
+      for (int kb = 0; kb < 2; ++kb) {
+#pragma unroll
+        for (int i = 0; i < 16; ++i) s[kb][i] = 0.f;
+#pragma unroll
+        for (int st = 0; st < 4; ++st) s[kb] = MFMA32(row_frag(lk, kb * 32, st, lane), qf[st], s[kb]);
+      }
+      const bool need_mask = (p.causal && kt0 + KT - 1 > q0) || (kt0 + KT > S) || pad;
+      float mx = -INFINITY;
+#pragma unroll
+      for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          float v = s[kb][r] * c;
+          if (need_mask) {
+            const int key = kt0 + kb * 32 + acc_row(r, lane);
+            if (key >= S || (p.causal && key > q) || (pad && pad[key])) v = -INFINITY;
+          }
+          s[kb][r] = v;
+          mx = fmaxf(mx, v);
+        }
+      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+      const float mn = fmaxf(m, mx);
+      const float mu = (mn == -INFINITY) ? 0.f : mn;
+      const float alpha = exp2f(m - mu);
+      float ls = 0.f;
+#pragma unroll
+      for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const float e = exp2f(s[kb][r] - mu);
+          s[kb][r] = e;
+          ls += e;
+        }
+      ls += __shfl_xor(ls, 32, 64);
+      l = l * alpha + ls;
+      m = mn;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) { o[0][i] *= alpha; o[1][i] *= alpha; }
+#pragma unroll
+      for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+        for (int ss = 0; ss < 2; ++ss) {
+          const bf16x8 pb = acc_frag(s[kb], ss);
+#pragma unroll
+          for (int dt = 0; dt < 2; ++dt) o[dt] = MFMA32(tr_frag(lv, kb * 32, ss, dt * 32, lane), pb, o[dt]);
+        }
+    }
+    if (more) {
+      bf16_t* nx = smem + (cur ^ 1) * 2 * KT * HD;
+      tile_store(rk, nx);
+      tile_store(rv, nx + KT * HD);
+    }
+    __syncthreads();
+  }
+
+  if (q < S) {
+    const float inv = l > 0.f ? 1.f / l : 0.f;
+    bf16_t* O = static_cast<bf16_t*>(p.o) + (tok0 + q) * p.ld_o + h * HD;
+#pragma unroll
+    for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int d = dt * 32 + 8 * g + 4 * hh;
+        uint2 w;
+        w.x = pack2bf(o[dt][4 * g + 0] * inv, o[dt][4 * g + 1] * inv);
+        w.y = pack2bf(o[dt][4 * g + 2] * inv, o[dt][4 * g + 3] * inv);
+        *reinterpret_cast<uint2*>(O + d) = w;
+      }
+    if (hh == 0) {
+      const float lse = (l > 0.f) ? (m + log2f(l)) / LOG2E : INFINITY;
+      p.lse[(long long)bh * S + q] = lse;
+    }
+  }
+}
+
+// ------------------------------------------------------------------ backward
+// delta[n,h,s] = sum_d dO * O   (one 8-lane group per (token, head))
+__global__ __launch_bounds__(256) void attn_bwd_pre_kernel(AttnArgs p) {
+  const long long T = (long long)p.N * p.S;
+  const long long row = ((long long)blockIdx.x * 256 + threadIdx.x) >> 3;  // (token, head)
+  const int sub = threadIdx.x & 7;
+  float acc = 0.f;
+  long long t = 0; int h = 0;
+  if (row < T * p.H) {
+    t = row / p.H; h = (int)(row % p.H);
+    const bf16_t* o = static_cast<const bf16_t*>(p.o) + t * p.ld_o + h * HD + sub * 8;
+    const bf16_t* d = static_cast<const bf16_t*>(p.dout) + t * p.ld_o + h * HD + sub * 8;
+    float fo[8], fd[8];
+    unpack8(*reinterpret_cast<const uint4*>(o), fo);
+    unpack8(*reinterpret_cast<const uint4*>(d), fd);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) acc += fo[i] * fd[i];
+  }
+  acc += __shfl_xor(acc, 1, 64);
+  acc += __shfl_xor(acc, 2, 64);
+  acc += __shfl_xor(acc, 4, 64);
+  if (row < T * p.H && sub == 0) {
+    const long long n = t / p.S, s = t % p.S;
+    p.delta[(n * p.H + h) * p.S + s] = acc;
+  }
+}
+
+// dK, dV: workgroup = 128 keys (4 waves x 32), sweep all queries >= first key.
+__global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(AttnArgs p) {
+  __shared__ __attribute__((aligned(16))) bf16_t smem[2 * 2 * KT * HD];  // [stage][Q|dO]
+  __shared__ float srow[2][2][KT];                                      // [stage][lse2|delta]
+  const int S = p.S, H = p.H;
+  const int nkb = (S + QB - 1) / QB;
+  const int kb = blockIdx.x;
+  (void)nkb;
+  const int bh = blockIdx.y, n = bh / H, h = bh % H;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, hh = lane >> 5;
+  const int k0 = kb * QB + wid * 32;
+  const int key = k0 + (lane & 31);
+  const long long tok0 = (long long)n * S;
+  const bf16_t* Q = static_cast<const bf16_t*>(p.q) + tok0 * p.ld_qkv + h * HD;
+  const bf16_t* Kp = static_cast<const bf16_t*>(p.k) + h * HD;
+  const bf16_t* Vp = static_cast<const bf16_t*>(p.v) + h * HD;
+  const bf16_t* dO = static_cast<const bf16_t*>(p.dout) + tok0 * p.ld_o + h * HD;
+  const float* lse = p.lse + (long long)bh * S;
+  const float* delta = p.delta + (long long)bh * S;
+  const bool key_ok = key < S && !(p.pad && p.pad[(long long)n * S + min(key, S - 1)]);
+
+  bf16x8 kf[4], vf[4];
+#pragma unroll
+  for (int st = 0; st < 4; ++st) {
+    if (key < S) {
+      kf[st] = load_row8(Kp + (tok0 + key) * p.ld_qkv + 16 * st + 8 * hh);
+      vf[st] = load_row8(Vp + (tok0 + key) * p.ld_qkv + 16 * st + 8 * hh);
+    } else {
+      kf[st] = bf16x8{};
+      vf[st] = bf16x8{};
+    }
+  }
+  const float c = p.scale * LOG2E;
+  floatx16 dvt[2], dkt[2];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) { dvt[0][i] = dvt[1][i] = dkt[0][i] = dkt[1][i] = 0.f; }
+
+  const int qt_begin = p.causal ? (kb * QB) / KT : 0;
+  const int nqt = (S + KT - 1) / KT;
+
+  uint4 rq[2], rd[2];
+  float rl = 0.f, rdl = 0.f;
+  auto load_rows = [&](int qt) {
+    tile_load(rq, Q, p.ld_qkv, qt * KT, S);
+    tile_load(rd, dO, p.ld_o, qt * KT, S);
+    if (threadIdx.x < KT) {
+      const int qq = qt * KT + threadIdx.x;
+      rl = qq < S ? lse[qq] * LOG2E : INFINITY;
+      rdl = qq < S ? delta[qq] : 0.f;
+    }
+  };
+  auto store_rows = [&](int stg) {
+    tile_store(rq, smem + stg * 2 * KT * HD);
+    tile_store(rd, smem + stg * 2 * KT * HD + KT * HD);
+    if (threadIdx.x < KT) { srow[stg][0][threadIdx.x] = rl; srow[stg][1][threadIdx.x] = rdl; }
+  };
+  if (qt_begin < nqt) { load_rows(qt_begin); store_rows(0); }
+  __syncthreads();
+
+  for (int qt = qt_begin; qt < nqt; ++qt) {
+    const int cur = (qt - qt_begin) & 1;
+    const bool more = qt + 1 < nqt;
+    if (more) load_rows(qt + 1);
+    const bf16_t* lq = smem + cur * 2 * KT * HD;
+    const bf16_t* ld = lq + KT * HD;
+    const int qt0 = qt * KT;
+    const bool active = !(p.causal && qt0 + KT - 1 < k0);  // wave-uniform
+    if (active) {
+#pragma unroll
+      for (int qs = 0; qs < 2; ++qs) {
+        floatx16 sa, dp;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) { sa[i] = 0.f; dp[i] = 0.f; }
+#pragma unroll
+        for (int st = 0; st < 4; ++st) {
+          sa = MFMA32(row_frag(lq, qs * 32, st, lane), kf[st], sa);
+          dp = MFMA32(row_frag(ld, qs * 32, st, lane), vf[st], dp);
+        }
+        // sa[r]: query qt0 + qs*32 + acc_row(r), key = lane's key
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int qi = qs * 32 + acc_row(r, lane);
+          const int qq = qt0 + qi;
+          float pv = exp2f(sa[r] * c - srow[cur][0][qi]);
+          if (!key_ok || (p.causal && key > qq)) pv = 0.f;
+          sa[r] = pv;
+          dp[r] = pv * (dp[r] - srow[cur][1][qi]);
+        }
+#pragma unroll
+        for (int ss = 0; ss < 2; ++ss) {
+          const bf16x8 pb = acc_frag(sa, ss);
+          const bf16x8 db = acc_frag(dp, ss);
+#pragma unroll
+          for (int dt = 0; dt < 2; ++dt) {
+            dvt[dt] = MFMA32(tr_frag(ld, qs * 32, ss, dt * 32, lane), pb, dvt[dt]);
+            dkt[dt] = MFMA32(tr_frag(lq, qs * 32, ss, dt * 32, lane), db, dkt[dt]);
+          }
+        }
+      }
+    }
+    if (more) store_rows(cur ^ 1);
+    __syncthreads();
+  }
+
+  if (key < S) {
+    bf16_t* dK = static_cast<bf16_t*>(p.dk) + (tok0 + key) * p.ld_dqkv + h * HD;
+    bf16_t* dV = static_cast<bf16_t*>(p.dv) + (tok0 + key) * p.ld_dqkv + h * HD;
+#pragma unroll
+    for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int d = dt * 32 + 8 * g + 4 * hh;
+        uint2 w;
+        w.x = pack2bf(dkt[dt][4 * g + 0] * p.scale, dkt[dt][4 * g + 1] * p.scale);
+        w.y = pack2bf(dkt[dt][4 * g + 2] * p.scale, dkt[dt][4 * g + 3] * p.scale);
+        *reinterpret_cast<uint2*>(dK + d) = w;
+        w.x = pack2bf(dvt[dt][4 * g + 0], dvt[dt][4 * g + 1]);
+        w.y = pack2bf(dvt[dt][4 * g + 2], dvt[dt][4 * g + 3]);
+        *reinterpret_cast<uint2*>(dV + d) = w;
+      }
+  }
+}
+
+// dQ: workgroup = 128 queries (4 waves x 32), sweep keys <= last query.
+__global__ __launch_bounds__(256) void attn_bwd_dq_kernel(AttnArgs p) {
+  __shared__ __attribute__((aligned(16))) bf16_t smem[2 * 2 * KT * HD];  // [stage][K|V]
+  const int S = p.S, H = p.H;
+  const int nqb = (S + QB - 1) / QB;
+  const int qb = nqb - 1 - (int)blockIdx.x;
+  const int bh = blockIdx.y, n = bh / H, h = bh % H;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, hh = lane >> 5;
+  const int q0 = qb * QB + wid * 32;
+  const int q = q0 + (lane & 31);
+  const long long tok0 = (long long)n * S;
+  const bf16_t* Q = static_cast<const bf16_t*>(p.q) + h * HD;
+  const bf16_t* K = static_cast<const bf16_t*>(p.k) + tok0 * p.ld_qkv + h * HD;
+  const bf16_t* V = static_cast<const bf16_t*>(p.v) + tok0 * p.ld_qkv + h * HD;
+  const bf16_t* dO = static_cast<const bf16_t*>(p.dout) + h * HD;
+  const unsigned char* pad = p.pad ? p.pad + (long long)n * S : nullptr;
+
+  bf16x8 qf[4], df[4];
+#pragma unroll
+  for (int st = 0; st < 4; ++st) {
+    if (q < S) {
+      qf[st] = load_row8(Q + (tok0 + q) * p.ld_qkv + 16 * st + 8 * hh);
+      df[st] = load_row8(dO + (tok0 + q) * p.ld_o + 16 * st + 8 * hh);
+    } else {
+      qf[st] = bf16x8{};
+      df[st] = bf16x8{};
+    }
+  }
+  const float c = p.scale * LOG2E;
+  const float lse2 = q < S ? p.lse[(long long)bh * S + q] * LOG2E : INFINITY;
+  const float dl = q < S ? p.delta[(long long)bh * S + q] : 0.f;
+  floatx16 dqt[2];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) { dqt[0][i] = 0.f; dqt[1][i] = 0.f; }
+
+  const int kend = p.causal ? min(S, qb * QB + QB) : S;
+  const int ntiles = (kend + KT - 1) / KT;
+  uint4 rk[2], rv[2];
+  tile_load(rk, K, p.ld_qkv, 0, S);
+  tile_load(rv, V, p.ld_qkv, 0, S);
+  tile_store(rk, smem);
+  tile_store(rv, smem + KT * HD);
+  __syncthreads();
+
+  for (int t = 0; t < ntiles; ++t) {
+    const int cur = t & 1;
+    const bool more = t + 1 < ntiles;
+    if (more) {
+      tile_load(rk, K, p.ld_qkv, (t + 1) * KT, S);
+      tile_load(rv, V, p.ld_qkv, (t + 1) * KT, S);
+    }
+    const bf16_t* lk = smem + cur * 2 * KT * HD;
+    const bf16_t* lv = lk + KT * HD;
+    const int kt0 = t * KT;
+    const bool active = !(p.causal && kt0 > q0 + 31);
+    if (active) {
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        floatx16 sa, dp;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) { sa[i] = 0.f; dp[i] = 0.f; }
+#pragma unroll
+        for (int st = 0; st < 4; ++st) {
+          sa = MFMA32(row_frag(lk, ks * 32, st, lane), qf[st], sa);
+          dp = MFMA32(row_frag(lv, ks * 32, st, lane), df[st], dp);
+        }
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int key = kt0 + ks * 32 + acc_row(r, lane);
+          float pv = exp2f(sa[r] * c - lse2);
+          if (key >= S || (p.causal && key > q) || (pad && pad[key])) pv = 0.f;
+          dp[r] = pv * (dp[r] - dl);
+        }
+#pragma unroll
+        for (int ss = 0; ss < 2; ++ss) {
+          const bf16x8 db = acc_frag(dp, ss);
+#pragma unroll
+          for (int dt = 0; dt < 2; ++dt) dqt[dt] = MFMA32(tr_frag(lk, ks * 32, ss, dt * 32, lane), db, dqt[dt]);
+        }
+      }
+    }
+    if (more) {
+      bf16_t* nx = smem + (cur ^ 1) * 2 * KT * HD;
+      tile_store(rk, nx);
+      tile_store(rv, nx + KT * HD);
+    }
+    __syncthreads();
+  }
+
+  if (q < S) {
+    bf16_t* dQ = static_cast<bf16_t*>(p.dq) + (tok0 + q) * p.ld_dqkv + h * HD;
+#pragma unroll
+    for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int d = dt * 32 + 8 * g + 4 * hh;
+        uint2 w;
+        w.x = pack2bf(dqt[dt][4 * g + 0] * p.scale, dqt[dt][4 * g + 1] * p.scale);
+        w.y = pack2bf(dqt[dt][4 * g + 2] * p.scale, dqt[dt][4 * g + 3] * p.scale);
+        *reinterpret_cast<uint2*>(dQ + d) = w;
+      }
+  }
+}
+
+}  // namespace dpc
+
+using namespace dpc;
+
+DPC_API int dpc_attn_fwd(const AttnArgs* a, hipStream_t stream) {
+  dim3 grid((a->S + QB - 1) / QB, a->N * a->H);
+  hipLaunchKernelGGL(attn_fwd_kernel, grid, dim3(256), 0, stream, *a);
+  return (int)hipGetLastError();
+}
+
+DPC_API int dpc_attn_bwd(const AttnArgs* a, hipStream_t stream) {
+  const long long rows = (long long)a->N * a->S * a->H;
+  dim3 gpre((unsigned)((rows * 8 + 255) / 256));
+  hipLaunchKernelGGL(attn_bwd_pre_kernel, gpre, dim3(256), 0, stream, *a);
+  dim3 grid((a->S + QB - 1) / QB, a->N * a->H);
+  hipLaunchKernelGGL(attn_bwd_dkdv_kernel, grid, dim3(256), 0, stream, *a);
+  hipLaunchKernelGGL(attn_bwd_dq_kernel, grid, dim3(256), 0, stream, *a);
+  return (int)hipGetLastError();
+}

@@ -1,0 +1,128 @@
+// Shared device helpers for the CDNA4 (gfx950 / MI355X) kernels of the cookbook.
+//
+// Conventions used by every kernel in this directory:
+//   * wave64 everywhere: lane = threadIdx.x & 63, block sizes are multiples of 64.
+//   * bf16 is carried as raw 16-bit payloads (unsigned short) in memory and widened
+//     to f32 with a shift; narrowing uses the compiler's round-to-nearest-even cast
+//     (hipcc emits v_cvt_pk_bf16_f32, which keeps NaNs NaN).
+//   * memory-bound kernels move 16 B per lane (uint4 = 8 x bf16 or 4 x f32).
+//   * every launcher is a C-ABI function taking an argument struct by pointer and a
+//     hipStream_t, returning the hipError_t of the launch (0 == success).  Python
+//     binds them with ctypes (ops/_lib.py); no torch headers are needed here, so the
+//     whole library cross-compiles in seconds.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define DPC_API extern "C" __attribute__((visibility("default")))
+
+typedef unsigned short bf16_t;  // raw bf16 payload
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef short short4_t __attribute__((ext_vector_type(4)));
+typedef float floatx4 __attribute__((ext_vector_type(4)));
+typedef float floatx16 __attribute__((ext_vector_type(16)));
+
+namespace dpc {
+
+__device__ __forceinline__ float bf2f(bf16_t v) {
+  return __uint_as_float(((unsigned)v) << 16);
+}
+
+__device__ __forceinline__ bf16_t f2bf(float f) {
+  __bf16 b = (__bf16)f;  // RNE, NaN-preserving (v_cvt_pk_bf16_f32)
+  return *reinterpret_cast<bf16_t*>(&b);
+}
+
+// pack two floats into one dword of 2 x bf16 (lo = a, hi = b)
+__device__ __forceinline__ unsigned pack2bf(float a, float b) {
+  return (unsigned)f2bf(a) | ((unsigned)f2bf(b) << 16);
+}
+
+__device__ __forceinline__ void unpack8(const uint4& v, float* f) {
+  const unsigned w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    f[2 * i] = __uint_as_float(w[i] << 16);
+    f[2 * i + 1] = __uint_as_float(w[i] & 0xffff0000u);
+  }
+}
+
+__device__ __forceinline__ uint4 pack8(const float* f) {
+  uint4 r;
+  r.x = pack2bf(f[0], f[1]);
+  r.y = pack2bf(f[2], f[3]);
+  r.z = pack2bf(f[4], f[5]);
+  r.w = pack2bf(f[6], f[7]);
+  return r;
+}
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// Block-wide sum for blocks of NW waves; `red` must hold NW floats of LDS.
+template <int NW>
+__device__ __forceinline__ float block_sum(float v, float* red) {
+  v = wave_sum(v);
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  __syncthreads();
+  if (lane == 0) red[w] = v;
+  __syncthreads();
+  float t = 0.f;
+#pragma unroll
+  for (int i = 0; i < NW; ++i) t += red[i];
+  return t;
+}
+
+template <int NW>
+__device__ __forceinline__ float block_max(float v, float* red) {
+  v = wave_max(v);
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  __syncthreads();
+  if (lane == 0) red[w] = v;
+  __syncthreads();
+  float t = -INFINITY;
+#pragma unroll
+  for (int i = 0; i < NW; ++i) t = fmaxf(t, red[i]);
+  return t;
+}
+
+// GPT-2 "gelu_new": 0.5 x (1 + tanh(sqrt(2/pi) (x + 0.044715 x^3)))
+__device__ __forceinline__ float gelu_tanh(float x) {
+  const float k0 = 0.7978845608028654f, k1 = 0.044715f;
+  float u = k0 * (x + k1 * x * x * x);
+  return 0.5f * x * (1.f + tanhf(u));
+}
+
+__device__ __forceinline__ float gelu_tanh_grad(float x) {
+  const float k0 = 0.7978845608028654f, k1 = 0.044715f;
+  float x2 = x * x;
+  float u = k0 * (x + k1 * x2 * x);
+  float t = tanhf(u);
+  return 0.5f * (1.f + t) + 0.5f * x * (1.f - t * t) * k0 * (1.f + 3.f * k1 * x2);
+}
+
+enum Act { ACT_NONE = 0, ACT_RELU = 1, ACT_GELU = 2 };
+
+__device__ __forceinline__ float act_fwd(float v, int act) {
+  if (act == ACT_RELU) return fmaxf(v, 0.f);
+  if (act == ACT_GELU) return gelu_tanh(v);
+  return v;
+}
+
+// derivative of act evaluated from the saved pre-activation z
+__device__ __forceinline__ float act_grad(float z, int act) {
+  if (act == ACT_RELU) return z > 0.f ? 1.f : 0.f;
+  if (act == ACT_GELU) return gelu_tanh_grad(z);
+  return 1.f;
+}
+
+}  // namespace dpc

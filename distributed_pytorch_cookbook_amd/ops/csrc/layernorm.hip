@@ -1,0 +1,186 @@
+// LayerNorm forward / backward (eps as nn.LayerNorm, default 1e-5) for gfx950.
+//
+// Reference: models/gpt.py:119,122,217 (nn.LayerNorm on the fp32 residual stream under
+// autocast).  Forward reads the f32 residual row once (16 B per lane), keeps it in
+// registers, and writes the bf16 normalised row that feeds the next MFMA GEMM plus the
+// (mean, rstd) pair.  Backward recomputes x_hat from the f32 row, writes
+// dx_total = dres + LN'(dy) IN PLACE into the residual-gradient buffer (the residual add
+// of gpt.py:129/133 fused away), and reduces dgamma / dbeta per workgroup in registers
+// before ONE f32 atomic per column per workgroup.
+//
+// One wave per row, NV float4 per lane (D <= 256 * NV), 4 rows (waves) per workgroup.
+#include "common.h"
+
+namespace dpc {
+
+struct LNArgs {
+  const float* x;      // [T][ldx] f32
+  const float* gamma;  // [D]
+  const float* beta;   // [D]
+  void* y;             // fwd: [T][ldy] bf16 (or f32 if y_f32)
+  float* mean;         // [T]
+  float* rstd;         // [T]
+  const float* dy;     // bwd: [T][lddy] f32
+  float* dx;           // bwd: [T][lddx] f32, accumulated (dx += LN'(dy))
+  float* dgamma;       // bwd: [D] f32 accumulated
+  float* dbeta;        // bwd: [D] f32 accumulated
+  long long ldx, ldy, lddy, lddx;
+  int T, D;
+  float eps;
+  int y_f32;
+};
+
+template <int NV>
+__global__ __launch_bounds__(256) void ln_fwd_kernel(LNArgs p) {
+  const int lane = threadIdx.x & 63;
+  const long long row = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= p.T) return;
+  const float4* xr = reinterpret_cast<const float4*>(p.x + row * p.ldx);
+  const int nv4 = p.D >> 2;
+  float4 v[NV];
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    const int c = lane + i * 64;
+    v[i] = c < nv4 ? xr[c] : make_float4(0.f, 0.f, 0.f, 0.f);
+    s += v[i].x + v[i].y + v[i].z + v[i].w;
+  }
+  const float mu = wave_sum(s) / p.D;
+  float ss = 0.f;
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    const int c = lane + i * 64;
+    if (c < nv4) {
+      const float a = v[i].x - mu, b = v[i].y - mu, cc = v[i].z - mu, d = v[i].w - mu;
+      ss += a * a + b * b + cc * cc + d * d;
+    }
+  }
+  const float rs = rsqrtf(wave_sum(ss) / p.D + p.eps);
+  const float4* g4 = reinterpret_cast<const float4*>(p.gamma);
+  const float4* b4 = reinterpret_cast<const float4*>(p.beta);
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    const int c = lane + i * 64;
+    if (c < nv4) {
+      const float4 g = g4[c], b = b4[c];
+      float4 o;
+      o.x = (v[i].x - mu) * rs * g.x + b.x;
+      o.y = (v[i].y - mu) * rs * g.y + b.y;
+      o.z = (v[i].z - mu) * rs * g.z + b.z;
+      o.w = (v[i].w - mu) * rs * g.w + b.w;
+      if (p.y_f32) {
+        reinterpret_cast<float4*>(static_cast<float*>(p.y) + row * p.ldy)[c] = o;
+      } else {
+        uint2 w;
+        w.x = pack2bf(o.x, o.y);
+        w.y = pack2bf(o.z, o.w);
+        reinterpret_cast<uint2*>(static_cast<bf16_t*>(p.y) + row * p.ldy)[c] = w;
+      }
+    }
+  }
+  if (lane == 0) {
+    p.mean[row] = mu;
+    p.rstd[row] = rs;
+  }
+}
+
+template <int NV>
+__global__ __launch_bounds__(256) void ln_bwd_kernel(LNArgs p) {
+  __shared__ float red[4][2][NV * 256];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int nv4 = p.D >> 2;
+  const float4* g4 = reinterpret_cast<const float4*>(p.gamma);
+  float4 gacc[NV], bacc[NV], gam[NV];
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    const int c = lane + i * 64;
+    gacc[i] = bacc[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+    gam[i] = c < nv4 ? g4[c] : make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+  for (long long row = (long long)blockIdx.x * 4 + w; row < p.T; row += (long long)gridDim.x * 4) {
+    const float4* xr = reinterpret_cast<const float4*>(p.x + row * p.ldx);
+    const float4* dyr = reinterpret_cast<const float4*>(p.dy + row * p.lddy);
+    const float mu = p.mean[row], rs = p.rstd[row];
+    float4 xh[NV], dg[NV];
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      const int c = lane + i * 64;
+      if (c < nv4) {
+        const float4 xv = xr[c], d = dyr[c];
+        xh[i] = make_float4((xv.x - mu) * rs, (xv.y - mu) * rs, (xv.z - mu) * rs, (xv.w - mu) * rs);
+        dg[i] = make_float4(d.x * gam[i].x, d.y * gam[i].y, d.z * gam[i].z, d.w * gam[i].w);
+        s1 += dg[i].x + dg[i].y + dg[i].z + dg[i].w;
+        s2 += dg[i].x * xh[i].x + dg[i].y * xh[i].y + dg[i].z * xh[i].z + dg[i].w * xh[i].w;
+        gacc[i].x += d.x * xh[i].x; gacc[i].y += d.y * xh[i].y;
+        gacc[i].z += d.z * xh[i].z; gacc[i].w += d.w * xh[i].w;
+        bacc[i].x += d.x; bacc[i].y += d.y; bacc[i].z += d.z; bacc[i].w += d.w;
+      } else {
+        xh[i] = dg[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+    }
+    s1 = wave_sum(s1) / p.D;
+    s2 = wave_sum(s2) / p.D;
+    float4* dxr = reinterpret_cast<float4*>(p.dx + row * p.lddx);
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      const int c = lane + i * 64;
+      if (c < nv4) {
+        float4 o = dxr[c];
+        o.x += rs * (dg[i].x - s1 - xh[i].x * s2);
+        o.y += rs * (dg[i].y - s1 - xh[i].y * s2);
+        o.z += rs * (dg[i].z - s1 - xh[i].z * s2);
+        o.w += rs * (dg[i].w - s1 - xh[i].w * s2);
+        dxr[c] = o;
+      }
+    }
+  }
+  // reduce dgamma / dbeta across the 4 waves, then one atomic per column per workgroup
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    const int c = lane + i * 64;
+    reinterpret_cast<float4*>(&red[w][0][0])[c] = gacc[i];
+    reinterpret_cast<float4*>(&red[w][1][0])[c] = bacc[i];
+  }
+  __syncthreads();
+  for (int c = threadIdx.x; c < p.D; c += 256) {
+    float g = red[0][0][c] + red[1][0][c] + red[2][0][c] + red[3][0][c];
+    float b = red[0][1][c] + red[1][1][c] + red[2][1][c] + red[3][1][c];
+    atomicAdd(p.dgamma + c, g);
+    atomicAdd(p.dbeta + c, b);
+  }
+}
+
+}  // namespace dpc
+
+using namespace dpc;
+
+#define LN_DISPATCH(KERNEL, GRID)                                                     \
+  switch ((a->D + 255) / 256) {                                                        \
+    case 1: hipLaunchKernelGGL(KERNEL<1>, GRID, dim3(256), 0, stream, *a); break;      \
+    case 2: hipLaunchKernelGGL(KERNEL<2>, GRID, dim3(256), 0, stream, *a); break;      \
+    case 3: hipLaunchKernelGGL(KERNEL<3>, GRID, dim3(256), 0, stream, *a); break;      \
+    case 4: hipLaunchKernelGGL(KERNEL<4>, GRID, dim3(256), 0, stream, *a); break;      \
+    case 5: hipLaunchKernelGGL(KERNEL<5>, GRID, dim3(256), 0, stream, *a); break;      \
+    case 6: hipLaunchKernelGGL(KERNEL<6>, GRID, dim3(256), 0, stream, *a); break;      \
+    case 7: hipLaunchKernelGGL(KERNEL<7>, GRID, dim3(256), 0, stream, *a); break;      \
+    case 8: hipLaunchKernelGGL(KERNEL<8>, GRID, dim3(256), 0, stream, *a); break;      \
+    default: return (int)hipErrorInvalidValue;                                         \
+  }
+
+DPC_API int dpc_layernorm_fwd(const LNArgs* a, hipStream_t stream) {
+  if (a->T <= 0) return 0;
+  if (a->D % 4) return (int)hipErrorInvalidValue;
+  dim3 grid((unsigned)((a->T + 3) / 4));
+  LN_DISPATCH(ln_fwd_kernel, grid);
+  return (int)hipGetLastError();
+}
+
+DPC_API int dpc_layernorm_bwd(const LNArgs* a, hipStream_t stream) {
+  if (a->T <= 0) return 0;
+  if (a->D % 4) return (int)hipErrorInvalidValue;
+  const long long blocks = (a->T + 3) / 4;
+  dim3 grid((unsigned)(blocks < 1024 ? blocks : 1024));
+  LN_DISPATCH(ln_bwd_kernel, grid);
+  return (int)hipGetLastError();
+}

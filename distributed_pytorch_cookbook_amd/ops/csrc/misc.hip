@@ -1,0 +1,330 @@
+// Memory-bound training kernels for gfx950: embedding gather / scatter-add, fused
+// softmax-cross-entropy (forward + backward in one pass pair), flat AdamW, and the
+// bias/activation-backward + column-sum kernel.  All move 16 B per lane.
+//
+// Reference parity:
+//   embedding      models/gpt.py:177-185 (token + learned position embedding, summed, f32 out)
+//   cross entropy  main-single.py:95-96  (F.cross_entropy, ignore_index=-100, mean over valid)
+//                  + main-single.py:128-131 (eval argmax accuracy) fused into the same pass
+//   adamw          main-single.py:42     (torch.optim.AdamW defaults: betas (0.9, 0.999),
+//                  eps 1e-8, weight_decay 0.01, decoupled decay) over ONE flat buffer
+//   bias/act bwd   gradient of nn.Linear bias + F.relu / gelu (models/gpt.py:34-38)
+#include "common.h"
+
+namespace dpc {
+
+// ------------------------------------------------------------------ embedding
+struct EmbArgs {
+  const long long* ids;  // [T]
+  const long long* pos;  // [T]
+  const void* tok;       // [V][D] (f32 or bf16)
+  const void* ptab;      // [P][D]
+  float* out;            // [T][D] f32
+  const float* dout;     // bwd [T][D]
+  float* dtok;           // bwd [V][D] f32 (accumulate)
+  float* dpos;           // bwd [P][D] f32 (accumulate)
+  int T, D, V, P;
+  int table_bf16;
+};
+
+__global__ __launch_bounds__(256) void emb_fwd_kernel(EmbArgs p) {
+  const int lane = threadIdx.x & 63;
+  const long long row = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= p.T) return;
+  long long id = p.ids[row], ps = p.pos[row];
+  id = id < 0 ? 0 : (id >= p.V ? p.V - 1 : id);
+  ps = ps < 0 ? 0 : (ps >= p.P ? p.P - 1 : ps);
+  float4* o = reinterpret_cast<float4*>(p.out + row * p.D);
+  const int nv4 = p.D >> 2;
+  for (int c = lane; c < nv4; c += 64) {
+    float4 a, b;
+    if (p.table_bf16) {
+      const uint2 ua = reinterpret_cast<const uint2*>(static_cast<const bf16_t*>(p.tok) + id * p.D)[c];
+      const uint2 ub = reinterpret_cast<const uint2*>(static_cast<const bf16_t*>(p.ptab) + ps * p.D)[c];
+      a = make_float4(__uint_as_float(ua.x << 16), __uint_as_float(ua.x & 0xffff0000u),
+                      __uint_as_float(ua.y << 16), __uint_as_float(ua.y & 0xffff0000u));
+      b = make_float4(__uint_as_float(ub.x << 16), __uint_as_float(ub.x & 0xffff0000u),
+                      __uint_as_float(ub.y << 16), __uint_as_float(ub.y & 0xffff0000u));
+    } else {
+      a = reinterpret_cast<const float4*>(static_cast<const float*>(p.tok) + id * p.D)[c];
+      b = reinterpret_cast<const float4*>(static_cast<const float*>(p.ptab) + ps * p.D)[c];
+    }
+    o[c] = make_float4(a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w);
+  }
+}
+
+// scatter-add: one wave per token row, each wave-instruction adds 256 contiguous bytes
+__global__ __launch_bounds__(256) void emb_bwd_kernel(EmbArgs p) {
+  const int lane = threadIdx.x & 63;
+  const long long row = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= p.T) return;
+  long long id = p.ids[row], ps = p.pos[row];
+  if (id < 0 || id >= p.V || ps < 0 || ps >= p.P) return;
+  const float* g = p.dout + row * p.D;
+  float* dt = p.dtok + id * p.D;
+  float* dp = p.dpos + ps * p.D;
+  for (int c = lane; c < p.D; c += 64) {
+    const float v = g[c];
+    if (p.dtok) atomicAdd(dt + c, v);
+    if (p.dpos) atomicAdd(dp + c, v);
+  }
+}
+
+// ------------------------------------------------------------------ cross entropy
+struct CEArgs {
+  const void* logits;          // [T][ld] bf16
+  void* dlogits;               // [T][ld] bf16 (may alias logits)
+  const long long* targets;    // [T]
+  const float* inv_count;      // device scalar: 1 / #valid targets
+  float* row_loss;             // [T] f32
+  float* row_correct;          // [T] f32 (optional, argmax == target)
+  long long ld;
+  int T, V;
+  int write_grad;
+  int ignore_index;
+};
+
+__device__ __forceinline__ void ms_combine(float& m, float& s, float m2, float s2) {
+  const float mn = fmaxf(m, m2);
+  if (mn == -INFINITY) return;
+  s = s * __expf(m - mn) + s2 * __expf(m2 - mn);
+  m = mn;
+}
+
+__global__ __launch_bounds__(256) void ce_kernel(CEArgs p) {
+  __shared__ float sm[4], ss[4], sv[4];
+  __shared__ int si[4];
+  const long long row = blockIdx.x;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const bf16_t* x = static_cast<const bf16_t*>(p.logits) + row * p.ld;
+  const long long tgt = p.targets[row];
+  const bool valid = tgt != p.ignore_index && tgt >= 0 && tgt < p.V;
+  const int nch = (p.V + 7) >> 3;
+  float m = -INFINITY, s = 0.f, bv = -INFINITY;
+  int bi = 0x7fffffff;
+  for (int c = tid; c < nch; c += 256) {
+    float f[8];
+    unpack8(reinterpret_cast<const uint4*>(x)[c], f);
+    float cm = -INFINITY;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int idx = c * 8 + j;
+      if (idx >= p.V) f[j] = -INFINITY;
+      cm = fmaxf(cm, f[j]);
+      if (f[j] > bv) { bv = f[j]; bi = idx; }
+    }
+    float cs = 0.f;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) cs += __expf(f[j] - cm);
+    ms_combine(m, s, cm, cs);
+  }
+  // wave combine
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const float m2 = __shfl_xor(m, o, 64), s2 = __shfl_xor(s, o, 64);
+    ms_combine(m, s, m2, s2);
+    const float v2 = __shfl_xor(bv, o, 64);
+    const int i2 = __shfl_xor(bi, o, 64);
+    if (v2 > bv || (v2 == bv && i2 < bi)) { bv = v2; bi = i2; }
+  }
+  if (lane == 0) { sm[w] = m; ss[w] = s; sv[w] = bv; si[w] = bi; }
+  __syncthreads();
+  m = sm[0]; s = ss[0]; bv = sv[0]; bi = si[0];
+#pragma unroll
+  for (int i = 1; i < 4; ++i) {
+    ms_combine(m, s, sm[i], ss[i]);
+    if (sv[i] > bv || (sv[i] == bv && si[i] < bi)) { bv = sv[i]; bi = si[i]; }
+  }
+  const float lse = m + __logf(s);
+  if (tid == 0) {
+    p.row_loss[row] = valid ? lse - bf2f(x[tgt]) : 0.f;
+    if (p.row_correct) p.row_correct[row] = (valid && bi == tgt) ? 1.f : 0.f;
+  }
+  if (!p.write_grad) return;
+  const float scale = valid ? *p.inv_count : 0.f;
+  bf16_t* g = static_cast<bf16_t*>(p.dlogits) + row * p.ld;
+  const int nchl = (int)(p.ld >> 3);
+  for (int c = tid; c < nchl; c += 256) {
+    float f[8];
+    if (c < nch) unpack8(reinterpret_cast<const uint4*>(x)[c], f);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int idx = c * 8 + j;
+      float v = 0.f;
+      if (idx < p.V) v = (__expf(f[j] - lse) - (idx == tgt ? 1.f : 0.f)) * scale;
+      f[j] = v;
+    }
+    reinterpret_cast<uint4*>(g)[c] = pack8(f);
+  }
+}
+
+// ------------------------------------------------------------------ AdamW (flat)
+struct AdamArgs {
+  float* param;            // [n] f32 master
+  const float* grad;       // [n] f32
+  float* exp_avg;          // [n]
+  float* exp_avg_sq;       // [n]
+  void* shadow;            // [n] bf16 compute copy (optional)
+  const float* grad_scale_ptr;  // optional device scalar multiplier on the gradient
+  long long n;
+  float lr, beta1, beta2, eps, weight_decay;
+  float bias_correction1, bias_correction2_sqrt;
+  float grad_scale;
+};
+
+__global__ __launch_bounds__(256) void adamw_kernel(AdamArgs a) {
+  const long long n4 = a.n >> 2;
+  float gs = a.grad_scale;
+  if (a.grad_scale_ptr) gs *= *a.grad_scale_ptr;
+  const float step = a.lr / a.bias_correction1;
+  const float decay = 1.f - a.lr * a.weight_decay;
+  const float b1 = a.beta1, b2 = a.beta2;
+  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n4; i += (long long)gridDim.x * 256) {
+    float4 p = reinterpret_cast<float4*>(a.param)[i];
+    const float4 g = reinterpret_cast<const float4*>(a.grad)[i];
+    float4 m = reinterpret_cast<float4*>(a.exp_avg)[i];
+    float4 v = reinterpret_cast<float4*>(a.exp_avg_sq)[i];
+    float pp[4] = {p.x, p.y, p.z, p.w}, gg[4] = {g.x, g.y, g.z, g.w};
+    float mm[4] = {m.x, m.y, m.z, m.w}, vv[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const float gj = gg[j] * gs;
+      mm[j] = b1 * mm[j] + (1.f - b1) * gj;
+      vv[j] = b2 * vv[j] + (1.f - b2) * gj * gj;
+      const float denom = sqrtf(vv[j]) / a.bias_correction2_sqrt + a.eps;
+      pp[j] = pp[j] * decay - step * mm[j] / denom;
+    }
+    reinterpret_cast<float4*>(a.param)[i] = make_float4(pp[0], pp[1], pp[2], pp[3]);
+    reinterpret_cast<float4*>(a.exp_avg)[i] = make_float4(mm[0], mm[1], mm[2], mm[3]);
+    reinterpret_cast<float4*>(a.exp_avg_sq)[i] = make_float4(vv[0], vv[1], vv[2], vv[3]);
+    if (a.shadow) {
+      uint2 w;
+      w.x = pack2bf(pp[0], pp[1]);
+      w.y = pack2bf(pp[2], pp[3]);
+      reinterpret_cast<uint2*>(a.shadow)[i] = w;
+    }
+  }
+}
+
+// f32 -> bf16 copy of a flat buffer (shadow refresh after load / broadcast)
+struct CastArgs {
+  const float* src;
+  void* dst;
+  long long n;
+};
+
+__global__ __launch_bounds__(256) void cast_kernel(CastArgs a) {
+  const long long n4 = a.n >> 2;
+  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n4; i += (long long)gridDim.x * 256) {
+    const float4 v = reinterpret_cast<const float4*>(a.src)[i];
+    uint2 w;
+    w.x = pack2bf(v.x, v.y);
+    w.y = pack2bf(v.z, v.w);
+    reinterpret_cast<uint2*>(a.dst)[i] = w;
+  }
+}
+
+// ------------------------------------------------------------------ bias / activation backward
+// dz[t, c] = dy[t, c] * act'(z[t, c])  (bf16 out), db[c] += sum_t dz[t, c]
+// grid: (ceil(N / 512), ceil(T / 64)); each lane owns 8 columns, each wave 16 rows.
+struct BiasActArgs {
+  const float* dy;     // [T][lddy] f32
+  const void* z;       // [T][ldz] bf16 pre-activation (optional, needed when act != 0)
+  void* dz;            // [T][lddz] bf16
+  float* db;           // [N] f32 accumulate (optional)
+  long long lddy, ldz, lddz;
+  int T, N;
+  int act;
+};
+
+__global__ __launch_bounds__(256) void bias_act_bwd_kernel(BiasActArgs p) {
+  __shared__ float red[4][64][8];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int cg = blockIdx.x * 64 + lane;  // column group of 8
+  const bool colok = cg * 8 < p.N;
+  float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  const long long r0 = (long long)blockIdx.y * 64;
+  if (colok) {
+    for (int i = w; i < 64; i += 4) {
+      const long long t = r0 + i;
+      if (t >= p.T) break;
+      const float4* dyr = reinterpret_cast<const float4*>(p.dy + t * p.lddy + cg * 8);
+      const float4 a = dyr[0], b = dyr[1];
+      float f[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+      if (p.act) {
+        float zf[8];
+        unpack8(*reinterpret_cast<const uint4*>(static_cast<const bf16_t*>(p.z) + t * p.ldz + cg * 8), zf);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) f[j] *= act_grad(zf[j], p.act);
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[j] += f[j];
+      *reinterpret_cast<uint4*>(static_cast<bf16_t*>(p.dz) + t * p.lddz + cg * 8) = pack8(f);
+    }
+  }
+  if (!p.db) return;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) red[w][lane][j] = acc[j];
+  __syncthreads();
+  if (w == 0 && colok) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float s = red[0][lane][j] + red[1][lane][j] + red[2][lane][j] + red[3][lane][j];
+      atomicAdd(p.db + cg * 8 + j, s);
+    }
+  }
+}
+
+// column sum only (bias grad of a layer whose dz is already materialised, f32 input)
+}  // namespace dpc
+
+using namespace dpc;
+
+static inline unsigned grid_for(long long n4) {
+  long long b = (n4 + 255) / 256;
+  if (b > 8192) b = 8192;
+  if (b < 1) b = 1;
+  return (unsigned)b;
+}
+
+DPC_API int dpc_embedding_fwd(const EmbArgs* a, hipStream_t stream) {
+  if (a->T <= 0) return 0;
+  if (a->D % 4) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(emb_fwd_kernel, dim3((unsigned)((a->T + 3) / 4)), dim3(256), 0, stream, *a);
+  return (int)hipGetLastError();
+}
+
+DPC_API int dpc_embedding_bwd(const EmbArgs* a, hipStream_t stream) {
+  if (a->T <= 0) return 0;
+  hipLaunchKernelGGL(emb_bwd_kernel, dim3((unsigned)((a->T + 3) / 4)), dim3(256), 0, stream, *a);
+  return (int)hipGetLastError();
+}
+
+DPC_API int dpc_cross_entropy(const CEArgs* a, hipStream_t stream) {
+  if (a->T <= 0) return 0;
+  if (a->ld % 8) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(ce_kernel, dim3((unsigned)a->T), dim3(256), 0, stream, *a);
+  return (int)hipGetLastError();
+}
+
+DPC_API int dpc_adamw(const AdamArgs* a, hipStream_t stream) {
+  if (a->n <= 0) return 0;
+  if (a->n % 4) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(adamw_kernel, dim3(grid_for(a->n >> 2)), dim3(256), 0, stream, *a);
+  return (int)hipGetLastError();
+}
+
+DPC_API int dpc_cast_f32_bf16(const CastArgs* a, hipStream_t stream) {
+  if (a->n <= 0) return 0;
+  if (a->n % 4) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(cast_kernel, dim3(grid_for(a->n >> 2)), dim3(256), 0, stream, *a);
+  return (int)hipGetLastError();
+}
+
+DPC_API int dpc_bias_act_bwd(const BiasActArgs* a, hipStream_t stream) {
+  if (a->T <= 0) return 0;
+  if (a->N % 8) return (int)hipErrorInvalidValue;
+  dim3 grid((unsigned)((a->N / 8 + 63) / 64), (unsigned)((a->T + 63) / 64));
+  hipLaunchKernelGGL(bias_act_bwd_kernel, grid, dim3(256), 0, stream, *a);
+  return (int)hipGetLastError();
+}

@@ -1,0 +1,183 @@
+"""GEMM with fused epilogues -- the matmul behind every ``nn.Linear`` of ``models.gpt``.
+
+``gemm`` computes ``C = epilogue(alpha * A @ B^T)`` where A is ``[M, K]`` and B is
+``[N, K]`` logically; each operand may be stored k-contiguous ("kmaj") or
+m/n-contiguous, so the forward (``x @ W^T``), the input gradient (``dy @ W``) and the
+weight gradient (``dy^T @ x``) of a Linear are all one kernel family without transpose
+copies (reference: ``/root/reference/models/gpt.py:29-30,60-64,219`` -- every Linear).
+
+Epilogue order (identical in the HIP kernel and the torch reference below)::
+
+    v = acc * alpha (* alpha_t) + bias[n]
+    v = v * act'(aux_in)            if act_bwd
+    aux_out = bf16(v)               if aux_out (pre-activation saved for backward)
+    v = act(v)                      if act
+    v = v + residual                if residual
+    C = C + v                       if accumulate (f32 C only)
+
+On a HIP device with bf16 operands this runs ``dpc_gemm`` (MFMA, ``csrc/gemm.hip``);
+on CPU (or fp32 operands, the explicit ``--disable_amp`` precision mode) it runs the
+same math with torch ops -- that expression is also the numerics oracle of the tests.
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+import torch.nn.functional as F
+
+from . import _lib
+
+ACT_NONE, ACT_RELU, ACT_GELU = 0, 1, 2
+ACTS = {None: ACT_NONE, "none": ACT_NONE, "relu": ACT_RELU, "gelu": ACT_GELU}
+
+
+def act_code(act) -> int:
+    if isinstance(act, int):
+        return act
+    return ACTS[act]
+
+
+def act_fwd_ref(v: torch.Tensor, act: int) -> torch.Tensor:
+    if act == ACT_RELU:
+        return F.relu(v)
+    if act == ACT_GELU:
+        return F.gelu(v, approximate="tanh")
+    return v
+
+
+def act_grad_ref(z: torch.Tensor, act: int) -> torch.Tensor:
+    z = z.float()
+    if act == ACT_RELU:
+        return (z > 0).float()
+    if act == ACT_GELU:
+        k0, k1 = math.sqrt(2.0 / math.pi), 0.044715
+        u = k0 * (z + k1 * z * z * z)
+        t = torch.tanh(u)
+        return 0.5 * (1 + t) + 0.5 * z * (1 - t * t) * k0 * (1 + 3 * k1 * z * z)
+    return torch.ones_like(z)
+
+
+def _check_operand(t: torch.Tensor, rows: int, cols: int, name: str) -> None:
+    if t.dim() != 2 or t.shape[0] != rows or t.shape[1] != cols:
+        raise ValueError(f"{name}: expected shape ({rows}, {cols}), got {tuple(t.shape)}")
+    if t.stride(1) != 1:
+        raise ValueError(f"{name}: inner dimension must be contiguous (stride {t.stride()})")
+    if t.dtype != torch.bfloat16:
+        raise ValueError(f"{name}: expected bf16, got {t.dtype}")
+    if t.data_ptr() % 16 or t.stride(0) % 8:
+        raise ValueError(f"{name}: base must be 16-B aligned and row stride a multiple of 8")
+    # 16-B chunk reads may touch up to roundup8(cols) elements of the last row
+    need = (t.storage_offset() + (rows - 1) * t.stride(0) + ((cols + 7) // 8) * 8) * t.element_size()
+    if rows > 0 and need > t.untyped_storage().nbytes():
+        raise ValueError(f"{name}: storage too small for 16-B chunked reads (pad the row)")
+
+
+def gemm(
+    a: torch.Tensor,
+    b: torch.Tensor,
+    *,
+    a_kmaj: bool = True,
+    b_kmaj: bool = True,
+    out: torch.Tensor | None = None,
+    out_dtype: torch.dtype = torch.bfloat16,
+    bias: torch.Tensor | None = None,
+    act=ACT_NONE,
+    act_bwd=ACT_NONE,
+    aux_in: torch.Tensor | None = None,
+    aux_out: torch.Tensor | None = None,
+    residual: torch.Tensor | None = None,
+    alpha: float = 1.0,
+    alpha_t: torch.Tensor | None = None,
+    accumulate: bool = False,
+    colsum: torch.Tensor | None = None,
+) -> torch.Tensor:
+    act, act_bwd = act_code(act), act_code(act_bwd)
+    M, K = (a.shape[0], a.shape[1]) if a_kmaj else (a.shape[1], a.shape[0])
+    N, Kb = (b.shape[0], b.shape[1]) if b_kmaj else (b.shape[1], b.shape[0])
+    if K != Kb:
+        raise ValueError(f"gemm: K mismatch {K} vs {Kb}")
+    if out is None:
+        if accumulate:
+            raise ValueError("gemm: accumulate needs an out tensor")
+        out = torch.empty((M, N), device=a.device, dtype=out_dtype)
+    if out.shape != (M, N) or out.stride(1) != 1:
+        raise ValueError(f"gemm: bad out {tuple(out.shape)} stride {out.stride()}")
+    if accumulate and out.dtype != torch.float32:
+        raise ValueError("gemm: accumulate requires an f32 output")
+    if act_bwd and aux_in is None:
+        raise ValueError("gemm: act_bwd needs aux_in")
+
+    if a.is_cuda and a.dtype == torch.bfloat16:
+        _check_operand(a, *( (M, K) if a_kmaj else (K, M) ), "A")
+        _check_operand(b, *( (N, K) if b_kmaj else (K, N) ), "B")
+        for t, nm, dt in ((residual, "residual", torch.float32), (bias, "bias", torch.float32),
+                          (colsum, "colsum", torch.float32),
+                          (aux_in, "aux_in", torch.bfloat16), (aux_out, "aux_out", torch.bfloat16)):
+            if t is not None and (t.dtype != dt or t.stride(-1) != 1):
+                raise ValueError(f"gemm: {nm} must be contiguous-last {dt}")
+        if out.dtype not in (torch.float32, torch.bfloat16):
+            raise ValueError("gemm: out must be f32 or bf16")
+        args = _lib.GemmArgs(
+            A=a.data_ptr(), B=b.data_ptr(), C=out.data_ptr(),
+            bias=_lib.ptr(bias), residual=_lib.ptr(residual), aux_in=_lib.ptr(aux_in),
+            aux_out=_lib.ptr(aux_out), alpha_ptr=_lib.ptr(alpha_t), colsum=_lib.ptr(colsum),
+            lda=a.stride(0), ldb=b.stride(0), ldc=out.stride(0),
+            ldr=residual.stride(0) if residual is not None else 0,
+            ld_aux_in=aux_in.stride(0) if aux_in is not None else 0,
+            ld_aux_out=aux_out.stride(0) if aux_out is not None else 0,
+            M=M, N=N, K=K, alpha=float(alpha), act=act, act_bwd=act_bwd,
+            out_f32=int(out.dtype == torch.float32), accumulate=int(accumulate),
+            a_kmaj=int(a_kmaj), b_kmaj=int(b_kmaj),
+        )
+        _lib.call("dpc_gemm", args, a.device)
+        return out
+    return _gemm_ref(a, b, a_kmaj, b_kmaj, out, bias, act, act_bwd, aux_in, aux_out, residual,
+                     alpha, alpha_t, accumulate, colsum)
+
+
+def _gemm_ref(a, b, a_kmaj, b_kmaj, out, bias, act, act_bwd, aux_in, aux_out, residual,
+              alpha, alpha_t, accumulate, colsum=None):
+    am = a if a_kmaj else a.t()
+    bm = b if b_kmaj else b.t()
+    v = am.float() @ bm.float().t()
+    v = v * alpha
+    if alpha_t is not None:
+        v = v * alpha_t.float()
+    if bias is not None:
+        v = v + bias.float()
+    if act_bwd:
+        v = v * act_grad_ref(aux_in, act_bwd)
+    if colsum is not None:
+        colsum.add_(v.sum(0))
+    if aux_out is not None:
+        aux_out.copy_(v)
+    v = act_fwd_ref(v, act)
+    if residual is not None:
+        v = v + residual.float()
+    if accumulate:
+        out.add_(v)
+    else:
+        out.copy_(v)
+    return out
+
+
+# ---------------------------------------------------------------- Linear-shaped helpers
+def linear_fwd(x, w, *, bias=None, act=None, residual=None, aux_out=None, out=None,
+               out_dtype=torch.bfloat16):
+    """y = act(x @ w^T + bias) (+ residual); x [M, K], w [N, K] (nn.Linear layout)."""
+    return gemm(x, w, a_kmaj=True, b_kmaj=True, bias=bias, act=act, residual=residual,
+                aux_out=aux_out, out=out, out_dtype=out_dtype)
+
+
+def linear_dgrad(dy, w, *, act_bwd=None, aux_in=None, out=None, out_dtype=torch.bfloat16,
+                 alpha_t=None, colsum=None):
+    """dx = (dy @ w) * act'(aux_in); dy [M, N], w [N, K] -> dx [M, K]; colsum += sum_m dx."""
+    return gemm(dy, w, a_kmaj=True, b_kmaj=False, act_bwd=act_bwd, aux_in=aux_in, out=out,
+                out_dtype=out_dtype, alpha_t=alpha_t, colsum=colsum)
+
+
+def linear_wgrad(dy, x, *, out, accumulate=True, alpha_t=None):
+    """dW (+)= dy^T @ x; dy [T, N], x [T, K] -> dW [N, K] (f32 gradient buffer)."""
+    return gemm(dy, x, a_kmaj=False, b_kmaj=False, out=out, accumulate=accumulate,
+                alpha_t=alpha_t)

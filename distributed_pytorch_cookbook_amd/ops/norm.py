@@ -1,0 +1,73 @@
+"""LayerNorm forward/backward over the f32 residual stream.
+
+Reference: ``nn.LayerNorm`` at ``/root/reference/models/gpt.py:119,122,217`` (eps 1e-5,
+elementwise affine).  Forward: f32 x -> normalised y (bf16 on the HIP path, feeding the
+next GEMM) + per-row (mean, rstd).  Backward: ``dx += LN'(dy)`` accumulated in place
+into the residual-gradient buffer, with dgamma / dbeta accumulated into f32 grads.
+"""
+from __future__ import annotations
+
+import torch
+
+from . import _lib
+
+
+def _use_hip(x: torch.Tensor, y_dtype: torch.dtype) -> bool:
+    return x.is_cuda and y_dtype == torch.bfloat16
+
+
+def layernorm_fwd(x: torch.Tensor, gamma: torch.Tensor, beta: torch.Tensor, eps: float = 1e-5,
+                  out_dtype: torch.dtype = torch.bfloat16, out: torch.Tensor | None = None):
+    """x [T, D] f32 -> (y [T, D] out_dtype, mean [T], rstd [T])."""
+    T, D = x.shape
+    if not _use_hip(x, out_dtype):
+        xf = x.float()
+        mean = xf.mean(-1)
+        var = xf.var(-1, unbiased=False)
+        rstd = torch.rsqrt(var + eps)
+        y = (xf - mean[:, None]) * rstd[:, None] * gamma.float() + beta.float()
+        if out is not None:
+            out.copy_(y)
+            y = out
+        else:
+            y = y.to(out_dtype)
+        return y, mean, rstd
+    if x.dtype != torch.float32 or x.stride(1) != 1 or D % 4 or D > 2048:
+        raise ValueError("layernorm_fwd: need f32 x with contiguous rows, D % 4 == 0, D <= 2048")
+    if out is None:
+        out = torch.empty(T, D, device=x.device, dtype=out_dtype)
+    mean = torch.empty(T, device=x.device, dtype=torch.float32)
+    rstd = torch.empty(T, device=x.device, dtype=torch.float32)
+    args = _lib.LNArgs(
+        x=x.data_ptr(), gamma=gamma.data_ptr(), beta=beta.data_ptr(), y=out.data_ptr(),
+        mean=mean.data_ptr(), rstd=rstd.data_ptr(), ldx=x.stride(0), ldy=out.stride(0),
+        T=T, D=D, eps=float(eps), y_f32=int(out.dtype == torch.float32),
+    )
+    _lib.call("dpc_layernorm_fwd", args, x.device)
+    return out, mean, rstd
+
+
+def layernorm_bwd(dy: torch.Tensor, x: torch.Tensor, mean: torch.Tensor, rstd: torch.Tensor,
+                  gamma: torch.Tensor, dx: torch.Tensor, dgamma: torch.Tensor, dbeta: torch.Tensor):
+    """dx += LN'(dy); dgamma += sum dy*xhat; dbeta += sum dy.  dy, x, dx f32 [T, D]."""
+    T, D = x.shape
+    if not (x.is_cuda and dy.dtype == torch.float32 and gamma.dtype == torch.float32):
+        xh = (x.float() - mean[:, None]) * rstd[:, None]
+        dyf = dy.float()
+        dg = dyf * gamma.float()
+        s1 = dg.mean(-1, keepdim=True)
+        s2 = (dg * xh).mean(-1, keepdim=True)
+        dx.add_(rstd[:, None] * (dg - s1 - xh * s2))
+        dgamma.add_((dyf * xh).sum(0))
+        dbeta.add_(dyf.sum(0))
+        return dx
+    for t, nm in ((dy, "dy"), (x, "x"), (dx, "dx")):
+        if t.dtype != torch.float32 or t.stride(1) != 1:
+            raise ValueError(f"layernorm_bwd: {nm} must be f32 with contiguous rows")
+    args = _lib.LNArgs(
+        x=x.data_ptr(), gamma=gamma.data_ptr(), mean=mean.data_ptr(), rstd=rstd.data_ptr(),
+        dy=dy.data_ptr(), dx=dx.data_ptr(), dgamma=dgamma.data_ptr(), dbeta=dbeta.data_ptr(),
+        ldx=x.stride(0), lddy=dy.stride(0), lddx=dx.stride(0), T=T, D=D, eps=0.0,
+    )
+    _lib.call("dpc_layernorm_bwd", args, x.device)
+    return dx

@@ -1,0 +1,65 @@
+"""Fused AdamW over flat buffers.
+
+Reference: ``torch.optim.AdamW(model.parameters(), lr=args.learning_rate)``
+(``/root/reference/main-single.py:42``; defaults betas=(0.9, 0.999), eps=1e-8,
+weight_decay=1e-2, decoupled decay applied to every parameter).  Here the whole model
+(or the local FSDP shard) is ONE contiguous f32 buffer, so a step is one kernel launch
+that also refreshes the bf16 compute copy of the weights.
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+
+from . import _lib
+
+
+class FlatAdamW:
+    def __init__(self, param: torch.Tensor, grad: torch.Tensor, lr: float = 1e-3,
+                 betas=(0.9, 0.999), eps: float = 1e-8, weight_decay: float = 1e-2,
+                 shadow: torch.Tensor | None = None):
+        assert param.dim() == 1 and param.shape == grad.shape and param.dtype == torch.float32
+        self.param, self.grad, self.shadow = param, grad, shadow
+        self.lr, self.betas, self.eps, self.weight_decay = lr, betas, eps, weight_decay
+        self.exp_avg = torch.zeros_like(param)
+        self.exp_avg_sq = torch.zeros_like(param)
+        self.step_count = 0
+
+    def state_dict(self):
+        return {"step": self.step_count, "exp_avg": self.exp_avg, "exp_avg_sq": self.exp_avg_sq,
+                "lr": self.lr, "betas": self.betas, "eps": self.eps,
+                "weight_decay": self.weight_decay}
+
+    def load_state_dict(self, sd):
+        self.step_count = int(sd["step"])
+        self.exp_avg.copy_(sd["exp_avg"])
+        self.exp_avg_sq.copy_(sd["exp_avg_sq"])
+
+    @torch.no_grad()
+    def step(self, grad_scale: float = 1.0, grad_scale_t: torch.Tensor | None = None) -> None:
+        self.step_count += 1
+        b1, b2 = self.betas
+        bc1 = 1.0 - b1 ** self.step_count
+        bc2s = math.sqrt(1.0 - b2 ** self.step_count)
+        p, g = self.param, self.grad
+        if p.is_cuda and p.numel() % 4 == 0:
+            args = _lib.AdamArgs(
+                param=p.data_ptr(), grad=g.data_ptr(), exp_avg=self.exp_avg.data_ptr(),
+                exp_avg_sq=self.exp_avg_sq.data_ptr(), shadow=_lib.ptr(self.shadow),
+                grad_scale_ptr=_lib.ptr(grad_scale_t), n=p.numel(), lr=self.lr, beta1=b1,
+                beta2=b2, eps=self.eps, weight_decay=self.weight_decay, bias_correction1=bc1,
+                bias_correction2_sqrt=bc2s, grad_scale=grad_scale,
+            )
+            _lib.call("dpc_adamw", args, p.device)
+            return
+        gs = g * grad_scale
+        if grad_scale_t is not None:
+            gs = gs * grad_scale_t
+        p.mul_(1.0 - self.lr * self.weight_decay)
+        self.exp_avg.mul_(b1).add_(gs, alpha=1 - b1)
+        self.exp_avg_sq.mul_(b2).addcmul_(gs, gs, value=1 - b2)
+        denom = (self.exp_avg_sq.sqrt() / bc2s).add_(self.eps)
+        p.addcdiv_(self.exp_avg, denom, value=-self.lr / bc1)
+        if self.shadow is not None:
+            self.shadow.copy_(p)

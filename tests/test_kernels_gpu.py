@@ -1,0 +1,221 @@
+"""Numerics of every HIP kernel against a plain PyTorch f32 reference of the same op."""
+import math
+
+import pytest
+import torch
+
+from distributed_pytorch_cookbook_amd.ops import _lib
+from distributed_pytorch_cookbook_amd.ops.attention import attention_bwd, attention_fwd, attention_ref
+from distributed_pytorch_cookbook_amd.ops.elementwise import bias_act_bwd
+from distributed_pytorch_cookbook_amd.ops.embedding import embedding_bwd, embedding_fwd
+from distributed_pytorch_cookbook_amd.ops.gemm import _gemm_ref, gemm
+from distributed_pytorch_cookbook_amd.ops.loss import cross_entropy_fused
+from distributed_pytorch_cookbook_amd.ops.norm import layernorm_bwd, layernorm_fwd
+from distributed_pytorch_cookbook_amd.ops.optim import FlatAdamW
+
+pytestmark = pytest.mark.gpu
+dev = "cuda"
+
+
+def rel_err(a, b):
+    a, b = a.float(), b.float()
+    return ((a - b).norm() / b.norm().clamp_min(1e-12)).item()
+
+
+@pytest.mark.parametrize("a_kmaj,b_kmaj", [(True, True), (True, False), (False, False), (False, True)])
+@pytest.mark.parametrize("M,N,K", [(256, 256, 128), (200, 300, 136), (1023, 768, 768), (64, 50257, 64)])
+def test_gemm_layouts(a_kmaj, b_kmaj, M, N, K):
+    torch.manual_seed(0)
+    a = torch.randn(M, K, device=dev).bfloat16()
+    b = torch.randn(N, K, device=dev).bfloat16()
+    # pad the contiguous extent of mn-major operands to a multiple of 8 (as the model does)
+    def store(x, kmaj):
+        if kmaj:
+            return x
+        r, c = x.shape  # logical [mn, K] -> stored [K, mn_pad]
+        buf = torch.zeros(c, (r + 7) // 8 * 8, device=dev, dtype=x.dtype)
+        buf[:, :r] = x.t()
+        return buf[:, :r]
+    A, B = store(a, a_kmaj), store(b, b_kmaj)
+    out = gemm(A, B, a_kmaj=a_kmaj, b_kmaj=b_kmaj, out_dtype=torch.float32)
+    ref = a.float() @ b.float().t()
+    assert rel_err(out, ref) < 2e-3
+
+
+def test_gemm_identity_asymmetric():
+    # A = I with an asymmetric B catches a transposed C write
+    n = 128
+    a = torch.eye(n, device=dev).bfloat16()
+    b = torch.arange(n * n, device=dev).reshape(n, n).float().remainder(251).bfloat16()
+    out = gemm(a, b, out_dtype=torch.float32)
+    assert torch.equal(out, b.float().t())
+
+
+@pytest.mark.parametrize("act", [0, 1, 2])
+def test_gemm_epilogues(act):
+    torch.manual_seed(1)
+    M, N, K = 333, 264, 192
+    a = torch.randn(M, K, device=dev).bfloat16()
+    w = torch.randn(N, K, device=dev).bfloat16() * 0.1
+    bias = torch.randn(N, device=dev)
+    res = torch.randn(M, N, device=dev)
+    aux = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+    out = gemm(a, w, bias=bias, act=act, residual=res, aux_out=aux, out_dtype=torch.float32)
+    aux_r = torch.empty_like(aux)
+    ref = _gemm_ref(a, w, True, True, torch.empty(M, N, device=dev), bias, act, 0, None, aux_r, res,
+                    1.0, None, False)
+    assert rel_err(out, ref) < 2e-3
+    assert rel_err(aux, aux_r) < 1e-2
+    # act-backward epilogue + accumulate into f32
+    z = torch.randn(M, N, device=dev).bfloat16()
+    acc0 = torch.randn(M, N, device=dev)
+    acc = acc0.clone()
+    gemm(a, w, act_bwd=act, aux_in=z, out=acc, accumulate=True)
+    ref2 = acc0.clone()
+    _gemm_ref(a, w, True, True, ref2, None, 0, act, z, None, None, 1.0, None, True)
+    assert rel_err(acc, ref2) < 2e-3
+
+
+@pytest.mark.parametrize("S", [1023, 200, 64])
+@pytest.mark.parametrize("with_pad", [False, True])
+def test_attention_fwd_bwd(S, with_pad):
+    torch.manual_seed(2)
+    N, H, hd = 2, 3, 64
+    T = N * S
+    qkv = (torch.randn(T, 3 * H * hd, device=dev)).bfloat16()
+    pad = None
+    if with_pad:
+        pad = torch.zeros(N, S, dtype=torch.bool, device=dev)
+        pad[0, S - S // 4:] = True  # right padding
+        pad[1, 5:9] = True
+    o, lse = attention_fwd(qkv, N, S, H, hd, pad, causal=True)
+    o_r, lse_r = attention_ref(qkv, N, S, H, hd, pad, causal=True)
+    assert rel_err(o, o_r) < 1e-2
+    fin = torch.isfinite(lse_r)
+    assert torch.allclose(lse[fin], lse_r[fin], atol=2e-2, rtol=1e-3)
+    do = torch.randn(T, H * hd, device=dev).bfloat16()
+    dqkv = attention_bwd(do, qkv, o, lse, N, S, H, hd, pad, causal=True)
+    x = qkv.float().requires_grad_(True)
+    o_ref, _ = attention_ref(x, N, S, H, hd, pad, causal=True)
+    (g,) = torch.autograd.grad(o_ref, x, do.float())
+    for i, name in enumerate("qkv"):
+        sl = slice(i * H * hd, (i + 1) * H * hd)
+        assert rel_err(dqkv[:, sl], g[:, sl]) < 2e-2, name
+
+
+def test_attention_head_dim_32_padded():
+    torch.manual_seed(3)
+    N, S, H, hd = 2, 100, 4, 32
+    qkv = torch.randn(N * S, 3 * H * hd, device=dev).bfloat16()
+    o, lse = attention_fwd(qkv, N, S, H, hd)
+    o_r, _ = attention_ref(qkv, N, S, H, hd)
+    assert rel_err(o, o_r) < 1e-2
+    do = torch.randn_like(o)
+    d = attention_bwd(do, qkv, o, lse, N, S, H, hd)
+    x = qkv.float().requires_grad_(True)
+    (g,) = torch.autograd.grad(attention_ref(x, N, S, H, hd)[0], x, do.float())
+    assert rel_err(d, g) < 2e-2
+
+
+@pytest.mark.parametrize("D", [256, 768, 1600])
+def test_layernorm(D):
+    torch.manual_seed(4)
+    T = 517
+    x = torch.randn(T, D, device=dev) * 3 + 1
+    g = torch.randn(D, device=dev)
+    b = torch.randn(D, device=dev)
+    y, mean, rstd = layernorm_fwd(x, g, b)
+    yr = torch.nn.functional.layer_norm(x, (D,), g, b, 1e-5)
+    assert rel_err(y, yr) < 5e-3
+    dy = torch.randn(T, D, device=dev)
+    dres = torch.randn(T, D, device=dev)
+    dx = dres.clone()
+    dg = torch.zeros(D, device=dev)
+    db = torch.zeros(D, device=dev)
+    layernorm_bwd(dy, x, mean, rstd, g, dx, dg, db)
+    xx = x.clone().requires_grad_(True)
+    gg = g.clone().requires_grad_(True)
+    bb = b.clone().requires_grad_(True)
+    torch.nn.functional.layer_norm(xx, (D,), gg, bb, 1e-5).backward(dy)
+    assert rel_err(dx - dres, xx.grad) < 1e-4
+    assert rel_err(dg, gg.grad) < 1e-4
+    assert rel_err(db, bb.grad) < 1e-4
+
+
+@pytest.mark.parametrize("tdt", [torch.float32, torch.bfloat16])
+def test_embedding(tdt):
+    torch.manual_seed(5)
+    V, P, D, T = 1000, 64, 768, 4 * 63
+    tok = torch.randn(V, D, device=dev).to(tdt)
+    pt = torch.randn(P, D, device=dev).to(tdt)
+    ids = torch.randint(0, V, (T,), device=dev)
+    pos = torch.arange(63, device=dev).repeat(4)
+    x = embedding_fwd(ids, pos, tok, pt)
+    assert torch.allclose(x, tok[ids].float() + pt[pos].float(), atol=1e-6)
+    dx = torch.randn(T, D, device=dev)
+    dt = torch.zeros(V, D, device=dev)
+    dp = torch.zeros(P, D, device=dev)
+    embedding_bwd(dx, ids, pos, dt, dp)
+    rt = torch.zeros(V, D, device=dev).index_add_(0, ids, dx)
+    rp = torch.zeros(P, D, device=dev).index_add_(0, pos, dx)
+    assert torch.allclose(dt, rt, atol=1e-4) and torch.allclose(dp, rp, atol=1e-4)
+
+
+def test_cross_entropy():
+    torch.manual_seed(6)
+    T, V = 300, 50257
+    ld = (V + 63) // 64 * 64
+    buf = torch.zeros(T, ld, device=dev, dtype=torch.bfloat16)
+    buf[:, :V] = (torch.randn(T, V, device=dev) * 2).bfloat16()
+    logits = buf.clone()
+    tg = torch.randint(0, V, (T,), device=dev)
+    tg[::7] = -100
+    loss, n, correct = cross_entropy_fused(buf, tg, V, write_grad=True, want_correct=True)
+    lf = logits[:, :V].float().requires_grad_(True)
+    lr = torch.nn.functional.cross_entropy(lf, tg, ignore_index=-100)
+    lr.backward()
+    assert abs(loss.item() - lr.item()) < 1e-3 * abs(lr.item())
+    assert rel_err(buf[:, :V], lf.grad) < 1e-2
+    assert buf[:, V:].abs().max().item() == 0
+    valid = tg != -100
+    rc = (lf.argmax(-1) == tg)[valid].sum().item()
+    assert abs(correct.item() - rc) <= 1
+
+
+def test_adamw_matches_torch():
+    torch.manual_seed(7)
+    n = 4096
+    p = torch.randn(n, device=dev)
+    g = torch.randn(n, device=dev)
+    sh = torch.empty(n, device=dev, dtype=torch.bfloat16)
+    opt = FlatAdamW(p, g, lr=1e-3, shadow=sh)
+    pr = p.clone().requires_grad_(True)
+    ref = torch.optim.AdamW([pr], lr=1e-3)
+    for _ in range(3):
+        g.normal_()
+        pr.grad = g.clone()
+        opt.step()
+        ref.step()
+    assert rel_err(p, pr.detach()) < 1e-6
+    assert rel_err(sh, pr.detach()) < 5e-3
+
+
+@pytest.mark.parametrize("act", [0, 1, 2])
+def test_bias_act_bwd(act):
+    torch.manual_seed(8)
+    T, N = 777, 3072
+    dy = torch.randn(T, N, device=dev)
+    z = torch.randn(T, N, device=dev).bfloat16()
+    db = torch.zeros(N, device=dev)
+    dz = bias_act_bwd(dy, z, act, db)
+    db_r = torch.zeros(N, device=dev)
+    dz_r = bias_act_bwd(dy.cpu(), z.cpu(), act, db_r.cpu().clone(), out_dtype=torch.float32)
+    from distributed_pytorch_cookbook_amd.ops.gemm import act_grad_ref
+    ref = dy * act_grad_ref(z, act) if act else dy
+    assert rel_err(dz, ref) < 5e-3
+    assert rel_err(db, ref.sum(0)) < 1e-4
+    assert dz_r.shape == dz.shape
+
+
+def test_native_library_loaded():
+    assert _lib.is_loaded()
