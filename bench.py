@@ -1,0 +1,148 @@
+#!/usr/bin/env python
+"""Headline benchmark: GPT-2 training tokens/sec (whole node) on N MI355X GPUs.
+
+    python bench.py [--gpus 1] [--steps 20] [--warmup 5]            # 1 GPU
+    torchrun --nproc-per-node N --master-addr 127.0.0.1 --master-port P \
+        bench.py --gpus N --steps K --warmup W                        # N GPUs
+
+Metric and config follow BASELINE.json ("tokens/sec (node) GPT-2 training per recipe"):
+default is the ``main-ddp.py`` north-star config -- GPT-2 small (untied lm_head, 163M
+params), seq_len 1024, bf16 compute, data parallel over all ranks, weak scaling
+(``--batch_size`` sequences per GPU).  ``--recipe fsdp|pipe|pipe_ddp`` and ``--model``
+select the other north-star configs.  Random-init weights, synthetic token batches
+(no network); every timed step is a full forward + backward + gradient all-reduce +
+AdamW update.  W untimed warmup steps, then exactly K steps bracketed by barrier +
+device synchronize; the time is the MAX over ranks; rank 0 prints one JSON line.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+
+from distributed_pytorch_cookbook_amd.config import apply_preset, build_parser  # noqa: E402
+from distributed_pytorch_cookbook_amd.parallel import comm  # noqa: E402
+
+METRIC = "tokens/sec (node) GPT-2 training per recipe (DDP/FSDP/PP) at 1/2/4/8 MI355X"
+BASELINE_TOKS = {}  # BASELINE.md publishes no numbers for any config
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--recipe", default="ddp", choices=["ddp", "fsdp", "pipe", "pipe_ddp"])
+    ap.add_argument("--model", default=None)
+    ap.add_argument("--batch_size", type=int, default=16, help="sequences per GPU (per DP replica for PP)")
+    ap.add_argument("--seq_len", type=int, default=1024)
+    ap.add_argument("--bucket_mb", type=float, default=128.0)
+    ap.add_argument("--reduce_dtype", default="fp32", choices=["fp32", "bf16"])
+    ap.add_argument("--num_microbatches", type=int, default=0)
+    ap.add_argument("--schedule", default="1f1b", choices=["1f1b", "gpipe"])
+    ap.add_argument("--dp_size", type=int, default=0)
+    ap.add_argument("--json", default=None, help="also write the result line to this file")
+    a = ap.parse_args()
+
+    default_model = {"ddp": "gpt2-small", "fsdp": "gpt2-xl", "pipe": "gpt2-medium",
+                     "pipe_ddp": "gpt2-large"}[a.recipe]
+    model_name = a.model or default_model
+    rec = "pipe_ddp" if a.recipe == "pipe_ddp" else a.recipe
+    argv = ["--model", model_name, "--batch_size", str(a.batch_size), "--bucket_mb", str(a.bucket_mb),
+            "--reduce_dtype", a.reduce_dtype, "--synthetic_data"]
+    if rec in ("pipe", "pipe_ddp"):
+        argv += ["--schedule", a.schedule, "--num_microbatches", str(a.num_microbatches)]
+    if rec == "pipe_ddp" and a.dp_size:
+        argv += ["--dp_size", str(a.dp_size)]
+    args = build_parser(rec).parse_args(argv)
+    apply_preset(args)
+    args.sequence_length = a.seq_len
+
+    info = comm.init_dist()
+    if info.world_size != a.gpus and info.is_main:
+        print(f"warning: --gpus {a.gpus} but WORLD_SIZE {info.world_size}", file=sys.stderr)
+    from distributed_pytorch_cookbook_amd.recipes import build_engine, build_model
+
+    vocab = 50257
+    model = build_model(args, vocab, info.device)
+    engine = build_engine(rec, model, info, args)
+
+    # synthetic batches: a small pool of distinct random token batches per DP replica
+    S = a.seq_len
+    B = a.batch_size
+    g = torch.Generator(device="cpu").manual_seed(1000 + engine.dp_rank)
+    pool = []
+    for _ in range(4):
+        ids = torch.randint(0, vocab, (B, S), generator=g)
+        inputs = ids[:, :-1].to(info.device)
+        targets = ids[:, 1:].to(info.device)
+        pos = torch.arange(S - 1, device=info.device).unsqueeze(0).expand(B, -1)
+        pool.append((dict(input_ids=inputs, position_ids=pos, mask=None), targets))
+
+    def step(i):
+        b, t = pool[i % len(pool)]
+        return engine.train_step(b, t)
+
+    for i in range(a.warmup):
+        step(i)
+    if info.device.type == "cuda":
+        torch.cuda.synchronize()
+    comm.barrier()
+    if info.device.type == "cuda":
+        torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    loss = None
+    for i in range(a.steps):
+        loss = step(i)
+    if info.device.type == "cuda":
+        torch.cuda.synchronize()
+    comm.barrier()
+    if info.device.type == "cuda":
+        torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    dt_t = torch.tensor([dt], dtype=torch.float64, device=info.device)
+    if info.world_size > 1:
+        torch.distributed.all_reduce(dt_t, op=torch.distributed.ReduceOp.MAX)
+    dt = float(dt_t.item())
+    loss_v = float(loss.item()) if loss is not None else float("nan")
+    tokens_per_step = B * (S - 1) * engine.dp_world
+    value = tokens_per_step * a.steps / dt
+    n = info.world_size
+    par = {"ddp": f"dp{n}", "fsdp": f"fsdp{n}", "pipe": f"pp{n}",
+           "pipe_ddp": f"pp{n // max(engine.dp_world, 1)}xdp{engine.dp_world}"}[a.recipe]
+    base = BASELINE_TOKS.get((a.recipe, model_name, n))
+    out = {
+        "metric": METRIC,
+        "value": round(value, 1),
+        "unit": "tokens/s",
+        "n_gpus": n,
+        "steps": a.steps,
+        "warmup": a.warmup,
+        "ms_per_step": round(1000 * dt / a.steps, 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": (round(value / base, 3) if base else None),
+        "dtype": "bf16",
+        "data": "synthetic",
+        "config": {"model": model_name, "global_batch": B * engine.dp_world, "seq_len": S,
+                   "parallelism": par, "recipe": f"main-{a.recipe.replace('_', '-')}.py",
+                   "tokens_per_step": tokens_per_step, "final_loss": round(loss_v, 4)},
+    }
+    if info.is_main:
+        line = json.dumps(out)
+        print(line, flush=True)
+        if a.json:
+            os.makedirs(os.path.dirname(a.json) or ".", exist_ok=True)
+            with open(a.json, "w") as f:
+                f.write(line + "\n")
+    comm.cleanup_dist()
+
+
+if __name__ == "__main__":
+    main()

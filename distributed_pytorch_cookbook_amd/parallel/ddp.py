@@ -1,0 +1,108 @@
+"""Data parallel: bucketed gradient all-reduce over RCCL, overlapped with backward.
+
+Reference: ``DistributedDataParallel(sp_model, device_ids=[device_id])``
+(``/root/reference/main-ddp.py:55``) -- rank-0 broadcast of the parameters in the
+constructor, fp32 gradient buckets (1 MiB first, then 25 MiB) all-reduced by the C++
+Reducer as autograd hooks fire, averaged by the world size.
+
+MI355X-first design:
+* gradients already live in ONE flat f32 buffer (``LocalStore``), unit by unit, so a
+  bucket is a contiguous slice -- nothing is copied into or out of bucket storage;
+* buckets are whole units taken in backward order (head, layer L-1, ..., layer 0,
+  embeddings) up to ``bucket_mb``; the fused layer's backward calls ``post_backward``
+  the moment its weight gradients are written, and the bucket's all-reduce is enqueued
+  right then on RCCL's stream while the next layer's backward runs on the compute stream;
+* sizes are chosen for xGMI (7 point-to-point links per GPU, ring collectives are
+  per-link bound): fewer, larger buckets (default 128 MiB) keep RCCL at its bus
+  bandwidth instead of paying per-call latency 25x per step;
+* the 1/W average is folded into the AdamW kernel (``grad_scale``), so no extra pass;
+* optional bf16 reduction (``reduce_dtype``) halves the bytes on the links.
+"""
+from __future__ import annotations
+
+import torch
+import torch.distributed as dist
+
+from . import comm
+from .store import LocalStore
+
+
+class DDPStore(LocalStore):
+    def __init__(self, model, device, group=None, bucket_mb: float = 128.0,
+                 reduce_dtype: torch.dtype = torch.float32, overlap: bool = True,
+                 compute_dtype=None, units=None, broadcast_src: int | None = None):
+        super().__init__(model, device, compute_dtype=compute_dtype, units=units)
+        self.group = group
+        self.world = comm.world_size(group)
+        self.reduce_dtype = reduce_dtype
+        self.overlap = overlap
+        if self.world > 1:
+            src = broadcast_src if broadcast_src is not None else (
+                dist.get_global_rank(group, 0) if group is not None else 0)
+            with torch.no_grad():
+                comm.broadcast(self.master, src=src, group=group)
+            self.refresh_shadow()
+        # buckets of whole units in backward order
+        cap = int(bucket_mb * 2**20 / 4)
+        self.buckets = []  # (lo, hi, [units])
+        cur = []
+        for u in reversed(self.units):
+            sl = self.unit_slice(u)
+            if cur and (sum(self.unit_slice(x).stop - self.unit_slice(x).start for x in cur)
+                        + sl.stop - sl.start) > cap:
+                self.buckets.append(cur)
+                cur = []
+            cur.append(u)
+        if cur:
+            self.buckets.append(cur)
+        self.bucket_of = {}
+        for bi, us in enumerate(self.buckets):
+            for u in us:
+                self.bucket_of[u] = bi
+        self._ready = [0] * len(self.buckets)
+        self._works = {}
+        self._tmp = {}
+
+    def _range(self, bi):
+        us = self.buckets[bi]
+        lo = min(self.unit_slice(u).start for u in us)
+        hi = max(self.unit_slice(u).stop for u in us)
+        return lo, hi
+
+    def _launch(self, bi):
+        if self.world == 1 or bi in self._works:
+            return
+        lo, hi = self._range(bi)
+        g = self.grads[lo:hi]
+        if self.reduce_dtype != torch.float32:
+            t = g.to(self.reduce_dtype)
+            self._tmp[bi] = t
+            self._works[bi] = comm.all_reduce(t, group=self.group, async_op=True)
+        else:
+            self._works[bi] = comm.all_reduce(g, group=self.group, async_op=True)
+
+    def post_backward(self, u):
+        if self.world == 1:
+            return
+        bi = self.bucket_of[u]
+        self._ready[bi] += 1
+        if self.overlap and self._ready[bi] == len(self.buckets[bi]):
+            self._launch(bi)
+
+    def finish_grads(self):
+        """Wait for every bucket (launching any not yet launched, e.g. overlap off)."""
+        if self.world > 1:
+            for bi in range(len(self.buckets)):
+                self._launch(bi)
+            for bi in range(len(self.buckets)):
+                self._works[bi].wait()
+                if bi in self._tmp:
+                    lo, hi = self._range(bi)
+                    self.grads[lo:hi].copy_(self._tmp[bi])
+        self._works.clear()
+        self._tmp.clear()
+        self._ready = [0] * len(self.buckets)
+
+    @property
+    def grad_scale(self) -> float:
+        return 1.0 / self.world

@@ -1,0 +1,88 @@
+"""Recipe driver: the body of ``main-single.py`` / ``main-ddp.py`` / ``main-fsdp.py`` /
+``main-pipe.py`` / ``main-pipe-ddp.py``.
+
+Reference entrypoints: ``/root/reference/main-single.py:18-151`` (single device),
+``main-ddp.py:38-187`` (DDP), ``main-fsdp.py:42-202`` (FSDP + CPU offload),
+``main-pipe.py:85-221`` (GPipe), ``main-pipe-ddp.py:1`` (an empty stub in the reference;
+implemented here as a PP x DP mesh).  All share flags (``config.py``), data, model and
+the trainer; only the engine differs.
+"""
+from __future__ import annotations
+
+import os
+
+import torch
+
+from .config import parse
+from .engine.trainer import Trainer
+from .models.gpt import TransformerDecoderLM
+from .parallel import comm
+from .utils.data import get_dataset, get_tokenizer, transform_dataset
+
+PAD_ID = 2  # reference main-single.py:23
+
+
+def build_model(args, vocab_size: int, device) -> TransformerDecoderLM:
+    torch.manual_seed(args.seed)
+    with torch.device(device):
+        model = TransformerDecoderLM(
+            dim=args.dim, head_dim=args.head_dim, heads=args.heads, num_layers=args.num_layers,
+            vocab_size=vocab_size, max_position_embeddings=args.sequence_length,
+            dropout=args.dropout, activation=args.activation,
+        )
+    return model
+
+
+def build_engine(recipe: str, model, info, args):
+    compute_dtype = torch.float32 if args.disable_amp else None
+    if recipe in ("single", "ddp"):
+        from .engine.data_parallel import DataParallelEngine
+
+        return DataParallelEngine(
+            model, info.device, lr=args.learning_rate, bucket_mb=args.bucket_mb,
+            reduce_dtype=torch.bfloat16 if args.reduce_dtype == "bf16" else torch.float32,
+            overlap=not args.no_overlap, compute_dtype=compute_dtype,
+        )
+    if recipe == "fsdp":
+        from .engine.fsdp import FSDPEngine
+
+        return FSDPEngine(model, info.device, lr=args.learning_rate, prefetch=args.prefetch,
+                          reshard_after_forward=not args.no_reshard_after_forward,
+                          cpu_offload=args.cpu_offload, compute_dtype=compute_dtype)
+    if recipe in ("pipe", "pipe_ddp"):
+        from .engine.pipeline import PipelineEngine
+
+        dp = getattr(args, "dp_size", 0) or 1
+        if recipe == "pipe_ddp" and not getattr(args, "dp_size", 0):
+            dp = 2 if info.world_size % 2 == 0 and info.world_size > 2 else 1
+        pp = args.pp_size or max(1, info.world_size // dp)
+        return PipelineEngine(model, info.device, lr=args.learning_rate, pp=pp, dp=dp,
+                              num_microbatches=args.num_microbatches or 2 * pp,
+                              schedule=args.schedule, bucket_mb=args.bucket_mb,
+                              compute_dtype=compute_dtype)
+    raise ValueError(recipe)
+
+
+def run(recipe: str, argv=None):
+    args = parse("pipe_ddp" if recipe == "pipe_ddp" else recipe, argv)
+    info = comm.init_dist(force_cpu=args.cpu)
+    if recipe == "single" and info.world_size > 1:
+        raise SystemExit("main-single.py runs one process; use main-ddp.py under torchrun")
+    if info.is_main:
+        print(f"[{recipe}] world={info.world_size} device={info.device} backend={info.backend}")
+    synthetic = True if args.synthetic_data else None
+    tokenizer = get_tokenizer(max_length=args.sequence_length, offline_stub=synthetic)
+    tokenizer.pad_token_id = PAD_ID
+    model = build_model(args, tokenizer.vocab_size, info.device)
+    engine = build_engine(recipe, model, info, args)
+    train, val = get_dataset(slice_size=args.dataset_slice, synthetic=synthetic,
+                             seq_len=args.sequence_length, n_train=args.train_samples,
+                             n_val=args.val_samples, seed=args.seed)
+    train = transform_dataset(train, tokenizer, max_length=args.sequence_length, num_proc=args.num_workers)
+    val = transform_dataset(val, tokenizer, max_length=args.sequence_length, num_proc=args.num_workers)
+    trainer = Trainer(args, engine, tokenizer, PAD_ID)
+    try:
+        path = trainer.fit(train, val)
+    finally:
+        comm.cleanup_dist()
+    return trainer, path
