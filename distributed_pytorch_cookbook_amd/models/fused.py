@@ -68,12 +68,12 @@ def _qkv_grad(store, attn):
 
 class _EmbedFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, anchor, ids, pos, mod, store):
+    def forward(ctx, anchor, ids, pos, mod, store, training):
         u = mod._unit_id
         store.pre_forward(u)
         x = embedding_fwd(ids, pos, store.weight(mod.input_embeddings.weight),
                           store.weight(mod.position_embeddings.weight))
-        store.post_forward(u)
+        store.post_forward(u, training)
         ctx.save_for_backward(ids, pos)
         ctx.mod, ctx.store = mod, store
         return x
@@ -87,7 +87,7 @@ class _EmbedFn(torch.autograd.Function):
         embedding_bwd(dx.contiguous(), ids, pos, store.grad(mod.input_embeddings.weight),
                       store.grad(mod.position_embeddings.weight))
         store.post_backward(u)
-        return None, None, None, None, None
+        return None, None, None, None, None, None
 
 
 class _LayerFn(torch.autograd.Function):
@@ -106,14 +106,14 @@ class _LayerFn(torch.autograd.Function):
         x2 = linear_fwd(o, w(attn.to_out.weight), bias=w(attn.to_out.bias), residual=x,
                         out_dtype=torch.float32)
         h2, mu2, rs2 = layernorm_fwd(x2, w(layer.norm2.weight), w(layer.norm2.bias), LN_EPS, cdt)
-        F4 = fc.up_proj.weight.shape[0]
+        F4 = w(fc.up_proj.weight).shape[0]
         z1 = torch.empty(T, F4, device=x.device, dtype=cdt) if (training and act == ACT_GELU) else None
         uact = linear_fwd(h2, w(fc.up_proj.weight), bias=w(fc.up_proj.bias), act=act, aux_out=z1,
                           out_dtype=cdt)
         z2 = torch.empty(T, D, device=x.device, dtype=cdt) if training else None
         x3 = linear_fwd(uact, w(fc.down_proj.weight), bias=w(fc.down_proj.bias), act=act,
                         residual=x2, aux_out=z2, out_dtype=torch.float32)
-        store.post_forward(u)
+        store.post_forward(u, training)
         if training:
             ctx.save_for_backward(x, h1, mu1, rs1, qkv, o, lse, x2, h2, mu2, rs2,
                                   z1 if z1 is not None else uact, uact, z2, mask)
@@ -167,7 +167,7 @@ class _HeadFn(torch.autograd.Function):
         store.pre_forward(unit)
         w = store.weight
         cdt = store.compute_dtype
-        V = head.weight.shape[0]
+        V = w(head.weight).shape[0]
         T = x.shape[0]
         hf, mu, rs = layernorm_fwd(x, w(norm.weight), w(norm.bias), LN_EPS, cdt)
         ld = vocab_ld(V) if x.is_cuda else V
@@ -175,7 +175,7 @@ class _HeadFn(torch.autograd.Function):
         linear_fwd(hf, w(head.weight), out=buf[:, :V])
         loss, n_valid, n_correct = cross_entropy_fused(buf, targets, V, write_grad=training,
                                                        want_correct=want_correct)
-        store.post_forward(unit)
+        store.post_forward(unit, training)
         if training:
             ctx.save_for_backward(x, hf, mu, rs, buf)
             ctx.mods, ctx.store, ctx.unit, ctx.V = (norm, head), store, unit, V
@@ -204,15 +204,15 @@ class _HeadFn(torch.autograd.Function):
 def head_logits(model, x, store):
     """Inference head: logits [T, V] (view of a row-padded buffer), no loss."""
     w = store.weight
-    V = model.lm_head.weight.shape[0]
     unit = model._head_unit_id
     store.pre_forward(unit)
+    V = w(model.lm_head.weight).shape[0]
     hf, _, _ = layernorm_fwd(x, w(model.norm_out.weight), w(model.norm_out.bias), LN_EPS,
                              store.compute_dtype)
     ld = vocab_ld(V) if x.is_cuda else V
     buf = torch.empty(x.shape[0], ld, device=x.device, dtype=store.compute_dtype)
     linear_fwd(hf, w(model.lm_head.weight), out=buf[:, :V])
-    store.post_forward(unit)
+    store.post_forward(unit, False)
     return buf[:, :V]
 
 
@@ -229,7 +229,7 @@ def ensure_store(model):
 def run_embeddings(model, store, input_ids, position_ids, training):
     anchor = store.anchor if training else store.anchor.detach()
     return _EmbedFn.apply(anchor, input_ids.reshape(-1), position_ids.reshape(-1),
-                          model.embeddings, store)
+                          model.embeddings, store, training)
 
 
 def run_layers(model, store, x, mask, N, S, layers, training):

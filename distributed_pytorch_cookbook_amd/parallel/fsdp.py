@@ -1,0 +1,234 @@
+"""Fully-sharded data parallel (ZeRO-3) store: per-unit flat shards over RCCL.
+
+Reference: ``FSDP(sp_model, auto_wrap_policy=size_based(min_num_params=100),
+cpu_offload=CPUOffload(offload_params=...))`` (``/root/reference/main-fsdp.py:60-69``),
+which makes every leaf Linear / Embedding / LayerNorm its own unit (8L+5 units: 389 for
+GPT-2 XL) and all-gathers fp32 parameters.
+
+MI355X-first design:
+* one unit per decoder layer (+ embeddings, + head): GPT-2 XL has 50 units of up to
+  30.7M parameters -- few, large collectives that run at RCCL's bus bandwidth over xGMI
+  instead of hundreds of latency-bound ones;
+* every rank owns a contiguous 1/W slice of each unit (padded to W x 64 elements) in
+  f32 (master) + f32 (gradient) + bf16 (compute copy written by the AdamW kernel);
+* forward / backward all-gather the *bf16* shards (half the bytes of the reference's
+  fp32 gathers) into a full-unit buffer, prefetched ``prefetch`` units ahead on RCCL's
+  stream while the current unit computes; buffers are released after use
+  (``reshard_after_forward``) so activation-time memory holds only the prefetch window;
+* backward reduce-scatters each unit's f32 gradient straight into the shard gradient
+  as soon as the unit's backward has written it (overlapped with the next unit);
+* ``cpu_offload``: master shard and Adam moments live in pinned host memory, the
+  optimizer runs on the host, the bf16 shard is copied back asynchronously.
+"""
+from __future__ import annotations
+
+import torch
+import torch.distributed as dist
+
+from ..ops.elementwise import cast_f32_bf16
+from . import comm
+from .store import ALIGN, FlatLayout, ParamStore, default_compute_dtype
+
+
+def _placeholder(shape, device):
+    """A tensor with the parameter's shape but one element of storage (the real data
+    lives in the shards)."""
+    return torch.empty(1, device=device).expand(*shape) if len(shape) else torch.empty((), device=device)
+
+
+class FSDPStore(ParamStore):
+    def __init__(self, model, device, group=None, compute_dtype=None, prefetch: int = 1,
+                 reshard_after_forward: bool = True, cpu_offload: bool = False,
+                 reduce_dtype: torch.dtype = torch.float32):
+        self.device = torch.device(device)
+        self.group = group
+        self.W = comm.world_size(group)
+        self.rank = comm.rank(group)
+        self.compute_dtype = compute_dtype or default_compute_dtype(self.device)
+        self.prefetch = max(0, prefetch)
+        self.reshard = reshard_after_forward
+        self.cpu_offload = cpu_offload and self.device.type == "cuda"
+        self.reduce_dtype = reduce_dtype
+        self.layout = FlatLayout(model, unit_align=self.W * ALIGN)
+        self.nunits = len(self.layout.units)
+        self.units = list(range(self.nunits))
+        # shard geometry
+        self.unit_len = [b - a for a, b in self.layout.unit_ranges]
+        self.shard_len = [n // self.W for n in self.unit_len]
+        self.shard_off = [0]
+        for n in self.shard_len[:-1]:
+            self.shard_off.append(self.shard_off[-1] + n)
+        total = sum(self.shard_len)
+        host = self.cpu_offload
+        mdev = torch.device("cpu") if host else self.device
+        self.master = torch.zeros(total, dtype=torch.float32, device=mdev,
+                                  pin_memory=host)
+        self.grads = torch.zeros(total, dtype=torch.float32, device=self.device)
+        self.grads_host = torch.zeros(total, dtype=torch.float32, pin_memory=True) if host else None
+        self.shadow = torch.empty(total, dtype=self.compute_dtype, device=self.device)
+        # fill my shards from the (identically seeded) full parameters, then free them
+        with torch.no_grad():
+            for u in self.units:
+                lo, hi = self.layout.unit_ranges[u]
+                mine0 = lo + self.rank * self.shard_len[u]
+                mine1 = mine0 + self.shard_len[u]
+                for e in self.layout.unit_entries(u):
+                    a, b = max(e.offset, mine0), min(e.offset + e.numel, mine1)
+                    if a < b:
+                        src = e.param.data.reshape(-1)[a - e.offset:b - e.offset]
+                        dst0 = self.shard_off[u] + (a - mine0)
+                        self.master[dst0:dst0 + (b - a)].copy_(src)
+                for e in self.layout.unit_entries(u):
+                    e.param.data = _placeholder(e.shape, self.device)
+                    e.param.grad = None
+        self.refresh_shadow()
+        self.anchor = torch.zeros((), device=self.device, requires_grad=True)
+        object.__setattr__(model, "param_store", self)
+        self.model = model
+        self._full = {}       # unit -> (buffer, work or None)
+        self._vec32 = {}      # unit -> {param id: f32 copy of 1-D params}
+        self._gfull = {}      # unit -> f32 full-unit gradient buffer
+        self._rs = {}         # unit -> (work, tmp)
+        self._in_backward = False
+
+    # ------------------------------------------------------------------ shards
+    def shard(self, flat, u):
+        o = self.shard_off[u]
+        return flat[o:o + self.shard_len[u]]
+
+    def refresh_shadow(self):
+        src = self.master.to(self.device, non_blocking=True) if self.cpu_offload else self.master
+        if self.compute_dtype == torch.float32:
+            self.shadow.copy_(src)
+        else:
+            cast_f32_bf16(src, self.shadow)
+
+    # ------------------------------------------------------------------ gather / release
+    def _gather(self, u):
+        if u in self._full or not (0 <= u < self.nunits):
+            return
+        buf = torch.empty(self.unit_len[u], dtype=self.compute_dtype, device=self.device)
+        sh = self.shard(self.shadow, u)
+        if self.W == 1:
+            buf.copy_(sh)
+            self._full[u] = (buf, None)
+        else:
+            w = comm.all_gather_into(buf, sh, group=self.group, async_op=True)
+            self._full[u] = (buf, w)
+
+    def _ensure(self, u):
+        self._gather(u)
+        buf, w = self._full[u]
+        if w is not None:
+            w.wait()
+            self._full[u] = (buf, None)
+        return buf
+
+    def _release(self, u):
+        self._full.pop(u, None)
+        self._vec32.pop(u, None)
+
+    def weight(self, p):
+        e = self.layout.by_param[id(p)]
+        buf = self._full[e.unit][0]
+        lo = self.layout.unit_ranges[e.unit][0]
+        v = buf[e.offset - lo:e.offset - lo + e.numel].view(e.shape)
+        if p.dim() < 2 and v.dtype != torch.float32:
+            cache = self._vec32.setdefault(e.unit, {})
+            if id(p) not in cache:
+                cache[id(p)] = v.float()
+            return cache[id(p)]
+        return v
+
+    def grad(self, p):
+        e = self.layout.by_param[id(p)]
+        g = self._gfull[e.unit]
+        lo = self.layout.unit_ranges[e.unit][0]
+        return g[e.offset - lo:e.offset - lo + e.numel].view(e.shape)
+
+    # ------------------------------------------------------------------ hooks
+    def pre_forward(self, u):
+        self._ensure(u)
+        for k in range(1, self.prefetch + 1):
+            self._gather(u + k)
+
+    def post_forward(self, u, training=True):
+        last = u == self.nunits - 1
+        if not training:
+            self._release(u)
+        elif self.reshard and not last:
+            self._release(u)
+
+    def pre_backward(self, u, need_weights=True):
+        self._in_backward = True
+        if need_weights:
+            self._ensure(u)
+            for k in range(1, self.prefetch + 1):
+                if u - k >= 1:  # the embeddings unit needs no weights in backward
+                    self._gather(u - k)
+        self._gfull[u] = torch.zeros(self.unit_len[u], dtype=torch.float32, device=self.device)
+
+    def post_backward(self, u):
+        self._release(u)
+        g = self._gfull.pop(u)
+        out = self.shard(self.grads, u)
+        if self.W == 1:
+            out.add_(g)
+            return
+        if self.reduce_dtype != torch.float32:
+            gt = g.to(self.reduce_dtype)
+            tmp = torch.empty(self.shard_len[u], dtype=self.reduce_dtype, device=self.device)
+            w = comm.reduce_scatter_into(tmp, gt, group=self.group, async_op=True)
+            self._rs[u] = (w, tmp, gt)
+        else:
+            tmp = torch.empty(self.shard_len[u], dtype=torch.float32, device=self.device)
+            w = comm.reduce_scatter_into(tmp, g, group=self.group, async_op=True)
+            self._rs[u] = (w, tmp, g)
+
+    def finish_grads(self):
+        for u, (w, tmp, _) in sorted(self._rs.items()):
+            w.wait()
+            self.shard(self.grads, u).add_(tmp.float())
+        self._rs.clear()
+        self._in_backward = False
+        # anything still gathered from the forward (e.g. the head) is released now
+        for u in list(self._full):
+            self._release(u)
+        if self.cpu_offload:
+            self.grads_host.copy_(self.grads, non_blocking=True)
+
+    def zero_grad(self):
+        self.grads.zero_()
+
+    # ------------------------------------------------------------------ full state
+    @torch.no_grad()
+    def gather_full(self, flat_shards, dst_rank: int = 0, dtype=torch.float32):
+        """Canonical {name: tensor} of a sharded flat f32 buffer (params or optimizer
+        moments), materialised on ``dst_rank`` (others return None).  Collective."""
+        out = {} if self.rank == dst_rank else None
+        for u in self.units:
+            sh = self.shard(flat_shards, u).to(self.device)
+            full = torch.empty(self.unit_len[u], dtype=sh.dtype, device=self.device)
+            if self.W > 1:
+                comm.all_gather_into(full, sh.contiguous(), group=self.group)
+            else:
+                full.copy_(sh)
+            if out is not None:
+                lo = self.layout.unit_ranges[u][0]
+                for e in self.layout.unit_entries(u):
+                    out[e.name] = full[e.offset - lo:e.offset - lo + e.numel].view(e.shape).to(
+                        "cpu", dtype=dtype, copy=True)
+        return out
+
+    @torch.no_grad()
+    def load_full(self, sd: dict, flat_shards):
+        for u in self.units:
+            lo = self.layout.unit_ranges[u][0]
+            mine0 = lo + self.rank * self.shard_len[u]
+            mine1 = mine0 + self.shard_len[u]
+            for e in self.layout.unit_entries(u):
+                a, b = max(e.offset, mine0), min(e.offset + e.numel, mine1)
+                if a < b:
+                    src = sd[e.name].reshape(-1)[a - e.offset:b - e.offset]
+                    dst0 = self.shard_off[u] + (a - mine0)
+                    flat_shards[dst0:dst0 + (b - a)].copy_(src)

@@ -94,7 +94,7 @@ class ParamStore:
     def pre_forward(self, u):
         pass
 
-    def post_forward(self, u):
+    def post_forward(self, u, training=True):
         pass
 
     def pre_backward(self, u, need_weights=True):
