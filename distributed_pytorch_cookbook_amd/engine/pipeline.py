@@ -1,0 +1,289 @@
+"""Pipeline (and pipeline x data parallel) engine: recipes ``main-pipe.py`` and
+``main-pipe-ddp.py``.
+
+Reference: ``/root/reference/main-pipe.py:85-221`` (GPipe via torch Pipe, chunks =
+stages, single process) and ``main-pipe-ddp.py`` (an empty stub).  Here: one process per
+GPU on a (pp, dp) mesh -- rank = stage * dp + replica -- each stage owning a contiguous,
+cost-balanced run of units (``parallel/pipeline.py``), micro-batches scheduled 1F1B
+(default) or GPipe, activations exchanged by grouped RCCL send/recv between neighbouring
+stages, and, for dp > 1, each stage's gradients all-reduced across its replicas with the
+bucketed DDP store once the last micro-batch's backward has produced them.
+
+The loss is the exact mean over all valid tokens of the batch: micro-batch losses are
+weighted by their share of valid targets (computed on device, no sync).
+"""
+from __future__ import annotations
+
+import torch
+import torch.distributed as dist
+
+from ..models.fused import run_embeddings, run_head, run_layers
+from ..ops.optim import FlatAdamW
+from ..parallel import comm
+from ..parallel.ddp import DDPStore
+from ..parallel.fsdp import _placeholder
+from ..parallel.pipeline import P2P, partition, schedule_1f1b, schedule_gpipe, unit_costs
+from ..parallel.store import LocalStore
+from .base import Engine
+
+
+class PipelineEngine(Engine):
+    name = "pipe"
+    collective_generate = True
+
+    def __init__(self, model, device, lr: float, pp: int, dp: int = 1, num_microbatches: int = 0,
+                 schedule: str = "1f1b", bucket_mb: float = 128.0, compute_dtype=None,
+                 seq_len: int | None = None):
+        self.device = torch.device(device)
+        self.model = model
+        world = comm.world_size()
+        if pp * dp != world:
+            raise ValueError(f"pp ({pp}) x dp ({dp}) must equal the world size ({world})")
+        self.pp, self.dp = pp, dp
+        if world > 1:
+            self.pp_group, self.dp_group, self.stage, self.replica, pp_ranks = comm.make_mesh(pp, dp)
+        else:
+            self.pp_group = self.dp_group = None
+            self.stage, self.replica, pp_ranks = 0, 0, [0]
+        self.dp_world = dp
+        self.dp_rank = self.replica
+        self.first = self.stage == 0
+        self.last = self.stage == pp - 1
+        self.is_logger = comm.rank() == 0
+        self.n_micro = max(1, num_microbatches or 2 * pp)
+        self.schedule = schedule
+        S = seq_len or model.max_position_embeddings
+        groups = partition(unit_costs(model, S), pp)
+        self.groups = groups
+        self.my_units = groups[self.stage]
+        nunits = model.num_layers + 2
+        self.layers = [model.decoder.layers[u - 1] for u in self.my_units if 1 <= u <= model.num_layers]
+        # free parameters of units owned by other stages before building the store
+        mine = set(self.my_units)
+        for ui, (_, mods) in enumerate(model.units()):
+            if ui not in mine:
+                for mod in mods:
+                    for p in mod.parameters():
+                        p.data = _placeholder(p.shape, self.device)
+        if dp > 1:
+            self.store = DDPStore(model, device, group=self.dp_group, bucket_mb=bucket_mb,
+                                  compute_dtype=compute_dtype, units=self.my_units)
+        else:
+            self.store = LocalStore(model, device, compute_dtype=compute_dtype, units=self.my_units)
+        self.store.accum_steps = self.n_micro
+        self.opt = FlatAdamW(self.store.master, self.store.grads, lr=lr, shadow=self.store.shadow)
+        self.p2p = P2P(pp_ranks, self.stage, self.device)
+        self.pp_ranks = pp_ranks
+        self.D = model.dim
+        assert nunits == len(model.units())
+        if world > 1:
+            # bring up the communicators before the first (grouped) p2p
+            t = torch.zeros(1, device=self.device)
+            if self.pp_group is not None:
+                dist.all_reduce(t, group=self.pp_group)
+            if self.dp_group is not None:
+                dist.all_reduce(t, group=self.dp_group)
+
+    # ------------------------------------------------------------------ pieces
+    def _split(self, batch, targets):
+        N = batch["input_ids"].shape[0]
+        M = self.n_micro
+        if N % M:
+            raise ValueError(f"batch {N} not divisible by {M} micro-batches")
+        mb = N // M
+        out = []
+        for m in range(M):
+            sl = slice(m * mb, (m + 1) * mb)
+            out.append((batch["input_ids"][sl], batch["position_ids"][sl],
+                        None if batch.get("mask") is None else batch["mask"][sl],
+                        targets[sl] if targets is not None else None))
+        return out, mb
+
+    def _fwd(self, mbatch, x_in, training, want_correct=False):
+        ids, pos, mask, tg = mbatch
+        mb, S = ids.shape
+        st = self.store
+        if mask is not None:
+            mask = mask.to(torch.bool).contiguous()
+        if self.first:
+            x = run_embeddings(self.model, st, ids, pos, training)
+        else:
+            x = x_in
+        x = run_layers(self.model, st, x, mask, mb, S, self.layers, training)
+        if self.last:
+            return run_head(self.model, st, x, tg, training, want_correct)
+        return x
+
+    def _act_shape(self, mb, S):
+        return (mb * S, self.D)
+
+    # ------------------------------------------------------------------ training
+    def train_step(self, batch, targets):
+        st = self.store
+        st.zero_grad()
+        micro, mb = self._split(batch, targets)
+        S = batch["input_ids"].shape[1]
+        shape = self._act_shape(mb, S)
+        n_total = (targets != -100).sum().float().clamp_min(1.0) if self.last else None
+        inputs, outputs = {}, {}
+        acc = {"loss": torch.zeros((), device=self.device)} if self.last else {}
+        p2p = self.p2p
+
+        def forward(m, x):
+            if x is not None:
+                x.requires_grad_(True)
+            out = self._fwd(micro[m], x, True)
+            inputs[m] = x
+            if self.last:
+                loss, n_valid, _ = out
+                w = n_valid / n_total
+                outputs[m] = loss * w
+                acc["loss"] = acc["loss"] + (loss * w).detach()
+                return None
+            outputs[m] = out
+            return out
+
+        def backward(m, g):
+            y = outputs.pop(m)
+            if self.last:
+                y.backward()
+            else:
+                torch.autograd.backward(y, g)
+            x = inputs.pop(m)
+            return None if x is None else x.grad
+
+        first, last = self.first, self.last
+        rp = None if first else shape
+        rn = None if last else shape
+        M = self.n_micro
+        if self.schedule == "gpipe":
+            for m in range(M):
+                x, _ = p2p.exchange(recv_prev_shape=rp)
+                y = forward(m, x)
+                p2p.exchange(send_next=y)
+            for m in range(M):
+                _, g = p2p.exchange(recv_next_shape=rn)
+                dx = backward(m, g)
+                p2p.exchange(send_prev=dx)
+        else:
+            warm = min(self.pp - self.stage - 1, M)
+            rem = M - warm
+            for m in range(warm):
+                x, _ = p2p.exchange(recv_prev_shape=rp)
+                y = forward(m, x)
+                p2p.exchange(send_next=y)
+            x = None
+            if rem > 0:
+                x, _ = p2p.exchange(recv_prev_shape=rp)
+            for i in range(rem):
+                y = forward(warm + i, x)
+                _, g = p2p.exchange(send_next=y, recv_next_shape=rn)
+                dx = backward(i, g)
+                if i == rem - 1:
+                    p2p.exchange(send_prev=dx)
+                    x = None
+                else:
+                    x, _ = p2p.exchange(send_prev=dx, recv_prev_shape=rp)
+            for i in range(warm):
+                _, g = p2p.exchange(recv_next_shape=rn)
+                dx = backward(rem + i, g)
+                p2p.exchange(send_prev=dx)
+        if self.dp > 1:
+            st.finish_grads()
+        self.opt.step(grad_scale=1.0 / self.dp)
+        return acc.get("loss")
+
+    @torch.no_grad()
+    def eval_step(self, batch, targets):
+        micro, mb = self._split(batch, targets)
+        S = batch["input_ids"].shape[1]
+        shape = self._act_shape(mb, S)
+        tot = [torch.zeros((), device=self.device) for _ in range(3)]
+        for m in range(self.n_micro):
+            x, _ = self.p2p.exchange(recv_prev_shape=None if self.first else shape)
+            out = self._fwd(micro[m], x, False, want_correct=True)
+            if self.last:
+                loss, n_valid, n_corr = out
+                tot[0] = tot[0] + loss * n_valid
+                tot[1] = tot[1] + n_valid
+                tot[2] = tot[2] + n_corr
+            else:
+                self.p2p.exchange(send_next=out)
+        return tot if self.last else None
+
+    # ------------------------------------------------------------------ generation
+    def lm(self):
+        eng = self
+
+        @torch.no_grad()
+        def forward(input_ids, position_ids, mask=None):
+            from ..models.fused import head_logits
+
+            N, S = input_ids.shape
+            shape = (N * S, eng.D)
+            x, _ = eng.p2p.exchange(recv_prev_shape=None if eng.first else shape)
+            st = eng.store
+            if eng.first:
+                x = run_embeddings(eng.model, st, input_ids, position_ids, False)
+            x = run_layers(eng.model, st, x, None, N, S, eng.layers, False)
+            V = eng.model.vocab_size
+            tok = torch.zeros(1, dtype=torch.int64, device=eng.device)
+            if eng.last:
+                logits = head_logits(eng.model, x, st).reshape(N, S, -1)
+                tok[0] = logits[0, -1].argmax()
+            else:
+                eng.p2p.exchange(send_next=x)
+            if eng.pp > 1:
+                dist.broadcast(tok, src=eng.pp_ranks[-1], group=eng.pp_group)
+            out = torch.zeros(1, 1, V, device=eng.device)
+            out[0, 0, tok[0]] = 1.0
+            return out
+
+        return forward
+
+    # ------------------------------------------------------------------ state
+    def _gather_named(self, named: dict):
+        """Merge per-stage {name: cpu tensor} dicts onto global rank 0 (replica 0 only)."""
+        if self.pp == 1:
+            return named if self.is_logger else None
+        if self.replica != 0:
+            return None
+        objs = [None] * self.pp if self.stage == 0 else None
+        dist.gather_object(named, objs, dst=self.pp_ranks[0], group=self.pp_group)
+        if self.stage != 0:
+            return None
+        merged = {}
+        for o in objs:
+            merged.update(o)
+        # canonical order
+        order = [n for n, _ in self.model.named_parameters()]
+        return {k: merged[k] for k in order if k in merged}
+
+    def _named_flat(self, flat):
+        return {e.name: self.store._view(flat, e).detach().to("cpu", copy=True) for e in self.store.entries}
+
+    def full_state_dict(self):
+        return self._gather_named(self._named_flat(self.store.master))
+
+    def load_model_state(self, sd):
+        self.store.load_state_dict(sd, strict=False)
+
+    def train_state(self):
+        m = self._gather_named(self._named_flat(self.opt.exp_avg))
+        v = self._gather_named(self._named_flat(self.opt.exp_avg_sq))
+        return {"optimizer": {"step": self.opt.step_count, "exp_avg": m, "exp_avg_sq": v,
+                              "format": "canonical"}}
+
+    def load_train_state(self, st):
+        o = st["optimizer"]
+        self.opt.step_count = int(o["step"])
+        for key, flat in (("exp_avg", self.opt.exp_avg), ("exp_avg_sq", self.opt.exp_avg_sq)):
+            d = o.get(key)
+            if isinstance(d, dict):
+                for e in self.store.entries:
+                    if e.name in d:
+                        self.store._view(flat, e).copy_(d[e.name])
+
+    @property
+    def step_count(self):
+        return self.opt.step_count

@@ -62,6 +62,7 @@ class DDPStore(LocalStore):
         self._ready = [0] * len(self.buckets)
         self._works = {}
         self._tmp = {}
+        self.accum_steps = 1
 
     def _range(self, bi):
         us = self.buckets[bi]
@@ -86,7 +87,9 @@ class DDPStore(LocalStore):
             return
         bi = self.bucket_of[u]
         self._ready[bi] += 1
-        if self.overlap and self._ready[bi] == len(self.buckets[bi]):
+        # with gradient accumulation (pipeline micro-batches) a unit's backward runs
+        # accum_steps times; the bucket is final after the last one
+        if self.overlap and self._ready[bi] == self.accum_steps * len(self.buckets[bi]):
             self._launch(bi)
 
     def finish_grads(self):

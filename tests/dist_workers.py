@@ -1,0 +1,103 @@
+"""Worker bodies for the multi-process engine tests (importable by spawned children)."""
+from __future__ import annotations
+
+import torch
+
+V, S, D, H, HD, L = 97, 24, 32, 2, 16, 3
+LR = 1e-2
+
+
+def make_model(seed=0, act="relu", layers=L):
+    from distributed_pytorch_cookbook_amd.models.gpt import TransformerDecoderLM
+
+    torch.manual_seed(seed)
+    return TransformerDecoderLM(dim=D, head_dim=HD, heads=H, num_layers=layers, vocab_size=V,
+                                max_position_embeddings=S, activation=act)
+
+
+def full_batch(N=8, seed=3, step=0):
+    g = torch.Generator().manual_seed(seed + 17 * step)
+    ids = torch.randint(0, V, (N, S), generator=g)
+    inputs, targets = ids[:, :-1].contiguous(), ids[:, 1:].contiguous()
+    pos = torch.arange(S - 1).unsqueeze(0).expand(N, -1).contiguous()
+    return dict(input_ids=inputs, position_ids=pos, mask=None), targets
+
+
+def shard(batch, targets, i, n):
+    N = targets.shape[0]
+    sl = slice(i * N // n, (i + 1) * N // n)
+    return {k: (v[sl] if torch.is_tensor(v) else v) for k, v in batch.items()}, targets[sl]
+
+
+def reference_state(steps=2, layers=L):
+    """Single-process result on the full batch."""
+    from distributed_pytorch_cookbook_amd.engine.data_parallel import DataParallelEngine
+
+    m = make_model(layers=layers)
+    eng = DataParallelEngine(m, "cpu", lr=LR)
+    losses = []
+    for s in range(steps):
+        b, t = full_batch(step=s)
+        losses.append(float(eng.train_step(b, t)))
+    return {k: v.clone() for k, v in eng.full_state_dict().items()}, losses
+
+
+def worker_ddp(rank, world, out, steps, bucket_mb, reduce_dtype):
+    from distributed_pytorch_cookbook_amd.engine.data_parallel import DataParallelEngine
+    from distributed_pytorch_cookbook_amd.parallel import comm
+
+    comm.init_dist(force_cpu=True)
+    m = make_model()
+    eng = DataParallelEngine(m, "cpu", lr=LR, bucket_mb=bucket_mb,
+                             reduce_dtype=getattr(torch, reduce_dtype))
+    assert len(eng.store.buckets) >= 2 or bucket_mb > 1
+    for s in range(steps):
+        b, t = shard(*full_batch(step=s), rank, world)
+        eng.train_step(b, t)
+    sd = eng.full_state_dict()
+    if rank == 0:
+        torch.save({k: v.clone() for k, v in sd.items()}, out)
+
+
+def worker_fsdp(rank, world, out, steps, prefetch, reshard):
+    from distributed_pytorch_cookbook_amd.engine.fsdp import FSDPEngine
+    from distributed_pytorch_cookbook_amd.parallel import comm
+
+    comm.init_dist(force_cpu=True)
+    m = make_model()
+    eng = FSDPEngine(m, "cpu", lr=LR, prefetch=prefetch, reshard_after_forward=reshard)
+    for s in range(steps):
+        b, t = shard(*full_batch(step=s), rank, world)
+        eng.train_step(b, t)
+    sd = eng.full_state_dict()
+    # eval + generation must run collectively without hanging
+    with torch.no_grad():
+        b, t = shard(*full_batch(step=99), rank, world)
+        r = eng.eval_step(b, t)
+        assert r[1].item() > 0
+    if rank == 0:
+        torch.save(sd, out)
+
+
+def worker_pipe(rank, world, out, steps, pp, dp, micro, schedule):
+    from distributed_pytorch_cookbook_amd.engine.pipeline import PipelineEngine
+    from distributed_pytorch_cookbook_amd.parallel import comm
+
+    comm.init_dist(force_cpu=True)
+    m = make_model()
+    eng = PipelineEngine(m, "cpu", lr=LR, pp=pp, dp=dp, num_microbatches=micro, schedule=schedule,
+                         bucket_mb=0.01, seq_len=S)
+    losses = []
+    for s in range(steps):
+        b, t = shard(*full_batch(step=s), eng.replica, dp)
+        loss = eng.train_step(b, t)
+        losses.append(None if loss is None else float(loss))
+    sd = eng.full_state_dict()
+    # eval and a generate-style forward must stay matched on every rank
+    b, t = shard(*full_batch(step=99), eng.replica, dp)
+    eng.eval_step(b, t)
+    f = eng.lm()
+    ids = torch.randint(0, V, (1, 5))
+    f(input_ids=ids, position_ids=torch.arange(5).unsqueeze(0))
+    if rank == 0:
+        torch.save({"sd": sd, "groups": eng.groups}, out)

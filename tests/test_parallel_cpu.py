@@ -1,0 +1,79 @@
+"""DDP / FSDP / pipeline / pipeline x DDP engines on CPU (gloo, multi-process) must produce
+the same parameters as the single-process engine on the same global batch."""
+import pytest
+import torch
+
+from dist_helpers import run_workers
+from dist_workers import (reference_state, worker_ddp, worker_fsdp, worker_pipe)
+
+from distributed_pytorch_cookbook_amd.parallel.pipeline import partition, schedule_1f1b
+
+pytestmark = pytest.mark.slow
+
+
+def assert_close_sd(a, b, atol=2e-5):
+    assert list(a.keys()) == list(b.keys())
+    for k in a:
+        assert torch.allclose(a[k].float(), b[k].float(), atol=atol, rtol=1e-4), \
+            (k, (a[k] - b[k]).abs().max().item())
+
+
+@pytest.fixture(scope="module")
+def ref():
+    return reference_state(steps=2)
+
+
+@pytest.mark.parametrize("reduce_dtype", ["float32"])
+def test_ddp_matches_single(tmp_path, ref, reduce_dtype):
+    out = tmp_path / "ddp.pt"
+    run_workers(worker_ddp, 2, str(out), 2, 0.05, reduce_dtype)
+    assert_close_sd(torch.load(out, weights_only=True), ref[0])
+
+
+@pytest.mark.parametrize("prefetch,reshard", [(1, True), (2, False)])
+def test_fsdp_matches_single(tmp_path, ref, prefetch, reshard):
+    out = tmp_path / "fsdp.pt"
+    run_workers(worker_fsdp, 2, str(out), 2, prefetch, reshard)
+    assert_close_sd(torch.load(out, weights_only=True), ref[0])
+
+
+@pytest.mark.parametrize("schedule,micro", [("1f1b", 4), ("gpipe", 2)])
+def test_pipeline_matches_single(tmp_path, ref, schedule, micro):
+    out = tmp_path / "pp.pt"
+    run_workers(worker_pipe, 2, str(out), 2, 2, 1, micro, schedule)
+    r = torch.load(out, weights_only=True)
+    assert_close_sd(r["sd"], ref[0])
+
+
+def test_pipeline_three_stages(tmp_path, ref):
+    out = tmp_path / "pp3.pt"
+    run_workers(worker_pipe, 3, str(out), 2, 3, 1, 4, "1f1b")
+    assert_close_sd(torch.load(out, weights_only=True)["sd"], ref[0])
+
+
+def test_pipe_ddp_mesh_matches_single(tmp_path, ref):
+    out = tmp_path / "ppdp.pt"
+    run_workers(worker_pipe, 4, str(out), 2, 2, 2, 2, "1f1b")
+    assert_close_sd(torch.load(out, weights_only=True)["sd"], ref[0])
+
+
+def test_partition_balanced_and_contiguous():
+    costs = [0.1] + [1.0] * 24 + [3.5]
+    g = partition(costs, 8)
+    assert [u for grp in g for u in grp] == list(range(26))
+    loads = [sum(costs[u] for u in grp) for grp in g]
+    assert max(loads) <= 4.1
+    assert g[-1][-1] == 25 and len(g[-1]) < len(g[1])
+
+
+def test_1f1b_order_counts():
+    for st in range(4):
+        o = schedule_1f1b(8, st, 4)
+        assert [m for k, m in o if k == "F"] == list(range(8))
+        assert [m for k, m in o if k == "B"] == list(range(8))
+        # at most (stages - stage) micro-batches in flight
+        inflight = mx = 0
+        for k, _ in o:
+            inflight += 1 if k == "F" else -1
+            mx = max(mx, inflight)
+        assert mx <= 4 - st
