@@ -239,6 +239,7 @@ class PipelineEngine(Engine):
             out[0, 0, tok[0]] = 1.0
             return out
 
+        forward.max_position_embeddings = self.model.max_position_embeddings
         return forward
 
     # ------------------------------------------------------------------ state

@@ -38,10 +38,13 @@ def prepare_batch(batch, pad_id: int, device):
 def generate(model, prompt: str, tokenizer, device, max_new_tokens: int = 20) -> str:
     batch = tokenizer([prompt], truncation=True, max_length=256, return_tensors="pt")
     input_ids = batch["input_ids"].to(device)
+    # the learned position table bounds the context: slide a window past it
+    max_pos = getattr(model, "max_position_embeddings", None) or 1 << 30
     for _ in range(max_new_tokens):
-        s = input_ids.shape[1]
+        ctx = input_ids[:, -max_pos:]
+        s = ctx.shape[1]
         position_ids = torch.arange(s, device=device).unsqueeze(0)
-        logits = model(input_ids=input_ids, position_ids=position_ids)
+        logits = model(input_ids=ctx, position_ids=position_ids)
         new_token = int(logits[0, -1].argmax(dim=-1))
         if new_token == tokenizer.eos_token_id:
             break
