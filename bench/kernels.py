@@ -41,6 +41,8 @@ def main():
     ap.add_argument("--vocab", type=int, default=50257)
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--json", type=str, default=None)
+    ap.add_argument("--impls", type=int, nargs="+", default=[1, 2, 3])
+    ap.add_argument("--gemm_only", action="store_true")
     a = ap.parse_args()
     dev = "cuda"
     T, D, V = a.tokens, a.dim, a.vocab
@@ -54,30 +56,44 @@ def main():
         ("qkv_fwd", T, 3 * D, D), ("out_fwd", T, D, D), ("up_fwd", T, 4 * D, D),
         ("down_fwd", T, D, 4 * D), ("lm_head_fwd", T, V, D),
     ]
+    from distributed_pytorch_cookbook_amd.ops import _lib
+
+    def ours_impls(fn):
+        res = {}
+        for impl in a.impls:
+            _lib.set_gemm_impl(impl)
+            res[impl] = timeit(fn, a.iters)
+        _lib.set_gemm_impl(-1)
+        return res
+
+    def add(name, M, N, K, fn, ref_fn):
+        fl = 2 * M * N * K
+        t = ours_impls(fn)
+        ref = timeit(ref_fn, a.iters)
+        best = min(t.values())
+        r = dict(case=name, M=M, N=N, K=K, ours_ms=best, torch_ms=ref,
+                 ours_tflops=fl / best / 1e9, torch_tflops=fl / ref / 1e9)
+        for impl, v in t.items():
+            r[f"impl{impl}_tflops"] = fl / v / 1e9
+        rows.append(r)
+
     for name, M, N, K in cases:
         x, w = rnd(M, K), rnd(N, K)
-        ours = timeit(lambda: gemm(x, w), a.iters)
-        ref = timeit(lambda: x @ w.t(), a.iters)
-        fl = 2 * M * N * K
-        rows.append(dict(case=name, M=M, N=N, K=K, ours_ms=ours, torch_ms=ref,
-                         ours_tflops=fl / ours / 1e9, torch_tflops=fl / ref / 1e9))
+        add(name, M, N, K, lambda: gemm(x, w), lambda: x @ w.t())
     # dgrad (B n-major) and wgrad (both mn-major) shapes
     for name, M, N, K in [("up_dgrad", T, D, 4 * D), ("qkv_dgrad", T, D, 3 * D), ("lm_dgrad", T, D, Vp)]:
         dy, w = rnd(M, K), rnd(K, N)
-        ours = timeit(lambda: gemm(dy, w, a_kmaj=True, b_kmaj=False), a.iters)
-        ref = timeit(lambda: dy @ w, a.iters)
-        fl = 2 * M * N * K
-        rows.append(dict(case=name, M=M, N=N, K=K, ours_ms=ours, torch_ms=ref,
-                         ours_tflops=fl / ours / 1e9, torch_tflops=fl / ref / 1e9))
+        add(name, M, N, K, lambda: gemm(dy, w, a_kmaj=True, b_kmaj=False), lambda: dy @ w)
     for name, M, N, K in [("up_wgrad", 4 * D, D, T), ("qkv_wgrad", 3 * D, D, T), ("lm_wgrad", V, D, T)]:
         dy = rnd(K, (M + 7) // 8 * 8)[:, :M]
         x = rnd(K, N)
         out = torch.zeros(M, N, device=dev)
-        ours = timeit(lambda: gemm(dy, x, a_kmaj=False, b_kmaj=False, out=out, accumulate=True), a.iters)
-        ref = timeit(lambda: out.add_(dy.t() @ x), a.iters)
-        fl = 2 * M * N * K
-        rows.append(dict(case=name, M=M, N=N, K=K, ours_ms=ours, torch_ms=ref,
-                         ours_tflops=fl / ours / 1e9, torch_tflops=fl / ref / 1e9))
+        add(name, M, N, K, lambda: gemm(dy, x, a_kmaj=False, b_kmaj=False, out=out, accumulate=True),
+            lambda: out.add_(dy.t() @ x))
+    if a.gemm_only:
+        for r in rows:
+            print(json.dumps(r))
+        return
     # attention (GPT-2 small: H=12, hd=64, S=1023)
     S, H, hd = 1023, 12, 64
     N = max(1, T // S)

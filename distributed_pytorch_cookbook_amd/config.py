@@ -46,6 +46,8 @@ def build_parser(recipe: str = "single") -> argparse.ArgumentParser:
     p.add_argument("--seed", type=int, default=0)
     p.add_argument("--resume", type=str, default=None, help="checkpoint file or 'latest'")
     p.add_argument("--checkpoint_dir", type=str, default="checkpoints")
+    p.add_argument("--save_every", type=int, default=0,
+                   help="also checkpoint (model + optimizer + RNG) every N optimizer steps")
     p.add_argument("--no_save", action="store_true")
     p.add_argument("--no_generate", action="store_true")
     p.add_argument("--bucket_mb", type=float, default=128.0, help="DDP gradient bucket size")

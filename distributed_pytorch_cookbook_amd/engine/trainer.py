@@ -24,6 +24,7 @@ from ..parallel import comm
 from ..utils.batch import generate, prepare_batch
 from ..utils.checkpoint import (latest_checkpoint, load_model_state, load_train_state, rng_state,
                                 save_model_state, save_train_state, set_rng_state)
+from ..utils.profiling import StepProfiler, mark, maybe_inject_fault
 
 PRINT_FREQ = 8
 PROMPTS = ("The big brown cat ", "One day, ", "She said ")
@@ -124,11 +125,17 @@ class Trainer:
         window, nwin = None, 0
         t0 = time.perf_counter()
         tokens = 0
+        prof = StepProfiler(a.profile if ei == self.start_epoch else None, comm.rank())
         for i, batch in enumerate(pb):
             if a.max_steps and i >= a.max_steps:
                 break
+            maybe_inject_fault(e.step_count, comm.rank())
             inputs, targets = prepare_batch(batch, self.pad_id, self.device)
-            loss = e.train_step(inputs, targets)
+            with mark("train_step"):
+                loss = e.train_step(inputs, targets)
+            prof.step()
+            if getattr(a, "save_every", 0) and e.step_count % a.save_every == 0:
+                self.save(ei)  # resume restarts this epoch with the saved weights/moments
             tokens += targets.numel() * e.dp_world
             if loss is not None:
                 window = loss if window is None else window + loss
@@ -144,6 +151,7 @@ class Trainer:
                 self.history.append(rec)
                 self._jsonl(rec)
                 window, nwin, tokens, t0 = None, 0, 0, time.perf_counter()
+        prof.close()
         if window is not None and nwin:
             avg = (window / nwin).item()
             self.history.append({"epoch": ei + 1, "step": e.step_count, "loss": avg})

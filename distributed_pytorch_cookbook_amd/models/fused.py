@@ -172,7 +172,7 @@ class _HeadFn(torch.autograd.Function):
         hf, mu, rs = layernorm_fwd(x, w(norm.weight), w(norm.bias), LN_EPS, cdt)
         ld = vocab_ld(V) if x.is_cuda else V
         buf = torch.empty(T, ld, device=x.device, dtype=cdt)
-        linear_fwd(hf, w(head.weight), out=buf[:, :V])
+        linear_fwd(hf, w(head.weight), out=buf)  # padded columns come out 0 (B rows >= V read as 0)
         loss, n_valid, n_correct = cross_entropy_fused(buf, targets, V, write_grad=training,
                                                        want_correct=want_correct)
         store.post_forward(unit, training)
@@ -194,7 +194,8 @@ class _HeadFn(torch.autograd.Function):
         dl = dlogits[:, :V]
         scale = dloss.reshape(()).float().contiguous()
         linear_wgrad(dl, hf, out=g(head.weight), alpha_t=scale)
-        dhf = linear_dgrad(dl, w(head.weight), out_dtype=torch.float32, alpha_t=scale)
+        # K = padded vocab: the CE kernel zeroed dlogits' pad columns, W_lm rows >= V read as 0
+        dhf = linear_dgrad(dlogits, w(head.weight), out_dtype=torch.float32, alpha_t=scale)
         dx = torch.zeros_like(x)
         layernorm_bwd(dhf, x, mu, rs, w(norm.weight), dx, g(norm.weight), g(norm.bias))
         store.post_backward(unit)
@@ -211,7 +212,7 @@ def head_logits(model, x, store):
                              store.compute_dtype)
     ld = vocab_ld(V) if x.is_cuda else V
     buf = torch.empty(x.shape[0], ld, device=x.device, dtype=store.compute_dtype)
-    linear_fwd(hf, w(model.lm_head.weight), out=buf[:, :V])
+    linear_fwd(hf, w(model.lm_head.weight), out=buf)
     store.post_forward(unit, False)
     return buf[:, :V]
 

@@ -31,6 +31,7 @@ class GemmArgs(ctypes.Structure):
         ("alpha", c_float),
         ("act", c_int), ("act_bwd", c_int), ("out_f32", c_int), ("accumulate", c_int),
         ("a_kmaj", c_int), ("b_kmaj", c_int),
+        ("a_r", c_int), ("a_c", c_int), ("b_r", c_int), ("b_c", c_int),
     ]
 
 
@@ -131,8 +132,15 @@ def lib() -> ctypes.CDLL:
                 fn = getattr(handle, name)
                 fn.argtypes = [ctypes.POINTER(st), c_void_p]
                 fn.restype = c_int
+            handle.dpc_gemm_set_impl.argtypes = [c_int]
+            handle.dpc_gemm_set_impl.restype = None
             _lib = handle
     return _lib
+
+
+def set_gemm_impl(impl: int) -> None:
+    """-1 auto (default), 1 register-staged v1, 2 / 3 LDS-DMA v2 with 2 / 3 stages."""
+    lib().dpc_gemm_set_impl(int(impl))
 
 
 def is_loaded() -> bool:

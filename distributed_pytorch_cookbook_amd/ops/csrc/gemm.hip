@@ -43,6 +43,9 @@ struct GemmArgs {
   int out_f32;     // C is f32 (else bf16)
   int accumulate;  // C += result (f32 output only)
   int a_kmaj, b_kmaj;
+  // stored extents of the operands ([rows][cols] as laid out in memory); reads beyond them
+  // return zeros.  k-major: rows = M or N, cols = K;  mn-major: rows = K, cols = M or N.
+  int a_r, a_c, b_r, b_c;
 };
 
 constexpr int BM = 128, BN = 128, BKT = 64, NT = 256;
@@ -154,8 +157,10 @@ __global__ __launch_bounds__(NT, 2) void gemm_kernel(GemmArgs p) {
 
   const int nk = (p.K + BKT - 1) / BKT;
   uint4 ra[4], rb[4];
-  g_load<AK>(ra, A, p.lda, m0, 0, p.M, p.K);
-  g_load<BK>(rb, B, p.ldb, n0, 0, p.N, p.K);
+  const int a_mn = AK ? p.a_r : p.a_c, a_k = AK ? min(p.K, p.a_c) : min(p.K, p.a_r);
+  const int b_mn = BK ? p.b_r : p.b_c, b_k = BK ? min(p.K, p.b_c) : min(p.K, p.b_r);
+  g_load<AK>(ra, A, p.lda, m0, 0, a_mn, a_k);
+  g_load<BK>(rb, B, p.ldb, n0, 0, b_mn, b_k);
   s_store<AK>(ra, smem);
   s_store<BK>(rb, smem + TILE_ELEMS);
   __syncthreads();
@@ -164,8 +169,8 @@ __global__ __launch_bounds__(NT, 2) void gemm_kernel(GemmArgs p) {
     const int cur = kt & 1;
     const bool more = kt + 1 < nk;
     if (more) {
-      g_load<AK>(ra, A, p.lda, m0, (kt + 1) * BKT, p.M, p.K);
-      g_load<BK>(rb, B, p.ldb, n0, (kt + 1) * BKT, p.N, p.K);
+      g_load<AK>(ra, A, p.lda, m0, (kt + 1) * BKT, a_mn, a_k);
+      g_load<BK>(rb, B, p.ldb, n0, (kt + 1) * BKT, b_mn, b_k);
     }
     const bf16_t* la = smem + cur * 2 * TILE_ELEMS;
     const bf16_t* lb = la + TILE_ELEMS;
@@ -231,14 +236,270 @@ __global__ __launch_bounds__(NT, 2) void gemm_kernel(GemmArgs p) {
   }
 }
 
+// =====================================================================================
+// v2: LDS-DMA pipeline.  Operand tiles stream HBM/L2 -> LDS with buffer_load_dwordx4 ... lds
+// (no VGPR round trip, no ds_write), STAGES-deep ring with ONE raw s_barrier per k-tile and a
+// counted vmcnt that keeps STAGES-2 tiles in flight across it.  The buffer descriptor's
+// num_records bounds every operand, so out-of-range rows / k-rows land in LDS as zeros (the
+// M/N/K edges need no predicates).  Because the DMA writes LDS lane-linearly (1 KiB per
+// wave-instruction), the bank swizzle is applied to the per-lane SOURCE address and read back
+// with the same involution.  Epilogue: the f32 tile goes through LDS so that bias / residual /
+// aux / C traffic is 16-B-per-lane row-contiguous.
+// =====================================================================================
+typedef __attribute__((address_space(3))) void* lds_void_t;
+
+template <bool KMAJ>
+__device__ __forceinline__ void issue_tile(__amdgpu_buffer_rsrc_t rs, const int (&voff)[4], unsigned soff,
+                                           bf16_t* lds_tile, int wave) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int j = wave * 4 + i;  // wave-instruction index: 1 KiB of the 16 KiB tile
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void_t)(lds_tile + j * 512), 16, voff[i], soff, 0, 0);
+  }
+}
+
+template <int STAGES, bool AK, bool BK>
+__global__ __launch_bounds__(NT, (STAGES == 2 ? 2 : 1)) void gemm2_kernel(GemmArgs p, unsigned a_bytes,
+                                                                       unsigned b_bytes) {
+  __shared__ __attribute__((aligned(16))) bf16_t smem[STAGES * 2 * TILE_ELEMS];
+  const int tiles_m = (p.M + BM - 1) / BM, tiles_n = (p.N + BN - 1) / BN;
+  const int nwg = tiles_m * tiles_n;
+  int bid = blockIdx.x;
+  {
+    const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
+    bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+  }
+  const int group = GROUP_M * tiles_n;
+  const int gid = bid / group, first_m = gid * GROUP_M;
+  const int gsz = min(tiles_m - first_m, GROUP_M);
+  const int tm = first_m + (bid % group) % gsz;
+  const int tn = (bid % group) / gsz;
+  const int m0 = tm * BM, n0 = tn * BN;
+
+  const int lane = threadIdx.x & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wr = wid >> 1, wc = wid & 1;
+
+  const __amdgpu_buffer_rsrc_t rsa = __builtin_amdgcn_make_buffer_rsrc((void*)p.A, 0, a_bytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rsb = __builtin_amdgcn_make_buffer_rsrc((void*)p.B, 0, b_bytes, 0x00020000);
+
+  // per-lane source byte offsets (k-tile 0); the k advance goes into the scalar soffset
+  int va[4], vb[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int j = wid * 4 + i;
+    if (AK) {
+      const int row = 8 * j + (lane >> 3), pos = lane & 7, c = pos ^ ((row >> 1) & 7);
+      va[i] = (int)(((long long)(m0 + row) * p.lda + c * 8) * 2);
+    } else {
+      const int kr = 4 * j + (lane >> 4), pos = lane & 15;
+      const int c = (((pos >> 1) ^ mn_swz(kr)) << 1) | (pos & 1);
+      va[i] = (int)(((long long)kr * p.lda + m0 + c * 8) * 2);
+    }
+    if (BK) {
+      const int row = 8 * j + (lane >> 3), pos = lane & 7, c = pos ^ ((row >> 1) & 7);
+      vb[i] = (int)(((long long)(n0 + row) * p.ldb + c * 8) * 2);
+    } else {
+      const int kr = 4 * j + (lane >> 4), pos = lane & 15;
+      const int c = (((pos >> 1) ^ mn_swz(kr)) << 1) | (pos & 1);
+      vb[i] = (int)(((long long)kr * p.ldb + n0 + c * 8) * 2);
+    }
+  }
+  const unsigned sa_step = AK ? BKT * 2u : (unsigned)(BKT * p.lda * 2);
+  const unsigned sb_step = BK ? BKT * 2u : (unsigned)(BKT * p.ldb * 2);
+
+  floatx4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+
+  // split-K: blockIdx.y owns a contiguous run of k-tiles (the host only splits plain
+  // f32-accumulating products, whose partial tiles are combined with f32 atomics)
+  const int nk_all = (p.K + BKT - 1) / BKT;
+  const int splits = gridDim.y;
+  const int per = (nk_all + splits - 1) / splits;
+  const int kt0 = blockIdx.y * per;
+  const int nk = max(0, min(nk_all, kt0 + per) - kt0);
+  auto issue = [&](int it) {
+    bf16_t* base = smem + (it % STAGES) * 2 * TILE_ELEMS;
+    const unsigned kt = (unsigned)(kt0 + it);
+    issue_tile<AK>(rsa, va, sa_step * kt, base, wid);
+    issue_tile<BK>(rsb, vb, sb_step * kt, base + TILE_ELEMS, wid);
+  };
+#pragma unroll
+  for (int s = 0; s < STAGES - 1; ++s)
+    if (s < nk) issue(s);
+
+  for (int kt = 0; kt < nk; ++kt) {
+    // tile kt landed for THIS wave: allow the younger tiles' 8 loads each to stay in flight
+    if (STAGES >= 3 && kt + 1 < nk) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();  // ... and for every wave; also: all waves finished tile kt-1
+    asm volatile("" ::: "memory");
+    if (kt + STAGES - 1 < nk) issue(kt + STAGES - 1);
+    const bf16_t* la = smem + (kt % STAGES) * 2 * TILE_ELEMS;
+    const bf16_t* lb = la + TILE_ELEMS;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      bf16x8 fa[4], fb[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) fa[i] = frag<AK>(la, wr * 64 + i * 16, ks, lane);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) fb[j] = frag<BK>(lb, wc * 64 + j * 16, ks, lane);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+    }
+  }
+
+  // ---------------- epilogue through LDS: wave tile 64x64 f32, columns swizzled by row group
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  float* ct = reinterpret_cast<float*>(smem) + wid * 64 * 64;
+  float alpha = p.alpha;
+  if (p.alpha_ptr) alpha *= *p.alpha_ptr;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = i * 16 + (lane >> 4) * 4 + r;
+        const int col = (j * 16 + (lane & 15)) ^ (((row >> 2) & 3) << 4);
+        ct[row * 64 + col] = acc[i][j][r] * alpha;
+      }
+  __syncthreads();
+  const int c4 = lane & 15;
+  const int n = n0 + wc * 64 + c4 * 4;
+  const bool nok = n < p.N;  // N % 4 == 0 is required by the host for v2
+  float4 bias4 = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (p.bias && nok) bias4 = *reinterpret_cast<const float4*>(p.bias + n);
+  float cs[4] = {0.f, 0.f, 0.f, 0.f};
+  const bf16_t* aux_in = static_cast<const bf16_t*>(p.aux_in);
+  bf16_t* aux_out = static_cast<bf16_t*>(p.aux_out);
+#pragma unroll 4
+  for (int t = 0; t < 16; ++t) {
+    const int row = (lane >> 4) + 4 * t;
+    const int m = m0 + wr * 64 + row;
+    const int col = (c4 * 4) ^ (((row >> 2) & 3) << 4);
+    float4 v4 = *reinterpret_cast<const float4*>(ct + row * 64 + col);
+    if (m >= p.M || !nok) continue;
+    float v[4] = {v4.x + bias4.x, v4.y + bias4.y, v4.z + bias4.z, v4.w + bias4.w};
+    if (p.act_bwd) {
+      const uint2 z = *reinterpret_cast<const uint2*>(aux_in + (long long)m * p.ld_aux_in + n);
+      v[0] *= act_grad(__uint_as_float(z.x << 16), p.act_bwd);
+      v[1] *= act_grad(__uint_as_float(z.x & 0xffff0000u), p.act_bwd);
+      v[2] *= act_grad(__uint_as_float(z.y << 16), p.act_bwd);
+      v[3] *= act_grad(__uint_as_float(z.y & 0xffff0000u), p.act_bwd);
+    }
+#pragma unroll
+    for (int e = 0; e < 4; ++e) cs[e] += v[e];
+    if (aux_out) {
+      uint2 w;
+      w.x = pack2bf(v[0], v[1]);
+      w.y = pack2bf(v[2], v[3]);
+      *reinterpret_cast<uint2*>(aux_out + (long long)m * p.ld_aux_out + n) = w;
+    }
+#pragma unroll
+    for (int e = 0; e < 4; ++e) v[e] = act_fwd(v[e], p.act);
+    if (p.residual) {
+      const float4 r4 = *reinterpret_cast<const float4*>(p.residual + (long long)m * p.ldr + n);
+      v[0] += r4.x; v[1] += r4.y; v[2] += r4.z; v[3] += r4.w;
+    }
+    const long long ci = (long long)m * p.ldc + n;
+    if (splits > 1) {  // partial sums of a split-K product (C pre-zeroed or accumulating)
+      float* C = static_cast<float*>(p.C) + ci;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) atomicAdd(C + e, v[e]);
+    } else if (p.out_f32) {
+      float4* C = reinterpret_cast<float4*>(static_cast<float*>(p.C) + ci);
+      if (p.accumulate) {
+        const float4 o = *C;
+        v[0] += o.x; v[1] += o.y; v[2] += o.z; v[3] += o.w;
+      }
+      *C = make_float4(v[0], v[1], v[2], v[3]);
+    } else {
+      uint2 w;
+      w.x = pack2bf(v[0], v[1]);
+      w.y = pack2bf(v[2], v[3]);
+      *reinterpret_cast<uint2*>(static_cast<bf16_t*>(p.C) + ci) = w;
+    }
+  }
+  if (p.colsum) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      cs[e] += __shfl_xor(cs[e], 16, 64);
+      cs[e] += __shfl_xor(cs[e], 32, 64);
+    }
+    if ((lane >> 4) == 0 && nok) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) atomicAdd(p.colsum + n + e, cs[e]);
+    }
+  }
+}
+
 }  // namespace dpc
 
 using namespace dpc;
+
+static inline long long operand_bytes(long long rows, long long cols, long long ld) {
+  // bytes a tile load may legitimately touch: [rows][ld], 16-B chunks up to roundup8(cols)
+  if (rows <= 0 || cols <= 0) return 0;
+  return ((rows - 1) * ld + ((cols + 7) / 8) * 8) * 2;
+}
+
+template <int STAGES>
+static void launch_v2(const GemmArgs* a, dim3 grid, hipStream_t stream, unsigned ab, unsigned bb) {
+  if (a->a_kmaj && a->b_kmaj) hipLaunchKernelGGL((gemm2_kernel<STAGES, true, true>), grid, dim3(NT), 0, stream, *a, ab, bb);
+  else if (a->a_kmaj) hipLaunchKernelGGL((gemm2_kernel<STAGES, true, false>), grid, dim3(NT), 0, stream, *a, ab, bb);
+  else if (!a->b_kmaj) hipLaunchKernelGGL((gemm2_kernel<STAGES, false, false>), grid, dim3(NT), 0, stream, *a, ab, bb);
+  else hipLaunchKernelGGL((gemm2_kernel<STAGES, false, true>), grid, dim3(NT), 0, stream, *a, ab, bb);
+}
+
+static int g_gemm_impl = -1;  // -1: auto, 1: force v1, 2: force v2 (STAGES=2), 3: v2 STAGES=3
+
+DPC_API void dpc_gemm_set_impl(int impl) { g_gemm_impl = impl; }
+
+static inline bool al(const void* p, int b) { return ((uintptr_t)p % b) == 0; }
 
 DPC_API int dpc_gemm(const GemmArgs* a, hipStream_t stream) {
   if (a->M <= 0 || a->N <= 0) return 0;
   const int tiles = ((a->M + BM - 1) / BM) * ((a->N + BN - 1) / BN);
   dim3 grid(tiles), block(NT);
+  // v2 requirements: a k-major operand must hold exactly K (% 64) columns (its k-tail is not
+  // zeroed by the descriptor), N % 4 == 0 and 16-B aligned f32 epilogue operands (vector
+  // epilogue), every operand inside a 31-bit byte range.
+  const long long ab = operand_bytes(a->a_r, a->a_c, a->lda);
+  const long long bb = operand_bytes(a->b_r, a->b_c, a->ldb);
+  const bool kmaj_ok = (!a->a_kmaj || (a->a_c == a->K && a->K % BKT == 0)) &&
+                       (!a->b_kmaj || (a->b_c == a->K && a->K % BKT == 0));
+  const bool v2_ok = kmaj_ok && a->N % 4 == 0 && ab > 0 && bb > 0 && ab < 0x7fffffffLL &&
+                     bb < 0x7fffffffLL && a->K > 0 && a->ldc % 4 == 0 && a->ldr % 4 == 0 &&
+                     a->ld_aux_in % 4 == 0 && a->ld_aux_out % 4 == 0 &&
+                     al(a->C, a->out_f32 ? 16 : 8) && al(a->bias, 16) && al(a->residual, 16) &&
+                     al(a->aux_in, 8) && al(a->aux_out, 8) && al(a->colsum, 4);
+  int impl = g_gemm_impl;
+  if (impl < 0) impl = v2_ok ? 2 : 1;
+  if (impl >= 2 && !v2_ok) impl = 1;
+  if (impl >= 2) {
+    // split-K for plain f32 (accumulating) products whose tile grid under-fills the chip
+    int splits = 1;
+    const bool plain = a->out_f32 && !a->bias && !a->residual && !a->aux_in && !a->aux_out &&
+                       !a->colsum && !a->act && !a->act_bwd;
+    const int nk = (a->K + BKT - 1) / BKT;
+    if (plain) {
+      while (splits < 8 && tiles * splits < 512 && nk / (splits * 2) >= 8) splits *= 2;
+    }
+    if (splits > 1 && !a->accumulate)
+      hipMemset2DAsync(a->C, (size_t)a->ldc * 4, 0, (size_t)a->N * 4, (size_t)a->M, stream);
+    grid.y = splits;
+    if (impl == 2) launch_v2<2>(a, grid, stream, (unsigned)ab, (unsigned)bb);
+    else launch_v2<3>(a, grid, stream, (unsigned)ab, (unsigned)bb);
+    return (int)hipGetLastError();
+  }
   if (a->a_kmaj && a->b_kmaj) hipLaunchKernelGGL((gemm_kernel<true, true>), grid, block, 0, stream, *a);
   else if (a->a_kmaj && !a->b_kmaj) hipLaunchKernelGGL((gemm_kernel<true, false>), grid, block, 0, stream, *a);
   else if (!a->a_kmaj && !a->b_kmaj) hipLaunchKernelGGL((gemm_kernel<false, false>), grid, block, 0, stream, *a);

@@ -93,10 +93,15 @@ def gemm(
     colsum: torch.Tensor | None = None,
 ) -> torch.Tensor:
     act, act_bwd = act_code(act), act_code(act_bwd)
-    M, K = (a.shape[0], a.shape[1]) if a_kmaj else (a.shape[1], a.shape[0])
-    N, Kb = (b.shape[0], b.shape[1]) if b_kmaj else (b.shape[1], b.shape[0])
-    if K != Kb:
-        raise ValueError(f"gemm: K mismatch {K} vs {Kb}")
+    Ma, Ka = (a.shape[0], a.shape[1]) if a_kmaj else (a.shape[1], a.shape[0])
+    Nb, Kb = (b.shape[0], b.shape[1]) if b_kmaj else (b.shape[1], b.shape[0])
+    # logical sizes; an operand may be stored smaller than them (rows / k-rows beyond its
+    # stored extent read as zeros), e.g. the lm_head over a 64-padded vocabulary
+    M = out.shape[0] if out is not None else Ma
+    N = out.shape[1] if out is not None else Nb
+    K = max(Ka, Kb)
+    if Ma > M or Nb > N or (Ka != K and a_kmaj) or (Kb != K and b_kmaj):
+        raise ValueError(f"gemm: incompatible operands A{tuple(a.shape)} B{tuple(b.shape)} -> ({M},{N},{K})")
     if out is None:
         if accumulate:
             raise ValueError("gemm: accumulate needs an out tensor")
@@ -109,8 +114,8 @@ def gemm(
         raise ValueError("gemm: act_bwd needs aux_in")
 
     if a.is_cuda and a.dtype == torch.bfloat16:
-        _check_operand(a, *( (M, K) if a_kmaj else (K, M) ), "A")
-        _check_operand(b, *( (N, K) if b_kmaj else (K, N) ), "B")
+        _check_operand(a, a.shape[0], a.shape[1], "A")
+        _check_operand(b, b.shape[0], b.shape[1], "B")
         for t, nm, dt in ((residual, "residual", torch.float32), (bias, "bias", torch.float32),
                           (colsum, "colsum", torch.float32),
                           (aux_in, "aux_in", torch.bfloat16), (aux_out, "aux_out", torch.bfloat16)):
@@ -129,6 +134,7 @@ def gemm(
             M=M, N=N, K=K, alpha=float(alpha), act=act, act_bwd=act_bwd,
             out_f32=int(out.dtype == torch.float32), accumulate=int(accumulate),
             a_kmaj=int(a_kmaj), b_kmaj=int(b_kmaj),
+            a_r=a.shape[0], a_c=a.shape[1], b_r=b.shape[0], b_c=b.shape[1],
         )
         _lib.call("dpc_gemm", args, a.device)
         return out
@@ -136,11 +142,21 @@ def gemm(
                      alpha, alpha_t, accumulate, colsum)
 
 
+def _pad_to(x: torch.Tensor, rows: int, cols: int) -> torch.Tensor:
+    if x.shape[0] == rows and x.shape[1] == cols:
+        return x
+    out = torch.zeros(rows, cols, dtype=x.dtype, device=x.device)
+    out[:x.shape[0], :x.shape[1]] = x
+    return out
+
+
 def _gemm_ref(a, b, a_kmaj, b_kmaj, out, bias, act, act_bwd, aux_in, aux_out, residual,
               alpha, alpha_t, accumulate, colsum=None):
-    am = a if a_kmaj else a.t()
-    bm = b if b_kmaj else b.t()
-    v = am.float() @ bm.float().t()
+    am = (a if a_kmaj else a.t()).float()
+    bm = (b if b_kmaj else b.t()).float()
+    M, N = out.shape
+    K = max(am.shape[1], bm.shape[1])
+    v = _pad_to(am, M, K) @ _pad_to(bm, N, K).t()
     v = v * alpha
     if alpha_t is not None:
         v = v * alpha_t.float()

@@ -42,6 +42,51 @@ def test_gemm_layouts(a_kmaj, b_kmaj, M, N, K):
     assert rel_err(out, ref) < 2e-3
 
 
+@pytest.mark.parametrize("impl", [1, 2, 3])
+@pytest.mark.parametrize("a_kmaj,b_kmaj", [(True, True), (True, False), (False, False), (False, True)])
+@pytest.mark.parametrize("M,N,K", [(256, 256, 128), (200, 296, 192), (1023, 768, 768), (77, 1000, 1023)])
+def test_gemm_impls_with_epilogue(impl, a_kmaj, b_kmaj, M, N, K):
+    torch.manual_seed(11)
+    a = torch.randn(M, K, device=dev).bfloat16()
+    b = torch.randn(N, K, device=dev).bfloat16()
+
+    def store(x, kmaj):
+        r, c = x.shape
+        if kmaj:  # rows padded to a multiple of 8 elements (16-B aligned row starts)
+            buf = torch.zeros(r, (c + 7) // 8 * 8, device=dev, dtype=x.dtype)
+            buf[:, :c] = x
+            return buf[:, :c]
+        buf = torch.zeros(c, (r + 7) // 8 * 8, device=dev, dtype=x.dtype)
+        buf[:, :r] = x.t()
+        return buf[:, :r]
+
+    A, B = store(a, a_kmaj), store(b, b_kmaj)
+    bias = torch.randn(N, device=dev)
+    res = torch.randn(M, N, device=dev)
+    z = torch.randn(M, N, device=dev).bfloat16()
+    aux = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+    cs = torch.zeros(N, device=dev)
+    _lib.set_gemm_impl(impl)
+    try:
+        out = gemm(A, B, a_kmaj=a_kmaj, b_kmaj=b_kmaj, bias=bias, act=2, act_bwd=1, aux_in=z,
+                   aux_out=aux, residual=res, colsum=cs, out_dtype=torch.float32)
+        acc0 = torch.randn(M, N, device=dev)
+        acc = acc0.clone()
+        gemm(A, B, a_kmaj=a_kmaj, b_kmaj=b_kmaj, out=acc, accumulate=True)
+        ob = gemm(A, B, a_kmaj=a_kmaj, b_kmaj=b_kmaj)  # bf16 out
+    finally:
+        _lib.set_gemm_impl(-1)
+    ref_out = torch.empty(M, N, device=dev)
+    aux_r = torch.empty_like(aux)
+    cs_r = torch.zeros(N, device=dev)
+    _gemm_ref(a, b, True, True, ref_out, bias, 2, 1, z, aux_r, res, 1.0, None, False, cs_r)
+    assert rel_err(out, ref_out) < 2e-3
+    assert rel_err(aux, aux_r) < 1e-2
+    assert rel_err(cs, cs_r) < 2e-3
+    assert rel_err(acc - acc0, a.float() @ b.float().t()) < 2e-3
+    assert rel_err(ob, a.float() @ b.float().t()) < 1e-2
+
+
 def test_gemm_identity_asymmetric():
     # A = I with an asymmetric B catches a transposed C write
     n = 128
@@ -219,3 +264,35 @@ def test_bias_act_bwd(act):
 
 def test_native_library_loaded():
     assert _lib.is_loaded()
+
+
+@pytest.mark.parametrize("impl", [1, 2])
+def test_gemm_padded_vocab_head(impl):
+    """lm_head over a 64-padded vocab: B has V < N rows (read as zeros), and the dgrad runs
+    with K = padded vocab while W_lm holds only V k-rows."""
+    torch.manual_seed(12)
+    T, D, V = 300, 256, 1001
+    ld = (V + 63) // 64 * 64
+    h = torch.randn(T, D, device=dev).bfloat16()
+    w = torch.randn(V, D, device=dev).bfloat16()
+    _lib.set_gemm_impl(impl)
+    try:
+        buf = torch.full((T, ld), 7.0, device=dev).bfloat16()
+        gemm(h, w, out=buf)
+        g = torch.zeros(T, ld, device=dev).bfloat16()
+        g[:, :V] = torch.randn(T, V, device=dev).bfloat16()
+        dh = gemm(g, w, a_kmaj=True, b_kmaj=False, out_dtype=torch.float32)
+        # split-K plain f32 product (wgrad shape) with and without accumulate
+        dy = torch.randn(8192, 256, device=dev).bfloat16()
+        x = torch.randn(8192, 128, device=dev).bfloat16()
+        o1 = gemm(dy, x, a_kmaj=False, b_kmaj=False, out_dtype=torch.float32)
+        o2 = torch.ones(256, 128, device=dev)
+        gemm(dy, x, a_kmaj=False, b_kmaj=False, out=o2, accumulate=True)
+    finally:
+        _lib.set_gemm_impl(-1)
+    ref = h.float() @ w.float().t()
+    assert rel_err(buf[:, :V], ref) < 1e-2
+    assert buf[:, V:].abs().max().item() == 0
+    assert rel_err(dh, g[:, :V].float() @ w.float()) < 2e-3
+    r = dy.float().t() @ x.float()
+    assert rel_err(o1, r) < 2e-3 and rel_err(o2 - 1, r) < 2e-3
