@@ -39,6 +39,9 @@ def build_parser(recipe: str = "single") -> argparse.ArgumentParser:
     p.add_argument("--dropout", type=float, default=0.0)
     p.add_argument("--synthetic_data", action="store_true",
                    help="use the synthetic token corpus (default when HF data is unavailable)")
+    p.add_argument("--data_path", type=str, default=None,
+                   help="pre-tokenised flat token file (.bin) read by the native mmap loader")
+    p.add_argument("--token_bytes", type=int, default=2, choices=[2, 4], help="bytes per token in --data_path")
     p.add_argument("--train_samples", type=int, default=20000, help="synthetic corpus size")
     p.add_argument("--val_samples", type=int, default=256)
     p.add_argument("--max_steps", type=int, default=0, help="stop each epoch after this many steps (0 = all)")

@@ -100,10 +100,35 @@ class Trainer:
         a = self.args
         e = self.engine
         self.maybe_resume()
-        train_loader, sampler = make_loader(train_ds, a.batch_size, a.num_workers, e.dp_world, e.dp_rank,
-                                            True, a.seed, self.device)
-        val_loader, _ = make_loader(val_ds, a.batch_size, min(a.num_workers, 2), e.dp_world, e.dp_rank,
-                                    False, a.seed, self.device)
+        if getattr(a, "data_path", None):
+            # pre-tokenised corpus through the native mmap loader (runtime/csrc/runtime.cpp)
+            from itertools import islice
+
+            from ..runtime import NativeBatchLoader, TokenFile
+
+            tf = TokenFile(a.data_path, a.token_bytes)
+            steps = a.max_steps or max(1, a.train_samples // (a.batch_size * e.dp_world))
+            tl = NativeBatchLoader(tf, a.batch_size, a.sequence_length, a.seed, e.dp_rank, e.dp_world)
+            vl = NativeBatchLoader(tf, a.batch_size, a.sequence_length, a.seed + 7919, e.dp_rank, e.dp_world)
+            vsteps = a.eval_steps or max(1, a.val_samples // (a.batch_size * e.dp_world))
+
+            class _Epoch:
+                def __init__(self, it, n):
+                    self.it, self.n = it, n
+
+                def __iter__(self):
+                    return islice(self.it, self.n)
+
+                def __len__(self):
+                    return self.n
+
+            train_loader, sampler = _Epoch(tl, steps), None
+            val_loader = _Epoch(vl, vsteps)
+        else:
+            train_loader, sampler = make_loader(train_ds, a.batch_size, a.num_workers, e.dp_world, e.dp_rank,
+                                                True, a.seed, self.device)
+            val_loader, _ = make_loader(val_ds, a.batch_size, min(a.num_workers, 2), e.dp_world, e.dp_rank,
+                                        False, a.seed, self.device)
         for ei in range(self.start_epoch, a.epochs):
             if sampler is not None:
                 sampler.set_epoch(ei)

@@ -53,6 +53,27 @@ class FlatAdamW:
             )
             _lib.call("dpc_adamw", args, p.device)
             return
+        if p.device.type == "cpu" and grad_scale_t is None and g.device.type == "cpu":
+            # host path (FSDP --cpu_offload): one fused native pass (runtime/csrc/runtime.cpp)
+            try:
+                from .. import runtime
+
+                host_shadow = None
+                bf16_shadow = self.shadow is not None and self.shadow.dtype == torch.bfloat16
+                if bf16_shadow:
+                    if getattr(self, "_host_shadow", None) is None:
+                        self._host_shadow = torch.empty(p.numel(), dtype=torch.bfloat16,
+                                                        pin_memory=torch.cuda.is_available())
+                    host_shadow = self._host_shadow
+                runtime.adamw_host(p, g, self.exp_avg, self.exp_avg_sq, self.lr, b1, b2, self.eps,
+                                   self.weight_decay, self.step_count, grad_scale, host_shadow)
+                if bf16_shadow:
+                    self.shadow.copy_(host_shadow, non_blocking=True)
+                elif self.shadow is not None:
+                    self.shadow.copy_(p, non_blocking=True)
+                return
+            except (ImportError, OSError, RuntimeError):
+                pass
         gs = g * grad_scale
         if grad_scale_t is not None:
             gs = gs * grad_scale_t

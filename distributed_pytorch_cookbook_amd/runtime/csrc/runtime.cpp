@@ -185,9 +185,20 @@ API void dpc_loader_destroy(void* h) {
 // uniform noise), drawn from a counter-based generator so any row is reproducible alone.
 API void dpc_synth_markov(int64_t* out, int64_t rows, int S, int vocab, uint64_t seed, int branching,
                           int64_t row0) {
-  std::vector<int32_t> succ((size_t)vocab * branching);
-  uint64_t ts = 1234567;
-  for (auto& v : succ) v = (int32_t)(splitmix64(ts) % (uint64_t)vocab);
+  static std::mutex table_mu;
+  static std::vector<int32_t> table;
+  static int t_vocab = -1, t_branch = -1;
+  {
+    std::lock_guard<std::mutex> lk(table_mu);
+    if (t_vocab != vocab || t_branch != branching) {
+      table.assign((size_t)vocab * branching, 0);
+      uint64_t ts = 1234567;
+      for (auto& v : table) v = (int32_t)(splitmix64(ts) % (uint64_t)vocab);
+      t_vocab = vocab;
+      t_branch = branching;
+    }
+  }
+  const std::vector<int32_t>& succ = table;
 #pragma omp parallel for schedule(static)
   for (int64_t r = 0; r < rows; ++r) {
     uint64_t st = seed * 1000003ULL + (uint64_t)(row0 + r) * 0x9E3779B97F4A7C15ULL;

@@ -20,6 +20,16 @@ from torch.utils.data import Dataset
 from .tokenizer import GPT2_VOCAB, ByteTokenizer
 
 
+def _native_markov(i, seq_len, vocab, seed, branching):
+    """Row i of the Markov corpus from the C++ runtime (None if it is unavailable)."""
+    try:
+        from ..runtime import synth_markov
+
+        return synth_markov(1, seq_len, vocab, seed, branching, row0=int(i))[0]
+    except Exception:
+        return None
+
+
 class SyntheticTokenDataset(Dataset):
     """``n`` rows of ``seq_len`` tokens; row i is a pure function of (seed, i)."""
 
@@ -41,6 +51,10 @@ class SyntheticTokenDataset(Dataset):
         return self._succ_cache
 
     def __getitem__(self, i):
+        if self.pad_fraction == 0 and self.vocab > 0:
+            ids = _native_markov(i, self.seq_len, self.vocab, self.seed, self.branching)
+            if ids is not None:
+                return {"input_ids": ids, "attention_mask": torch.ones(self.seq_len, dtype=torch.long)}
         g = torch.Generator().manual_seed(self.seed * 1_000_003 + int(i))
         S = self.seq_len
         choice = torch.randint(0, self.branching, (S,), generator=g).tolist()
@@ -82,7 +96,10 @@ def get_tokenizer(name: str = "roneneldan/TinyStories-1M", max_length: int = 512
         try:
             from transformers import GPT2Tokenizer
 
-            return GPT2Tokenizer.from_pretrained(name, model_max_length=max_length, local_files_only=True)
+            tok = GPT2Tokenizer.from_pretrained(name, model_max_length=max_length, local_files_only=True)
+            if tok.vocab_size < 256:  # an empty stand-in (no vocab files cached)
+                raise OSError("tokenizer files not available offline")
+            return tok
         except Exception:
             if offline_stub is False:
                 raise

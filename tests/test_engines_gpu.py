@@ -1,0 +1,56 @@
+"""Every engine runs on one MI355X (world 1) and agrees with the data-parallel engine."""
+import pytest
+import torch
+
+from distributed_pytorch_cookbook_amd.engine.data_parallel import DataParallelEngine
+from distributed_pytorch_cookbook_amd.engine.fsdp import FSDPEngine
+from distributed_pytorch_cookbook_amd.engine.pipeline import PipelineEngine
+from distributed_pytorch_cookbook_amd.models.gpt import TransformerDecoderLM
+
+pytestmark = pytest.mark.gpu
+
+
+def make():
+    torch.manual_seed(0)
+    with torch.device("cuda"):
+        return TransformerDecoderLM(dim=256, head_dim=64, heads=4, num_layers=3, vocab_size=4000,
+                                    max_position_embeddings=128, activation="gelu")
+
+
+def batch(step):
+    g = torch.Generator(device="cpu").manual_seed(step)
+    ids = torch.randint(0, 4000, (8, 128), generator=g).cuda()
+    pos = torch.arange(127, device="cuda").expand(8, -1)
+    return dict(input_ids=ids[:, :-1], position_ids=pos, mask=None), ids[:, 1:]
+
+
+def run(eng, steps=3):
+    losses = [float(eng.train_step(*batch(s))) for s in range(steps)]
+    return losses, {k: v.float().cpu() for k, v in eng.full_state_dict().items()}
+
+
+@pytest.fixture(scope="module")
+def ref():
+    return run(DataParallelEngine(make(), "cuda", lr=1e-3))
+
+
+def close(sd_a, sd_b, tol=2e-2):
+    for k in sd_b:
+        err = ((sd_a[k] - sd_b[k]).norm() / sd_b[k].norm().clamp_min(1e-6)).item()
+        assert err < tol, (k, err)
+
+
+@pytest.mark.parametrize("offload", [False, True])
+def test_fsdp_single_gpu(ref, offload):
+    losses, sd = run(FSDPEngine(make(), "cuda", lr=1e-3, cpu_offload=offload))
+    assert abs(losses[-1] - ref[0][-1]) < 5e-2
+    close(sd, ref[1])
+
+
+@pytest.mark.parametrize("schedule", ["1f1b", "gpipe"])
+def test_pipeline_single_stage_microbatched(ref, schedule):
+    eng = PipelineEngine(make(), "cuda", lr=1e-3, pp=1, dp=1, num_microbatches=4, schedule=schedule,
+                         seq_len=127)
+    losses, sd = run(eng)
+    assert abs(losses[-1] - ref[0][-1]) < 5e-2
+    close(sd, ref[1])
