@@ -259,8 +259,8 @@ __device__ __forceinline__ void issue_tile(__amdgpu_buffer_rsrc_t rs, const int 
 }
 
 template <int STAGES, bool AK, bool BK>
-__global__ __launch_bounds__(NT, (STAGES == 2 ? 2 : 1)) void gemm2_kernel(GemmArgs p, unsigned a_bytes,
-                                                                       unsigned b_bytes) {
+__global__ __launch_bounds__(NT, (STAGES == 2 ? 2 : 1)) void gemm2_kernel(GemmArgs p, unsigned long long a_bytes,
+                                                                       unsigned long long b_bytes) {
   __shared__ __attribute__((aligned(16))) bf16_t smem[STAGES * 2 * TILE_ELEMS];
   const int tiles_m = (p.M + BM - 1) / BM, tiles_n = (p.N + BN - 1) / BN;
   const int nwg = tiles_m * tiles_n;
@@ -280,33 +280,40 @@ __global__ __launch_bounds__(NT, (STAGES == 2 ? 2 : 1)) void gemm2_kernel(GemmAr
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int wr = wid >> 1, wc = wid & 1;
 
-  const __amdgpu_buffer_rsrc_t rsa = __builtin_amdgcn_make_buffer_rsrc((void*)p.A, 0, a_bytes, 0x00020000);
-  const __amdgpu_buffer_rsrc_t rsb = __builtin_amdgcn_make_buffer_rsrc((void*)p.B, 0, b_bytes, 0x00020000);
-
-  // per-lane source byte offsets (k-tile 0); the k advance goes into the scalar soffset
+  // Per-lane source byte offsets relative to the tile origin of the current k-tile.  The
+  // descriptor base itself moves (64-bit scalar math) with the tile origin and k, so the
+  // 32-bit voffsets stay small for operands of any size, and num_records = bytes left in the
+  // operand makes every out-of-range lane read zeros.
   int va[4], vb[4];
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const int j = wid * 4 + i;
     if (AK) {
       const int row = 8 * j + (lane >> 3), pos = lane & 7, c = pos ^ ((row >> 1) & 7);
-      va[i] = (int)(((long long)(m0 + row) * p.lda + c * 8) * 2);
+      va[i] = (int)(((long long)row * p.lda + c * 8) * 2);
     } else {
       const int kr = 4 * j + (lane >> 4), pos = lane & 15;
       const int c = (((pos >> 1) ^ mn_swz(kr)) << 1) | (pos & 1);
-      va[i] = (int)(((long long)kr * p.lda + m0 + c * 8) * 2);
+      va[i] = (int)(((long long)kr * p.lda + c * 8) * 2);
     }
     if (BK) {
       const int row = 8 * j + (lane >> 3), pos = lane & 7, c = pos ^ ((row >> 1) & 7);
-      vb[i] = (int)(((long long)(n0 + row) * p.ldb + c * 8) * 2);
+      vb[i] = (int)(((long long)row * p.ldb + c * 8) * 2);
     } else {
       const int kr = 4 * j + (lane >> 4), pos = lane & 15;
       const int c = (((pos >> 1) ^ mn_swz(kr)) << 1) | (pos & 1);
-      vb[i] = (int)(((long long)kr * p.ldb + n0 + c * 8) * 2);
+      vb[i] = (int)(((long long)kr * p.ldb + c * 8) * 2);
     }
   }
-  const unsigned sa_step = AK ? BKT * 2u : (unsigned)(BKT * p.lda * 2);
-  const unsigned sb_step = BK ? BKT * 2u : (unsigned)(BKT * p.ldb * 2);
+  const unsigned long long a_org = AK ? (unsigned long long)m0 * p.lda * 2 : (unsigned long long)m0 * 2;
+  const unsigned long long b_org = BK ? (unsigned long long)n0 * p.ldb * 2 : (unsigned long long)n0 * 2;
+  const unsigned long long a_step = AK ? BKT * 2ull : (unsigned long long)BKT * p.lda * 2;
+  const unsigned long long b_step = BK ? BKT * 2ull : (unsigned long long)BKT * p.ldb * 2;
+  auto rsrc = [](const void* base, unsigned long long total, unsigned long long off) {
+    const unsigned long long left = off < total ? total - off : 0ull;
+    const unsigned nrec = left > 0xffffffffull ? 0xffffffffu : (unsigned)left;
+    return __builtin_amdgcn_make_buffer_rsrc((void*)((const char*)base + off), 0, nrec, 0x00020000);
+  };
 
   floatx4 acc[4][4];
 #pragma unroll
@@ -323,9 +330,9 @@ __global__ __launch_bounds__(NT, (STAGES == 2 ? 2 : 1)) void gemm2_kernel(GemmAr
   const int nk = max(0, min(nk_all, kt0 + per) - kt0);
   auto issue = [&](int it) {
     bf16_t* base = smem + (it % STAGES) * 2 * TILE_ELEMS;
-    const unsigned kt = (unsigned)(kt0 + it);
-    issue_tile<AK>(rsa, va, sa_step * kt, base, wid);
-    issue_tile<BK>(rsb, vb, sb_step * kt, base + TILE_ELEMS, wid);
+    const unsigned long long kt = (unsigned long long)(kt0 + it);
+    issue_tile<AK>(rsrc(p.A, a_bytes, a_org + a_step * kt), va, 0u, base, wid);
+    issue_tile<BK>(rsrc(p.B, b_bytes, b_org + b_step * kt), vb, 0u, base + TILE_ELEMS, wid);
   };
 #pragma unroll
   for (int s = 0; s < STAGES - 1; ++s)
@@ -452,7 +459,8 @@ static inline long long operand_bytes(long long rows, long long cols, long long 
 }
 
 template <int STAGES>
-static void launch_v2(const GemmArgs* a, dim3 grid, hipStream_t stream, unsigned ab, unsigned bb) {
+static void launch_v2(const GemmArgs* a, dim3 grid, hipStream_t stream, unsigned long long ab,
+                      unsigned long long bb) {
   if (a->a_kmaj && a->b_kmaj) hipLaunchKernelGGL((gemm2_kernel<STAGES, true, true>), grid, dim3(NT), 0, stream, *a, ab, bb);
   else if (a->a_kmaj) hipLaunchKernelGGL((gemm2_kernel<STAGES, true, false>), grid, dim3(NT), 0, stream, *a, ab, bb);
   else if (!a->b_kmaj) hipLaunchKernelGGL((gemm2_kernel<STAGES, false, false>), grid, dim3(NT), 0, stream, *a, ab, bb);
@@ -476,8 +484,7 @@ DPC_API int dpc_gemm(const GemmArgs* a, hipStream_t stream) {
   const long long bb = operand_bytes(a->b_r, a->b_c, a->ldb);
   const bool kmaj_ok = (!a->a_kmaj || (a->a_c == a->K && a->K % BKT == 0)) &&
                        (!a->b_kmaj || (a->b_c == a->K && a->K % BKT == 0));
-  const bool v2_ok = kmaj_ok && a->N % 4 == 0 && ab > 0 && bb > 0 && ab < 0x7fffffffLL &&
-                     bb < 0x7fffffffLL && a->K > 0 && a->ldc % 4 == 0 && a->ldr % 4 == 0 &&
+  const bool v2_ok = kmaj_ok && a->N % 4 == 0 && ab > 0 && bb > 0 && a->K > 0 && a->ldc % 4 == 0 && a->ldr % 4 == 0 &&
                      a->ld_aux_in % 4 == 0 && a->ld_aux_out % 4 == 0 &&
                      al(a->C, a->out_f32 ? 16 : 8) && al(a->bias, 16) && al(a->residual, 16) &&
                      al(a->aux_in, 8) && al(a->aux_out, 8) && al(a->colsum, 4);
@@ -496,8 +503,8 @@ DPC_API int dpc_gemm(const GemmArgs* a, hipStream_t stream) {
     if (splits > 1 && !a->accumulate)
       hipMemset2DAsync(a->C, (size_t)a->ldc * 4, 0, (size_t)a->N * 4, (size_t)a->M, stream);
     grid.y = splits;
-    if (impl == 2) launch_v2<2>(a, grid, stream, (unsigned)ab, (unsigned)bb);
-    else launch_v2<3>(a, grid, stream, (unsigned)ab, (unsigned)bb);
+    if (impl == 2) launch_v2<2>(a, grid, stream, ab, bb);
+    else launch_v2<3>(a, grid, stream, ab, bb);
     return (int)hipGetLastError();
   }
   if (a->a_kmaj && a->b_kmaj) hipLaunchKernelGGL((gemm_kernel<true, true>), grid, block, 0, stream, *a);

@@ -34,9 +34,12 @@ def ref():
     return run(DataParallelEngine(make(), "cuda", lr=1e-3))
 
 
-def close(sd_a, sd_b, tol=2e-2):
+def close(sd_a, sd_b, tol=2e-2, lr=1e-3, steps=3):
+    # Adam moves every element by ~lr per step whatever its gradient's size, so for tensors
+    # that start at 0 (biases) compare against the size of that motion, not their norm
     for k in sd_b:
-        err = ((sd_a[k] - sd_b[k]).norm() / sd_b[k].norm().clamp_min(1e-6)).item()
+        scale = max(sd_b[k].norm().item(), lr * steps * sd_b[k].numel() ** 0.5)
+        err = (sd_a[k] - sd_b[k]).norm().item() / scale
         assert err < tol, (k, err)
 
 
