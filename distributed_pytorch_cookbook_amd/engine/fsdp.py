@@ -35,6 +35,7 @@ class FSDPEngine(Engine):
         st = self.store
         grad = st.grads_host if st.cpu_offload else st.grads
         self.opt = FlatAdamW(st.master, grad, lr=lr, shadow=st.shadow)
+        self.opt_rep = FlatAdamW(st.rep_master, st.rep_grads, lr=lr)  # replicated 1-D params
 
     def train_step(self, batch, targets):
         st = self.store
@@ -45,6 +46,7 @@ class FSDPEngine(Engine):
         if st.cpu_offload:
             torch.cuda.current_stream().synchronize()  # grads_host D2H landed
         self.opt.step(grad_scale=1.0 / self.dp_world)
+        self.opt_rep.step(grad_scale=1.0 / self.dp_world)
         return out.loss.detach()
 
     @torch.no_grad()
@@ -64,17 +66,18 @@ class FSDPEngine(Engine):
 
     def train_state(self):
         st = self.store
-        m = st.gather_full(self.opt.exp_avg, dst_rank=0)
-        v = st.gather_full(self.opt.exp_avg_sq, dst_rank=0)
+        m = st.gather_full(self.opt.exp_avg, dst_rank=0, rep_flat=self.opt_rep.exp_avg)
+        v = st.gather_full(self.opt.exp_avg_sq, dst_rank=0, rep_flat=self.opt_rep.exp_avg_sq)
         return {"optimizer": {"step": self.opt.step_count, "exp_avg": m, "exp_avg_sq": v,
                               "format": "canonical"}}
 
     def load_train_state(self, st):
         o = st["optimizer"]
         self.opt.step_count = int(o["step"])
+        self.opt_rep.step_count = int(o["step"])
         if isinstance(o.get("exp_avg"), dict):
-            self.store.load_full(o["exp_avg"], self.opt.exp_avg)
-            self.store.load_full(o["exp_avg_sq"], self.opt.exp_avg_sq)
+            self.store.load_full(o["exp_avg"], self.opt.exp_avg, rep_flat=self.opt_rep.exp_avg)
+            self.store.load_full(o["exp_avg_sq"], self.opt.exp_avg_sq, rep_flat=self.opt_rep.exp_avg_sq)
 
     @property
     def step_count(self):

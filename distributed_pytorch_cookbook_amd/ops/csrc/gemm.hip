@@ -248,20 +248,78 @@ __global__ __launch_bounds__(NT, 2) void gemm_kernel(GemmArgs p) {
 // =====================================================================================
 typedef __attribute__((address_space(3))) void* lds_void_t;
 
-template <bool KMAJ>
-__device__ __forceinline__ void issue_tile(__amdgpu_buffer_rsrc_t rs, const int (&voff)[4], unsigned soff,
-                                           bf16_t* lds_tile, int wave) {
+// ---- v2 geometry, templated on the k-depth KB of a stage (64 or 32)
+template <int KB>
+__device__ __forceinline__ int swz_k(int row) {  // 16-B chunk swizzle of a k-major [row][KB] tile
+  if (KB == 64) return (row >> 1) & 7;
+  const int q = (row >> 2) & 3;  // KB == 32: 4 chunks per 64-B row, 4 rows per bank row
+  return (0x1320 >> (q * 4)) & 3;  // {0, 2, 3, 1}[q]
+}
+template <int KB>
+__device__ __forceinline__ int kmaj_off_k(int row, int chunk) {
+  return row * KB + ((chunk ^ swz_k<KB>(row)) << 3);
+}
+
+template <int KB, bool KMAJ>
+__device__ __forceinline__ bf16x8 frag_k(const bf16_t* lds, int r0, int kstep, int lane) {
+  if (KMAJ) {
+    const int row = r0 + (lane & 15);
+    const int chunk = kstep * 4 + (lane >> 4);
+    return *reinterpret_cast<const bf16x8*>(lds + kmaj_off_k<KB>(row, chunk));
+  }
+  return frag<false>(lds, r0, kstep, lane);  // [KB][128] mn-major image, 256-B rows
+}
+
+// per-thread DMA source offsets of one operand tile (relative to the tile origin)
+template <int KB, bool KMAJ>
+__device__ __forceinline__ void dma_offsets(int (&v)[KB / 16], long long ld, int wid, int lane) {
+  constexpr int NL = KB / 16;  // 1-KiB wave-instructions per wave per operand tile
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int j = wave * 4 + i;  // wave-instruction index: 1 KiB of the 16 KiB tile
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void_t)(lds_tile + j * 512), 16, voff[i], soff, 0, 0);
+  for (int i = 0; i < NL; ++i) {
+    const int j = wid * NL + i;
+    if (KMAJ) {
+      constexpr int LPR = KB / 8;       // lanes per row (16 B each)
+      constexpr int RPI = 64 / LPR;     // rows per wave-instruction
+      const int row = RPI * j + lane / LPR, pos = lane % LPR, c = pos ^ swz_k<KB>(row);
+      v[i] = (int)(((long long)row * ld + c * 8) * 2);
+    } else {
+      const int kr = 4 * j + (lane >> 4), pos = lane & 15;
+      const int c = (((pos >> 1) ^ mn_swz(kr)) << 1) | (pos & 1);
+      v[i] = (int)(((long long)kr * ld + c * 8) * 2);
+    }
   }
 }
 
-template <int STAGES, bool AK, bool BK>
-__global__ __launch_bounds__(NT, (STAGES == 2 ? 2 : 1)) void gemm2_kernel(GemmArgs p, unsigned long long a_bytes,
-                                                                       unsigned long long b_bytes) {
-  __shared__ __attribute__((aligned(16))) bf16_t smem[STAGES * 2 * TILE_ELEMS];
+template <int NL>
+__device__ __forceinline__ void issue_tile(__amdgpu_buffer_rsrc_t rs, const int (&voff)[NL], bf16_t* lds_tile,
+                                           int wave) {
+#pragma unroll
+  for (int i = 0; i < NL; ++i) {
+    const int j = wave * NL + i;  // wave-instruction index: 1 KiB of the tile
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void_t)(lds_tile + j * 512), 16, voff[i], 0, 0, 0);
+  }
+}
+
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+template <int KB, int STAGES>
+struct V2Cfg {
+  static constexpr int TILE = BM * KB;                  // bf16 elements per operand per stage
+  static constexpr int PIPE = STAGES * 2 * TILE;        // pipeline ring (elements)
+  static constexpr int EPI = 4 * 32 * 64 * 2;           // epilogue: 4 waves x [32][64] f32 (as bf16 units)
+  static constexpr int SMEM = PIPE > EPI ? PIPE : EPI;
+  static constexpr int WGS = (160 * 1024) / (SMEM * 2) > 4 ? 4 : (160 * 1024) / (SMEM * 2);
+};
+
+template <int KB, int STAGES, bool AK, bool BK>
+__global__ __launch_bounds__(NT, (V2Cfg<KB, STAGES>::WGS)) void gemm2_kernel(GemmArgs p, unsigned long long a_bytes,
+                                                                          unsigned long long b_bytes) {
+  using Cfg = V2Cfg<KB, STAGES>;
+  constexpr int NL = KB / 16;
+  __shared__ __attribute__((aligned(16))) bf16_t smem[Cfg::SMEM];
   const int tiles_m = (p.M + BM - 1) / BM, tiles_n = (p.N + BN - 1) / BN;
   const int nwg = tiles_m * tiles_n;
   int bid = blockIdx.x;
@@ -284,31 +342,13 @@ __global__ __launch_bounds__(NT, (STAGES == 2 ? 2 : 1)) void gemm2_kernel(GemmAr
   // descriptor base itself moves (64-bit scalar math) with the tile origin and k, so the
   // 32-bit voffsets stay small for operands of any size, and num_records = bytes left in the
   // operand makes every out-of-range lane read zeros.
-  int va[4], vb[4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int j = wid * 4 + i;
-    if (AK) {
-      const int row = 8 * j + (lane >> 3), pos = lane & 7, c = pos ^ ((row >> 1) & 7);
-      va[i] = (int)(((long long)row * p.lda + c * 8) * 2);
-    } else {
-      const int kr = 4 * j + (lane >> 4), pos = lane & 15;
-      const int c = (((pos >> 1) ^ mn_swz(kr)) << 1) | (pos & 1);
-      va[i] = (int)(((long long)kr * p.lda + c * 8) * 2);
-    }
-    if (BK) {
-      const int row = 8 * j + (lane >> 3), pos = lane & 7, c = pos ^ ((row >> 1) & 7);
-      vb[i] = (int)(((long long)row * p.ldb + c * 8) * 2);
-    } else {
-      const int kr = 4 * j + (lane >> 4), pos = lane & 15;
-      const int c = (((pos >> 1) ^ mn_swz(kr)) << 1) | (pos & 1);
-      vb[i] = (int)(((long long)kr * p.ldb + c * 8) * 2);
-    }
-  }
+  int va[NL], vb[NL];
+  dma_offsets<KB, AK>(va, p.lda, wid, lane);
+  dma_offsets<KB, BK>(vb, p.ldb, wid, lane);
   const unsigned long long a_org = AK ? (unsigned long long)m0 * p.lda * 2 : (unsigned long long)m0 * 2;
   const unsigned long long b_org = BK ? (unsigned long long)n0 * p.ldb * 2 : (unsigned long long)n0 * 2;
-  const unsigned long long a_step = AK ? BKT * 2ull : (unsigned long long)BKT * p.lda * 2;
-  const unsigned long long b_step = BK ? BKT * 2ull : (unsigned long long)BKT * p.ldb * 2;
+  const unsigned long long a_step = AK ? KB * 2ull : (unsigned long long)KB * p.lda * 2;
+  const unsigned long long b_step = BK ? KB * 2ull : (unsigned long long)KB * p.ldb * 2;
   auto rsrc = [](const void* base, unsigned long long total, unsigned long long off) {
     const unsigned long long left = off < total ? total - off : 0ull;
     const unsigned nrec = left > 0xffffffffull ? 0xffffffffu : (unsigned)left;
@@ -323,37 +363,40 @@ __global__ __launch_bounds__(NT, (STAGES == 2 ? 2 : 1)) void gemm2_kernel(GemmAr
 
   // split-K: blockIdx.y owns a contiguous run of k-tiles (the host only splits plain
   // f32-accumulating products, whose partial tiles are combined with f32 atomics)
-  const int nk_all = (p.K + BKT - 1) / BKT;
+  const int nk_all = (p.K + KB - 1) / KB;
   const int splits = gridDim.y;
   const int per = (nk_all + splits - 1) / splits;
   const int kt0 = blockIdx.y * per;
   const int nk = max(0, min(nk_all, kt0 + per) - kt0);
   auto issue = [&](int it) {
-    bf16_t* base = smem + (it % STAGES) * 2 * TILE_ELEMS;
+    bf16_t* base = smem + (it % STAGES) * 2 * Cfg::TILE;
     const unsigned long long kt = (unsigned long long)(kt0 + it);
-    issue_tile<AK>(rsrc(p.A, a_bytes, a_org + a_step * kt), va, 0u, base, wid);
-    issue_tile<BK>(rsrc(p.B, b_bytes, b_org + b_step * kt), vb, 0u, base + TILE_ELEMS, wid);
+    issue_tile<NL>(rsrc(p.A, a_bytes, a_org + a_step * kt), va, base, wid);
+    issue_tile<NL>(rsrc(p.B, b_bytes, b_org + b_step * kt), vb, base + Cfg::TILE, wid);
   };
 #pragma unroll
   for (int s = 0; s < STAGES - 1; ++s)
     if (s < nk) issue(s);
 
   for (int kt = 0; kt < nk; ++kt) {
-    // tile kt landed for THIS wave: allow the younger tiles' 8 loads each to stay in flight
-    if (STAGES >= 3 && kt + 1 < nk) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    // tile kt landed for THIS wave: the tiles issued after it (at most STAGES-2, fewer at the
+    // tail) may stay in flight -- 2*NL loads each
+    const int after = min(STAGES - 2, nk - 1 - kt);
+    if (STAGES >= 4 && after >= 2) wait_vm<(STAGES >= 4 ? 4 * NL : 0)>();
+    else if (STAGES >= 3 && after >= 1) wait_vm<(STAGES >= 3 ? 2 * NL : 0)>();
+    else wait_vm<0>();
     __builtin_amdgcn_s_barrier();  // ... and for every wave; also: all waves finished tile kt-1
     asm volatile("" ::: "memory");
     if (kt + STAGES - 1 < nk) issue(kt + STAGES - 1);
-    const bf16_t* la = smem + (kt % STAGES) * 2 * TILE_ELEMS;
-    const bf16_t* lb = la + TILE_ELEMS;
+    const bf16_t* la = smem + (kt % STAGES) * 2 * Cfg::TILE;
+    const bf16_t* lb = la + Cfg::TILE;
 #pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
+    for (int ks = 0; ks < KB / 32; ++ks) {
       bf16x8 fa[4], fb[4];
 #pragma unroll
-      for (int i = 0; i < 4; ++i) fa[i] = frag<AK>(la, wr * 64 + i * 16, ks, lane);
+      for (int i = 0; i < 4; ++i) fa[i] = frag_k<KB, AK>(la, wr * 64 + i * 16, ks, lane);
 #pragma unroll
-      for (int j = 0; j < 4; ++j) fb[j] = frag<BK>(lb, wc * 64 + j * 16, ks, lane);
+      for (int j = 0; j < 4; ++j) fb[j] = frag_k<KB, BK>(lb, wc * 64 + j * 16, ks, lane);
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -362,23 +405,12 @@ __global__ __launch_bounds__(NT, (STAGES == 2 ? 2 : 1)) void gemm2_kernel(GemmAr
     }
   }
 
-  // ---------------- epilogue through LDS: wave tile 64x64 f32, columns swizzled by row group
+  // ---------------- epilogue through LDS, two passes of 32 rows per wave: the f32 tile is
+  // re-read row-contiguously so bias / residual / aux / C move 16 B per lane
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  float* ct = reinterpret_cast<float*>(smem) + wid * 64 * 64;
   float alpha = p.alpha;
   if (p.alpha_ptr) alpha *= *p.alpha_ptr;
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int row = i * 16 + (lane >> 4) * 4 + r;
-        const int col = (j * 16 + (lane & 15)) ^ (((row >> 2) & 3) << 4);
-        ct[row * 64 + col] = acc[i][j][r] * alpha;
-      }
-  __syncthreads();
+  float* ct = reinterpret_cast<float*>(smem) + wid * 32 * 64;
   const int c4 = lane & 15;
   const int n = n0 + wc * 64 + c4 * 4;
   const bool nok = n < p.N;  // N % 4 == 0 is required by the host for v2
@@ -387,52 +419,67 @@ __global__ __launch_bounds__(NT, (STAGES == 2 ? 2 : 1)) void gemm2_kernel(GemmAr
   float cs[4] = {0.f, 0.f, 0.f, 0.f};
   const bf16_t* aux_in = static_cast<const bf16_t*>(p.aux_in);
   bf16_t* aux_out = static_cast<bf16_t*>(p.aux_out);
-#pragma unroll 4
-  for (int t = 0; t < 16; ++t) {
-    const int row = (lane >> 4) + 4 * t;
-    const int m = m0 + wr * 64 + row;
-    const int col = (c4 * 4) ^ (((row >> 2) & 3) << 4);
-    float4 v4 = *reinterpret_cast<const float4*>(ct + row * 64 + col);
-    if (m >= p.M || !nok) continue;
-    float v[4] = {v4.x + bias4.x, v4.y + bias4.y, v4.z + bias4.z, v4.w + bias4.w};
-    if (p.act_bwd) {
-      const uint2 z = *reinterpret_cast<const uint2*>(aux_in + (long long)m * p.ld_aux_in + n);
-      v[0] *= act_grad(__uint_as_float(z.x << 16), p.act_bwd);
-      v[1] *= act_grad(__uint_as_float(z.x & 0xffff0000u), p.act_bwd);
-      v[2] *= act_grad(__uint_as_float(z.y << 16), p.act_bwd);
-      v[3] *= act_grad(__uint_as_float(z.y & 0xffff0000u), p.act_bwd);
-    }
 #pragma unroll
-    for (int e = 0; e < 4; ++e) cs[e] += v[e];
-    if (aux_out) {
-      uint2 w;
-      w.x = pack2bf(v[0], v[1]);
-      w.y = pack2bf(v[2], v[3]);
-      *reinterpret_cast<uint2*>(aux_out + (long long)m * p.ld_aux_out + n) = w;
-    }
+  for (int h = 0; h < 2; ++h) {
+    __syncthreads();  // ring (h = 0) / previous pass (h = 1) fully consumed
 #pragma unroll
-    for (int e = 0; e < 4; ++e) v[e] = act_fwd(v[e], p.act);
-    if (p.residual) {
-      const float4 r4 = *reinterpret_cast<const float4*>(p.residual + (long long)m * p.ldr + n);
-      v[0] += r4.x; v[1] += r4.y; v[2] += r4.z; v[3] += r4.w;
-    }
-    const long long ci = (long long)m * p.ldc + n;
-    if (splits > 1) {  // partial sums of a split-K product (C pre-zeroed or accumulating)
-      float* C = static_cast<float*>(p.C) + ci;
+    for (int ii = 0; ii < 2; ++ii)
 #pragma unroll
-      for (int e = 0; e < 4; ++e) atomicAdd(C + e, v[e]);
-    } else if (p.out_f32) {
-      float4* C = reinterpret_cast<float4*>(static_cast<float*>(p.C) + ci);
-      if (p.accumulate) {
-        const float4 o = *C;
-        v[0] += o.x; v[1] += o.y; v[2] += o.z; v[3] += o.w;
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int row = ii * 16 + (lane >> 4) * 4 + r;
+          const int col = (j * 16 + (lane & 15)) ^ (((row >> 2) & 3) << 4);
+          ct[row * 64 + col] = acc[2 * h + ii][j][r] * alpha;
+        }
+    __syncthreads();
+#pragma unroll 2
+    for (int t = 0; t < 8; ++t) {
+      const int row = (lane >> 4) + 4 * t;
+      const int m = m0 + wr * 64 + h * 32 + row;
+      const int col = (c4 * 4) ^ (((row >> 2) & 3) << 4);
+      float4 v4 = *reinterpret_cast<const float4*>(ct + row * 64 + col);
+      if (m >= p.M || !nok) continue;
+      float v[4] = {v4.x + bias4.x, v4.y + bias4.y, v4.z + bias4.z, v4.w + bias4.w};
+      if (p.act_bwd) {
+        const uint2 z = *reinterpret_cast<const uint2*>(aux_in + (long long)m * p.ld_aux_in + n);
+        v[0] *= act_grad(__uint_as_float(z.x << 16), p.act_bwd);
+        v[1] *= act_grad(__uint_as_float(z.x & 0xffff0000u), p.act_bwd);
+        v[2] *= act_grad(__uint_as_float(z.y << 16), p.act_bwd);
+        v[3] *= act_grad(__uint_as_float(z.y & 0xffff0000u), p.act_bwd);
       }
-      *C = make_float4(v[0], v[1], v[2], v[3]);
-    } else {
-      uint2 w;
-      w.x = pack2bf(v[0], v[1]);
-      w.y = pack2bf(v[2], v[3]);
-      *reinterpret_cast<uint2*>(static_cast<bf16_t*>(p.C) + ci) = w;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) cs[e] += v[e];
+      if (aux_out) {
+        uint2 w;
+        w.x = pack2bf(v[0], v[1]);
+        w.y = pack2bf(v[2], v[3]);
+        *reinterpret_cast<uint2*>(aux_out + (long long)m * p.ld_aux_out + n) = w;
+      }
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[e] = act_fwd(v[e], p.act);
+      if (p.residual) {
+        const float4 r4 = *reinterpret_cast<const float4*>(p.residual + (long long)m * p.ldr + n);
+        v[0] += r4.x; v[1] += r4.y; v[2] += r4.z; v[3] += r4.w;
+      }
+      const long long ci = (long long)m * p.ldc + n;
+      if (splits > 1) {  // partial sums of a split-K product (C pre-zeroed or accumulating)
+        float* C = static_cast<float*>(p.C) + ci;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) atomicAdd(C + e, v[e]);
+      } else if (p.out_f32) {
+        float4* C = reinterpret_cast<float4*>(static_cast<float*>(p.C) + ci);
+        if (p.accumulate) {
+          const float4 o = *C;
+          v[0] += o.x; v[1] += o.y; v[2] += o.z; v[3] += o.w;
+        }
+        *C = make_float4(v[0], v[1], v[2], v[3]);
+      } else {
+        uint2 w;
+        w.x = pack2bf(v[0], v[1]);
+        w.y = pack2bf(v[2], v[3]);
+        *reinterpret_cast<uint2*>(static_cast<bf16_t*>(p.C) + ci) = w;
+      }
     }
   }
   if (p.colsum) {
@@ -458,16 +505,17 @@ static inline long long operand_bytes(long long rows, long long cols, long long 
   return ((rows - 1) * ld + ((cols + 7) / 8) * 8) * 2;
 }
 
-template <int STAGES>
+template <int KB, int STAGES>
 static void launch_v2(const GemmArgs* a, dim3 grid, hipStream_t stream, unsigned long long ab,
                       unsigned long long bb) {
-  if (a->a_kmaj && a->b_kmaj) hipLaunchKernelGGL((gemm2_kernel<STAGES, true, true>), grid, dim3(NT), 0, stream, *a, ab, bb);
-  else if (a->a_kmaj) hipLaunchKernelGGL((gemm2_kernel<STAGES, true, false>), grid, dim3(NT), 0, stream, *a, ab, bb);
-  else if (!a->b_kmaj) hipLaunchKernelGGL((gemm2_kernel<STAGES, false, false>), grid, dim3(NT), 0, stream, *a, ab, bb);
-  else hipLaunchKernelGGL((gemm2_kernel<STAGES, false, true>), grid, dim3(NT), 0, stream, *a, ab, bb);
+  if (a->a_kmaj && a->b_kmaj) hipLaunchKernelGGL((gemm2_kernel<KB, STAGES, true, true>), grid, dim3(NT), 0, stream, *a, ab, bb);
+  else if (a->a_kmaj) hipLaunchKernelGGL((gemm2_kernel<KB, STAGES, true, false>), grid, dim3(NT), 0, stream, *a, ab, bb);
+  else if (!a->b_kmaj) hipLaunchKernelGGL((gemm2_kernel<KB, STAGES, false, false>), grid, dim3(NT), 0, stream, *a, ab, bb);
+  else hipLaunchKernelGGL((gemm2_kernel<KB, STAGES, false, true>), grid, dim3(NT), 0, stream, *a, ab, bb);
 }
 
-static int g_gemm_impl = -1;  // -1: auto, 1: force v1, 2: force v2 (STAGES=2), 3: v2 STAGES=3
+// -1: auto; 1: v1; 2: v2 KB64 x2 stages; 3: KB64 x3; 4: KB32 x3; 5: KB32 x4
+static int g_gemm_impl = -1;
 
 DPC_API void dpc_gemm_set_impl(int impl) { g_gemm_impl = impl; }
 
@@ -482,8 +530,8 @@ DPC_API int dpc_gemm(const GemmArgs* a, hipStream_t stream) {
   // epilogue), every operand inside a 31-bit byte range.
   const long long ab = operand_bytes(a->a_r, a->a_c, a->lda);
   const long long bb = operand_bytes(a->b_r, a->b_c, a->ldb);
-  const bool kmaj_ok = (!a->a_kmaj || (a->a_c == a->K && a->K % BKT == 0)) &&
-                       (!a->b_kmaj || (a->b_c == a->K && a->K % BKT == 0));
+  const bool kmaj_ok = (!a->a_kmaj || (a->a_c == a->K && a->K % 64 == 0)) &&
+                       (!a->b_kmaj || (a->b_c == a->K && a->K % 64 == 0));
   const bool v2_ok = kmaj_ok && a->N % 4 == 0 && ab > 0 && bb > 0 && a->K > 0 && a->ldc % 4 == 0 && a->ldr % 4 == 0 &&
                      a->ld_aux_in % 4 == 0 && a->ld_aux_out % 4 == 0 &&
                      al(a->C, a->out_f32 ? 16 : 8) && al(a->bias, 16) && al(a->residual, 16) &&
@@ -503,8 +551,12 @@ DPC_API int dpc_gemm(const GemmArgs* a, hipStream_t stream) {
     if (splits > 1 && !a->accumulate)
       hipMemset2DAsync(a->C, (size_t)a->ldc * 4, 0, (size_t)a->N * 4, (size_t)a->M, stream);
     grid.y = splits;
-    if (impl == 2) launch_v2<2>(a, grid, stream, ab, bb);
-    else launch_v2<3>(a, grid, stream, ab, bb);
+    switch (impl) {
+      case 3: launch_v2<64, 3>(a, grid, stream, ab, bb); break;
+      case 4: launch_v2<32, 3>(a, grid, stream, ab, bb); break;
+      case 5: launch_v2<32, 4>(a, grid, stream, ab, bb); break;
+      default: launch_v2<64, 2>(a, grid, stream, ab, bb); break;
+    }
     return (int)hipGetLastError();
   }
   if (a->a_kmaj && a->b_kmaj) hipLaunchKernelGGL((gemm_kernel<true, true>), grid, block, 0, stream, *a);

@@ -66,6 +66,22 @@ class FSDPStore(ParamStore):
         self.grads = torch.zeros(total, dtype=torch.float32, device=self.device)
         self.grads_host = torch.zeros(total, dtype=torch.float32, pin_memory=True) if host else None
         self.shadow = torch.empty(total, dtype=self.compute_dtype, device=self.device)
+        # 1-D parameters (biases, LayerNorm affine: ~0.1% of the model) stay REPLICATED in f32
+        # like DDP parameters: the kernels read them in f32 (a bf16-gathered LayerNorm gain
+        # near 1.0 would round away every update smaller than 2^-8) and their gradients are
+        # all-reduced once per step in a single small collective.
+        self.rep = [e for e in self.layout.entries if len(e.shape) < 2]
+        self.rep_off = {}
+        off = 0
+        for e in self.rep:
+            self.rep_off[id(e.param)] = off
+            off += (e.numel + 63) // 64 * 64
+        self.rep_master = torch.zeros(max(off, 64), dtype=torch.float32, device=self.device)
+        self.rep_grads = torch.zeros_like(self.rep_master)
+        with torch.no_grad():
+            for e in self.rep:
+                o = self.rep_off[id(e.param)]
+                self.rep_master[o:o + e.numel].copy_(e.param.data.reshape(-1))
         # fill my shards from the (identically seeded) full parameters, then free them
         with torch.no_grad():
             for u in self.units:
@@ -128,20 +144,22 @@ class FSDPStore(ParamStore):
         self._full.pop(u, None)
         self._vec32.pop(u, None)
 
+    def _rep_view(self, flat, e):
+        o = self.rep_off[id(e.param)]
+        return flat[o:o + e.numel].view(e.shape)
+
     def weight(self, p):
         e = self.layout.by_param[id(p)]
+        if len(e.shape) < 2:
+            return self._rep_view(self.rep_master, e)
         buf = self._full[e.unit][0]
         lo = self.layout.unit_ranges[e.unit][0]
-        v = buf[e.offset - lo:e.offset - lo + e.numel].view(e.shape)
-        if p.dim() < 2 and v.dtype != torch.float32:
-            cache = self._vec32.setdefault(e.unit, {})
-            if id(p) not in cache:
-                cache[id(p)] = v.float()
-            return cache[id(p)]
-        return v
+        return buf[e.offset - lo:e.offset - lo + e.numel].view(e.shape)
 
     def grad(self, p):
         e = self.layout.by_param[id(p)]
+        if len(e.shape) < 2:
+            return self._rep_view(self.rep_grads, e)
         g = self._gfull[e.unit]
         lo = self.layout.unit_ranges[e.unit][0]
         return g[e.offset - lo:e.offset - lo + e.numel].view(e.shape)
@@ -186,10 +204,15 @@ class FSDPStore(ParamStore):
             self._rs[u] = (w, tmp, g)
 
     def finish_grads(self):
+        rep_w = None
+        if self.W > 1:
+            rep_w = comm.all_reduce(self.rep_grads, group=self.group, async_op=True)
         for u, (w, tmp, _) in sorted(self._rs.items()):
             w.wait()
             self.shard(self.grads, u).add_(tmp.float())
         self._rs.clear()
+        if rep_w is not None:
+            rep_w.wait()
         self._in_backward = False
         # anything still gathered from the forward (e.g. the head) is released now
         for u in list(self._full):
@@ -199,12 +222,15 @@ class FSDPStore(ParamStore):
 
     def zero_grad(self):
         self.grads.zero_()
+        self.rep_grads.zero_()
 
     # ------------------------------------------------------------------ full state
     @torch.no_grad()
-    def gather_full(self, flat_shards, dst_rank: int = 0, dtype=torch.float32):
+    def gather_full(self, flat_shards, dst_rank: int = 0, dtype=torch.float32, rep_flat=None):
         """Canonical {name: tensor} of a sharded flat f32 buffer (params or optimizer
-        moments), materialised on ``dst_rank`` (others return None).  Collective."""
+        moments), materialised on ``dst_rank`` (others return None).  Collective.
+        ``rep_flat``: the replicated buffer holding the 1-D entries (default: rep_master)."""
+        rep_flat = self.rep_master if rep_flat is None else rep_flat
         out = {} if self.rank == dst_rank else None
         for u in self.units:
             sh = self.shard(flat_shards, u).to(self.device)
@@ -216,12 +242,16 @@ class FSDPStore(ParamStore):
             if out is not None:
                 lo = self.layout.unit_ranges[u][0]
                 for e in self.layout.unit_entries(u):
-                    out[e.name] = full[e.offset - lo:e.offset - lo + e.numel].view(e.shape).to(
-                        "cpu", dtype=dtype, copy=True)
+                    src = (self._rep_view(rep_flat, e) if len(e.shape) < 2 else
+                           full[e.offset - lo:e.offset - lo + e.numel].view(e.shape))
+                    out[e.name] = src.to("cpu", dtype=dtype, copy=True)
         return out
 
     @torch.no_grad()
-    def load_full(self, sd: dict, flat_shards):
+    def load_full(self, sd: dict, flat_shards, rep_flat=None):
+        rep_flat = self.rep_master if rep_flat is None else rep_flat
+        for e in self.rep:
+            self._rep_view(rep_flat, e).copy_(sd[e.name].reshape(e.shape))
         for u in self.units:
             lo = self.layout.unit_ranges[u][0]
             mine0 = lo + self.rank * self.shard_len[u]

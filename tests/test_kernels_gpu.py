@@ -42,9 +42,10 @@ def test_gemm_layouts(a_kmaj, b_kmaj, M, N, K):
     assert rel_err(out, ref) < 2e-3
 
 
-@pytest.mark.parametrize("impl", [1, 2, 3])
+@pytest.mark.parametrize("impl", [1, 2, 3, 4, 5])
 @pytest.mark.parametrize("a_kmaj,b_kmaj", [(True, True), (True, False), (False, False), (False, True)])
-@pytest.mark.parametrize("M,N,K", [(256, 256, 128), (200, 296, 192), (1023, 768, 768), (77, 1000, 1023)])
+@pytest.mark.parametrize("M,N,K", [(256, 256, 128), (200, 296, 192), (1023, 768, 768), (77, 1000, 1023),
+                                   (130, 136, 4160)])
 def test_gemm_impls_with_epilogue(impl, a_kmaj, b_kmaj, M, N, K):
     torch.manual_seed(11)
     a = torch.randn(M, K, device=dev).bfloat16()
