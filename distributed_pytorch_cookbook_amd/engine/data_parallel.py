@@ -40,6 +40,7 @@ class DataParallelEngine(Engine):
         self.opt = FlatAdamW(self.store.master, self.store.grads, lr=lr, shadow=self.store.shadow)
         self.graph = graph and self.device.type == "cuda" and self.dp_world == 1
         self._graph = None
+        self._gkey = None
 
     # ------------------------------------------------------------------ training
     def _step_body(self, batch, targets):
@@ -57,7 +58,46 @@ class DataParallelEngine(Engine):
         return self._graph_step(batch, targets)
 
     def _graph_step(self, batch, targets):
-        raise NotImplementedError("HIP-graph step capture is not available yet")
+        """The whole step (memset of the grads, forward, backward, AdamW) as ONE HIP graph.
+
+        Call 1 for a given input signature runs eagerly (lazy init, allocator warm-up), call 2
+        captures the step into a graph against static input buffers and replays it, later
+        calls copy the batch into the static buffers and replay.  AdamW reads its step count
+        from a device counter, so replays apply the right bias corrections."""
+        mask = batch.get("mask")
+        key = (tuple(batch["input_ids"].shape), mask is None)
+        if self._graph is not None and key == self._gkey:
+            self._static["ids"].copy_(batch["input_ids"], non_blocking=True)
+            self._static["pos"].copy_(batch["position_ids"], non_blocking=True)
+            self._static["tg"].copy_(targets, non_blocking=True)
+            if mask is not None:
+                self._static["mask"].copy_(mask, non_blocking=True)
+            self._graph.replay()
+            self.opt.step_count += 1
+            return self._static_loss.clone()
+        if self._gkey != key:  # first call for this signature: eager (warm-up)
+            self._gkey = key
+            self._graph = None
+            return self._step_body(batch, targets)
+        st = {"ids": batch["input_ids"].clone(), "pos": batch["position_ids"].clone(),
+              "tg": targets.clone(), "mask": None if mask is None else mask.clone()}
+        self._static = st
+        self.opt.device_step = True
+        g = torch.cuda.CUDAGraph()
+        torch.cuda.synchronize()
+        try:
+            with torch.cuda.graph(g):
+                b = {"input_ids": st["ids"], "position_ids": st["pos"], "mask": st["mask"]}
+                self._static_loss = self._step_body(b, st["tg"])
+        except Exception as exc:  # capture not possible: stay eager
+            self.opt.device_step = False
+            self.graph = False
+            if self.is_logger:
+                print(f"[hip-graph] capture failed ({exc!r}); running eagerly")
+            return self._step_body(batch, targets)
+        self._graph = g
+        self._graph.replay()
+        return self._static_loss.clone()
 
     @torch.no_grad()
     def eval_step(self, batch, targets):

@@ -84,6 +84,7 @@ class AdamArgs(ctypes.Structure):
         ("lr", c_float), ("beta1", c_float), ("beta2", c_float), ("eps", c_float),
         ("weight_decay", c_float), ("bias_correction1", c_float),
         ("bias_correction2_sqrt", c_float), ("grad_scale", c_float),
+        ("step_ptr", P),
     ]
 
 
@@ -116,17 +117,24 @@ _FUNCS = {
 
 _lock = threading.Lock()
 _lib = None
+_error = None
 
 
 def lib() -> ctypes.CDLL:
     """Load (building if needed) the kernel library. Raises if it cannot be had."""
-    global _lib
+    global _lib, _error
     if _lib is not None:
         return _lib
+    if _error is not None:  # fail fast: do not re-run a failed build on every call
+        raise RuntimeError(f"kernel library unavailable: {_error}")
     with _lock:
         if _lib is None:
             if _build.needs_build():
-                _build.build()
+                try:
+                    _build.build()
+                except Exception as exc:
+                    _error = exc
+                    raise
             handle = ctypes.CDLL(str(_build.LIB_PATH), mode=ctypes.RTLD_GLOBAL)
             for name, st in _FUNCS.items():
                 fn = getattr(handle, name)

@@ -55,11 +55,24 @@ def _newest(paths) -> float:
     return max(p.stat().st_mtime for p in paths)
 
 
+HASH_PATH = LIB_PATH.with_suffix(".so.srchash")
+
+
+def source_hash() -> str:
+    """Content hash of the sources + flags (mtimes do not survive snapshot copies)."""
+    import hashlib
+
+    h = hashlib.sha256(" ".join(CFLAGS).encode())
+    for name in SOURCES + HEADERS:
+        h.update(name.encode())
+        h.update((CSRC / name).read_bytes())
+    return h.hexdigest()
+
+
 def needs_build() -> bool:
-    if not LIB_PATH.exists():
+    if not LIB_PATH.exists() or not HASH_PATH.exists():
         return True
-    srcs = [CSRC / s for s in SOURCES] + [CSRC / h for h in HEADERS]
-    return _newest(srcs) > LIB_PATH.stat().st_mtime
+    return HASH_PATH.read_text().strip() != source_hash()
 
 
 def _compile(src: Path, obj: Path, verbose: bool) -> None:
@@ -93,6 +106,7 @@ def build(force: bool = False, jobs: int = 4, verbose: bool = False) -> Path:
     if r.returncode != 0:
         raise RuntimeError(f"link failed:\n{r.stdout}\n{r.stderr}")
     os.replace(tmp, LIB_PATH)
+    HASH_PATH.write_text(source_hash() + "\n")
     return LIB_PATH
 
 

@@ -109,6 +109,16 @@ __device__ __forceinline__ bf16x8 acc_frag(const floatx16& x, int s) {
 
 __device__ __forceinline__ int acc_row(int r, int lane) { return (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5); }
 
+// raw v_exp_f32 (2^x): inputs here are <= 0 or -inf, no denormal range reduction needed
+__device__ __forceinline__ float fast_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
+
+// 64-key padding bitmask of the tile starting at key k0 (bit i = key k0+i is padded); wave-uniform
+__device__ __forceinline__ unsigned long long pad_bits(const unsigned char* pad, int k0, int S, int lane) {
+  if (!pad) return 0ull;
+  const int k = k0 + lane;
+  return __ballot(k < S && pad[k] != 0);
+}
+
 __device__ __forceinline__ bf16x8 load_row8(const bf16_t* p) {
   return *reinterpret_cast<const bf16x8*>(p);
 }
@@ -116,7 +126,7 @@ __device__ __forceinline__ bf16x8 load_row8(const bf16_t* p) {
 #define MFMA32(a, b, c) __builtin_amdgcn_mfma_f32_32x32x16_bf16((a), (b), (c), 0, 0, 0)
 
 // ------------------------------------------------------------------ forward
-__global__ __launch_bounds__(256) void attn_fwd_kernel(AttnArgs p) {
+__global__ __launch_bounds__(256, 2) void attn_fwd_kernel(AttnArgs p) {
   __shared__ __attribute__((aligned(16))) bf16_t smem[2 * 2 * KT * HD];  // [stage][K|V]
   const int S = p.S, H = p.H;
   const int nqb = (S + QB - 1) / QB;
@@ -173,30 +183,31 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(AttnArgs p) {
 #pragma unroll
         for (int st = 0; st < 4; ++st) s[kb] = MFMA32(row_frag(lk, kb * 32, st, lane), qf[st], s[kb]);
       }
-      const bool need_mask = (p.causal && kt0 + KT - 1 > q0) || (kt0 + KT > S) || pad;
+      const bool need_mask = (p.causal && kt0 + KT - 1 > q0) || (kt0 + KT > S) || pad;  // wave-uniform
       float mx = -INFINITY;
+      // branch-free: key > lim is causal / past-the-end, pm is the tile's padding bitmask
+      const unsigned long long pm = need_mask ? pad_bits(pad, kt0, S, lane) : 0ull;
+      const int lim = need_mask ? (p.causal ? min(q, S - 1) : S - 1) - kt0 : KT;
 #pragma unroll
       for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-          float v = s[kb][r] * c;
-          if (need_mask) {
-            const int key = kt0 + kb * 32 + acc_row(r, lane);
-            if (key >= S || (p.causal && key > q) || (pad && pad[key])) v = -INFINITY;
-          }
+          const int kl = kb * 32 + acc_row(r, lane);
+          const bool dead = kl > lim || ((pm >> kl) & 1ull);
+          const float v = dead ? -INFINITY : s[kb][r] * c;
           s[kb][r] = v;
           mx = fmaxf(mx, v);
         }
       mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
       const float mn = fmaxf(m, mx);
       const float mu = (mn == -INFINITY) ? 0.f : mn;
-      const float alpha = exp2f(m - mu);
+      const float alpha = fast_exp2(m - mu);
       float ls = 0.f;
 #pragma unroll
       for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-          const float e = exp2f(s[kb][r] - mu);
+          const float e = fast_exp2(s[kb][r] - mu);
           s[kb][r] = e;
           ls += e;
         }
@@ -270,9 +281,9 @@ __global__ __launch_bounds__(256) void attn_bwd_pre_kernel(AttnArgs p) {
 }
 
 // dK, dV: workgroup = 128 keys (4 waves x 32), sweep all queries >= first key.
-__global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(AttnArgs p) {
+__global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_kernel(AttnArgs p) {
   __shared__ __attribute__((aligned(16))) bf16_t smem[2 * 2 * KT * HD];  // [stage][Q|dO]
-  __shared__ float srow[2][2][KT];                                      // [stage][lse2|delta]
+  __shared__ __attribute__((aligned(16))) float srow[2][2][KT];                                    // [stage][lse2|delta]
   const int S = p.S, H = p.H;
   const int nkb = (S + QB - 1) / QB;
   const int kb = blockIdx.x;
@@ -347,15 +358,24 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(AttnArgs p) {
           sa = MFMA32(row_frag(lq, qs * 32, st, lane), kf[st], sa);
           dp = MFMA32(row_frag(ld, qs * 32, st, lane), vf[st], dp);
         }
-        // sa[r]: query qt0 + qs*32 + acc_row(r), key = lane's key
+        // sa[r]: query qt0 + qs*32 + acc_row(r), key = lane's key.  Rows 8g+4h..+3 are
+        // consecutive queries, so their (lse, delta) come in as one 16-B LDS read each.
+        const bool diag = p.causal && qt0 + qs * 32 < k0 + 32;  // wave-uniform: mask needed
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int qi = qs * 32 + acc_row(r, lane);
-          const int qq = qt0 + qi;
-          float pv = exp2f(sa[r] * c - srow[cur][0][qi]);
-          if (!key_ok || (p.causal && key > qq)) pv = 0.f;
-          sa[r] = pv;
-          dp[r] = pv * (dp[r] - srow[cur][1][qi]);
+        for (int g = 0; g < 4; ++g) {
+          const int qi0 = qs * 32 + 8 * g + 4 * hh;
+          const float4 l4 = *reinterpret_cast<const float4*>(&srow[cur][0][qi0]);
+          const float4 d4 = *reinterpret_cast<const float4*>(&srow[cur][1][qi0]);
+          const float lv[4] = {l4.x, l4.y, l4.z, l4.w}, dv[4] = {d4.x, d4.y, d4.z, d4.w};
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const int r = 4 * g + e;
+            float pv = fast_exp2(sa[r] * c - lv[e]);
+            if (diag) pv = (key > qt0 + qi0 + e) ? 0.f : pv;
+            pv = key_ok ? pv : 0.f;
+            sa[r] = pv;
+            dp[r] = pv * (dp[r] - dv[e]);
+          }
         }
 #pragma unroll
         for (int ss = 0; ss < 2; ++ss) {
@@ -393,7 +413,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(AttnArgs p) {
 }
 
 // dQ: workgroup = 128 queries (4 waves x 32), sweep keys <= last query.
-__global__ __launch_bounds__(256) void attn_bwd_dq_kernel(AttnArgs p) {
+__global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(AttnArgs p) {
   __shared__ __attribute__((aligned(16))) bf16_t smem[2 * 2 * KT * HD];  // [stage][K|V]
   const int S = p.S, H = p.H;
   const int nqb = (S + QB - 1) / QB;
@@ -448,6 +468,9 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(AttnArgs p) {
     const int kt0 = t * KT;
     const bool active = !(p.causal && kt0 > q0 + 31);
     if (active) {
+      const bool need_mask = (p.causal && kt0 + KT - 1 > q0) || (kt0 + KT > S) || pad;  // uniform
+      const unsigned long long pm = need_mask ? pad_bits(pad, kt0, S, lane) : 0ull;
+      const int lim = need_mask ? (p.causal ? min(q, S - 1) : S - 1) - kt0 : KT;
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks) {
         floatx16 sa, dp;
@@ -460,9 +483,9 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(AttnArgs p) {
         }
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-          const int key = kt0 + ks * 32 + acc_row(r, lane);
-          float pv = exp2f(sa[r] * c - lse2);
-          if (key >= S || (p.causal && key > q) || (pad && pad[key])) pv = 0.f;
+          const int kl = ks * 32 + acc_row(r, lane);
+          float pv = fast_exp2(sa[r] * c - lse2);
+          pv = (kl > lim || ((pm >> kl) & 1ull)) ? 0.f : pv;
           dp[r] = pv * (dp[r] - dl);
         }
 #pragma unroll

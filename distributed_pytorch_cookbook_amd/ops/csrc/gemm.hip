@@ -291,13 +291,26 @@ __device__ __forceinline__ void dma_offsets(int (&v)[KB / 16], long long ld, int
 }
 
 template <int NL>
-__device__ __forceinline__ void issue_tile(__amdgpu_buffer_rsrc_t rs, const int (&voff)[NL], bf16_t* lds_tile,
-                                           int wave) {
+__device__ __forceinline__ void issue_tile(const void* base, unsigned long long total, unsigned long long off,
+                                           const int* voff, bf16_t* lds_tile, int wave) {
+  // descriptor whose base is `off` bytes into the operand and whose range ends with it
+  const unsigned long long left = off < total ? total - off : 0ull;
+  const unsigned nrec = left > 0xffffffffull ? 0xffffffffu : (unsigned)left;
+  const __amdgpu_buffer_rsrc_t rs =
+      __builtin_amdgcn_make_buffer_rsrc((void*)((const char*)base + off), 0, nrec, 0x00020000);
 #pragma unroll
   for (int i = 0; i < NL; ++i) {
     const int j = wave * NL + i;  // wave-instruction index: 1 KiB of the tile
     __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void_t)(lds_tile + j * 512), 16, voff[i], 0, 0, 0);
   }
+}
+
+// buffer descriptor whose base is `off` bytes into the operand and whose range ends with it
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, unsigned long long total,
+                                                            unsigned long long off) {
+  const unsigned long long left = off < total ? total - off : 0ull;
+  const unsigned nrec = left > 0xffffffffull ? 0xffffffffu : (unsigned)left;
+  return __builtin_amdgcn_make_buffer_rsrc((void*)((const char*)base + off), 0, nrec, 0x00020000);
 }
 
 template <int N>
@@ -349,12 +362,6 @@ __global__ __launch_bounds__(NT, (V2Cfg<KB, STAGES>::WGS)) void gemm2_kernel(Gem
   const unsigned long long b_org = BK ? (unsigned long long)n0 * p.ldb * 2 : (unsigned long long)n0 * 2;
   const unsigned long long a_step = AK ? KB * 2ull : (unsigned long long)KB * p.lda * 2;
   const unsigned long long b_step = BK ? KB * 2ull : (unsigned long long)KB * p.ldb * 2;
-  auto rsrc = [](const void* base, unsigned long long total, unsigned long long off) {
-    const unsigned long long left = off < total ? total - off : 0ull;
-    const unsigned nrec = left > 0xffffffffull ? 0xffffffffu : (unsigned)left;
-    return __builtin_amdgcn_make_buffer_rsrc((void*)((const char*)base + off), 0, nrec, 0x00020000);
-  };
-
   floatx4 acc[4][4];
 #pragma unroll
   for (int i = 0; i < 4; ++i)
@@ -368,15 +375,16 @@ __global__ __launch_bounds__(NT, (V2Cfg<KB, STAGES>::WGS)) void gemm2_kernel(Gem
   const int per = (nk_all + splits - 1) / splits;
   const int kt0 = blockIdx.y * per;
   const int nk = max(0, min(nk_all, kt0 + per) - kt0);
-  auto issue = [&](int it) {
-    bf16_t* base = smem + (it % STAGES) * 2 * Cfg::TILE;
-    const unsigned long long kt = (unsigned long long)(kt0 + it);
-    issue_tile<NL>(rsrc(p.A, a_bytes, a_org + a_step * kt), va, base, wid);
-    issue_tile<NL>(rsrc(p.B, b_bytes, b_org + b_step * kt), vb, base + Cfg::TILE, wid);
-  };
+#define DPC_ISSUE(it_)                                                                              \
+  do {                                                                                              \
+    bf16_t* base_ = smem + ((it_) % STAGES) * 2 * Cfg::TILE;                                        \
+    const unsigned long long ktg_ = (unsigned long long)(kt0 + (it_));                              \
+    issue_tile<NL>(p.A, a_bytes, a_org + a_step * ktg_, va, base_, wid);                            \
+    issue_tile<NL>(p.B, b_bytes, b_org + b_step * ktg_, vb, base_ + Cfg::TILE, wid);                \
+  } while (0)
 #pragma unroll
   for (int s = 0; s < STAGES - 1; ++s)
-    if (s < nk) issue(s);
+    if (s < nk) DPC_ISSUE(s);
 
   for (int kt = 0; kt < nk; ++kt) {
     // tile kt landed for THIS wave: the tiles issued after it (at most STAGES-2, fewer at the
@@ -387,7 +395,7 @@ __global__ __launch_bounds__(NT, (V2Cfg<KB, STAGES>::WGS)) void gemm2_kernel(Gem
     else wait_vm<0>();
     __builtin_amdgcn_s_barrier();  // ... and for every wave; also: all waves finished tile kt-1
     asm volatile("" ::: "memory");
-    if (kt + STAGES - 1 < nk) issue(kt + STAGES - 1);
+    if (kt + STAGES - 1 < nk) DPC_ISSUE(kt + STAGES - 1);
     const bf16_t* la = smem + (kt % STAGES) * 2 * Cfg::TILE;
     const bf16_t* lb = la + Cfg::TILE;
 #pragma unroll

@@ -170,15 +170,24 @@ struct AdamArgs {
   float lr, beta1, beta2, eps, weight_decay;
   float bias_correction1, bias_correction2_sqrt;
   float grad_scale;
+  const float* step_ptr;  // optional device step counter (HIP-graph replay): bias corrections
+                          // are then computed on the device from it
 };
 
 __global__ __launch_bounds__(256) void adamw_kernel(AdamArgs a) {
   const long long n4 = a.n >> 2;
   float gs = a.grad_scale;
   if (a.grad_scale_ptr) gs *= *a.grad_scale_ptr;
-  const float step = a.lr / a.bias_correction1;
-  const float decay = 1.f - a.lr * a.weight_decay;
   const float b1 = a.beta1, b2 = a.beta2;
+  float bc1 = a.bias_correction1, bc2s = a.bias_correction2_sqrt;
+  if (a.step_ptr) {
+    const float t = *a.step_ptr;
+    bc1 = 1.f - powf(b1, t);
+    bc2s = sqrtf(1.f - powf(b2, t));
+  }
+  a.bias_correction2_sqrt = bc2s;
+  const float step = a.lr / bc1;
+  const float decay = 1.f - a.lr * a.weight_decay;
   for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n4; i += (long long)gridDim.x * 256) {
     float4 p = reinterpret_cast<float4*>(a.param)[i];
     const float4 g = reinterpret_cast<const float4*>(a.grad)[i];

@@ -25,6 +25,10 @@ class FlatAdamW:
         self.exp_avg = torch.zeros_like(param)
         self.exp_avg_sq = torch.zeros_like(param)
         self.step_count = 0
+        # device-side step counter: lets a captured HIP graph replay the update with the
+        # right bias corrections every step (host scalars would be frozen at capture)
+        self.step_t = torch.zeros((), device=param.device, dtype=torch.float32)
+        self.device_step = False
 
     def state_dict(self):
         return {"step": self.step_count, "exp_avg": self.exp_avg, "exp_avg_sq": self.exp_avg_sq,
@@ -44,12 +48,18 @@ class FlatAdamW:
         bc2s = math.sqrt(1.0 - b2 ** self.step_count)
         p, g = self.param, self.grad
         if p.is_cuda and p.numel() % 4 == 0:
+            step_ptr = None
+            if self.device_step:
+                self.step_t.add_(1.0)
+                step_ptr = self.step_t.data_ptr()
+            else:
+                self.step_t.fill_(float(self.step_count))
             args = _lib.AdamArgs(
                 param=p.data_ptr(), grad=g.data_ptr(), exp_avg=self.exp_avg.data_ptr(),
                 exp_avg_sq=self.exp_avg_sq.data_ptr(), shadow=_lib.ptr(self.shadow),
                 grad_scale_ptr=_lib.ptr(grad_scale_t), n=p.numel(), lr=self.lr, beta1=b1,
                 beta2=b2, eps=self.eps, weight_decay=self.weight_decay, bias_correction1=bc1,
-                bias_correction2_sqrt=bc2s, grad_scale=grad_scale,
+                bias_correction2_sqrt=bc2s, grad_scale=grad_scale, step_ptr=step_ptr,
             )
             _lib.call("dpc_adamw", args, p.device)
             return

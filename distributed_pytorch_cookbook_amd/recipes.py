@@ -42,6 +42,8 @@ def build_engine(recipe: str, model, info, args):
             model, info.device, lr=args.learning_rate, bucket_mb=args.bucket_mb,
             reduce_dtype=torch.bfloat16 if args.reduce_dtype == "bf16" else torch.float32,
             overlap=not args.no_overlap, compute_dtype=compute_dtype,
+            # the cookbook's "compile": capture the whole single-GPU step into a HIP graph
+            graph=not args.disable_compile and not args.disable_amp,
         )
     if recipe == "fsdp":
         from .engine.fsdp import FSDPEngine

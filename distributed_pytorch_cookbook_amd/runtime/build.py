@@ -13,8 +13,19 @@ LIB_PATH = HERE / "libdpc_runtime.so"
 FLAGS = ["-O3", "-std=c++17", "-fPIC", "-shared", "-fopenmp", "-march=x86-64-v3", "-pthread"]
 
 
+HASH_PATH = LIB_PATH.with_suffix(".so.srchash")
+
+
+def source_hash() -> str:
+    import hashlib
+
+    return hashlib.sha256(" ".join(FLAGS).encode() + SRC.read_bytes()).hexdigest()
+
+
 def needs_build() -> bool:
-    return not LIB_PATH.exists() or SRC.stat().st_mtime > LIB_PATH.stat().st_mtime
+    if not LIB_PATH.exists() or not HASH_PATH.exists():
+        return True
+    return HASH_PATH.read_text().strip() != source_hash()
 
 
 def build(force: bool = False, verbose: bool = False) -> Path:
@@ -31,6 +42,7 @@ def build(force: bool = False, verbose: bool = False) -> Path:
     if r.returncode != 0:
         raise RuntimeError(f"runtime build failed:\n{r.stdout}\n{r.stderr}")
     os.replace(tmp, LIB_PATH)
+    HASH_PATH.write_text(source_hash() + "\n")
     return LIB_PATH
 
 

@@ -43,6 +43,15 @@ def close(sd_a, sd_b, tol=2e-2, lr=1e-3, steps=3):
         assert err < tol, (k, err)
 
 
+def test_hip_graph_step_matches_eager(ref):
+    eng = DataParallelEngine(make(), "cuda", lr=1e-3, graph=True)
+    losses, sd = run(eng, steps=3)  # eager, capture+replay, replay
+    assert eng._graph is not None, "step was not captured"
+    assert eng.step_count == 3
+    assert abs(losses[-1] - ref[0][-1]) < 2e-2
+    close(sd, ref[1], tol=1e-2)
+
+
 @pytest.mark.parametrize("offload", [False, True])
 def test_fsdp_single_gpu(ref, offload):
     losses, sd = run(FSDPEngine(make(), "cuda", lr=1e-3, cpu_offload=offload))
