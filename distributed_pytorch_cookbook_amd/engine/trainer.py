@@ -145,6 +145,7 @@ class Trainer:
 
     def train_epoch(self, ei, loader):
         a, e = self.args, self.engine
+        e.model.train()  # reference main-single.py:35 / main-ddp.py:109 (dropout on)
         pb = _tqdm(loader, self.log) if self.log else _NoBar(loader)
         pb.set_description(f"[training] Epoch {ei+1}/{a.epochs} | loss: ?????")
         window, nwin = None, 0
@@ -184,6 +185,7 @@ class Trainer:
     @torch.no_grad()
     def validate(self, ei, loader):
         a, e = self.args, self.engine
+        e.model.eval()  # reference main-ddp.py:135 (dropout off for validation and sampling)
         tot = torch.zeros(3, device=self.device)
         pb = _tqdm(loader, self.log) if self.log else _NoBar(loader)
         pb.set_description(f"[validation] Epoch {ei+1}/{a.epochs} | loss: ?????, accuracy: ?????")

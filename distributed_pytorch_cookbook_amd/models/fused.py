@@ -28,6 +28,7 @@ import torch
 
 from ..ops.attention import attention_bwd, attention_fwd
 from ..ops.elementwise import bias_act_bwd
+from ..ops.dropout import dropout_residual
 from ..ops.embedding import embedding_bwd, embedding_fwd
 from ..ops.gemm import ACT_GELU, ACT_RELU, act_code, linear_dgrad, linear_fwd, linear_wgrad
 from ..ops.loss import cross_entropy_fused
@@ -92,8 +93,9 @@ class _EmbedFn(torch.autograd.Function):
 
 class _LayerFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, mask, layer, store, N, S, act, training):
+    def forward(ctx, x, mask, layer, store, N, S, act, training, drops=(None, None)):
         u = layer._unit_id
+        drop_attn, drop_ffn = drops
         store.pre_forward(u)
         attn, fc = layer.attn, layer.fc
         H, hd = attn.heads, attn.head_dim
@@ -103,21 +105,31 @@ class _LayerFn(torch.autograd.Function):
         h1, mu1, rs1 = layernorm_fwd(x, w(layer.norm1.weight), w(layer.norm1.bias), LN_EPS, cdt)
         qkv = linear_fwd(h1, _qkv_weight(store, attn), out_dtype=cdt)
         o, lse = attention_fwd(qkv, N, S, H, hd, mask, causal=True)
-        x2 = linear_fwd(o, w(attn.to_out.weight), bias=w(attn.to_out.bias), residual=x,
-                        out_dtype=torch.float32)
+        if drop_attn is None:
+            x2 = linear_fwd(o, w(attn.to_out.weight), bias=w(attn.to_out.bias), residual=x,
+                            out_dtype=torch.float32)
+        else:
+            x2 = linear_fwd(o, w(attn.to_out.weight), bias=w(attn.to_out.bias), out_dtype=torch.float32)
+            dropout_residual(x2, x, drop_attn, out=x2)
         h2, mu2, rs2 = layernorm_fwd(x2, w(layer.norm2.weight), w(layer.norm2.bias), LN_EPS, cdt)
         F4 = w(fc.up_proj.weight).shape[0]
         z1 = torch.empty(T, F4, device=x.device, dtype=cdt) if (training and act == ACT_GELU) else None
         uact = linear_fwd(h2, w(fc.up_proj.weight), bias=w(fc.up_proj.bias), act=act, aux_out=z1,
                           out_dtype=cdt)
         z2 = torch.empty(T, D, device=x.device, dtype=cdt) if training else None
-        x3 = linear_fwd(uact, w(fc.down_proj.weight), bias=w(fc.down_proj.bias), act=act,
-                        residual=x2, aux_out=z2, out_dtype=torch.float32)
+        if drop_ffn is None:
+            x3 = linear_fwd(uact, w(fc.down_proj.weight), bias=w(fc.down_proj.bias), act=act,
+                            residual=x2, aux_out=z2, out_dtype=torch.float32)
+        else:
+            x3 = linear_fwd(uact, w(fc.down_proj.weight), bias=w(fc.down_proj.bias), act=act,
+                            aux_out=z2, out_dtype=torch.float32)
+            dropout_residual(x3, x2, drop_ffn, out=x3)
         store.post_forward(u, training)
         if training:
             ctx.save_for_backward(x, h1, mu1, rs1, qkv, o, lse, x2, h2, mu2, rs2,
                                   z1 if z1 is not None else uact, uact, z2, mask)
             ctx.layer, ctx.store, ctx.dims, ctx.act = layer, store, (N, S, H, hd), act
+            ctx.drops = drops
         return x3
 
     @staticmethod
@@ -132,7 +144,8 @@ class _LayerFn(torch.autograd.Function):
         cdt = store.compute_dtype
         dx = dx3.contiguous()  # becomes dx2 then dx (in place)
         # FFN down projection: x3 = x2 + act(z2), z2 = u W2^T + b2
-        dz2 = bias_act_bwd(dx, z2, act, g(fc.down_proj.bias), out_dtype=cdt)
+        drop_attn, drop_ffn = ctx.drops
+        dz2 = bias_act_bwd(dx, z2, act, g(fc.down_proj.bias), out_dtype=cdt, drop=drop_ffn)
         linear_wgrad(dz2, uact, out=g(fc.down_proj.weight))
         # up projection gradient with act' fused (relu' from its output, gelu' from z1)
         dz1 = linear_dgrad(dz2, w(fc.down_proj.weight), act_bwd=act, aux_in=zup, out_dtype=cdt,
@@ -142,7 +155,7 @@ class _LayerFn(torch.autograd.Function):
         layernorm_bwd(dh2, x2, mu2, rs2, w(layer.norm2.weight), dx, g(layer.norm2.weight),
                       g(layer.norm2.bias))
         # attention output projection: x2 = x + o Wo^T + bo
-        dyo = bias_act_bwd(dx, None, 0, g(attn.to_out.bias), out_dtype=cdt)
+        dyo = bias_act_bwd(dx, None, 0, g(attn.to_out.bias), out_dtype=cdt, drop=drop_attn)
         linear_wgrad(dyo, o, out=g(attn.to_out.weight))
         do = linear_dgrad(dyo, w(attn.to_out.weight), out_dtype=cdt)
         dqkv = attention_bwd(do, qkv, o, lse, N, S, H, hd, mask, causal=True)
@@ -156,7 +169,7 @@ class _LayerFn(torch.autograd.Function):
         layernorm_bwd(dh1, x, mu1, rs1, w(layer.norm1.weight), dx, g(layer.norm1.weight),
                       g(layer.norm1.bias))
         store.post_backward(u)
-        return dx, None, None, None, None, None, None, None
+        return dx, None, None, None, None, None, None, None, None
 
 
 class _HeadFn(torch.autograd.Function):
@@ -233,12 +246,16 @@ def run_embeddings(model, store, input_ids, position_ids, training):
                           model.embeddings, store, training)
 
 
-def run_layers(model, store, x, mask, N, S, layers, training):
+def run_layers(model, store, x, mask, N, S, layers, training, dropout_seed=None):
+    """``training``: keep activations for the backward.  Dropout follows the module mode
+    (``model.train()`` / ``model.eval()``) like ``nn.Dropout``."""
     act = act_code(model.activation)
-    if model.dropout and training:
-        raise NotImplementedError("dropout > 0 is not supported on the fused path yet")
+    use_drop = model.training and model.dropout > 0
+    if use_drop and dropout_seed is None:
+        dropout_seed = model.next_dropout_seed()
     for layer in layers:
-        x = _LayerFn.apply(x, mask, layer, store, N, S, act, training)
+        drops = model.dropout_specs(layer, dropout_seed) if use_drop else (None, None)
+        x = _LayerFn.apply(x, mask, layer, store, N, S, act, training, drops)
     return x
 
 
@@ -247,14 +264,15 @@ def run_head(model, store, x, targets, training, want_correct):
                          model._head_unit_id, training, want_correct)
 
 
-def fused_lm_forward(model, input_ids, position_ids, mask=None, targets=None, want_correct=False):
+def fused_lm_forward(model, input_ids, position_ids, mask=None, targets=None, want_correct=False,
+                     dropout_seed=None):
     store = ensure_store(model)
     N, S = input_ids.shape
     training = torch.is_grad_enabled()
     if mask is not None:
         mask = mask.to(device=input_ids.device, dtype=torch.bool).contiguous()
     x = run_embeddings(model, store, input_ids, position_ids, training)
-    x = run_layers(model, store, x, mask, N, S, model.decoder.layers, training)
+    x = run_layers(model, store, x, mask, N, S, model.decoder.layers, training, dropout_seed)
     if targets is None:
         return head_logits(model, x, store).reshape(N, S, -1)
     loss, n_valid, n_correct = run_head(model, store, x, targets, training, want_correct)

@@ -40,6 +40,25 @@ def activation_name(fn) -> str:
     raise ValueError(f"unsupported activation {fn}")
 
 
+class SiteDropout(nn.Dropout):
+    """``nn.Dropout`` whose mask can be pinned to the fused path's counter-based mask.
+
+    With ``spec`` unset it is ``nn.Dropout``.  ``TransformerDecoderLM.reference_forward(...,
+    dropout_seed=s)`` sets ``spec`` to the same :class:`DropSpec` the fused kernels use for
+    seed ``s``, so the reference math and the fused path drop identical elements.
+    """
+
+    spec = None
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        if self.spec is None or not self.training:
+            return super().forward(x)
+        from ..ops.dropout import keep_mask
+
+        flat = x.reshape(-1, x.shape[-1])
+        return (flat * keep_mask(self.spec, flat.shape[0], flat.shape[1], x.device).to(x.dtype)).reshape(x.shape)
+
+
 class FeedForward(nn.Module):
     """x -> up_proj -> act -> down_proj -> act -> dropout (reference gpt.py:10-41)."""
 
@@ -53,7 +72,7 @@ class FeedForward(nn.Module):
         self.bias = bias
         self.up_proj = nn.Linear(dim, dim * mult, bias=bias)
         self.down_proj = nn.Linear(dim * mult, self.out_dim, bias=bias)
-        self.dropout = nn.Dropout(dropout)
+        self.dropout = SiteDropout(dropout)
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         x = self.activation(self.up_proj(x))
@@ -75,7 +94,7 @@ class SelfAttention(nn.Module):
         self.to_k = nn.Linear(dim, head_dim * heads, bias=qkv_bias)
         self.to_v = nn.Linear(dim, head_dim * heads, bias=qkv_bias)
         self.to_out = nn.Linear(head_dim * heads, dim, bias=True)
-        self.dropout = nn.Dropout(dropout)
+        self.dropout = SiteDropout(dropout)
         self.attn_scale = 1 / sqrt(head_dim)
 
     def forward(self, x: torch.Tensor, mask: Optional[torch.Tensor] = None) -> torch.Tensor:
@@ -173,6 +192,25 @@ class TransformerDecoderLM(nn.Module):
         # execution state (not modules / not in the state_dict)
         object.__setattr__(self, "param_store", None)
         object.__setattr__(self, "stage", None)  # pipeline stage descriptor (None = whole model)
+        # dropout: per-forward seeds = (dropout_seed_base << 32) | call counter
+        self.dropout_seed_base = 0
+        self._dropout_calls = 0
+        for i, layer in enumerate(self.decoder.layers):
+            layer._layer_index = i
+
+    # ------------------------------------------------------------------ dropout
+    def next_dropout_seed(self) -> int:
+        """Seed of the next training forward (each call advances the stream)."""
+        seed = ((self.dropout_seed_base & 0xFFFFFFFF) << 32) | (self._dropout_calls & 0xFFFFFFFF)
+        self._dropout_calls += 1
+        return seed
+
+    def dropout_specs(self, layer, seed):
+        """(attention-output, FFN-output) :class:`DropSpec` of ``layer`` for ``seed``."""
+        from ..ops.dropout import DropSpec
+
+        i = layer._layer_index
+        return DropSpec.make(self.dropout, seed, 2 * i), DropSpec.make(self.dropout, seed, 2 * i + 1)
 
     # ------------------------------------------------------------------ structure
     def units(self):
@@ -183,17 +221,29 @@ class TransformerDecoderLM(nn.Module):
         out.append(("head", [self.norm_out, self.lm_head]))
         return out
 
-    def reference_forward(self, input_ids, position_ids, mask=None):
-        """The reference's math with plain torch modules (autograd does the backward)."""
-        x = self.embeddings(input_ids, position_ids)
-        x = self.decoder(x, mask=mask)
-        x = self.norm_out(x)
-        return self.lm_head(x)
+    def reference_forward(self, input_ids, position_ids, mask=None, dropout_seed=None):
+        """The reference's math with plain torch modules (autograd does the backward).
 
-    def forward(self, input_ids, position_ids, mask=None, targets=None, want_correct=False):
+        ``dropout_seed`` pins the dropout masks to those the fused path draws for that seed.
+        """
+        if dropout_seed is not None:
+            for layer in self.decoder.layers:
+                layer.attn.dropout.spec, layer.fc.dropout.spec = self.dropout_specs(layer, dropout_seed)
+        try:
+            x = self.embeddings(input_ids, position_ids)
+            x = self.decoder(x, mask=mask)
+            x = self.norm_out(x)
+            return self.lm_head(x)
+        finally:
+            if dropout_seed is not None:
+                for layer in self.decoder.layers:
+                    layer.attn.dropout.spec = layer.fc.dropout.spec = None
+
+    def forward(self, input_ids, position_ids, mask=None, targets=None, want_correct=False,
+                dropout_seed=None):
         from .fused import fused_lm_forward
 
-        return fused_lm_forward(self, input_ids, position_ids, mask, targets, want_correct)
+        return fused_lm_forward(self, input_ids, position_ids, mask, targets, want_correct, dropout_seed)
 
 
 PRESETS = {

@@ -12,7 +12,7 @@ from __future__ import annotations
 
 import ctypes
 import threading
-from ctypes import c_float, c_int, c_longlong, c_void_p
+from ctypes import c_float, c_int, c_longlong, c_uint, c_void_p
 
 import torch
 
@@ -98,6 +98,17 @@ class BiasActArgs(ctypes.Structure):
         ("lddy", LL), ("ldz", LL), ("lddz", LL),
         ("T", c_int), ("N", c_int),
         ("act", c_int),
+        ("drop_key", c_uint), ("drop_thresh", c_uint), ("drop_scale", c_float),
+    ]
+
+
+class DropResArgs(ctypes.Structure):
+    _fields_ = [
+        ("y", P), ("res", P), ("out", P),
+        ("ldy", LL), ("ldr", LL), ("ldo", LL),
+        ("T", c_int), ("N", c_int),
+        ("key", c_uint), ("thresh", c_uint),
+        ("scale", c_float),
     ]
 
 
@@ -113,6 +124,7 @@ _FUNCS = {
     "dpc_adamw": AdamArgs,
     "dpc_cast_f32_bf16": CastArgs,
     "dpc_bias_act_bwd": BiasActArgs,
+    "dpc_dropout_residual": DropResArgs,
 }
 
 _lock = threading.Lock()

@@ -233,8 +233,56 @@ __global__ __launch_bounds__(256) void cast_kernel(CastArgs a) {
   }
 }
 
+// ------------------------------------------------------------------ dropout
+// Counter-based keep mask: element (t, c) of a [T, N] site is kept iff
+// fmix32((t*N + c) * 0x9E3779B1 ^ key) >= thresh.  The map idx -> hash is a bijection for
+// a fixed key, so nothing is stored between forward and backward: both regenerate it.
+// The torch twin is ops/dropout.py:keep_mask (bit-identical, used on CPU and in tests).
+__device__ __forceinline__ uint32_t fmix32(uint32_t x) {
+  x ^= x >> 16;
+  x *= 0x85ebca6bu;
+  x ^= x >> 13;
+  x *= 0xc2b2ae35u;
+  x ^= x >> 16;
+  return x;
+}
+
+__device__ __forceinline__ float drop_factor(uint32_t idx, uint32_t key, uint32_t thresh, float scale) {
+  return fmix32((idx * 0x9E3779B1u) ^ key) >= thresh ? scale : 0.f;
+}
+
+// out[t, c] = res[t, c] + y[t, c] * keep(t, c) / (1 - p)   (f32; out may alias y or res)
+struct DropResArgs {
+  const float* y;
+  const float* res;
+  float* out;
+  long long ldy, ldr, ldo;
+  int T, N;
+  unsigned key, thresh;
+  float scale;
+};
+
+__global__ __launch_bounds__(256) void dropout_residual_kernel(DropResArgs p) {
+  const int nq = p.N >> 2;
+  const long long total = (long long)p.T * nq;
+  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < total; i += (long long)gridDim.x * 256) {
+    const long long t = i / nq;
+    const int c = (int)(i - t * nq) * 4;
+    const float4 y = *reinterpret_cast<const float4*>(p.y + t * p.ldy + c);
+    const float4 r = *reinterpret_cast<const float4*>(p.res + t * p.ldr + c);
+    const uint32_t idx = (uint32_t)(t * p.N + c);
+    float4 o;
+    o.x = r.x + y.x * drop_factor(idx + 0, p.key, p.thresh, p.scale);
+    o.y = r.y + y.y * drop_factor(idx + 1, p.key, p.thresh, p.scale);
+    o.z = r.z + y.z * drop_factor(idx + 2, p.key, p.thresh, p.scale);
+    o.w = r.w + y.w * drop_factor(idx + 3, p.key, p.thresh, p.scale);
+    *reinterpret_cast<float4*>(p.out + t * p.ldo + c) = o;
+  }
+}
+
 // ------------------------------------------------------------------ bias / activation backward
-// dz[t, c] = dy[t, c] * act'(z[t, c])  (bf16 out), db[c] += sum_t dz[t, c]
+// dz[t, c] = dy[t, c] * keep(t, c) * act'(z[t, c])  (bf16 out), db[c] += sum_t dz[t, c]
+// (keep = 1 when drop_scale == 0).
 // grid: (ceil(N / 512), ceil(T / 64)); each lane owns 8 columns, each wave 16 rows.
 struct BiasActArgs {
   const float* dy;     // [T][lddy] f32
@@ -244,6 +292,8 @@ struct BiasActArgs {
   long long lddy, ldz, lddz;
   int T, N;
   int act;
+  unsigned drop_key, drop_thresh;
+  float drop_scale;    // 0: no dropout
 };
 
 __global__ __launch_bounds__(256) void bias_act_bwd_kernel(BiasActArgs p) {
@@ -266,6 +316,11 @@ __global__ __launch_bounds__(256) void bias_act_bwd_kernel(BiasActArgs p) {
 #pragma unroll
         for (int j = 0; j < 8; ++j) f[j] *= act_grad(zf[j], p.act);
       }
+      if (p.drop_scale != 0.f) {
+        const uint32_t idx = (uint32_t)(t * p.N + cg * 8);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) f[j] *= drop_factor(idx + j, p.drop_key, p.drop_thresh, p.drop_scale);
+      }
 #pragma unroll
       for (int j = 0; j < 8; ++j) acc[j] += f[j];
       *reinterpret_cast<uint4*>(static_cast<bf16_t*>(p.dz) + t * p.lddz + cg * 8) = pack8(f);
@@ -284,7 +339,6 @@ __global__ __launch_bounds__(256) void bias_act_bwd_kernel(BiasActArgs p) {
   }
 }
 
-// column sum only (bias grad of a layer whose dz is already materialised, f32 input)
 }  // namespace dpc
 
 using namespace dpc;
@@ -335,5 +389,13 @@ DPC_API int dpc_bias_act_bwd(const BiasActArgs* a, hipStream_t stream) {
   if (a->N % 8) return (int)hipErrorInvalidValue;
   dim3 grid((unsigned)((a->N / 8 + 63) / 64), (unsigned)((a->T + 63) / 64));
   hipLaunchKernelGGL(bias_act_bwd_kernel, grid, dim3(256), 0, stream, *a);
+  return (int)hipGetLastError();
+}
+
+DPC_API int dpc_dropout_residual(const DropResArgs* a, hipStream_t stream) {
+  if (a->T <= 0) return 0;
+  if (a->N % 4 || a->ldy % 4 || a->ldr % 4 || a->ldo % 4) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(dropout_residual_kernel, dim3(grid_for((long long)a->T * (a->N / 4))), dim3(256), 0,
+                     stream, *a);
   return (int)hipGetLastError();
 }

@@ -10,15 +10,20 @@ from __future__ import annotations
 import torch
 
 from . import _lib
+from .dropout import DropSpec, keep_mask
 from .gemm import act_code, act_grad_ref
 
 
 def bias_act_bwd(dy: torch.Tensor, z: torch.Tensor | None, act, db: torch.Tensor | None,
-                 out: torch.Tensor | None = None, out_dtype=torch.bfloat16) -> torch.Tensor:
+                 out: torch.Tensor | None = None, out_dtype=torch.bfloat16,
+                 drop: DropSpec | None = None) -> torch.Tensor:
+    """``dz = dy * keep * act'(z)``; ``drop`` is the forward's dropout of this site."""
     act = act_code(act)
     T, N = dy.shape
     if not (dy.is_cuda and out_dtype == torch.bfloat16):
         g = dy.float()
+        if drop is not None:
+            g = g * keep_mask(drop, T, N, dy.device)
         if act:
             g = g * act_grad_ref(z, act)
         if db is not None:
@@ -38,6 +43,10 @@ def bias_act_bwd(dy: torch.Tensor, z: torch.Tensor | None, act, db: torch.Tensor
         lddy=dy.stride(0), ldz=z.stride(0) if z is not None else 0, lddz=out.stride(0),
         T=T, N=N, act=act,
     )
+    if drop is not None:
+        if T * N >= 2 ** 32:
+            raise ValueError("bias_act_bwd: dropout needs T * N < 2^32")
+        args.drop_key, args.drop_thresh, args.drop_scale = drop.key, drop.thresh, drop.scale
     _lib.call("dpc_bias_act_bwd", args, dy.device)
     return out
 

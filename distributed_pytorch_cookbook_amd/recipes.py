@@ -43,7 +43,8 @@ def build_engine(recipe: str, model, info, args):
             reduce_dtype=torch.bfloat16 if args.reduce_dtype == "bf16" else torch.float32,
             overlap=not args.no_overlap, compute_dtype=compute_dtype,
             # the cookbook's "compile": capture the whole single-GPU step into a HIP graph
-            graph=not args.disable_compile and not args.disable_amp,
+            # (dropout masks are drawn per step on the host: not graph-replayable)
+            graph=not args.disable_compile and not args.disable_amp and not args.dropout,
         )
     if recipe == "fsdp":
         from .engine.fsdp import FSDPEngine
@@ -76,6 +77,7 @@ def run(recipe: str, argv=None):
     tokenizer = get_tokenizer(max_length=args.sequence_length, offline_stub=synthetic)
     tokenizer.pad_token_id = PAD_ID
     model = build_model(args, tokenizer.vocab_size, info.device)
+    model.dropout_seed_base = args.seed * 65537 + info.rank  # distinct masks per rank
     engine = build_engine(recipe, model, info, args)
     train, val = get_dataset(slice_size=args.dataset_slice, synthetic=synthetic,
                              seq_len=args.sequence_length, n_train=args.train_samples,

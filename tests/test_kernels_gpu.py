@@ -297,3 +297,31 @@ def test_gemm_padded_vocab_head(impl):
     assert rel_err(dh, g[:, :V].float() @ w.float()) < 2e-3
     r = dy.float().t() @ x.float()
     assert rel_err(o1, r) < 2e-3 and rel_err(o2 - 1, r) < 2e-3
+
+
+def test_dropout_kernels_match_torch_twin():
+    """The device hash mask is bit-identical to ops/dropout.py:keep_mask."""
+    from distributed_pytorch_cookbook_amd.ops.dropout import DropSpec, dropout_residual, keep_mask
+
+    torch.manual_seed(13)
+    T, N = 1031, 768
+    spec = DropSpec.make(0.1, seed=(5 << 32) | 17, site=9)
+    y = torch.randn(T, N, device=dev)
+    r = torch.randn(T, N, device=dev)
+    out = dropout_residual(y, r, spec)
+    keep = keep_mask(spec, T, N, dev)
+    assert torch.equal(out == r, (keep == 0) | (y == 0))
+    assert rel_err(out, r + y * keep) < 1e-6
+    # in place, aliasing y
+    y2 = y.clone()
+    dropout_residual(y2, r, spec, out=y2)
+    assert torch.equal(y2, out)
+    # backward: dz = dy * keep * act'(z)
+    from distributed_pytorch_cookbook_amd.ops.gemm import act_grad_ref
+    z = torch.randn(T, N, device=dev).bfloat16()
+    db = torch.zeros(N, device=dev)
+    dz = bias_act_bwd(y, z, 2, db, drop=spec)
+    ref = y * keep * act_grad_ref(z, 2)
+    assert rel_err(dz, ref) < 5e-3
+    assert rel_err(db, ref.sum(0)) < 1e-4
+    assert torch.equal(dz == 0, (ref == 0))

@@ -117,3 +117,54 @@ def test_store_views_and_flat_layout():
     assert st.master.numel() >= sum(p.numel() for p in m.parameters())
     sd = st.state_dict()
     assert list(sd.keys()) == list(m.state_dict().keys())
+
+
+@pytest.mark.parametrize("act", ["relu", "gelu"])
+def test_fused_dropout_matches_pinned_reference(act):
+    """Counter-based dropout: the fused path and the reference math (masks pinned to the same
+    seed) agree on loss and gradients; eval mode disables it; seeds advance per forward."""
+    torch.manual_seed(0)
+    m = TransformerDecoderLM(dim=64, head_dim=16, heads=4, num_layers=2, vocab_size=97,
+                             max_position_embeddings=24, activation=act, dropout=0.2)
+    ref = copy.deepcopy(m)
+    ids, pos, mask, tg = batch(pad=True)
+    store = LocalStore(m, "cpu")
+    store.zero_grad()
+    seed = 1234567
+    out = m(ids, pos, mask, targets=tg, dropout_seed=seed)
+    out.loss.backward()
+    logits = ref.reference_forward(ids, pos, mask, dropout_seed=seed)
+    loss = F.cross_entropy(logits.reshape(-1, logits.shape[-1]), tg.reshape(-1), ignore_index=-100)
+    loss.backward()
+    assert abs(out.loss.item() - loss.item()) < 1e-5
+    gp = dict(m.named_parameters())
+    for n, p in ref.named_parameters():
+        err = (gp[n].grad - p.grad).norm() / p.grad.norm().clamp_min(1e-12)
+        assert err < 1e-4, (n, err.item())
+    # a different seed gives a different loss; eval mode is deterministic and dropout-free
+    with torch.no_grad():
+        l1 = m(ids, pos, mask, targets=tg).loss.item()
+        l2 = m(ids, pos, mask, targets=tg).loss.item()
+        assert l1 != l2
+        m.eval()
+        ref.eval()
+        e1 = m(ids, pos, mask, targets=tg).loss.item()
+        e2 = m(ids, pos, mask, targets=tg).loss.item()
+        want = ref.reference_forward(ids, pos, mask)
+        want = F.cross_entropy(want.reshape(-1, want.shape[-1]), tg.reshape(-1), ignore_index=-100)
+    assert e1 == e2 and abs(e1 - want.item()) < 1e-5
+
+
+def test_dropout_mask_statistics():
+    from distributed_pytorch_cookbook_amd.ops.dropout import DropSpec, keep_mask
+
+    spec = DropSpec.make(0.25, seed=99, site=3)
+    k = keep_mask(spec, 512, 384)
+    frac = (k == 0).float().mean().item()
+    assert abs(frac - 0.25) < 0.01
+    assert torch.allclose(k[k > 0], torch.full_like(k[k > 0], 1 / 0.75))
+    # different sites / seeds decorrelate
+    k2 = keep_mask(DropSpec.make(0.25, seed=99, site=4), 512, 384)
+    both = ((k == 0) & (k2 == 0)).float().mean().item()
+    assert abs(both - 0.0625) < 0.01
+    assert DropSpec.make(0.0, 1, 1) is None
