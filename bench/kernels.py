@@ -54,7 +54,7 @@ def main():
 
     cases = [
         ("qkv_fwd", T, 3 * D, D), ("out_fwd", T, D, D), ("up_fwd", T, 4 * D, D),
-        ("down_fwd", T, D, 4 * D), ("lm_head_fwd", T, V, D),
+        ("down_fwd", T, D, 4 * D), ("lm_head_fwd", T, Vp, D),
     ]
     from distributed_pytorch_cookbook_amd.ops import _lib
 

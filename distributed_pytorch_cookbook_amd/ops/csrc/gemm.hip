@@ -503,9 +503,240 @@ __global__ __launch_bounds__(NT, (V2Cfg<KB, STAGES>::WGS)) void gemm2_kernel(Gem
   }
 }
 
+// =====================================================================================
+// v3: large tiles.  A 128x128 tile re-reads each operand byte from L2 once per 128 output
+// columns: at the MFMA rate that is ~39 TB/s of L2->LDS traffic chip-wide, the whole L2
+// bandwidth, so v2 is L2-bound (PMC: WAIT_ANY 44 %).  v3 keeps v2's LDS-DMA pipeline,
+// swizzles and epilogue but runs 8 waves on a 256x256 (or 256x128) tile: half (3/4) the
+// L2 bytes per FLOP, and each wave owns a 128x64 (64x64) sub-tile, so per k-step a wave
+// reads 12 (8) fragments for 32 (16) MFMAs.  mn-major operand tiles wider than 128 are
+// stored as 128-column halves so the v2 transposed-read swizzle applies unchanged.
+template <int BM_, int BN_, int WM, int WN, int KB, int STAGES>
+struct V3Cfg {
+  static constexpr int NW = WM * WN, NTH = 64 * NW;
+  static constexpr int WTM = BM_ / WM, WTN = BN_ / WN;
+  static constexpr int FM = WTM / 16, FN = WTN / 16;
+  static constexpr int TA = BM_ * KB, TB = BN_ * KB;        // bf16 elements per stage
+  static constexpr int NLA = TA / 512 / NW, NLB = TB / 512 / NW;  // 1-KiB DMA instr per wave
+  static constexpr int PIPE = STAGES * (TA + TB);
+  static constexpr int EPI = NW * 32 * WTN * 2;              // [32][WTN] f32 per wave
+  static constexpr int SMEM = PIPE > EPI ? PIPE : EPI;
+  static constexpr int WGS = (160 * 1024) / (SMEM * 2) >= 2 ? 2 : 1;
+  static_assert(WTN == 64 && (WTM == 64 || WTM == 128), "wave tile 64x64 or 128x64");
+  static_assert(NLA * 512 * NW == TA && NLB * 512 * NW == TB, "DMA split");
+  static_assert(SMEM * 2 <= 160 * 1024, "LDS");
+};
+
+template <int KB, bool KMAJ, int NL>
+__device__ __forceinline__ void dma_offsets3(int (&v)[NL], long long ld, int wid, int lane) {
+#pragma unroll
+  for (int i = 0; i < NL; ++i) {
+    const int j = wid * NL + i;
+    if (KMAJ) {
+      constexpr int LPR = KB / 8, RPI = 64 / LPR;
+      const int row = RPI * j + lane / LPR, pos = lane % LPR, c = pos ^ swz_k<KB>(row);
+      v[i] = (int)(((long long)row * ld + c * 8) * 2);
+    } else {
+      constexpr int IPH = KB / 4;  // wave-instructions per 128-column half
+      const int h = j / IPH, kr = 4 * (j % IPH) + (lane >> 4), pos = lane & 15;
+      const int c = (((pos >> 1) ^ mn_swz(kr)) << 1) | (pos & 1);
+      v[i] = (int)(((long long)kr * ld + h * 128 + c * 8) * 2);
+    }
+  }
+}
+
+template <int KB, bool KMAJ>
+__device__ __forceinline__ bf16x8 frag3(const bf16_t* lds, int r0, int kstep, int lane) {
+  if (KMAJ) return frag_k<KB, true>(lds, r0, kstep, lane);
+  return frag<false>(lds + (r0 >> 7) * KB * 128, r0 & 127, kstep, lane);
+}
+
+template <int BM_, int BN_, int WM, int WN, int KB, int STAGES, bool AK, bool BK>
+__global__ __launch_bounds__((V3Cfg<BM_, BN_, WM, WN, KB, STAGES>::NTH), 1) void gemm3_kernel(
+    GemmArgs p, unsigned long long a_bytes, unsigned long long b_bytes) {
+  using Cfg = V3Cfg<BM_, BN_, WM, WN, KB, STAGES>;
+  constexpr int FM = Cfg::FM, FN = Cfg::FN, NLA = Cfg::NLA, NLB = Cfg::NLB;
+  __shared__ __attribute__((aligned(16))) bf16_t smem[Cfg::SMEM];
+  const int tiles_m = (p.M + BM_ - 1) / BM_, tiles_n = (p.N + BN_ - 1) / BN_;
+  const int nwg = tiles_m * tiles_n;
+  int bid = blockIdx.x;
+  {
+    const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
+    bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+  }
+  const int group = GROUP_M * tiles_n;
+  const int gid = bid / group, first_m = gid * GROUP_M;
+  const int gsz = min(tiles_m - first_m, GROUP_M);
+  const int tm = first_m + (bid % group) % gsz;
+  const int tn = (bid % group) / gsz;
+  const int m0 = tm * BM_, n0 = tn * BN_;
+
+  const int lane = threadIdx.x & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wr = wid / WN, wc = wid % WN;
+
+  int va[NLA], vb[NLB];
+  dma_offsets3<KB, AK, NLA>(va, p.lda, wid, lane);
+  dma_offsets3<KB, BK, NLB>(vb, p.ldb, wid, lane);
+  const unsigned long long a_org = AK ? (unsigned long long)m0 * p.lda * 2 : (unsigned long long)m0 * 2;
+  const unsigned long long b_org = BK ? (unsigned long long)n0 * p.ldb * 2 : (unsigned long long)n0 * 2;
+  const unsigned long long a_step = AK ? KB * 2ull : (unsigned long long)KB * p.lda * 2;
+  const unsigned long long b_step = BK ? KB * 2ull : (unsigned long long)KB * p.ldb * 2;
+  floatx4 acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+
+  const int nk_all = (p.K + KB - 1) / KB;
+  const int splits = gridDim.y;
+  const int per = (nk_all + splits - 1) / splits;
+  const int kt0 = blockIdx.y * per;
+  const int nk = max(0, min(nk_all, kt0 + per) - kt0);
+#define DPC_ISSUE3(it_)                                                                             \
+  do {                                                                                              \
+    bf16_t* base_ = smem + ((it_) % STAGES) * (Cfg::TA + Cfg::TB);                                  \
+    const unsigned long long ktg_ = (unsigned long long)(kt0 + (it_));                              \
+    issue_tile<NLA>(p.A, a_bytes, a_org + a_step * ktg_, va, base_, wid);                           \
+    issue_tile<NLB>(p.B, b_bytes, b_org + b_step * ktg_, vb, base_ + Cfg::TA, wid);                 \
+  } while (0)
+#pragma unroll
+  for (int s = 0; s < STAGES - 1; ++s)
+    if (s < nk) DPC_ISSUE3(s);
+
+  constexpr int PER_TILE = NLA + NLB;  // DMA instructions per wave per k-tile
+  for (int kt = 0; kt < nk; ++kt) {
+    const int after = min(STAGES - 2, nk - 1 - kt);
+    if (STAGES >= 4 && after >= 2) wait_vm<(STAGES >= 4 ? 2 * PER_TILE : 0)>();
+    else if (STAGES >= 3 && after >= 1) wait_vm<(STAGES >= 3 ? PER_TILE : 0)>();
+    else wait_vm<0>();
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    if (kt + STAGES - 1 < nk) DPC_ISSUE3(kt + STAGES - 1);
+    const bf16_t* la = smem + (kt % STAGES) * (Cfg::TA + Cfg::TB);
+    const bf16_t* lb = la + Cfg::TA;
+#pragma unroll
+    for (int ks = 0; ks < KB / 32; ++ks) {
+      bf16x8 fa[FM], fb[FN];
+#pragma unroll
+      for (int j = 0; j < FN; ++j) fb[j] = frag3<KB, BK>(lb, wc * Cfg::WTN + j * 16, ks, lane);
+#pragma unroll
+      for (int i = 0; i < FM; ++i) fa[i] = frag3<KB, AK>(la, wr * Cfg::WTM + i * 16, ks, lane);
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+    }
+  }
+#undef DPC_ISSUE3
+
+  // ---------------- epilogue (as v2): WTM/32 passes of 32 rows per wave through LDS
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  float alpha = p.alpha;
+  if (p.alpha_ptr) alpha *= *p.alpha_ptr;
+  float* ct = reinterpret_cast<float*>(smem) + wid * 32 * 64;
+  const int c4 = lane & 15;
+  const int n = n0 + wc * 64 + c4 * 4;
+  const bool nok = n < p.N;
+  float4 bias4 = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (p.bias && nok) bias4 = *reinterpret_cast<const float4*>(p.bias + n);
+  float cs[4] = {0.f, 0.f, 0.f, 0.f};
+  const bf16_t* aux_in = static_cast<const bf16_t*>(p.aux_in);
+  bf16_t* aux_out = static_cast<bf16_t*>(p.aux_out);
+#pragma unroll
+  for (int h = 0; h < Cfg::WTM / 32; ++h) {
+    __syncthreads();
+#pragma unroll
+    for (int ii = 0; ii < 2; ++ii)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int row = ii * 16 + (lane >> 4) * 4 + r;
+          const int col = (j * 16 + (lane & 15)) ^ (((row >> 2) & 3) << 4);
+          ct[row * 64 + col] = acc[2 * h + ii][j][r] * alpha;
+        }
+    __syncthreads();
+#pragma unroll 2
+    for (int t = 0; t < 8; ++t) {
+      const int row = (lane >> 4) + 4 * t;
+      const int m = m0 + wr * Cfg::WTM + h * 32 + row;
+      const int col = (c4 * 4) ^ (((row >> 2) & 3) << 4);
+      float4 v4 = *reinterpret_cast<const float4*>(ct + row * 64 + col);
+      if (m >= p.M || !nok) continue;
+      float v[4] = {v4.x + bias4.x, v4.y + bias4.y, v4.z + bias4.z, v4.w + bias4.w};
+      if (p.act_bwd) {
+        const uint2 z = *reinterpret_cast<const uint2*>(aux_in + (long long)m * p.ld_aux_in + n);
+        v[0] *= act_grad(__uint_as_float(z.x << 16), p.act_bwd);
+        v[1] *= act_grad(__uint_as_float(z.x & 0xffff0000u), p.act_bwd);
+        v[2] *= act_grad(__uint_as_float(z.y << 16), p.act_bwd);
+        v[3] *= act_grad(__uint_as_float(z.y & 0xffff0000u), p.act_bwd);
+      }
+#pragma unroll
+      for (int e = 0; e < 4; ++e) cs[e] += v[e];
+      if (aux_out) {
+        uint2 w;
+        w.x = pack2bf(v[0], v[1]);
+        w.y = pack2bf(v[2], v[3]);
+        *reinterpret_cast<uint2*>(aux_out + (long long)m * p.ld_aux_out + n) = w;
+      }
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[e] = act_fwd(v[e], p.act);
+      if (p.residual) {
+        const float4 r4 = *reinterpret_cast<const float4*>(p.residual + (long long)m * p.ldr + n);
+        v[0] += r4.x; v[1] += r4.y; v[2] += r4.z; v[3] += r4.w;
+      }
+      const long long ci = (long long)m * p.ldc + n;
+      if (splits > 1) {
+        float* C = static_cast<float*>(p.C) + ci;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) atomicAdd(C + e, v[e]);
+      } else if (p.out_f32) {
+        float4* C = reinterpret_cast<float4*>(static_cast<float*>(p.C) + ci);
+        if (p.accumulate) {
+          const float4 o = *C;
+          v[0] += o.x; v[1] += o.y; v[2] += o.z; v[3] += o.w;
+        }
+        *C = make_float4(v[0], v[1], v[2], v[3]);
+      } else {
+        uint2 w;
+        w.x = pack2bf(v[0], v[1]);
+        w.y = pack2bf(v[2], v[3]);
+        *reinterpret_cast<uint2*>(static_cast<bf16_t*>(p.C) + ci) = w;
+      }
+    }
+  }
+  if (p.colsum) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      cs[e] += __shfl_xor(cs[e], 16, 64);
+      cs[e] += __shfl_xor(cs[e], 32, 64);
+    }
+    if ((lane >> 4) == 0 && nok) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) atomicAdd(p.colsum + n + e, cs[e]);
+    }
+  }
+}
+
 }  // namespace dpc
 
 using namespace dpc;
+
+template <int BM_, int BN_, int WM, int WN, int KB, int STAGES>
+static void launch_v3(const GemmArgs* a, dim3 grid, hipStream_t stream, unsigned long long ab,
+                      unsigned long long bb) {
+  constexpr int NTH = V3Cfg<BM_, BN_, WM, WN, KB, STAGES>::NTH;
+  if (a->a_kmaj && a->b_kmaj)
+    hipLaunchKernelGGL((gemm3_kernel<BM_, BN_, WM, WN, KB, STAGES, true, true>), grid, dim3(NTH), 0, stream, *a, ab, bb);
+  else if (a->a_kmaj)
+    hipLaunchKernelGGL((gemm3_kernel<BM_, BN_, WM, WN, KB, STAGES, true, false>), grid, dim3(NTH), 0, stream, *a, ab, bb);
+  else if (!a->b_kmaj)
+    hipLaunchKernelGGL((gemm3_kernel<BM_, BN_, WM, WN, KB, STAGES, false, false>), grid, dim3(NTH), 0, stream, *a, ab, bb);
+  else
+    hipLaunchKernelGGL((gemm3_kernel<BM_, BN_, WM, WN, KB, STAGES, false, true>), grid, dim3(NTH), 0, stream, *a, ab, bb);
+}
 
 static inline long long operand_bytes(long long rows, long long cols, long long ld) {
   // bytes a tile load may legitimately touch: [rows][ld], 16-B chunks up to roundup8(cols)
@@ -547,6 +778,28 @@ DPC_API int dpc_gemm(const GemmArgs* a, hipStream_t stream) {
   int impl = g_gemm_impl;
   if (impl < 0) impl = v2_ok ? 2 : 1;
   if (impl >= 2 && !v2_ok) impl = 1;
+  if (impl >= 6) {
+    const int bm = 256, bn = (impl == 8 || impl == 9 || impl == 10) ? 128 : 256;
+    const int t3 = ((a->M + bm - 1) / bm) * ((a->N + bn - 1) / bn);
+    int splits = 1;
+    const bool plain = a->out_f32 && !a->bias && !a->residual && !a->aux_in && !a->aux_out &&
+                       !a->colsum && !a->act && !a->act_bwd;
+    const int nk = (a->K + BKT - 1) / BKT;
+    if (plain) {
+      while (splits < 8 && t3 * splits < 256 && nk / (splits * 2) >= 8) splits *= 2;
+    }
+    if (splits > 1 && !a->accumulate)
+      hipMemset2DAsync(a->C, (size_t)a->ldc * 4, 0, (size_t)a->N * 4, (size_t)a->M, stream);
+    dim3 g3(t3, splits);
+    switch (impl) {
+      case 7: launch_v3<256, 256, 2, 4, 32, 4>(a, g3, stream, ab, bb); break;
+      case 8: launch_v3<256, 128, 4, 2, 64, 2>(a, g3, stream, ab, bb); break;
+      case 9: launch_v3<256, 128, 4, 2, 32, 4>(a, g3, stream, ab, bb); break;
+      case 10: launch_v3<256, 128, 4, 2, 32, 3>(a, g3, stream, ab, bb); break;
+      default: launch_v3<256, 256, 2, 4, 64, 2>(a, g3, stream, ab, bb); break;
+    }
+    return (int)hipGetLastError();
+  }
   if (impl >= 2) {
     // split-K for plain f32 (accumulating) products whose tile grid under-fills the chip
     int splits = 1;
