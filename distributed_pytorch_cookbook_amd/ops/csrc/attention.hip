@@ -112,6 +112,10 @@ __device__ __forceinline__ int acc_row(int r, int lane) { return (r & 3) + 8 * (
 // raw v_exp_f32 (2^x): inputs here are <= 0 or -inf, no denormal range reduction needed
 __device__ __forceinline__ float fast_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
 
+// v_max3_f32.  This file is built with -fno-honor-nans (nothing here produces a NaN), so
+// fmaxf on MFMA results needs no canonicalising v_max and pairs fold into v_max3.
+__device__ __forceinline__ float max3f(float a, float b, float c) { return fmaxf(fmaxf(a, b), c); }
+
 // 64-key padding bitmask of the tile starting at key k0 (bit i = key k0+i is padded); wave-uniform
 __device__ __forceinline__ unsigned long long pad_bits(const unsigned char* pad, int k0, int S, int lane) {
   if (!pad) return 0ull;
@@ -183,39 +187,51 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(AttnArgs p) {
 #pragma unroll
         for (int st = 0; st < 4; ++st) s[kb] = MFMA32(row_frag(lk, kb * 32, st, lane), qf[st], s[kb]);
       }
+      // Scores stay raw (unscaled) until the exponent: p = 2^(s*c - m) is one FMA + v_exp.
+      // Interior tiles (the vast majority) skip the mask arithmetic entirely (uniform branch).
       const bool need_mask = (p.causal && kt0 + KT - 1 > q0) || (kt0 + KT > S) || pad;  // wave-uniform
-      float mx = -INFINITY;
-      // branch-free: key > lim is causal / past-the-end, pm is the tile's padding bitmask
-      const unsigned long long pm = need_mask ? pad_bits(pad, kt0, S, lane) : 0ull;
-      const int lim = need_mask ? (p.causal ? min(q, S - 1) : S - 1) - kt0 : KT;
+      if (need_mask) {
+        // key > lim is causal / past-the-end, pm is the tile's padding bitmask
+        const unsigned long long pm = pad_bits(pad, kt0, S, lane);
+        const int lim = (p.causal ? min(q, S - 1) : S - 1) - kt0;
 #pragma unroll
-      for (int kb = 0; kb < 2; ++kb)
+        for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int kl = kb * 32 + acc_row(r, lane);
-          const bool dead = kl > lim || ((pm >> kl) & 1ull);
-          const float v = dead ? -INFINITY : s[kb][r] * c;
-          s[kb][r] = v;
-          mx = fmaxf(mx, v);
-        }
-      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-      const float mn = fmaxf(m, mx);
-      const float mu = (mn == -INFINITY) ? 0.f : mn;
-      const float alpha = fast_exp2(m - mu);
+          for (int r = 0; r < 16; ++r) {
+            const int kl = kb * 32 + acc_row(r, lane);
+            if (kl > lim || ((pm >> kl) & 1ull)) s[kb][r] = -INFINITY;
+          }
+      }
+      float mx = max3f(s[0][0], s[0][1], s[0][2]);
+#pragma unroll
+      for (int r = 3; r < 15; r += 2) mx = max3f(mx, s[0][r], s[0][r + 1]);
+      mx = max3f(mx, s[0][15], s[1][0]);
+#pragma unroll
+      for (int r = 1; r < 15; r += 2) mx = max3f(mx, s[1][r], s[1][r + 1]);
+      mx = fmaxf(mx, s[1][15]);
+      mx = fmaxf(mx, __shfl_xor(mx, 32, 64)) * c;  // scaled log2 units (c > 0)
+      // lazy rescale: the running max only moves when the tile max exceeds it by > 2^8, so
+      // p <= 256 (exact enough in f32 / bf16) and the O rescale is skipped on most tiles
+      if (__ballot(mx > m + 8.f)) {
+        const float mn = fmaxf(m, mx);
+        const float alpha = (mn == -INFINITY) ? 1.f : fast_exp2(m - mn);
+        m = mn;
+        l *= alpha;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) { o[0][i] *= alpha; o[1][i] *= alpha; }
+      }
+      const float nmu = (m == -INFINITY) ? 0.f : -m;
       float ls = 0.f;
 #pragma unroll
       for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-          const float e = fast_exp2(s[kb][r] - mu);
+          const float e = fast_exp2(fmaf(s[kb][r], c, nmu));
           s[kb][r] = e;
           ls += e;
         }
       ls += __shfl_xor(ls, 32, 64);
-      l = l * alpha + ls;
-      m = mn;
-#pragma unroll
-      for (int i = 0; i < 16; ++i) { o[0][i] *= alpha; o[1][i] *= alpha; }
+      l += ls;
 #pragma unroll
       for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
@@ -367,14 +383,24 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_kernel(AttnArgs p) {
           const float4 l4 = *reinterpret_cast<const float4*>(&srow[cur][0][qi0]);
           const float4 d4 = *reinterpret_cast<const float4*>(&srow[cur][1][qi0]);
           const float lv[4] = {l4.x, l4.y, l4.z, l4.w}, dv[4] = {d4.x, d4.y, d4.z, d4.w};
+          // a padded key's P only reaches this lane's own dK / dV column: zeroed at the store
+          if (diag) {
 #pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            const int r = 4 * g + e;
-            float pv = fast_exp2(sa[r] * c - lv[e]);
-            if (diag) pv = (key > qt0 + qi0 + e) ? 0.f : pv;
-            pv = key_ok ? pv : 0.f;
-            sa[r] = pv;
-            dp[r] = pv * (dp[r] - dv[e]);
+            for (int e = 0; e < 4; ++e) {
+              const int r = 4 * g + e;
+              float pv = fast_exp2(fmaf(sa[r], c, -lv[e]));
+              pv = (key > qt0 + qi0 + e) ? 0.f : pv;
+              sa[r] = pv;
+              dp[r] = pv * (dp[r] - dv[e]);
+            }
+          } else {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              const int r = 4 * g + e;
+              const float pv = fast_exp2(fmaf(sa[r], c, -lv[e]));
+              sa[r] = pv;
+              dp[r] = pv * (dp[r] - dv[e]);
+            }
           }
         }
 #pragma unroll
@@ -401,13 +427,15 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_kernel(AttnArgs p) {
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
         const int d = dt * 32 + 8 * g + 4 * hh;
-        uint2 w;
-        w.x = pack2bf(dkt[dt][4 * g + 0] * p.scale, dkt[dt][4 * g + 1] * p.scale);
-        w.y = pack2bf(dkt[dt][4 * g + 2] * p.scale, dkt[dt][4 * g + 3] * p.scale);
+        uint2 w = make_uint2(0u, 0u), u = make_uint2(0u, 0u);  // padded key: dK = dV = 0
+        if (key_ok) {
+          w.x = pack2bf(dkt[dt][4 * g + 0] * p.scale, dkt[dt][4 * g + 1] * p.scale);
+          w.y = pack2bf(dkt[dt][4 * g + 2] * p.scale, dkt[dt][4 * g + 3] * p.scale);
+          u.x = pack2bf(dvt[dt][4 * g + 0], dvt[dt][4 * g + 1]);
+          u.y = pack2bf(dvt[dt][4 * g + 2], dvt[dt][4 * g + 3]);
+        }
         *reinterpret_cast<uint2*>(dK + d) = w;
-        w.x = pack2bf(dvt[dt][4 * g + 0], dvt[dt][4 * g + 1]);
-        w.y = pack2bf(dvt[dt][4 * g + 2], dvt[dt][4 * g + 3]);
-        *reinterpret_cast<uint2*>(dV + d) = w;
+        *reinterpret_cast<uint2*>(dV + d) = u;
       }
   }
 }
@@ -481,12 +509,17 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(AttnArgs p) {
           sa = MFMA32(row_frag(lk, ks * 32, st, lane), qf[st], sa);
           dp = MFMA32(row_frag(lv, ks * 32, st, lane), df[st], dp);
         }
+        if (need_mask) {
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int kl = ks * 32 + acc_row(r, lane);
-          float pv = fast_exp2(sa[r] * c - lse2);
-          pv = (kl > lim || ((pm >> kl) & 1ull)) ? 0.f : pv;
-          dp[r] = pv * (dp[r] - dl);
+          for (int r = 0; r < 16; ++r) {
+            const int kl = ks * 32 + acc_row(r, lane);
+            float pv = fast_exp2(fmaf(sa[r], c, -lse2));
+            pv = (kl > lim || ((pm >> kl) & 1ull)) ? 0.f : pv;
+            dp[r] = pv * (dp[r] - dl);
+          }
+        } else {
+#pragma unroll
+          for (int r = 0; r < 16; ++r) dp[r] = fast_exp2(fmaf(sa[r], c, -lse2)) * (dp[r] - dl);
         }
 #pragma unroll
         for (int ss = 0; ss < 2; ++ss) {
