@@ -37,6 +37,8 @@ def build_parser(recipe: str = "single") -> argparse.ArgumentParser:
                    help="architecture preset (overrides dim/head_dim/heads/num_layers/sequence_length)")
     p.add_argument("--activation", type=str, default=None, choices=["relu", "gelu"])
     p.add_argument("--dropout", type=float, default=0.0)
+    p.add_argument("--recompute", action="store_true",
+                   help="activation recompute: keep only each layer's input, re-run its forward in backward")
     p.add_argument("--synthetic_data", action="store_true",
                    help="use the synthetic token corpus (default when HF data is unavailable)")
     p.add_argument("--data_path", type=str, default=None,

@@ -91,85 +91,110 @@ class _EmbedFn(torch.autograd.Function):
         return None, None, None, None, None, None
 
 
+def _layer_forward(x, mask, layer, store, N, S, act, training, drops):
+    """Decoder-layer forward on the store's compute weights (no store hooks).
+
+    Returns ``(x3, saved)``; ``saved`` holds what the backward needs when ``training``.
+    """
+    drop_attn, drop_ffn = drops
+    attn, fc = layer.attn, layer.fc
+    H, hd = attn.heads, attn.head_dim
+    w = store.weight
+    T, D = x.shape
+    cdt = store.compute_dtype
+    h1, mu1, rs1 = layernorm_fwd(x, w(layer.norm1.weight), w(layer.norm1.bias), LN_EPS, cdt)
+    qkv = linear_fwd(h1, _qkv_weight(store, attn), out_dtype=cdt)
+    o, lse = attention_fwd(qkv, N, S, H, hd, mask, causal=True)
+    if drop_attn is None:
+        x2 = linear_fwd(o, w(attn.to_out.weight), bias=w(attn.to_out.bias), residual=x,
+                        out_dtype=torch.float32)
+    else:
+        x2 = linear_fwd(o, w(attn.to_out.weight), bias=w(attn.to_out.bias), out_dtype=torch.float32)
+        dropout_residual(x2, x, drop_attn, out=x2)
+    h2, mu2, rs2 = layernorm_fwd(x2, w(layer.norm2.weight), w(layer.norm2.bias), LN_EPS, cdt)
+    F4 = w(fc.up_proj.weight).shape[0]
+    z1 = torch.empty(T, F4, device=x.device, dtype=cdt) if (training and act == ACT_GELU) else None
+    uact = linear_fwd(h2, w(fc.up_proj.weight), bias=w(fc.up_proj.bias), act=act, aux_out=z1,
+                      out_dtype=cdt)
+    z2 = torch.empty(T, D, device=x.device, dtype=cdt) if training else None
+    if drop_ffn is None:
+        x3 = linear_fwd(uact, w(fc.down_proj.weight), bias=w(fc.down_proj.bias), act=act,
+                        residual=x2, aux_out=z2, out_dtype=torch.float32)
+    else:
+        x3 = linear_fwd(uact, w(fc.down_proj.weight), bias=w(fc.down_proj.bias), act=act,
+                        aux_out=z2, out_dtype=torch.float32)
+        dropout_residual(x3, x2, drop_ffn, out=x3)
+    saved = None
+    if training:
+        saved = (h1, mu1, rs1, qkv, o, lse, x2, h2, mu2, rs2, z1 if z1 is not None else uact, uact, z2)
+    return x3, saved
+
+
 class _LayerFn(torch.autograd.Function):
+    """One decoder layer.  With ``recompute`` only the layer input is kept and the forward
+    is re-run at the start of the backward (activation recompute: the saved activations of
+    a layer drop from ~34 D bytes per token -- h1, qkv, o, x2, h2, u, z1, z2 -- to the 4 D
+    bytes of its f32 input, for one extra forward)."""
+
     @staticmethod
-    def forward(ctx, x, mask, layer, store, N, S, act, training, drops=(None, None)):
+    def forward(ctx, x, mask, layer, store, N, S, act, training, drops=(None, None), recompute=False):
         u = layer._unit_id
-        drop_attn, drop_ffn = drops
         store.pre_forward(u)
-        attn, fc = layer.attn, layer.fc
-        H, hd = attn.heads, attn.head_dim
-        w = store.weight
-        T, D = x.shape
-        cdt = store.compute_dtype
-        h1, mu1, rs1 = layernorm_fwd(x, w(layer.norm1.weight), w(layer.norm1.bias), LN_EPS, cdt)
-        qkv = linear_fwd(h1, _qkv_weight(store, attn), out_dtype=cdt)
-        o, lse = attention_fwd(qkv, N, S, H, hd, mask, causal=True)
-        if drop_attn is None:
-            x2 = linear_fwd(o, w(attn.to_out.weight), bias=w(attn.to_out.bias), residual=x,
-                            out_dtype=torch.float32)
-        else:
-            x2 = linear_fwd(o, w(attn.to_out.weight), bias=w(attn.to_out.bias), out_dtype=torch.float32)
-            dropout_residual(x2, x, drop_attn, out=x2)
-        h2, mu2, rs2 = layernorm_fwd(x2, w(layer.norm2.weight), w(layer.norm2.bias), LN_EPS, cdt)
-        F4 = w(fc.up_proj.weight).shape[0]
-        z1 = torch.empty(T, F4, device=x.device, dtype=cdt) if (training and act == ACT_GELU) else None
-        uact = linear_fwd(h2, w(fc.up_proj.weight), bias=w(fc.up_proj.bias), act=act, aux_out=z1,
-                          out_dtype=cdt)
-        z2 = torch.empty(T, D, device=x.device, dtype=cdt) if training else None
-        if drop_ffn is None:
-            x3 = linear_fwd(uact, w(fc.down_proj.weight), bias=w(fc.down_proj.bias), act=act,
-                            residual=x2, aux_out=z2, out_dtype=torch.float32)
-        else:
-            x3 = linear_fwd(uact, w(fc.down_proj.weight), bias=w(fc.down_proj.bias), act=act,
-                            aux_out=z2, out_dtype=torch.float32)
-            dropout_residual(x3, x2, drop_ffn, out=x3)
+        x3, saved = _layer_forward(x, mask, layer, store, N, S, act, training and not recompute, drops)
         store.post_forward(u, training)
         if training:
-            ctx.save_for_backward(x, h1, mu1, rs1, qkv, o, lse, x2, h2, mu2, rs2,
-                                  z1 if z1 is not None else uact, uact, z2, mask)
-            ctx.layer, ctx.store, ctx.dims, ctx.act = layer, store, (N, S, H, hd), act
-            ctx.drops = drops
+            ctx.save_for_backward(x, mask, *(saved or ()))
+            ctx.layer, ctx.store, ctx.dims, ctx.act = layer, store, (N, S), act
+            ctx.drops, ctx.recompute = drops, recompute
         return x3
 
     @staticmethod
     def backward(ctx, dx3):
-        (x, h1, mu1, rs1, qkv, o, lse, x2, h2, mu2, rs2, zup, uact, z2, mask) = ctx.saved_tensors
+        x, mask, *saved = ctx.saved_tensors
         layer, store, act = ctx.layer, ctx.store, ctx.act
-        N, S, H, hd = ctx.dims
-        u = layer._unit_id
-        store.pre_backward(u)
-        attn, fc = layer.attn, layer.fc
-        w, g = store.weight, store.grad
-        cdt = store.compute_dtype
-        dx = dx3.contiguous()  # becomes dx2 then dx (in place)
-        # FFN down projection: x3 = x2 + act(z2), z2 = u W2^T + b2
-        drop_attn, drop_ffn = ctx.drops
-        dz2 = bias_act_bwd(dx, z2, act, g(fc.down_proj.bias), out_dtype=cdt, drop=drop_ffn)
-        linear_wgrad(dz2, uact, out=g(fc.down_proj.weight))
-        # up projection gradient with act' fused (relu' from its output, gelu' from z1)
-        dz1 = linear_dgrad(dz2, w(fc.down_proj.weight), act_bwd=act, aux_in=zup, out_dtype=cdt,
-                           colsum=g(fc.up_proj.bias))
-        linear_wgrad(dz1, h2, out=g(fc.up_proj.weight))
-        dh2 = linear_dgrad(dz1, w(fc.up_proj.weight), out_dtype=torch.float32)
-        layernorm_bwd(dh2, x2, mu2, rs2, w(layer.norm2.weight), dx, g(layer.norm2.weight),
-                      g(layer.norm2.bias))
-        # attention output projection: x2 = x + o Wo^T + bo
-        dyo = bias_act_bwd(dx, None, 0, g(attn.to_out.bias), out_dtype=cdt, drop=drop_attn)
-        linear_wgrad(dyo, o, out=g(attn.to_out.weight))
-        do = linear_dgrad(dyo, w(attn.to_out.weight), out_dtype=cdt)
-        dqkv = attention_bwd(do, qkv, o, lse, N, S, H, hd, mask, causal=True)
-        gqkv, split = _qkv_grad(store, attn)
-        linear_wgrad(dqkv, h1, out=gqkv)
-        if split is not None:
-            n = split[0].shape[0]
-            for i, gi in enumerate(split):
-                gi.add_(gqkv[i * n:(i + 1) * n])
-        dh1 = linear_dgrad(dqkv, _qkv_weight(store, attn), out_dtype=torch.float32)
-        layernorm_bwd(dh1, x, mu1, rs1, w(layer.norm1.weight), dx, g(layer.norm1.weight),
-                      g(layer.norm1.bias))
-        store.post_backward(u)
-        return dx, None, None, None, None, None, None, None, None
+        N, S = ctx.dims
+        H, hd = layer.attn.heads, layer.attn.head_dim
+        store.pre_backward(layer._unit_id)
+        if ctx.recompute:
+            _, saved = _layer_forward(x, mask, layer, store, N, S, act, True, ctx.drops)
+        dx = _layer_backward(dx3, x, mask, saved, layer, store, N, S, H, hd, act, ctx.drops)
+        store.post_backward(layer._unit_id)
+        return dx, None, None, None, None, None, None, None, None, None
+
+
+def _layer_backward(dx3, x, mask, saved, layer, store, N, S, H, hd, act, drops):
+    """Hand-written backward of ``_layer_forward``; weight grads go into the store."""
+    (h1, mu1, rs1, qkv, o, lse, x2, h2, mu2, rs2, zup, uact, z2) = saved
+    attn, fc = layer.attn, layer.fc
+    w, g = store.weight, store.grad
+    cdt = store.compute_dtype
+    drop_attn, drop_ffn = drops
+    dx = dx3.contiguous()  # becomes dx2 then dx (in place)
+    # FFN down projection: x3 = x2 + drop(act(z2)), z2 = u W2^T + b2
+    dz2 = bias_act_bwd(dx, z2, act, g(fc.down_proj.bias), out_dtype=cdt, drop=drop_ffn)
+    linear_wgrad(dz2, uact, out=g(fc.down_proj.weight))
+    # up projection gradient with act' fused (relu' from its output, gelu' from z1)
+    dz1 = linear_dgrad(dz2, w(fc.down_proj.weight), act_bwd=act, aux_in=zup, out_dtype=cdt,
+                       colsum=g(fc.up_proj.bias))
+    linear_wgrad(dz1, h2, out=g(fc.up_proj.weight))
+    dh2 = linear_dgrad(dz1, w(fc.up_proj.weight), out_dtype=torch.float32)
+    layernorm_bwd(dh2, x2, mu2, rs2, w(layer.norm2.weight), dx, g(layer.norm2.weight),
+                  g(layer.norm2.bias))
+    # attention output projection: x2 = x + drop(o Wo^T + bo)
+    dyo = bias_act_bwd(dx, None, 0, g(attn.to_out.bias), out_dtype=cdt, drop=drop_attn)
+    linear_wgrad(dyo, o, out=g(attn.to_out.weight))
+    do = linear_dgrad(dyo, w(attn.to_out.weight), out_dtype=cdt)
+    dqkv = attention_bwd(do, qkv, o, lse, N, S, H, hd, mask, causal=True)
+    gqkv, split = _qkv_grad(store, attn)
+    linear_wgrad(dqkv, h1, out=gqkv)
+    if split is not None:
+        n = split[0].shape[0]
+        for i, gi in enumerate(split):
+            gi.add_(gqkv[i * n:(i + 1) * n])
+    dh1 = linear_dgrad(dqkv, _qkv_weight(store, attn), out_dtype=torch.float32)
+    layernorm_bwd(dh1, x, mu1, rs1, w(layer.norm1.weight), dx, g(layer.norm1.weight),
+                  g(layer.norm1.bias))
+    return dx
 
 
 class _HeadFn(torch.autograd.Function):
@@ -253,9 +278,10 @@ def run_layers(model, store, x, mask, N, S, layers, training, dropout_seed=None)
     use_drop = model.training and model.dropout > 0
     if use_drop and dropout_seed is None:
         dropout_seed = model.next_dropout_seed()
+    recompute = bool(getattr(model, "recompute", False)) and training
     for layer in layers:
         drops = model.dropout_specs(layer, dropout_seed) if use_drop else (None, None)
-        x = _LayerFn.apply(x, mask, layer, store, N, S, act, training, drops)
+        x = _LayerFn.apply(x, mask, layer, store, N, S, act, training, drops, recompute)
     return x
 
 

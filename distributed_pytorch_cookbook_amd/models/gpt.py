@@ -195,6 +195,7 @@ class TransformerDecoderLM(nn.Module):
         # dropout: per-forward seeds = (dropout_seed_base << 32) | call counter
         self.dropout_seed_base = 0
         self._dropout_calls = 0
+        self.recompute = False  # per-layer activation recompute in the backward
         for i, layer in enumerate(self.decoder.layers):
             layer._layer_index = i
 

@@ -720,9 +720,229 @@ __global__ __launch_bounds__((V3Cfg<BM_, BN_, WM, WN, KB, STAGES>::NTH), 1) void
   }
 }
 
+// =====================================================================================
+// v4: 256x256 tile, 8 waves (2 x 4, 128x64 per wave), a ring of four 32-deep k-slices
+// (32 KiB each, 128 KiB) filled by LDS-DMA, with fragment reads software-pipelined across
+// the one barrier per slice.  Per slice and wave: 12 ds_read_b128 feed 32 MFMAs, split as
+//   A_hi(s) reads | 8 MFMA (s, rows 0-31) | vmcnt + barrier + DMA(s+3) + B(s+1) reads |
+//   8 MFMA (s, rows 32-63) | A_lo(s+1) reads | 16 MFMA (s, rows 64-127)
+// so every read has >= 8 MFMAs (128 cycles/wave, 256 per SIMD) in front of its first use,
+// and the DMA of slice s+3 (issued at barrier s+1) has two slices of MFMA work to land.
+// WAR: slot (s+3)%4 last held slice s-1, whose reads all retired before the MFMAs of
+// slice s-1's second half -- i.e. before every wave reached barrier s+1.
+// RAW: slice s+1 is read only after barrier s+1, which each wave enters after waiting for
+// its own DMAs of slice s+1 (counted vmcnt: slice s+2's 4 loads may stay in flight).
+template <bool AK>
+__device__ __forceinline__ void v4_read_a(bf16x8 (&a)[4], const bf16_t* la, int r0, int lane) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) a[i] = frag3<32, AK>(la, r0 + i * 16, 0, lane);
+}
+template <bool BK>
+__device__ __forceinline__ void v4_read_b(bf16x8 (&b)[4], const bf16_t* lb, int c0, int lane) {
+#pragma unroll
+  for (int j = 0; j < 4; ++j) b[j] = frag3<32, BK>(lb, c0 + j * 16, 0, lane);
+}
+__device__ __forceinline__ void v4_mma(floatx4 (&acc)[8][4], const bf16x8 (&a)[4], const bf16x8 (&b)[4],
+                                       int i0, int i1) {
+#pragma unroll
+  for (int i = i0; i < i1; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i & 3], b[j], acc[i][j], 0, 0, 0);
+}
+
+template <bool AK, bool BK>
+__global__ __launch_bounds__(512, 1) void gemm4_kernel(GemmArgs p, unsigned long long a_bytes,
+                                                       unsigned long long b_bytes) {
+  using Cfg = V3Cfg<256, 256, 2, 4, 32, 4>;
+  constexpr int NS = 4, SLOT = Cfg::TA + Cfg::TB;
+  __shared__ __attribute__((aligned(16))) bf16_t smem[Cfg::SMEM];
+  const int tiles_m = (p.M + 255) / 256, tiles_n = (p.N + 255) / 256;
+  const int nwg = tiles_m * tiles_n;
+  int bid = blockIdx.x;
+  {
+    const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
+    bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+  }
+  const int group = GROUP_M * tiles_n;
+  const int gid = bid / group, first_m = gid * GROUP_M;
+  const int gsz = min(tiles_m - first_m, GROUP_M);
+  const int tm = first_m + (bid % group) % gsz;
+  const int tn = (bid % group) / gsz;
+  const int m0 = tm * 256, n0 = tn * 256;
+
+  const int lane = threadIdx.x & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wr = wid >> 2, wc = wid & 3;
+  const int ar = wr * 128, bc = wc * 64;
+
+  int va[Cfg::NLA], vb[Cfg::NLB];  // 2 + 2 DMA instructions per wave per slice
+  dma_offsets3<32, AK, Cfg::NLA>(va, p.lda, wid, lane);
+  dma_offsets3<32, BK, Cfg::NLB>(vb, p.ldb, wid, lane);
+  const unsigned long long a_org = AK ? (unsigned long long)m0 * p.lda * 2 : (unsigned long long)m0 * 2;
+  const unsigned long long b_org = BK ? (unsigned long long)n0 * p.ldb * 2 : (unsigned long long)n0 * 2;
+  const unsigned long long a_step = AK ? 64ull : 32ull * p.lda * 2;
+  const unsigned long long b_step = BK ? 64ull : 32ull * p.ldb * 2;
+  floatx4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+
+  const int nk_all = (p.K + 31) / 32;
+  const int splits = gridDim.y;
+  const int per = (nk_all + splits - 1) / splits;
+  const int kt0 = blockIdx.y * per;
+  const int nk = max(0, min(nk_all, kt0 + per) - kt0);
+#define DPC_ISSUE4(s_)                                                                              \
+  do {                                                                                              \
+    bf16_t* base_ = smem + ((s_) % NS) * SLOT;                                                      \
+    const unsigned long long kg_ = (unsigned long long)(kt0 + (s_));                                \
+    issue_tile<Cfg::NLA>(p.A, a_bytes, a_org + a_step * kg_, va, base_, wid);                       \
+    issue_tile<Cfg::NLB>(p.B, b_bytes, b_org + b_step * kg_, vb, base_ + Cfg::TA, wid);             \
+  } while (0)
+
+  bf16x8 alo[4], ahi[4], b0[4], b1[4];
+  if (nk > 0) {
+    DPC_ISSUE4(0);
+    if (nk > 1) DPC_ISSUE4(1);
+    if (nk > 2) DPC_ISSUE4(2);
+    if (nk > 2) wait_vm<2 * (Cfg::NLA + Cfg::NLB)>();
+    else if (nk > 1) wait_vm<Cfg::NLA + Cfg::NLB>();
+    else wait_vm<0>();
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    v4_read_b<BK>(b0, smem + Cfg::TA, bc, lane);
+    v4_read_a<AK>(alo, smem, ar, lane);
+  }
+  // one k-slice; bc_/bn_ = current / next B fragments (alternating register sets)
+#define DPC_SLICE4(s_, bcur_, bnext_)                                                               \
+  do {                                                                                              \
+    const bf16_t* la_ = smem + ((s_) % NS) * SLOT;                                                  \
+    v4_read_a<AK>(ahi, la_, ar + 64, lane);                                                         \
+    v4_mma(acc, alo, bcur_, 0, 2);                                                                  \
+    const bool more_ = (s_) + 1 < nk;                                                               \
+    if (more_) {                                                                                    \
+      if ((s_) + 2 < nk) wait_vm<Cfg::NLA + Cfg::NLB>();                                            \
+      else wait_vm<0>();                                                                            \
+      __builtin_amdgcn_s_barrier();                                                                 \
+      asm volatile("" ::: "memory");                                                                \
+      if ((s_) + 3 < nk) DPC_ISSUE4((s_) + 3);                                                      \
+      v4_read_b<BK>(bnext_, smem + (((s_) + 1) % NS) * SLOT + Cfg::TA, bc, lane);                   \
+    }                                                                                               \
+    v4_mma(acc, alo, bcur_, 2, 4);                                                                  \
+    if (more_) v4_read_a<AK>(alo, smem + (((s_) + 1) % NS) * SLOT, ar, lane);                       \
+    v4_mma(acc, ahi, bcur_, 4, 8);                                                                  \
+  } while (0)
+  int s = 0;
+  for (; s + 1 < nk; s += 2) {
+    DPC_SLICE4(s, b0, b1);
+    DPC_SLICE4(s + 1, b1, b0);
+  }
+  if (s < nk) DPC_SLICE4(s, b0, b1);
+#undef DPC_SLICE4
+#undef DPC_ISSUE4
+
+  // ---------------- epilogue: four passes of 32 rows per wave through LDS (as v3)
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  float alpha = p.alpha;
+  if (p.alpha_ptr) alpha *= *p.alpha_ptr;
+  float* ct = reinterpret_cast<float*>(smem) + wid * 32 * 64;
+  const int c4 = lane & 15;
+  const int n = n0 + bc + c4 * 4;
+  const bool nok = n < p.N;
+  float4 bias4 = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (p.bias && nok) bias4 = *reinterpret_cast<const float4*>(p.bias + n);
+  float cs[4] = {0.f, 0.f, 0.f, 0.f};
+  const bf16_t* aux_in = static_cast<const bf16_t*>(p.aux_in);
+  bf16_t* aux_out = static_cast<bf16_t*>(p.aux_out);
+#pragma unroll
+  for (int h = 0; h < 4; ++h) {
+    __syncthreads();
+#pragma unroll
+    for (int ii = 0; ii < 2; ++ii)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int row = ii * 16 + (lane >> 4) * 4 + r;
+          const int col = (j * 16 + (lane & 15)) ^ (((row >> 2) & 3) << 4);
+          ct[row * 64 + col] = acc[2 * h + ii][j][r] * alpha;
+        }
+    __syncthreads();
+#pragma unroll 2
+    for (int t = 0; t < 8; ++t) {
+      const int row = (lane >> 4) + 4 * t;
+      const int m = m0 + ar + h * 32 + row;
+      const int col = (c4 * 4) ^ (((row >> 2) & 3) << 4);
+      float4 v4 = *reinterpret_cast<const float4*>(ct + row * 64 + col);
+      if (m >= p.M || !nok) continue;
+      float v[4] = {v4.x + bias4.x, v4.y + bias4.y, v4.z + bias4.z, v4.w + bias4.w};
+      if (p.act_bwd) {
+        const uint2 z = *reinterpret_cast<const uint2*>(aux_in + (long long)m * p.ld_aux_in + n);
+        v[0] *= act_grad(__uint_as_float(z.x << 16), p.act_bwd);
+        v[1] *= act_grad(__uint_as_float(z.x & 0xffff0000u), p.act_bwd);
+        v[2] *= act_grad(__uint_as_float(z.y << 16), p.act_bwd);
+        v[3] *= act_grad(__uint_as_float(z.y & 0xffff0000u), p.act_bwd);
+      }
+#pragma unroll
+      for (int e = 0; e < 4; ++e) cs[e] += v[e];
+      if (aux_out) {
+        uint2 w;
+        w.x = pack2bf(v[0], v[1]);
+        w.y = pack2bf(v[2], v[3]);
+        *reinterpret_cast<uint2*>(aux_out + (long long)m * p.ld_aux_out + n) = w;
+      }
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[e] = act_fwd(v[e], p.act);
+      if (p.residual) {
+        const float4 r4 = *reinterpret_cast<const float4*>(p.residual + (long long)m * p.ldr + n);
+        v[0] += r4.x; v[1] += r4.y; v[2] += r4.z; v[3] += r4.w;
+      }
+      const long long ci = (long long)m * p.ldc + n;
+      if (splits > 1) {
+        float* C = static_cast<float*>(p.C) + ci;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) atomicAdd(C + e, v[e]);
+      } else if (p.out_f32) {
+        float4* C = reinterpret_cast<float4*>(static_cast<float*>(p.C) + ci);
+        if (p.accumulate) {
+          const float4 o = *C;
+          v[0] += o.x; v[1] += o.y; v[2] += o.z; v[3] += o.w;
+        }
+        *C = make_float4(v[0], v[1], v[2], v[3]);
+      } else {
+        uint2 w;
+        w.x = pack2bf(v[0], v[1]);
+        w.y = pack2bf(v[2], v[3]);
+        *reinterpret_cast<uint2*>(static_cast<bf16_t*>(p.C) + ci) = w;
+      }
+    }
+  }
+  if (p.colsum) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      cs[e] += __shfl_xor(cs[e], 16, 64);
+      cs[e] += __shfl_xor(cs[e], 32, 64);
+    }
+    if ((lane >> 4) == 0 && nok) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) atomicAdd(p.colsum + n + e, cs[e]);
+    }
+  }
+}
+
 }  // namespace dpc
 
 using namespace dpc;
+
+static void launch_v4(const GemmArgs* a, dim3 grid, hipStream_t stream, unsigned long long ab,
+                      unsigned long long bb) {
+  if (a->a_kmaj && a->b_kmaj) hipLaunchKernelGGL((gemm4_kernel<true, true>), grid, dim3(512), 0, stream, *a, ab, bb);
+  else if (a->a_kmaj) hipLaunchKernelGGL((gemm4_kernel<true, false>), grid, dim3(512), 0, stream, *a, ab, bb);
+  else if (!a->b_kmaj) hipLaunchKernelGGL((gemm4_kernel<false, false>), grid, dim3(512), 0, stream, *a, ab, bb);
+  else hipLaunchKernelGGL((gemm4_kernel<false, true>), grid, dim3(512), 0, stream, *a, ab, bb);
+}
 
 template <int BM_, int BN_, int WM, int WN, int KB, int STAGES>
 static void launch_v3(const GemmArgs* a, dim3 grid, hipStream_t stream, unsigned long long ab,
@@ -792,6 +1012,7 @@ DPC_API int dpc_gemm(const GemmArgs* a, hipStream_t stream) {
       hipMemset2DAsync(a->C, (size_t)a->ldc * 4, 0, (size_t)a->N * 4, (size_t)a->M, stream);
     dim3 g3(t3, splits);
     switch (impl) {
+      case 11: launch_v4(a, g3, stream, ab, bb); break;
       case 7: launch_v3<256, 256, 2, 4, 32, 4>(a, g3, stream, ab, bb); break;
       case 8: launch_v3<256, 128, 4, 2, 64, 2>(a, g3, stream, ab, bb); break;
       case 9: launch_v3<256, 128, 4, 2, 32, 4>(a, g3, stream, ab, bb); break;

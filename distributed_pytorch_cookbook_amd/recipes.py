@@ -30,6 +30,7 @@ def build_model(args, vocab_size: int, device) -> TransformerDecoderLM:
             vocab_size=vocab_size, max_position_embeddings=args.sequence_length,
             dropout=args.dropout, activation=args.activation,
         )
+    model.recompute = bool(getattr(args, "recompute", False))
     return model
 
 

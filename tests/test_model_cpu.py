@@ -168,3 +168,22 @@ def test_dropout_mask_statistics():
     both = ((k == 0) & (k2 == 0)).float().mean().item()
     assert abs(both - 0.0625) < 0.01
     assert DropSpec.make(0.0, 1, 1) is None
+
+
+def test_activation_recompute_matches():
+    """--recompute: identical loss and gradients (dropout masks regenerated from the seed)."""
+    torch.manual_seed(0)
+    base = TransformerDecoderLM(dim=64, head_dim=16, heads=4, num_layers=2, vocab_size=97,
+                                max_position_embeddings=24, activation="gelu", dropout=0.1)
+    ids, pos, mask, tg = batch(pad=True)
+    grads = []
+    for rc in (False, True):
+        m = copy.deepcopy(base)
+        m.recompute = rc
+        st = LocalStore(m, "cpu")
+        st.zero_grad()
+        out = m(ids, pos, mask, targets=tg, dropout_seed=77)
+        out.loss.backward()
+        grads.append((out.loss.item(), st.grads.clone()))
+    assert grads[0][0] == grads[1][0]
+    assert torch.allclose(grads[0][1], grads[1][1], atol=1e-7, rtol=1e-5)
