@@ -996,7 +996,20 @@ DPC_API int dpc_gemm(const GemmArgs* a, hipStream_t stream) {
                      al(a->C, a->out_f32 ? 16 : 8) && al(a->bias, 16) && al(a->residual, 16) &&
                      al(a->aux_in, 8) && al(a->aux_out, 8) && al(a->colsum, 4);
   int impl = g_gemm_impl;
-  if (impl < 0) impl = v2_ok ? 2 : 1;
+  if (impl < 0) {
+    // Default per operand layout and depth, from the GPT-2 shape sweep on MI355X
+    // (bench/kernels.py, profiles/kernels_r1_*.json): forward products with a short K
+    // (<= 1024) are epilogue/prologue heavy and run best as 256x128 tiles two workgroups
+    // per CU (impl 10); deep or mn-major products keep the 128x128 2-stage kernel (impl 2),
+    // except dgrad at K <= 2304 and mid-size wgrad, where the 3-stage 32-deep ring wins.
+    impl = 1;
+    if (v2_ok) {
+      impl = 2;
+      if (a->a_kmaj && a->b_kmaj && a->K <= 1024) impl = 10;
+      else if (a->a_kmaj && !a->b_kmaj && a->K <= 2304) impl = 4;
+      else if (!a->a_kmaj && !a->b_kmaj && a->M > 2304 && a->M <= 4096) impl = 4;
+    }
+  }
   if (impl >= 2 && !v2_ok) impl = 1;
   if (impl >= 6) {
     const int bm = 256, bn = (impl == 8 || impl == 9 || impl == 10) ? 128 : 256;
