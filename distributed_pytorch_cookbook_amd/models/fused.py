@@ -178,10 +178,11 @@ def _layer_backward(dx3, x, mask, saved, layer, store, N, S, H, hd, act, drops):
                        colsum=g(fc.up_proj.bias))
     linear_wgrad(dz1, h2, out=g(fc.up_proj.weight))
     dh2 = linear_dgrad(dz1, w(fc.up_proj.weight), out_dtype=torch.float32)
+    # LN2 backward with the attention output projection's bias/dropout backward fused in:
+    # x2 = x + drop(o Wo^T + bo)  ->  dYo = bf16(dx2 * keep), dbo += colsum
+    dyo = torch.empty(dx.shape, device=dx.device, dtype=cdt)
     layernorm_bwd(dh2, x2, mu2, rs2, w(layer.norm2.weight), dx, g(layer.norm2.weight),
-                  g(layer.norm2.bias))
-    # attention output projection: x2 = x + drop(o Wo^T + bo)
-    dyo = bias_act_bwd(dx, None, 0, g(attn.to_out.bias), out_dtype=cdt, drop=drop_attn)
+                  g(layer.norm2.bias), gout=dyo, gsum=g(attn.to_out.bias), drop=drop_attn)
     linear_wgrad(dyo, o, out=g(attn.to_out.weight))
     do = linear_dgrad(dyo, w(attn.to_out.weight), out_dtype=cdt)
     dqkv = attention_bwd(do, qkv, o, lse, N, S, H, hd, mask, causal=True)

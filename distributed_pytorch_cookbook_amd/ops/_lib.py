@@ -54,6 +54,8 @@ class LNArgs(ctypes.Structure):
         ("T", c_int), ("D", c_int),
         ("eps", c_float),
         ("y_f32", c_int),
+        ("gout", P), ("gsum", P), ("ld_gout", LL),
+        ("drop_key", c_uint), ("drop_thresh", c_uint), ("drop_scale", c_float),
     ]
 
 

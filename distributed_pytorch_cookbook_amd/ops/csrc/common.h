@@ -125,4 +125,19 @@ __device__ __forceinline__ float act_grad(float z, int act) {
   return 1.f;
 }
 
+// ---- counter-based dropout keep mask (torch twin: ops/dropout.py:keep_mask).  Element idx
+// of a site is kept iff fmix32(idx * 0x9E3779B1 ^ key) >= thresh; kept values are scaled.
+__device__ __forceinline__ uint32_t fmix32(uint32_t x) {
+  x ^= x >> 16;
+  x *= 0x85ebca6bu;
+  x ^= x >> 13;
+  x *= 0xc2b2ae35u;
+  x ^= x >> 16;
+  return x;
+}
+
+__device__ __forceinline__ float drop_factor(uint32_t idx, uint32_t key, uint32_t thresh, float scale) {
+  return fmix32((idx * 0x9E3779B1u) ^ key) >= thresh ? scale : 0.f;
+}
+
 }  // namespace dpc

@@ -28,6 +28,15 @@ struct LNArgs {
   int T, D;
   float eps;
   int y_f32;
+  // bwd, optional fused consumer of the new dx (the bias / dropout backward of the
+  // projection that produced the LayerNorm's input):  g = dx * keep  ->  gout (bf16),
+  // gsum += column sums of g.  keep = dropout factor of element (row, col) of a [T, D]
+  // site (misc.hip:drop_factor), 1 when drop_scale == 0.
+  void* gout;
+  float* gsum;
+  long long ld_gout;
+  unsigned drop_key, drop_thresh;
+  float drop_scale;
 };
 
 template <int NV>
@@ -90,13 +99,14 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(LNArgs p) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int nv4 = p.D >> 2;
   const float4* g4 = reinterpret_cast<const float4*>(p.gamma);
-  float4 gacc[NV], bacc[NV], gam[NV];
+  float4 gacc[NV], bacc[NV], gam[NV], cacc[NV];
 #pragma unroll
   for (int i = 0; i < NV; ++i) {
     const int c = lane + i * 64;
-    gacc[i] = bacc[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+    gacc[i] = bacc[i] = cacc[i] = make_float4(0.f, 0.f, 0.f, 0.f);
     gam[i] = c < nv4 ? g4[c] : make_float4(0.f, 0.f, 0.f, 0.f);
   }
+  bf16_t* gout = static_cast<bf16_t*>(p.gout);
   for (long long row = (long long)blockIdx.x * 4 + w; row < p.T; row += (long long)gridDim.x * 4) {
     const float4* xr = reinterpret_cast<const float4*>(p.x + row * p.ldx);
     const float4* dyr = reinterpret_cast<const float4*>(p.dy + row * p.lddy);
@@ -132,6 +142,20 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(LNArgs p) {
         o.z += rs * (dg[i].z - s1 - xh[i].z * s2);
         o.w += rs * (dg[i].w - s1 - xh[i].w * s2);
         dxr[c] = o;
+        if (gout) {
+          if (p.drop_scale != 0.f) {
+            const uint32_t idx = (uint32_t)(row * p.D + 4 * c);
+            o.x *= drop_factor(idx + 0, p.drop_key, p.drop_thresh, p.drop_scale);
+            o.y *= drop_factor(idx + 1, p.drop_key, p.drop_thresh, p.drop_scale);
+            o.z *= drop_factor(idx + 2, p.drop_key, p.drop_thresh, p.drop_scale);
+            o.w *= drop_factor(idx + 3, p.drop_key, p.drop_thresh, p.drop_scale);
+          }
+          uint2 wv;
+          wv.x = pack2bf(o.x, o.y);
+          wv.y = pack2bf(o.z, o.w);
+          *reinterpret_cast<uint2*>(gout + row * p.ld_gout + 4 * c) = wv;
+          cacc[i].x += o.x; cacc[i].y += o.y; cacc[i].z += o.z; cacc[i].w += o.w;
+        }
       }
     }
   }
@@ -149,6 +173,16 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(LNArgs p) {
     atomicAdd(p.dgamma + c, g);
     atomicAdd(p.dbeta + c, b);
   }
+  if (!gout || !p.gsum) return;
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    const int c = lane + i * 64;
+    if (c < nv4) reinterpret_cast<float4*>(&red[w][0][0])[c] = cacc[i];
+  }
+  __syncthreads();
+  for (int c = threadIdx.x; c < p.D; c += 256)
+    atomicAdd(p.gsum + c, red[0][0][c] + red[1][0][c] + red[2][0][c] + red[3][0][c]);
 }
 
 }  // namespace dpc

@@ -234,22 +234,9 @@ __global__ __launch_bounds__(256) void cast_kernel(CastArgs a) {
 }
 
 // ------------------------------------------------------------------ dropout
-// Counter-based keep mask: element (t, c) of a [T, N] site is kept iff
-// fmix32((t*N + c) * 0x9E3779B1 ^ key) >= thresh.  The map idx -> hash is a bijection for
-// a fixed key, so nothing is stored between forward and backward: both regenerate it.
-// The torch twin is ops/dropout.py:keep_mask (bit-identical, used on CPU and in tests).
-__device__ __forceinline__ uint32_t fmix32(uint32_t x) {
-  x ^= x >> 16;
-  x *= 0x85ebca6bu;
-  x ^= x >> 13;
-  x *= 0xc2b2ae35u;
-  x ^= x >> 16;
-  return x;
-}
-
-__device__ __forceinline__ float drop_factor(uint32_t idx, uint32_t key, uint32_t thresh, float scale) {
-  return fmix32((idx * 0x9E3779B1u) ^ key) >= thresh ? scale : 0.f;
-}
+// Counter-based keep mask (common.h:drop_factor): element (t, c) of a [T, N] site has index
+// t*N + c.  The map idx -> hash is a bijection for a fixed key, so nothing is stored between
+// forward and backward: both regenerate it.  The torch twin is ops/dropout.py:keep_mask.
 
 // out[t, c] = res[t, c] + y[t, c] * keep(t, c) / (1 - p)   (f32; out may alias y or res)
 struct DropResArgs {

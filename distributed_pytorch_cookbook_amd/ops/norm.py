@@ -10,6 +10,7 @@ from __future__ import annotations
 import torch
 
 from . import _lib
+from .dropout import keep_mask
 
 
 def _use_hip(x: torch.Tensor, y_dtype: torch.dtype) -> bool:
@@ -48,10 +49,19 @@ def layernorm_fwd(x: torch.Tensor, gamma: torch.Tensor, beta: torch.Tensor, eps:
 
 
 def layernorm_bwd(dy: torch.Tensor, x: torch.Tensor, mean: torch.Tensor, rstd: torch.Tensor,
-                  gamma: torch.Tensor, dx: torch.Tensor, dgamma: torch.Tensor, dbeta: torch.Tensor):
-    """dx += LN'(dy); dgamma += sum dy*xhat; dbeta += sum dy.  dy, x, dx f32 [T, D]."""
+                  gamma: torch.Tensor, dx: torch.Tensor, dgamma: torch.Tensor, dbeta: torch.Tensor,
+                  gout: torch.Tensor | None = None, gsum: torch.Tensor | None = None,
+                  drop=None):
+    """dx += LN'(dy); dgamma += sum dy*xhat; dbeta += sum dy.  dy, x, dx f32 [T, D].
+
+    Optional fused consumer of the updated dx (the backward of the bias + dropout of the
+    projection whose output fed this LayerNorm's residual): ``gout = dx * keep`` (bf16,
+    the next GEMM's operand) and ``gsum += colsum(dx * keep)`` (that projection's bias
+    gradient), saving a separate pass over the f32 dx.
+    """
     T, D = x.shape
-    if not (x.is_cuda and dy.dtype == torch.float32 and gamma.dtype == torch.float32):
+    if not (x.is_cuda and dy.dtype == torch.float32 and gamma.dtype == torch.float32
+            and (gout is None or gout.dtype == torch.bfloat16)):
         xh = (x.float() - mean[:, None]) * rstd[:, None]
         dyf = dy.float()
         dg = dyf * gamma.float()
@@ -60,6 +70,11 @@ def layernorm_bwd(dy: torch.Tensor, x: torch.Tensor, mean: torch.Tensor, rstd: t
         dx.add_(rstd[:, None] * (dg - s1 - xh * s2))
         dgamma.add_((dyf * xh).sum(0))
         dbeta.add_(dyf.sum(0))
+        if gout is not None:
+            g = dx if drop is None else dx * keep_mask(drop, T, D, dx.device)
+            gout.copy_(g)
+            if gsum is not None:
+                gsum.add_(g.sum(0))
         return dx
     for t, nm in ((dy, "dy"), (x, "x"), (dx, "dx")):
         if t.dtype != torch.float32 or t.stride(1) != 1:
@@ -69,5 +84,13 @@ def layernorm_bwd(dy: torch.Tensor, x: torch.Tensor, mean: torch.Tensor, rstd: t
         dy=dy.data_ptr(), dx=dx.data_ptr(), dgamma=dgamma.data_ptr(), dbeta=dbeta.data_ptr(),
         ldx=x.stride(0), lddy=dy.stride(0), lddx=dx.stride(0), T=T, D=D, eps=0.0,
     )
+    if gout is not None:
+        if gout.dtype != torch.bfloat16 or gout.stride(1) != 1 or gout.stride(0) % 4 or D % 4:
+            raise ValueError("layernorm_bwd: gout must be bf16 with 8-B aligned contiguous rows")
+        args.gout, args.gsum, args.ld_gout = gout.data_ptr(), _lib.ptr(gsum), gout.stride(0)
+        if drop is not None:
+            if T * D >= 2 ** 32:
+                raise ValueError("layernorm_bwd: dropout needs T * D < 2^32")
+            args.drop_key, args.drop_thresh, args.drop_scale = drop.key, drop.thresh, drop.scale
     _lib.call("dpc_layernorm_bwd", args, x.device)
     return dx

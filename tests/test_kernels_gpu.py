@@ -186,6 +186,17 @@ def test_layernorm(D):
     assert rel_err(dx - dres, xx.grad) < 1e-4
     assert rel_err(dg, gg.grad) < 1e-4
     assert rel_err(db, bb.grad) < 1e-4
+    # fused consumer: gout = bf16(dx * keep), gsum += colsum(dx * keep)
+    from distributed_pytorch_cookbook_amd.ops.dropout import DropSpec, keep_mask
+    for drop in (None, DropSpec.make(0.2, seed=3, site=5)):
+        dx2 = dres.clone()
+        gout = torch.empty(T, D, device=dev, dtype=torch.bfloat16)
+        gsum = torch.ones(D, device=dev)
+        layernorm_bwd(dy, x, mean, rstd, g, dx2, torch.zeros(D, device=dev), torch.zeros(D, device=dev),
+                      gout=gout, gsum=gsum, drop=drop)
+        ref = dx2 if drop is None else dx2 * keep_mask(drop, T, D, dev)
+        assert rel_err(gout, ref) < 5e-3
+        assert rel_err(gsum - 1, ref.sum(0)) < 1e-4
 
 
 @pytest.mark.parametrize("tdt", [torch.float32, torch.bfloat16])
