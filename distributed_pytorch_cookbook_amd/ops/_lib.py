@@ -32,6 +32,7 @@ class GemmArgs(ctypes.Structure):
         ("act", c_int), ("act_bwd", c_int), ("out_f32", c_int), ("accumulate", c_int),
         ("a_kmaj", c_int), ("b_kmaj", c_int),
         ("a_r", c_int), ("a_c", c_int), ("b_r", c_int), ("b_c", c_int),
+        ("ksplit", c_int),  # dispatcher-owned (pass 0)
     ]
 
 
@@ -161,7 +162,9 @@ def lib() -> ctypes.CDLL:
 
 
 def set_gemm_impl(impl: int) -> None:
-    """-1 auto (default), 1 register-staged v1, 2 / 3 LDS-DMA v2 with 2 / 3 stages."""
+    """Force a GEMM implementation (tests / sweeps): -1 auto (default), 1 register-staged v1,
+    2-5 LDS-DMA 128x128 v2 variants, 6-10 large-tile v3 variants, 11 pipelined 256x256 v4
+    (table at the dispatcher, ``csrc/gemm.hip``)."""
     lib().dpc_gemm_set_impl(int(impl))
 
 

@@ -46,7 +46,36 @@ struct GemmArgs {
   // stored extents of the operands ([rows][cols] as laid out in memory); reads beyond them
   // return zeros.  k-major: rows = M or N, cols = K;  mn-major: rows = K, cols = M or N.
   int a_r, a_c, b_r, b_c;
+  // set by the dispatcher (callers pass 0): > 1 = XCD-aligned split-K into this many k-ranges
+  int ksplit;
 };
+
+// Which output tile and k-range a workgroup computes.
+//  * default: an XCD-aware bijective remap (blocks b, b+8, ... share an XCD: each XCD gets a
+//    contiguous run of tile ids, walked in GROUP_M supertiles for L2 reuse); split-K, if
+//    any, on blockIdx.y.
+//  * ksplit > 1 (small outputs with a long K, i.e. weight gradients): block L runs on XCD
+//    L % 8, so split = L % ksplit pins every k-range to its own XCD(s) -- an XCD streams only
+//    its 1/ksplit of both operands, once, shared in its L2 by all the tiles it computes.
+//    (With the default mapping the same shapes hit L2 only ~53 % of the time: PMC
+//    TCC_HIT/MISS on the 3072x768x32736 weight gradient, profiles/r1_pmc_*.)
+struct TileSlot {
+  int bid, split, splits;
+};
+__device__ __forceinline__ TileSlot tile_slot(const GemmArgs& p, int nwg) {
+  TileSlot t;
+  if (p.ksplit > 1) {
+    t.splits = p.ksplit;
+    t.split = blockIdx.x % p.ksplit;
+    t.bid = blockIdx.x / p.ksplit;
+  } else {
+    const int b = blockIdx.x, xcd = b & 7, q = nwg >> 3, r = nwg & 7;
+    t.bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (b >> 3);
+    t.splits = gridDim.y;
+    t.split = blockIdx.y;
+  }
+  return t;
+}
 
 constexpr int BM = 128, BN = 128, BKT = 64, NT = 256;
 constexpr int TILE_ELEMS = BM * BKT;  // 8192 bf16 = 16 KiB per operand per stage
@@ -129,13 +158,8 @@ __global__ __launch_bounds__(NT, 2) void gemm_kernel(GemmArgs p) {
   __shared__ __attribute__((aligned(16))) bf16_t smem[4 * TILE_ELEMS];  // [stage][A|B]
   const int tiles_m = (p.M + BM - 1) / BM, tiles_n = (p.N + BN - 1) / BN;
   const int nwg = tiles_m * tiles_n;
-  // XCD-aware bijective remap: blocks b, b+8, ... share an XCD; give each XCD a
-  // contiguous run of logical tile ids.
-  int bid = blockIdx.x;
-  {
-    const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
-    bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
-  }
+  const TileSlot ts = tile_slot(p, nwg);
+  const int bid = ts.bid;
   // grouped ordering for L2 reuse
   const int group = GROUP_M * tiles_n;
   const int gid = bid / group, first_m = gid * GROUP_M;
@@ -335,11 +359,8 @@ __global__ __launch_bounds__(NT, (V2Cfg<KB, STAGES>::WGS)) void gemm2_kernel(Gem
   __shared__ __attribute__((aligned(16))) bf16_t smem[Cfg::SMEM];
   const int tiles_m = (p.M + BM - 1) / BM, tiles_n = (p.N + BN - 1) / BN;
   const int nwg = tiles_m * tiles_n;
-  int bid = blockIdx.x;
-  {
-    const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
-    bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
-  }
+  const TileSlot ts = tile_slot(p, nwg);
+  const int bid = ts.bid;
   const int group = GROUP_M * tiles_n;
   const int gid = bid / group, first_m = gid * GROUP_M;
   const int gsz = min(tiles_m - first_m, GROUP_M);
@@ -371,9 +392,9 @@ __global__ __launch_bounds__(NT, (V2Cfg<KB, STAGES>::WGS)) void gemm2_kernel(Gem
   // split-K: blockIdx.y owns a contiguous run of k-tiles (the host only splits plain
   // f32-accumulating products, whose partial tiles are combined with f32 atomics)
   const int nk_all = (p.K + KB - 1) / KB;
-  const int splits = gridDim.y;
+  const int splits = ts.splits;
   const int per = (nk_all + splits - 1) / splits;
-  const int kt0 = blockIdx.y * per;
+  const int kt0 = ts.split * per;
   const int nk = max(0, min(nk_all, kt0 + per) - kt0);
 #define DPC_ISSUE(it_)                                                                              \
   do {                                                                                              \
@@ -559,11 +580,8 @@ __global__ __launch_bounds__((V3Cfg<BM_, BN_, WM, WN, KB, STAGES>::NTH), 1) void
   __shared__ __attribute__((aligned(16))) bf16_t smem[Cfg::SMEM];
   const int tiles_m = (p.M + BM_ - 1) / BM_, tiles_n = (p.N + BN_ - 1) / BN_;
   const int nwg = tiles_m * tiles_n;
-  int bid = blockIdx.x;
-  {
-    const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
-    bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
-  }
+  const TileSlot ts = tile_slot(p, nwg);
+  const int bid = ts.bid;
   const int group = GROUP_M * tiles_n;
   const int gid = bid / group, first_m = gid * GROUP_M;
   const int gsz = min(tiles_m - first_m, GROUP_M);
@@ -589,9 +607,9 @@ __global__ __launch_bounds__((V3Cfg<BM_, BN_, WM, WN, KB, STAGES>::NTH), 1) void
     for (int j = 0; j < FN; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
 
   const int nk_all = (p.K + KB - 1) / KB;
-  const int splits = gridDim.y;
+  const int splits = ts.splits;
   const int per = (nk_all + splits - 1) / splits;
-  const int kt0 = blockIdx.y * per;
+  const int kt0 = ts.split * per;
   const int nk = max(0, min(nk_all, kt0 + per) - kt0);
 #define DPC_ISSUE3(it_)                                                                             \
   do {                                                                                              \
@@ -759,11 +777,8 @@ __global__ __launch_bounds__(512, 1) void gemm4_kernel(GemmArgs p, unsigned long
   __shared__ __attribute__((aligned(16))) bf16_t smem[Cfg::SMEM];
   const int tiles_m = (p.M + 255) / 256, tiles_n = (p.N + 255) / 256;
   const int nwg = tiles_m * tiles_n;
-  int bid = blockIdx.x;
-  {
-    const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
-    bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
-  }
+  const TileSlot ts = tile_slot(p, nwg);
+  const int bid = ts.bid;
   const int group = GROUP_M * tiles_n;
   const int gid = bid / group, first_m = gid * GROUP_M;
   const int gsz = min(tiles_m - first_m, GROUP_M);
@@ -790,9 +805,9 @@ __global__ __launch_bounds__(512, 1) void gemm4_kernel(GemmArgs p, unsigned long
     for (int j = 0; j < 4; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
 
   const int nk_all = (p.K + 31) / 32;
-  const int splits = gridDim.y;
+  const int splits = ts.splits;
   const int per = (nk_all + splits - 1) / splits;
-  const int kt0 = blockIdx.y * per;
+  const int kt0 = ts.split * per;
   const int nk = max(0, min(nk_all, kt0 + per) - kt0);
 #define DPC_ISSUE4(s_)                                                                              \
   do {                                                                                              \
@@ -973,7 +988,9 @@ static void launch_v2(const GemmArgs* a, dim3 grid, hipStream_t stream, unsigned
   else hipLaunchKernelGGL((gemm2_kernel<KB, STAGES, false, true>), grid, dim3(NT), 0, stream, *a, ab, bb);
 }
 
-// -1: auto; 1: v1; 2: v2 KB64 x2 stages; 3: KB64 x3; 4: KB32 x3; 5: KB32 x4
+// -1: auto; 1: v1; 2: v2 KB64 x2 stages; 3: KB64 x3; 4: KB32 x3; 5: KB32 x4;
+// 6-10: v3 (6: 256x256 KB64 x2, 7: 256x256 KB32 x4, 8: 256x128 KB64 x2, 9: 256x128 KB32 x4,
+// 10: 256x128 KB32 x3); 11: v4 (256x256, pipelined k32 ring)
 static int g_gemm_impl = -1;
 
 DPC_API void dpc_gemm_set_impl(int impl) { g_gemm_impl = impl; }
@@ -1011,52 +1028,55 @@ DPC_API int dpc_gemm(const GemmArgs* a, hipStream_t stream) {
     }
   }
   if (impl >= 2 && !v2_ok) impl = 1;
-  if (impl >= 6) {
-    const int bm = 256, bn = (impl == 8 || impl == 9 || impl == 10) ? 128 : 256;
-    const int t3 = ((a->M + bm - 1) / bm) * ((a->N + bn - 1) / bn);
-    int splits = 1;
-    const bool plain = a->out_f32 && !a->bias && !a->residual && !a->aux_in && !a->aux_out &&
-                       !a->colsum && !a->act && !a->act_bwd;
-    const int nk = (a->K + BKT - 1) / BKT;
-    if (plain) {
-      while (splits < 8 && t3 * splits < 256 && nk / (splits * 2) >= 8) splits *= 2;
-    }
-    if (splits > 1 && !a->accumulate)
-      hipMemset2DAsync(a->C, (size_t)a->ldc * 4, 0, (size_t)a->N * 4, (size_t)a->M, stream);
-    dim3 g3(t3, splits);
-    switch (impl) {
-      case 11: launch_v4(a, g3, stream, ab, bb); break;
-      case 7: launch_v3<256, 256, 2, 4, 32, 4>(a, g3, stream, ab, bb); break;
-      case 8: launch_v3<256, 128, 4, 2, 64, 2>(a, g3, stream, ab, bb); break;
-      case 9: launch_v3<256, 128, 4, 2, 32, 4>(a, g3, stream, ab, bb); break;
-      case 10: launch_v3<256, 128, 4, 2, 32, 3>(a, g3, stream, ab, bb); break;
-      default: launch_v3<256, 256, 2, 4, 64, 2>(a, g3, stream, ab, bb); break;
-    }
-    return (int)hipGetLastError();
-  }
+  GemmArgs b = *a;  // dispatcher-owned copy: split-K mode is decided here
+  b.ksplit = 0;
   if (impl >= 2) {
-    // split-K for plain f32 (accumulating) products whose tile grid under-fills the chip
-    int splits = 1;
+    int bm = BM, bn = BN;
+    if (impl >= 6) {
+      bm = 256;
+      bn = (impl == 8 || impl == 9 || impl == 10) ? 128 : 256;
+    }
+    const int t = ((a->M + bm - 1) / bm) * ((a->N + bn - 1) / bn);
+    // split-K for plain f32 (accumulating) products whose tile grid under-fills the chip;
+    // long-K small outputs (weight gradients) split 8 ways with one k-range per XCD
     const bool plain = a->out_f32 && !a->bias && !a->residual && !a->aux_in && !a->aux_out &&
                        !a->colsum && !a->act && !a->act_bwd;
     const int nk = (a->K + BKT - 1) / BKT;
+    int splits = 1;
+    bool xcd_split = false;
     if (plain) {
-      while (splits < 8 && tiles * splits < 512 && nk / (splits * 2) >= 8) splits *= 2;
+      if (t < 512 && nk >= 64) {
+        splits = 8;
+        xcd_split = true;
+      } else {
+        const int fill = impl >= 6 ? 256 : 512;
+        while (splits < 8 && t * splits < fill && nk / (splits * 2) >= 8) splits *= 2;
+      }
     }
     if (splits > 1 && !a->accumulate)
       hipMemset2DAsync(a->C, (size_t)a->ldc * 4, 0, (size_t)a->N * 4, (size_t)a->M, stream);
-    grid.y = splits;
+    dim3 g(t, splits);
+    if (xcd_split) {
+      g = dim3(t * splits, 1);
+      b.ksplit = splits;
+    }
     switch (impl) {
-      case 3: launch_v2<64, 3>(a, grid, stream, ab, bb); break;
-      case 4: launch_v2<32, 3>(a, grid, stream, ab, bb); break;
-      case 5: launch_v2<32, 4>(a, grid, stream, ab, bb); break;
-      default: launch_v2<64, 2>(a, grid, stream, ab, bb); break;
+      case 3: launch_v2<64, 3>(&b, g, stream, ab, bb); break;
+      case 4: launch_v2<32, 3>(&b, g, stream, ab, bb); break;
+      case 5: launch_v2<32, 4>(&b, g, stream, ab, bb); break;
+      case 6: launch_v3<256, 256, 2, 4, 64, 2>(&b, g, stream, ab, bb); break;
+      case 7: launch_v3<256, 256, 2, 4, 32, 4>(&b, g, stream, ab, bb); break;
+      case 8: launch_v3<256, 128, 4, 2, 64, 2>(&b, g, stream, ab, bb); break;
+      case 9: launch_v3<256, 128, 4, 2, 32, 4>(&b, g, stream, ab, bb); break;
+      case 10: launch_v3<256, 128, 4, 2, 32, 3>(&b, g, stream, ab, bb); break;
+      case 11: launch_v4(&b, g, stream, ab, bb); break;
+      default: launch_v2<64, 2>(&b, g, stream, ab, bb); break;
     }
     return (int)hipGetLastError();
   }
-  if (a->a_kmaj && a->b_kmaj) hipLaunchKernelGGL((gemm_kernel<true, true>), grid, block, 0, stream, *a);
-  else if (a->a_kmaj && !a->b_kmaj) hipLaunchKernelGGL((gemm_kernel<true, false>), grid, block, 0, stream, *a);
-  else if (!a->a_kmaj && !a->b_kmaj) hipLaunchKernelGGL((gemm_kernel<false, false>), grid, block, 0, stream, *a);
-  else hipLaunchKernelGGL((gemm_kernel<false, true>), grid, block, 0, stream, *a);
+  if (a->a_kmaj && a->b_kmaj) hipLaunchKernelGGL((gemm_kernel<true, true>), grid, block, 0, stream, b);
+  else if (a->a_kmaj && !a->b_kmaj) hipLaunchKernelGGL((gemm_kernel<true, false>), grid, block, 0, stream, b);
+  else if (!a->a_kmaj && !a->b_kmaj) hipLaunchKernelGGL((gemm_kernel<false, false>), grid, block, 0, stream, b);
+  else hipLaunchKernelGGL((gemm_kernel<false, true>), grid, block, 0, stream, b);
   return (int)hipGetLastError();
 }
