@@ -157,6 +157,8 @@ def lib() -> ctypes.CDLL:
                 fn.restype = c_int
             handle.dpc_gemm_set_impl.argtypes = [c_int]
             handle.dpc_gemm_set_impl.restype = None
+            handle.dpc_gemm_set_xcd_split.argtypes = [c_int]
+            handle.dpc_gemm_set_xcd_split.restype = None
             _lib = handle
     return _lib
 
@@ -166,6 +168,11 @@ def set_gemm_impl(impl: int) -> None:
     2-5 LDS-DMA 128x128 v2 variants, 6-10 large-tile v3 variants, 11 pipelined 256x256 v4
     (table at the dispatcher, ``csrc/gemm.hip``)."""
     lib().dpc_gemm_set_impl(int(impl))
+
+
+def set_gemm_xcd_split(on: bool) -> None:
+    """Split-K with one k-range per XCD instead of the default remap (experiments)."""
+    lib().dpc_gemm_set_xcd_split(int(bool(on)))
 
 
 def is_loaded() -> bool:
