@@ -4,8 +4,8 @@
 Reference semantics with the crash bugs fixed: the reference model math in plain torch
 modules (manual attention with a materialised [N,H,S,S] score tensor, as
 ``/root/reference/models/gpt.py:68-105``), ``torch.autocast(bf16)``, ``F.cross_entropy``,
-``torch.optim.AdamW`` (fused), torch DDP for N > 1, no torch.compile (Inductor/Triton is
-not the yardstick).  ``--sdpa`` swaps the manual attention for
+``torch.optim.AdamW`` (fused), torch DDP for N > 1; ``--compile`` adds the reference's
+default ``torch.compile`` (Inductor/Triton), ``--scaler`` its GradScaler.  ``--sdpa`` swaps the manual attention for
 ``F.scaled_dot_product_attention`` (a stronger stock baseline).
 
     python bench/baseline_torch.py --steps 10 --warmup 3 [--model gpt2-small] [--sdpa]
@@ -44,6 +44,10 @@ def main():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--sdpa", action="store_true")
+    ap.add_argument("--compile", action="store_true",
+                    help="torch.compile the forward (the reference's default: Inductor/Triton)")
+    ap.add_argument("--scaler", action="store_true",
+                    help="GradScaler around backward/step as the reference recipes do")
     a = ap.parse_args()
     info = comm.init_dist()
     dev = info.device
@@ -70,7 +74,10 @@ def main():
         call = lambda ids, pos: fwd_model(ids, pos)  # noqa: E731
     else:
         call = lambda ids, pos: model.reference_forward(ids, pos)  # noqa: E731
+    if a.compile:
+        call = torch.compile(call)
     opt = torch.optim.AdamW(model.parameters(), lr=1e-4, fused=True)
+    scaler = torch.amp.GradScaler("cuda") if a.scaler else None
     B, S = a.batch_size, a.seq_len
     ids = torch.randint(0, 50257, (B, S), device=dev)
     inp, tg = ids[:, :-1], ids[:, 1:]
@@ -81,8 +88,13 @@ def main():
         with torch.autocast("cuda", dtype=torch.bfloat16):
             logits = call(inp, pos)
             loss = F.cross_entropy(logits.reshape(-1, 50257), tg.reshape(-1), ignore_index=-100)
-        loss.backward()
-        opt.step()
+        if scaler is None:
+            loss.backward()
+            opt.step()
+        else:
+            scaler.scale(loss).backward()
+            scaler.step(opt)
+            scaler.update()
         return loss
 
     for _ in range(a.warmup):
@@ -97,7 +109,8 @@ def main():
     dt = time.perf_counter() - t0
     tps = B * (S - 1) * info.world_size * a.steps / dt
     if info.is_main:
-        print(json.dumps({"baseline": "stock-pytorch" + ("-sdpa" if a.sdpa else "-manual-attn"),
+        name = "stock-pytorch" + ("-sdpa" if a.sdpa else "-manual-attn") + ("-compile" if a.compile else "")
+        print(json.dumps({"baseline": name + ("-scaler" if a.scaler else ""),
                           "model": a.model, "n_gpus": info.world_size, "batch_per_gpu": B, "seq_len": S,
                           "tokens_per_s": round(tps, 1), "ms_per_step": round(1000 * dt / a.steps, 2),
                           "loss": round(loss.item(), 4),
