@@ -30,7 +30,12 @@ from distributed_pytorch_cookbook_amd.config import apply_preset, build_parser  
 from distributed_pytorch_cookbook_amd.parallel import comm  # noqa: E402
 
 METRIC = "tokens/sec (node) GPT-2 training per recipe (DDP/FSDP/PP) at 1/2/4/8 MI355X"
-BASELINE_TOKS = {}  # BASELINE.md publishes no numbers for any config
+# The reference publishes no numbers.  vs_baseline compares against the
+# stock-PyTorch run of the reference's own default recipe (manual attention + torch.compile,
+# bf16 autocast, fused AdamW) measured on one MI355X at 32 x 1024 tokens per GPU
+# (bench/baseline_torch.py --compile; profiles/r1_stock_pytorch_baselines.jsonl), scaled
+# linearly with the GPU count.
+BASELINE_TOKS_PER_GPU = {("ddp", "gpt2-small", 32, 1024): 276672.6}
 
 
 def main():
@@ -40,7 +45,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--recipe", default="ddp", choices=["ddp", "fsdp", "pipe", "pipe_ddp"])
     ap.add_argument("--model", default=None)
-    ap.add_argument("--batch_size", type=int, default=16, help="sequences per GPU (per DP replica for PP)")
+    ap.add_argument("--batch_size", type=int, default=32, help="sequences per GPU (per DP replica for PP)")
     ap.add_argument("--seq_len", type=int, default=1024)
     ap.add_argument("--bucket_mb", type=float, default=128.0)
     ap.add_argument("--reduce_dtype", default="fp32", choices=["fp32", "bf16"])
@@ -116,7 +121,8 @@ def main():
     n = info.world_size
     par = {"ddp": f"dp{n}", "fsdp": f"fsdp{n}", "pipe": f"pp{n}",
            "pipe_ddp": f"pp{n // max(engine.dp_world, 1)}xdp{engine.dp_world}"}[a.recipe]
-    base = BASELINE_TOKS.get((a.recipe, model_name, n))
+    base = BASELINE_TOKS_PER_GPU.get((a.recipe, model_name, B, S))
+    base = base * n if base else None
     out = {
         "metric": METRIC,
         "value": round(value, 1),
@@ -132,7 +138,9 @@ def main():
         "data": "synthetic",
         "config": {"model": model_name, "global_batch": B * engine.dp_world, "seq_len": S,
                    "parallelism": par, "recipe": f"main-{a.recipe.replace('_', '-')}.py",
-                   "tokens_per_step": tokens_per_step, "final_loss": round(loss_v, 4)},
+                   "tokens_per_step": tokens_per_step, "final_loss": round(loss_v, 4),
+                   "baseline": ("stock PyTorch reference-default recipe (manual attention + torch.compile)"
+                                " x n_gpus" if base else None)},
     }
     if info.is_main:
         line = json.dumps(out)

@@ -999,17 +999,6 @@ static int g_xcd_split = 0;
 DPC_API void dpc_gemm_set_impl(int impl) { g_gemm_impl = impl; }
 DPC_API void dpc_gemm_set_xcd_split(int on) { g_xcd_split = on; }
 
-// resident workgroups chip-wide (256 CUs x workgroups per CU by LDS / registers)
-static int gemm_slots(int impl) {
-  switch (impl) {
-    case 3: return 256;   // 96 KiB LDS
-    case 4: return 768;   // 48 KiB
-    case 10: return 512;  // 72 KiB
-    case 6: case 7: case 8: case 9: case 11: return 256;
-    default: return 512;  // 64 KiB
-  }
-}
-
 static inline bool al(const void* p, int b) { return ((uintptr_t)p % b) == 0; }
 
 DPC_API int dpc_gemm(const GemmArgs* a, hipStream_t stream) {
@@ -1058,20 +1047,11 @@ DPC_API int dpc_gemm(const GemmArgs* a, hipStream_t stream) {
                        !a->colsum && !a->act && !a->act_bwd;
     const int nk = (a->K + BKT - 1) / BKT;
     int splits = 1;
-    if (plain && t < 1024) {
-      // pick the split count whose workgroup count best fills whole waves of resident
-      // workgroups (tile grids like 144 = 12 x 12 otherwise leave a mostly idle last wave),
-      // keeping >= 16 k-tiles per split
-      const int slots = gemm_slots(impl);
-      double best = 0.0;
-      for (int s = 1; s <= 16 && nk / s >= 16; ++s) {
-        const long long wgs = (long long)t * s;
-        const double eff = (double)wgs / (double)(((wgs + slots - 1) / slots) * slots);
-        if (eff > best + 0.02) {
-          best = eff;
-          splits = s;
-        }
-      }
+    if (plain) {
+      // power-of-two splits until the grid reaches ~2 workgroups per CU.  (A wave-quantised
+      // choice of up to 16 splits measured 30 % slower on the GPT-2 weight gradients.)
+      const int fill = impl >= 6 ? 256 : 512;
+      while (splits < 8 && t * splits < fill && nk / (splits * 2) >= 8) splits *= 2;
     }
     const bool xcd_split = g_xcd_split && splits > 1;
     if (splits > 1 && !a->accumulate)
