@@ -52,6 +52,7 @@ def main():
     ap.add_argument("--num_microbatches", type=int, default=0)
     ap.add_argument("--schedule", default="1f1b", choices=["1f1b", "gpipe"])
     ap.add_argument("--dp_size", type=int, default=0)
+    ap.add_argument("--no_graph", action="store_true", help="eager steps (no HIP-graph capture at N=1)")
     ap.add_argument("--json", default=None, help="also write the result line to this file")
     a = ap.parse_args()
 
@@ -65,6 +66,8 @@ def main():
         argv += ["--schedule", a.schedule, "--num_microbatches", str(a.num_microbatches)]
     if rec == "pipe_ddp" and a.dp_size:
         argv += ["--dp_size", str(a.dp_size)]
+    if a.no_graph:
+        argv += ["--disable_compile"]
     args = build_parser(rec).parse_args(argv)
     apply_preset(args)
     args.sequence_length = a.seq_len
