@@ -8,6 +8,7 @@ parallelism shape and tuning knobs.
 from __future__ import annotations
 
 import argparse
+import os
 
 from .models.gpt import PRESETS
 
@@ -58,6 +59,9 @@ def build_parser(recipe: str = "single") -> argparse.ArgumentParser:
     p.add_argument("--bucket_mb", type=float, default=128.0, help="DDP gradient bucket size")
     p.add_argument("--reduce_dtype", type=str, default="fp32", choices=["fp32", "bf16"])
     p.add_argument("--no_overlap", action="store_true", help="all-reduce after backward instead of during")
+    p.add_argument("--comm", default=os.environ.get("DPC_COMM", "torch"), choices=["torch", "native"],
+                   help="gradient all-reduce through torch's nccl process group or the native C++ RCCL "
+                        "communicator (parallel/native_comm.py)")
     p.add_argument("--profile", type=str, default=None, help="write a torch.profiler trace here")
     p.add_argument("--log_jsonl", type=str, default=None, help="append step metrics as JSON lines")
     p.add_argument("--cpu", action="store_true", help="force CPU (gloo) even if a GPU is present")

@@ -25,7 +25,7 @@ class DataParallelEngine(Engine):
 
     def __init__(self, model, device, lr: float, group=None, bucket_mb: float = 128.0,
                  reduce_dtype=torch.float32, overlap: bool = True, compute_dtype=None,
-                 graph: bool = False):
+                 graph: bool = False, native_comm: bool = False):
         self.device = torch.device(device)
         self.model = model
         self.dp_group = group
@@ -34,7 +34,8 @@ class DataParallelEngine(Engine):
         self.is_logger = comm.rank() == 0
         if self.dp_world > 1:
             self.store = DDPStore(model, device, group=group, bucket_mb=bucket_mb,
-                                  reduce_dtype=reduce_dtype, overlap=overlap, compute_dtype=compute_dtype)
+                                  reduce_dtype=reduce_dtype, overlap=overlap, compute_dtype=compute_dtype,
+                                  native=native_comm)
         else:
             self.store = LocalStore(model, device, compute_dtype=compute_dtype)
         self.opt = FlatAdamW(self.store.master, self.store.grads, lr=lr, shadow=self.store.shadow)

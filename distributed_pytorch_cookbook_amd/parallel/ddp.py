@@ -16,7 +16,10 @@ MI355X-first design:
   per-link bound): fewer, larger buckets (default 128 MiB) keep RCCL at its bus
   bandwidth instead of paying per-call latency 25x per step;
 * the 1/W average is folded into the AdamW kernel (``grad_scale``), so no extra pass;
-* optional bf16 reduction (``reduce_dtype``) halves the bytes on the links.
+* optional bf16 reduction (``reduce_dtype``) halves the bytes on the links;
+* ``native=True`` issues the bucket all-reduces through the C++ RCCL communicator
+  (``parallel/native_comm.py``) on a dedicated high-priority HIP stream ordered with
+  events, instead of torch's process group.
 """
 from __future__ import annotations
 
@@ -27,15 +30,33 @@ from . import comm
 from .store import LocalStore
 
 
+class _EventWork:
+    """Completion of a collective enqueued on a side stream: ``wait`` orders the caller's
+    current stream after it (no host synchronisation)."""
+
+    def __init__(self, event: torch.cuda.Event):
+        self.event = event
+
+    def wait(self):
+        torch.cuda.current_stream().wait_event(self.event)
+
+
 class DDPStore(LocalStore):
     def __init__(self, model, device, group=None, bucket_mb: float = 128.0,
                  reduce_dtype: torch.dtype = torch.float32, overlap: bool = True,
-                 compute_dtype=None, units=None, broadcast_src: int | None = None):
+                 compute_dtype=None, units=None, broadcast_src: int | None = None,
+                 native: bool = False):
         super().__init__(model, device, compute_dtype=compute_dtype, units=units)
         self.group = group
         self.world = comm.world_size(group)
         self.reduce_dtype = reduce_dtype
         self.overlap = overlap
+        self.native = None
+        if native and self.world > 1 and self.master.is_cuda:
+            from .native_comm import NativeComm
+
+            self.native = NativeComm(group, device=self.master.device)
+            self._comm_stream = torch.cuda.Stream(device=self.master.device, priority=-1)
         if self.world > 1:
             src = broadcast_src if broadcast_src is not None else (
                 dist.get_global_rank(group, 0) if group is not None else 0)
@@ -75,7 +96,20 @@ class DDPStore(LocalStore):
             return
         lo, hi = self._range(bi)
         g = self.grads[lo:hi]
-        if self.reduce_dtype != torch.float32:
+        if self.native is not None:
+            t = g.to(self.reduce_dtype) if self.reduce_dtype != torch.float32 else g
+            ready = torch.cuda.Event()
+            ready.record()
+            cs = self._comm_stream
+            cs.wait_event(ready)
+            if t is not g:
+                t.record_stream(cs)
+                self._tmp[bi] = t
+            self.native.all_reduce(t, stream=cs)
+            done = torch.cuda.Event()
+            done.record(cs)
+            self._works[bi] = _EventWork(done)
+        elif self.reduce_dtype != torch.float32:
             t = g.to(self.reduce_dtype)
             self._tmp[bi] = t
             self._works[bi] = comm.all_reduce(t, group=self.group, async_op=True)

@@ -46,6 +46,7 @@ def build_engine(recipe: str, model, info, args):
             # the cookbook's "compile": capture the whole single-GPU step into a HIP graph
             # (dropout masks are drawn per step on the host: not graph-replayable)
             graph=not args.disable_compile and not args.disable_amp and not args.dropout,
+            native_comm=getattr(args, "comm", "torch") == "native",
         )
     if recipe == "fsdp":
         from .engine.fsdp import FSDPEngine

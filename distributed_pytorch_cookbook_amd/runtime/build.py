@@ -1,4 +1,8 @@
-"""Build the host runtime library (``libdpc_runtime.so``) in-tree with g++ (OpenMP)."""
+"""Build the host runtime library (``libdpc_runtime.so``) in-tree with g++ (OpenMP).
+
+Sources: ``csrc/runtime.cpp`` (token-file loader, synthetic corpus, host AdamW) and
+``csrc/rccl_comm.cpp`` (native RCCL communicator, resolved at run time with dlopen).
+"""
 from __future__ import annotations
 
 import os
@@ -8,9 +12,10 @@ import sys
 from pathlib import Path
 
 HERE = Path(__file__).resolve().parent
-SRC = HERE / "csrc" / "runtime.cpp"
+SRCS = [HERE / "csrc" / "runtime.cpp", HERE / "csrc" / "rccl_comm.cpp"]
 LIB_PATH = HERE / "libdpc_runtime.so"
 FLAGS = ["-O3", "-std=c++17", "-fPIC", "-shared", "-fopenmp", "-march=x86-64-v3", "-pthread"]
+LIBS = ["-ldl"]
 
 
 HASH_PATH = LIB_PATH.with_suffix(".so.srchash")
@@ -19,7 +24,11 @@ HASH_PATH = LIB_PATH.with_suffix(".so.srchash")
 def source_hash() -> str:
     import hashlib
 
-    return hashlib.sha256(" ".join(FLAGS).encode() + SRC.read_bytes()).hexdigest()
+    h = hashlib.sha256(" ".join(FLAGS + LIBS).encode())
+    for src in SRCS:
+        h.update(src.name.encode())
+        h.update(src.read_bytes())
+    return h.hexdigest()
 
 
 def needs_build() -> bool:
@@ -35,7 +44,7 @@ def build(force: bool = False, verbose: bool = False) -> Path:
     if not cxx:
         raise RuntimeError("no C++ compiler found for the host runtime")
     tmp = LIB_PATH.with_suffix(".so.tmp")
-    cmd = [cxx, *FLAGS, str(SRC), "-o", str(tmp)]
+    cmd = [cxx, *FLAGS, *map(str, SRCS), "-o", str(tmp), *LIBS]
     if verbose:
         print(" ".join(cmd), flush=True)
     r = subprocess.run(cmd, capture_output=True, text=True)

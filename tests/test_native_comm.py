@@ -1,0 +1,60 @@
+"""Native RCCL communicator (parallel/native_comm.py over runtime/csrc/rccl_comm.cpp)."""
+import socket
+
+import pytest
+import torch
+import torch.distributed as dist
+
+
+def test_rccl_symbols_resolve():
+    """The runtime library finds torch's librccl and every entry point the engines use."""
+    from distributed_pytorch_cookbook_amd.parallel import native_comm
+
+    h = native_comm._lib()
+    assert h.dpc_rccl_error() is not None
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+@pytest.mark.gpu
+def test_native_comm_single_rank_collectives():
+    from distributed_pytorch_cookbook_amd.parallel.native_comm import NativeComm
+
+    dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{_free_port()}", rank=0, world_size=1,
+                            device_id=torch.device("cuda:0"))
+    try:
+        c = NativeComm(device=torch.device("cuda:0"))
+        assert (c.rank, c.size) == (0, 1)
+        x = torch.randn(1000, device="cuda")
+        y = x.clone()
+        c.all_reduce(y)
+        torch.testing.assert_close(y, x)
+        b = torch.randn(512, device="cuda").bfloat16()
+        c.all_reduce(b, op="max")
+        out = torch.empty(1000, device="cuda")
+        c.all_gather(out, x)
+        torch.testing.assert_close(out, x)
+        rs = torch.empty(1000, device="cuda")
+        c.reduce_scatter(rs, x)
+        torch.testing.assert_close(rs, x)
+        c.broadcast(y, src=0)
+        r = torch.empty_like(x)
+        with c.grouped():
+            c.send(x, 0)
+            c.recv(r, 0)
+        torch.testing.assert_close(r, x)
+        sub = c.split(color=0, key=0)
+        assert (sub.rank, sub.size) == (0, 1)
+        sub.all_reduce(y)
+        torch.cuda.synchronize()
+        c.check_async()
+        sub.destroy()
+        c.destroy()
+    finally:
+        dist.destroy_process_group()
