@@ -118,7 +118,12 @@ def main():
     if info.world_size > 1:
         torch.distributed.all_reduce(dt_t, op=torch.distributed.ReduceOp.MAX)
     dt = float(dt_t.item())
-    loss_v = float(loss.item()) if loss is not None else float("nan")
+    # the loss lives on the ranks that own the head (last pipeline stage): average those
+    lt = torch.tensor([float(loss) if loss is not None else 0.0, 1.0 if loss is not None else 0.0],
+                      dtype=torch.float64, device=info.device)
+    if info.world_size > 1:
+        torch.distributed.all_reduce(lt)
+    loss_v = float(lt[0] / lt[1]) if lt[1] > 0 else float("nan")
     tokens_per_step = B * (S - 1) * engine.dp_world
     value = tokens_per_step * a.steps / dt
     n = info.world_size

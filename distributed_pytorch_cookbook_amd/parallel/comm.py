@@ -58,9 +58,12 @@ def init_dist(force_cpu: bool = False) -> DistInfo:
     backend = "none"
     if world > 1 and not dist.is_initialized():
         backend = "nccl" if use_gpu else "gloo"
+        # DPC_DIST_BACKEND=gloo: rehearse the multi-rank GPU path with several ranks on ONE
+        # device (RCCL refuses two ranks per GPU); collectives then stage through the host
+        backend = os.environ.get("DPC_DIST_BACKEND", backend)
         timeout = datetime.timedelta(seconds=float(os.environ.get("DPC_COLL_TIMEOUT", "1800")))
         kw = dict(backend=backend, timeout=timeout)
-        if use_gpu:
+        if use_gpu and backend == "nccl":
             kw["device_id"] = device
         dist.init_process_group(**kw)
     elif dist.is_initialized():
