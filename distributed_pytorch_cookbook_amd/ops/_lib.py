@@ -159,6 +159,8 @@ def lib() -> ctypes.CDLL:
             handle.dpc_gemm_set_impl.restype = None
             handle.dpc_gemm_set_xcd_split.argtypes = [c_int]
             handle.dpc_gemm_set_xcd_split.restype = None
+            handle.dpc_gemm_set_splits.argtypes = [c_int]
+            handle.dpc_gemm_set_splits.restype = None
             _lib = handle
     return _lib
 
@@ -168,6 +170,11 @@ def set_gemm_impl(impl: int) -> None:
     2-5 LDS-DMA 128x128 v2 variants, 6-10 large-tile v3 variants, 11 pipelined 256x256 v4
     (table at the dispatcher, ``csrc/gemm.hip``)."""
     lib().dpc_gemm_set_impl(int(impl))
+
+
+def set_gemm_splits(n: int) -> None:
+    """Force the split-K count of plain f32 products (0 = automatic; sweeps)."""
+    lib().dpc_gemm_set_splits(int(n))
 
 
 def set_gemm_xcd_split(on: bool) -> None:

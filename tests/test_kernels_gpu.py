@@ -88,6 +88,29 @@ def test_gemm_impls_with_epilogue(impl, a_kmaj, b_kmaj, M, N, K):
     assert rel_err(ob, a.float() @ b.float().t()) < 1e-2
 
 
+@pytest.mark.parametrize("impl", [2, 4, 7, 10, 11])
+@pytest.mark.parametrize("splits", [2, 3, 8])
+@pytest.mark.parametrize("M,N,K", [(77, 1000, 4160), (600, 520, 8192), (2304, 136, 4096)])
+def test_gemm_forced_split_k(impl, splits, M, N, K):
+    """Split-K partial sums (lane-contiguous atomic epilogue) on ragged M/N edges."""
+    torch.manual_seed(5)
+    A = torch.randn(K, (M + 7) // 8 * 8, device=dev).bfloat16()[:, :M]
+    B = torch.randn(K, (N + 7) // 8 * 8, device=dev).bfloat16()[:, :N]
+    acc0 = torch.randn(M, N, device=dev)
+    acc = acc0.clone()
+    _lib.set_gemm_impl(impl)
+    _lib.set_gemm_splits(splits)
+    try:
+        gemm(A, B, a_kmaj=False, b_kmaj=False, out=acc, accumulate=True)
+        fresh = gemm(A, B, a_kmaj=False, b_kmaj=False, out_dtype=torch.float32)
+    finally:
+        _lib.set_gemm_impl(-1)
+        _lib.set_gemm_splits(0)
+    ref = A.float().t() @ B.float()
+    assert rel_err(acc - acc0, ref) < 2e-3
+    assert rel_err(fresh, ref) < 2e-3
+
+
 def test_gemm_identity_asymmetric():
     # A = I with an asymmetric B catches a transposed C write
     n = 128
