@@ -99,19 +99,24 @@ __device__ __forceinline__ float block_max(float v, float* red) {
   return t;
 }
 
-// GPT-2 "gelu_new": 0.5 x (1 + tanh(sqrt(2/pi) (x + 0.044715 x^3)))
-__device__ __forceinline__ float gelu_tanh(float x) {
+// GPT-2 "gelu_new": 0.5 x (1 + tanh(sqrt(2/pi) (x + 0.044715 x^3))).
+// With 0.5 (1 + tanh(u)) = sigmoid(2u) this is x * sigmoid(2u): one v_exp_f32 and one
+// v_rcp_f32 instead of libm tanhf (a branchy ~40-instruction routine that dominated the
+// GEMM epilogues).  exp overflow (x << 0) gives rcp(inf) = 0, i.e. gelu -> -0.
+__device__ __forceinline__ float sigmoid2u(float x, float x2) {
   const float k0 = 0.7978845608028654f, k1 = 0.044715f;
-  float u = k0 * (x + k1 * x * x * x);
-  return 0.5f * x * (1.f + tanhf(u));
+  const float u2 = -2.f * k0 * (x + k1 * x2 * x);
+  return __builtin_amdgcn_rcpf(1.f + __expf(u2));
 }
 
+__device__ __forceinline__ float gelu_tanh(float x) { return x * sigmoid2u(x, x * x); }
+
+// d/dx: s + x * s (1 - s) * 2 k0 (1 + 3 k1 x^2), s = sigmoid(2u)  (1 - tanh^2 = 4 s (1 - s))
 __device__ __forceinline__ float gelu_tanh_grad(float x) {
   const float k0 = 0.7978845608028654f, k1 = 0.044715f;
-  float x2 = x * x;
-  float u = k0 * (x + k1 * x2 * x);
-  float t = tanhf(u);
-  return 0.5f * (1.f + t) + 0.5f * x * (1.f - t * t) * k0 * (1.f + 3.f * k1 * x2);
+  const float x2 = x * x;
+  const float s = sigmoid2u(x, x2);
+  return s + x * s * (1.f - s) * (2.f * k0) * (1.f + 3.f * k1 * x2);
 }
 
 enum Act { ACT_NONE = 0, ACT_RELU = 1, ACT_GELU = 2 };

@@ -270,7 +270,8 @@ __global__ __launch_bounds__(256) void dropout_residual_kernel(DropResArgs p) {
 // ------------------------------------------------------------------ bias / activation backward
 // dz[t, c] = dy[t, c] * keep(t, c) * act'(z[t, c])  (bf16 out), db[c] += sum_t dz[t, c]
 // (keep = 1 when drop_scale == 0).
-// grid: (ceil(N / 512), ceil(T / 64)); each lane owns 8 columns, each wave 16 rows.
+// grid: (ceil(N / 256), ceil(T / BA_ROWS)); each lane owns 4 columns (one float4 of a row), the
+// 4 waves of a block interleave its BA_ROWS rows, 4 rows in flight per wave.
 struct BiasActArgs {
   const float* dy;     // [T][lddy] f32
   const void* z;       // [T][ldz] bf16 pre-activation (optional, needed when act != 0)
@@ -283,47 +284,65 @@ struct BiasActArgs {
   float drop_scale;    // 0: no dropout
 };
 
+constexpr int BA_ROWS = 128;
+
 __global__ __launch_bounds__(256) void bias_act_bwd_kernel(BiasActArgs p) {
-  __shared__ float red[4][64][8];
+  __shared__ float red[4][256];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int cg = blockIdx.x * 64 + lane;  // column group of 8
-  const bool colok = cg * 8 < p.N;
-  float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-  const long long r0 = (long long)blockIdx.y * 64;
+  const int c = blockIdx.x * 256 + lane * 4;
+  const bool colok = c < p.N;
+  float acc[4] = {0.f, 0.f, 0.f, 0.f};
+  const long long r0 = (long long)blockIdx.y * BA_ROWS;
+  const int nrows = (int)min((long long)BA_ROWS, (long long)p.T - r0);
+  const bf16_t* z = static_cast<const bf16_t*>(p.z);
+  bf16_t* dz = static_cast<bf16_t*>(p.dz);
   if (colok) {
-    for (int i = w; i < 64; i += 4) {
-      const long long t = r0 + i;
-      if (t >= p.T) break;
-      const float4* dyr = reinterpret_cast<const float4*>(p.dy + t * p.lddy + cg * 8);
-      const float4 a = dyr[0], b = dyr[1];
-      float f[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
-      if (p.act) {
-        float zf[8];
-        unpack8(*reinterpret_cast<const uint4*>(static_cast<const bf16_t*>(p.z) + t * p.ldz + cg * 8), zf);
+    // rows w, w + 4, ...; four of them loaded before any is used (memory-level parallelism)
+    for (int i0 = w; i0 < nrows; i0 += 16) {
+      float4 y[4];
+      uint2 zz[4];
 #pragma unroll
-        for (int j = 0; j < 8; ++j) f[j] *= act_grad(zf[j], p.act);
-      }
-      if (p.drop_scale != 0.f) {
-        const uint32_t idx = (uint32_t)(t * p.N + cg * 8);
-#pragma unroll
-        for (int j = 0; j < 8; ++j) f[j] *= drop_factor(idx + j, p.drop_key, p.drop_thresh, p.drop_scale);
+      for (int u = 0; u < 4; ++u) {
+        const int i = i0 + 4 * u;
+        if (i < nrows) {
+          const long long t = r0 + i;
+          y[u] = *reinterpret_cast<const float4*>(p.dy + t * p.lddy + c);
+          if (p.act) zz[u] = *reinterpret_cast<const uint2*>(z + t * p.ldz + c);
+        }
       }
 #pragma unroll
-      for (int j = 0; j < 8; ++j) acc[j] += f[j];
-      *reinterpret_cast<uint4*>(static_cast<bf16_t*>(p.dz) + t * p.lddz + cg * 8) = pack8(f);
+      for (int u = 0; u < 4; ++u) {
+        const int i = i0 + 4 * u;
+        if (i >= nrows) break;
+        const long long t = r0 + i;
+        float f[4] = {y[u].x, y[u].y, y[u].z, y[u].w};
+        if (p.act) {
+          f[0] *= act_grad(__uint_as_float(zz[u].x << 16), p.act);
+          f[1] *= act_grad(__uint_as_float(zz[u].x & 0xffff0000u), p.act);
+          f[2] *= act_grad(__uint_as_float(zz[u].y << 16), p.act);
+          f[3] *= act_grad(__uint_as_float(zz[u].y & 0xffff0000u), p.act);
+        }
+        if (p.drop_scale != 0.f) {
+          const uint32_t idx = (uint32_t)(t * p.N + c);
+#pragma unroll
+          for (int j = 0; j < 4; ++j) f[j] *= drop_factor(idx + j, p.drop_key, p.drop_thresh, p.drop_scale);
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[j] += f[j];
+        uint2 o;
+        o.x = pack2bf(f[0], f[1]);
+        o.y = pack2bf(f[2], f[3]);
+        *reinterpret_cast<uint2*>(dz + t * p.lddz + c) = o;
+      }
     }
   }
   if (!p.db) return;
 #pragma unroll
-  for (int j = 0; j < 8; ++j) red[w][lane][j] = acc[j];
+  for (int j = 0; j < 4; ++j) red[w][lane * 4 + j] = acc[j];
   __syncthreads();
-  if (w == 0 && colok) {
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const float s = red[0][lane][j] + red[1][lane][j] + red[2][lane][j] + red[3][lane][j];
-      atomicAdd(p.db + cg * 8 + j, s);
-    }
-  }
+  // column sums of the block: lane-contiguous atomics (256 B per wave-instruction)
+  const int col = threadIdx.x, n = blockIdx.x * 256 + col;
+  if (n < p.N) atomicAdd(p.db + n, red[0][col] + red[1][col] + red[2][col] + red[3][col]);
 }
 
 }  // namespace dpc
@@ -373,8 +392,8 @@ DPC_API int dpc_cast_f32_bf16(const CastArgs* a, hipStream_t stream) {
 
 DPC_API int dpc_bias_act_bwd(const BiasActArgs* a, hipStream_t stream) {
   if (a->T <= 0) return 0;
-  if (a->N % 8) return (int)hipErrorInvalidValue;
-  dim3 grid((unsigned)((a->N / 8 + 63) / 64), (unsigned)((a->T + 63) / 64));
+  if (a->N % 4 || a->lddy % 4 || a->ldz % 4 || a->lddz % 4) return (int)hipErrorInvalidValue;
+  dim3 grid((unsigned)((a->N + 255) / 256), (unsigned)((a->T + BA_ROWS - 1) / BA_ROWS));
   hipLaunchKernelGGL(bias_act_bwd_kernel, grid, dim3(256), 0, stream, *a);
   return (int)hipGetLastError();
 }

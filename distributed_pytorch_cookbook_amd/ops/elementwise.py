@@ -32,9 +32,11 @@ def bias_act_bwd(dy: torch.Tensor, z: torch.Tensor | None, act, db: torch.Tensor
             out.copy_(g)
             return out
         return g.to(out_dtype)
-    if dy.dtype != torch.float32 or dy.stride(1) != 1 or N % 8 or dy.stride(0) % 4:
-        raise ValueError("bias_act_bwd: f32 dy with contiguous rows, N % 8 == 0")
-    if act and (z is None or z.dtype != torch.bfloat16 or z.stride(1) != 1):
+    if (dy.dtype != torch.float32 or dy.stride(1) != 1 or N % 4 or dy.stride(0) % 4
+            or dy.data_ptr() % 16):
+        raise ValueError("bias_act_bwd: f32 dy with 16-B aligned contiguous rows, N % 4 == 0")
+    if act and (z is None or z.dtype != torch.bfloat16 or z.stride(1) != 1 or z.stride(0) % 4
+                or z.data_ptr() % 8):
         raise ValueError("bias_act_bwd: bf16 pre-activation z required")
     if out is None:
         out = torch.empty(T, N, device=dy.device, dtype=torch.bfloat16)
