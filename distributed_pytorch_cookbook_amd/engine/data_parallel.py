@@ -48,6 +48,19 @@ class DataParallelEngine(Engine):
         self.store.zero_grad()
         out = self.model(**batch, targets=targets)
         out.loss.backward()
+        if self.dp_world > 1 and self.store.master.is_cuda:
+            # bucket by bucket: AdamW of the buckets already reduced runs on the compute stream
+            # while the last ones (the embeddings, whose backward comes last) are still being
+            # all-reduced on the comm stream
+            st = self.store
+            st.launch_all()
+            self.opt.begin_step()
+            for bi in range(len(st.buckets)):
+                st.wait_bucket(bi)
+                lo, hi = st.bucket_range(bi)
+                self.opt.update(lo, hi, grad_scale=1.0 / self.dp_world)
+            st.reset_buckets()
+            return out.loss.detach()
         if self.dp_world > 1:
             self.store.finish_grads()
         self.opt.step(grad_scale=1.0 / self.dp_world)

@@ -42,27 +42,45 @@ class FlatAdamW:
 
     @torch.no_grad()
     def step(self, grad_scale: float = 1.0, grad_scale_t: torch.Tensor | None = None) -> None:
+        self.begin_step()
+        self.update(0, self.param.numel(), grad_scale, grad_scale_t)
+
+    def begin_step(self) -> None:
+        """Advance the step count (host and, for HIP-graph replay, device counter)."""
         self.step_count += 1
+        p = self.param
+        if p.is_cuda and p.numel() % 4 == 0:
+            if self.device_step:
+                self.step_t.add_(1.0)
+            else:
+                self.step_t.fill_(float(self.step_count))
+
+    @torch.no_grad()
+    def update(self, lo: int, hi: int, grad_scale: float = 1.0,
+               grad_scale_t: torch.Tensor | None = None) -> None:
+        """Apply the current step to elements [lo, hi) of the flat buffers -- lets DDP update
+        the buckets whose all-reduce has finished while the last one is still on the links."""
         b1, b2 = self.betas
         bc1 = 1.0 - b1 ** self.step_count
         bc2s = math.sqrt(1.0 - b2 ** self.step_count)
         p, g = self.param, self.grad
-        if p.is_cuda and p.numel() % 4 == 0:
-            step_ptr = None
-            if self.device_step:
-                self.step_t.add_(1.0)
-                step_ptr = self.step_t.data_ptr()
-            else:
-                self.step_t.fill_(float(self.step_count))
+        if p.is_cuda and p.numel() % 4 == 0 and lo % 4 == 0 and (hi - lo) % 4 == 0:
+            if hi <= lo:
+                return
+            f4 = 4 * lo
             args = _lib.AdamArgs(
-                param=p.data_ptr(), grad=g.data_ptr(), exp_avg=self.exp_avg.data_ptr(),
-                exp_avg_sq=self.exp_avg_sq.data_ptr(), shadow=_lib.ptr(self.shadow),
-                grad_scale_ptr=_lib.ptr(grad_scale_t), n=p.numel(), lr=self.lr, beta1=b1,
+                param=p.data_ptr() + f4, grad=g.data_ptr() + f4, exp_avg=self.exp_avg.data_ptr() + f4,
+                exp_avg_sq=self.exp_avg_sq.data_ptr() + f4,
+                shadow=(self.shadow.data_ptr() + lo * self.shadow.element_size()) if self.shadow is not None else None,
+                grad_scale_ptr=_lib.ptr(grad_scale_t), n=hi - lo, lr=self.lr, beta1=b1,
                 beta2=b2, eps=self.eps, weight_decay=self.weight_decay, bias_correction1=bc1,
-                bias_correction2_sqrt=bc2s, grad_scale=grad_scale, step_ptr=step_ptr,
+                bias_correction2_sqrt=bc2s, grad_scale=grad_scale,
+                step_ptr=self.step_t.data_ptr() if self.device_step else None,
             )
             _lib.call("dpc_adamw", args, p.device)
             return
+        if lo != 0 or hi != p.numel():
+            raise ValueError("FlatAdamW.update: sub-ranges need the HIP path (4-aligned)")
         if p.device.type == "cpu" and grad_scale_t is None and g.device.type == "cpu":
             # host path (FSDP --cpu_offload): one fused native pass (runtime/csrc/runtime.cpp)
             try:

@@ -126,6 +126,28 @@ class DDPStore(LocalStore):
         if self.overlap and self._ready[bi] == self.accum_steps * len(self.buckets[bi]):
             self._launch(bi)
 
+    def bucket_range(self, bi):
+        return self._range(bi)
+
+    def launch_all(self):
+        """Enqueue every bucket not launched yet (overlap off, or buckets left partial)."""
+        if self.world > 1:
+            for bi in range(len(self.buckets)):
+                self._launch(bi)
+
+    def wait_bucket(self, bi):
+        """Order the current stream after bucket ``bi``'s all-reduce (no host sync)."""
+        if self.world > 1:
+            self._works[bi].wait()
+            if bi in self._tmp:
+                lo, hi = self._range(bi)
+                self.grads[lo:hi].copy_(self._tmp[bi])
+
+    def reset_buckets(self):
+        self._works.clear()
+        self._tmp.clear()
+        self._ready = [0] * len(self.buckets)
+
     def finish_grads(self):
         """Wait for every bucket (launching any not yet launched, e.g. overlap off)."""
         if self.world > 1:

@@ -74,6 +74,10 @@ class P2P:
         self.prev = pp_ranks[stage - 1] if stage > 0 else None
         self.next = pp_ranks[stage + 1] if stage < self.n - 1 else None
         self._pending = []
+        # gloo's send/recv take host memory only: when a GPU run is rehearsed over gloo
+        # (DPC_DIST_BACKEND=gloo, several ranks on one device) stage the payloads through host
+        self.host_staged = (torch.device(device).type == "cuda" and dist.is_initialized()
+                            and dist.get_backend() == "gloo")
 
     def _run(self, ops):
         if not ops:
@@ -87,17 +91,26 @@ class P2P:
         """One grouped p2p step. Returns (from_prev, from_next)."""
         ops = []
         fp = fn = None
+        bdev = "cpu" if self.host_staged else self.device
+
+        def payload(t):
+            t = t.detach().contiguous()
+            return t.cpu() if self.host_staged else t
+
         if send_next is not None:
-            ops.append(dist.P2POp(dist.isend, send_next.contiguous(), self.next))
+            ops.append(dist.P2POp(dist.isend, payload(send_next), self.next))
         if send_prev is not None:
-            ops.append(dist.P2POp(dist.isend, send_prev.contiguous(), self.prev))
+            ops.append(dist.P2POp(dist.isend, payload(send_prev), self.prev))
         if recv_prev_shape is not None:
-            fp = torch.empty(recv_prev_shape, device=self.device, dtype=dtype)
+            fp = torch.empty(recv_prev_shape, device=bdev, dtype=dtype)
             ops.append(dist.P2POp(dist.irecv, fp, self.prev))
         if recv_next_shape is not None:
-            fn = torch.empty(recv_next_shape, device=self.device, dtype=dtype)
+            fn = torch.empty(recv_next_shape, device=bdev, dtype=dtype)
             ops.append(dist.P2POp(dist.irecv, fn, self.next))
         self._run(ops)
+        if self.host_staged:
+            fp = fp.to(self.device) if fp is not None else None
+            fn = fn.to(self.device) if fn is not None else None
         return fp, fn
 
 
