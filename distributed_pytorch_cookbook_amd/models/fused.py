@@ -58,6 +58,19 @@ def _qkv_weight(store, attn):
     return torch.cat([wq, wk, wv], 0)
 
 
+def _head_weight_padded(store, head, rows: int):
+    """[rows, D] view of the head's compute weight including the zero rows the flat layout
+    reserves after it (``_dpc_pad_rows``); the plain [V, D] view if there are none."""
+    w = store.weight(head.weight)
+    V, D = w.shape
+    if rows == V or getattr(head.weight, "_dpc_pad_rows", 0) == 0 or w.stride() != (D, 1):
+        return w
+    end = w.storage_offset() + rows * D
+    if end * w.element_size() > w.untyped_storage().nbytes():
+        return w
+    return w.as_strided((rows, D), (D, 1))
+
+
 def _qkv_grad(store, attn):
     gq, gk, gv = (store.grad(m.weight) for m in (attn.to_q, attn.to_k, attn.to_v))
     n = gq.shape[0]
@@ -211,7 +224,8 @@ class _HeadFn(torch.autograd.Function):
         hf, mu, rs = layernorm_fwd(x, w(norm.weight), w(norm.bias), LN_EPS, cdt)
         ld = vocab_ld(V) if x.is_cuda else V
         buf = torch.empty(T, ld, device=x.device, dtype=cdt)
-        linear_fwd(hf, w(head.weight), out=buf)  # padded columns come out 0 (B rows >= V read as 0)
+        # padded columns come out 0 (B rows >= V are the layout's zero rows / read as 0)
+        linear_fwd(hf, _head_weight_padded(store, head, ld), out=buf)
         loss, n_valid, n_correct = cross_entropy_fused(buf, targets, V, write_grad=training,
                                                        want_correct=want_correct)
         store.post_forward(unit, training)
@@ -234,7 +248,8 @@ class _HeadFn(torch.autograd.Function):
         scale = dloss.reshape(()).float().contiguous()
         linear_wgrad(dl, hf, out=g(head.weight), alpha_t=scale)
         # K = padded vocab: the CE kernel zeroed dlogits' pad columns, W_lm rows >= V read as 0
-        dhf = linear_dgrad(dlogits, w(head.weight), out_dtype=torch.float32, alpha_t=scale)
+        dhf = linear_dgrad(dlogits, _head_weight_padded(store, head, dlogits.shape[1]),
+                           out_dtype=torch.float32, alpha_t=scale)
         dx = torch.zeros_like(x)
         layernorm_bwd(dhf, x, mu, rs, w(norm.weight), dx, g(norm.weight), g(norm.bias))
         store.post_backward(unit)

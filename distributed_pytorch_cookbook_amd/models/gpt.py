@@ -189,6 +189,9 @@ class TransformerDecoderLM(nn.Module):
                                           heads=heads, dropout=dropout, activation=act_fn)
         self.norm_out = nn.LayerNorm(dim)
         self.lm_head = nn.Linear(dim, vocab_size, bias=False)
+        # flat-layout hint: reserve zero rows up to a multiple of 64 after the head matrix
+        # (parallel/store.py) so the padded-vocab logits GEMMs see a whole [Vp, D] operand
+        self.lm_head.weight._dpc_pad_rows = 64
         # execution state (not modules / not in the state_dict)
         object.__setattr__(self, "param_store", None)
         object.__setattr__(self, "stage", None)  # pipeline stage descriptor (None = whole model)

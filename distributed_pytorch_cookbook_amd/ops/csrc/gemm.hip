@@ -23,6 +23,10 @@
 //     walked in GROUP_M-row supertiles for operand reuse.
 #include "common.h"
 
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+
 namespace dpc {
 
 struct GemmArgs {
@@ -1019,6 +1023,32 @@ DPC_API void dpc_gemm_set_splits(int s) { g_force_splits = s; }
 
 static inline bool al(const void* p, int b) { return ((uintptr_t)p % b) == 0; }
 
+// Per-class implementation override for sweeps, from the environment, e.g.
+// DPC_GEMM_POLICY="fs=11,dl=4": fs / fl = forward (both k-major) with K <= / > 1024,
+// ds / dl = dgrad (B mn-major) with K <= / > 2304, w = weight gradient (both mn-major).
+static int g_policy[5] = {0, 0, 0, 0, 0};
+static int g_policy_read = 0;
+static int policy_impl(const GemmArgs* a) {
+  if (!g_policy_read) {
+    g_policy_read = 1;
+    if (const char* e = getenv("DPC_GEMM_POLICY")) {
+      const char* names[5] = {"fs", "fl", "ds", "dl", "w"};
+      for (int c = 0; c < 5; ++c) {
+        char key[8];
+        snprintf(key, sizeof key, "%s=", names[c]);
+        for (const char* q = e; (q = strstr(q, key)) != nullptr; ++q)
+          if (q == e || q[-1] == ',') { g_policy[c] = atoi(q + strlen(key)); break; }
+      }
+    }
+  }
+  int c;
+  if (a->a_kmaj && a->b_kmaj) c = a->K <= 1024 ? 0 : 1;
+  else if (a->a_kmaj) c = a->K <= 2304 ? 2 : 3;
+  else if (!a->b_kmaj) c = 4;
+  else return 0;
+  return g_policy[c];
+}
+
 DPC_API int dpc_gemm(const GemmArgs* a, hipStream_t stream) {
   if (a->M <= 0 || a->N <= 0) return 0;
   const int tiles = ((a->M + BM - 1) / BM) * ((a->N + BN - 1) / BN);
@@ -1047,12 +1077,14 @@ DPC_API int dpc_gemm(const GemmArgs* a, hipStream_t stream) {
       if (a->a_kmaj && a->b_kmaj && a->K <= 1024) impl = 10;
       else if (a->a_kmaj && !a->b_kmaj && a->K <= 2304) impl = 4;
       else if (!a->a_kmaj && !a->b_kmaj && a->M > 2304 && a->M <= 4096) impl = 4;
+      const int pol = policy_impl(a);
+      if (pol > 0) impl = pol;
     }
   }
   // plain f32 products (weight gradients: small M x N, K = tokens) are split along K
   const bool plain = a->out_f32 && !a->bias && !a->residual && !a->aux_in && !a->aux_out &&
                      !a->colsum && !a->act && !a->act_bwd;
-  if (g_gemm_impl < 0 && v2_ok && plain && !a->a_kmaj && !a->b_kmaj) {
+  if (g_gemm_impl < 0 && v2_ok && plain && !a->a_kmaj && !a->b_kmaj && policy_impl(a) <= 0) {
     // weight gradient: the 3-deep 32-k ring (3 workgroups per CU) once there are enough
     // 128x128 tiles to spread over the k-splits, else the 2-stage 64-k kernel
     const int t128 = ((a->M + BM - 1) / BM) * ((a->N + BN - 1) / BN);

@@ -22,6 +22,7 @@ same math with torch ops -- that expression is also the numerics oracle of the t
 from __future__ import annotations
 
 import math
+import os
 
 import torch
 import torch.nn.functional as F
@@ -56,6 +57,39 @@ def act_grad_ref(z: torch.Tensor, act: int) -> torch.Tensor:
         t = torch.tanh(u)
         return 0.5 * (1 + t) + 0.5 * z * (1 - t * t) * k0 * (1 + 3 * k1 * z * z)
     return torch.ones_like(z)
+
+
+# Optional vendor path for plain products (no epilogue beyond a scale: the logits GEMM, the
+# f32 input gradients of the QKV / up / lm_head projections): DPC_BLAS_PLAIN=1 sends them to
+# hipBLASLt through torch.mm.  Off by default: in isolation hipBLASLt runs those shapes
+# 10-30 % faster (profiles/kernels_r1_v4_b32.json), but in the full GPT-2 step the
+# sustained-load clock absorbs it -- 2.3 ms/step less kernel time, identical step time
+# (profiles/r1_blas_plain_ab.txt) -- so every product stays on the hand-written dpc_gemm.
+_BLAS_PLAIN = os.environ.get("DPC_BLAS_PLAIN", "0") == "1"
+_BLAS_MIN_FLOP = 2 ** 34  # below ~17 GFLOP the choice does not matter: keep dpc_gemm
+
+
+def set_blas_plain(on: bool) -> None:
+    global _BLAS_PLAIN
+    _BLAS_PLAIN = bool(on)
+
+
+def _blas_plain(a, b, a_kmaj, b_kmaj, out, M, N, K, alpha, alpha_t) -> bool:
+    """out = alpha (* alpha_t) * A @ B^T through hipBLASLt; False if not applicable."""
+    am = a if a_kmaj else a.t()   # [M, K]
+    bm = b.t() if b_kmaj else b   # [K, N]
+    if (tuple(am.shape) != (M, K) or tuple(bm.shape) != (K, N) or not out.is_contiguous()
+            or 2.0 * M * N * K < _BLAS_MIN_FLOP):
+        return False
+    if out.dtype == torch.bfloat16:
+        torch.mm(am, bm, out=out)
+    else:
+        torch.ops.aten.mm.dtype_out(am, bm, out.dtype, out=out)
+    if alpha != 1.0:
+        out.mul_(alpha)
+    if alpha_t is not None:
+        out.mul_(alpha_t)
+    return True
 
 
 def _check_operand(t: torch.Tensor, rows: int, cols: int, name: str) -> None:
@@ -123,6 +157,11 @@ def gemm(
                 raise ValueError(f"gemm: {nm} must be contiguous-last {dt}")
         if out.dtype not in (torch.float32, torch.bfloat16):
             raise ValueError("gemm: out must be f32 or bf16")
+        plain = (bias is None and residual is None and aux_in is None and aux_out is None
+                 and colsum is None and not act and not act_bwd and not accumulate)
+        if (plain and _BLAS_PLAIN and _lib.forced_gemm_impl < 0
+                and _blas_plain(a, b, a_kmaj, b_kmaj, out, M, N, K, alpha, alpha_t)):
+            return out
         args = _lib.GemmArgs(
             A=a.data_ptr(), B=b.data_ptr(), C=out.data_ptr(),
             bias=_lib.ptr(bias), residual=_lib.ptr(residual), aux_in=_lib.ptr(aux_in),

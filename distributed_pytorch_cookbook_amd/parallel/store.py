@@ -61,7 +61,14 @@ class FlatLayout:
                     e = Entry(names[id(p)], p, ui, off, p.numel(), p.shape)
                     self.entries.append(e)
                     self.by_param[id(p)] = e
-                    off += _round(p.numel(), ALIGN)
+                    # a matrix flagged ``_dpc_pad_rows`` (the lm_head) gets zero rows up to
+                    # that multiple right after it, so a row-padded view (vocab 50257 ->
+                    # 50304) is a plain [Vp, D] operand; the zeros stay zero (grad 0, decay 0)
+                    reserve = p.numel()
+                    pad = getattr(p, "_dpc_pad_rows", 0)
+                    if pad and p.dim() == 2:
+                        reserve = _round(p.shape[0], pad) * p.shape[1]
+                    off += _round(reserve, ALIGN)
             end = _round(off, unit_align)
             self.unit_ranges.append((start, end))
             off = end
