@@ -170,7 +170,7 @@ forced_gemm_impl = -1
 
 def set_gemm_impl(impl: int) -> None:
     """Force a GEMM implementation (tests / sweeps): -1 auto (default), 1 register-staged v1,
-    2-5 LDS-DMA 128x128 v2 variants, 6-10 large-tile v3 variants, 11 pipelined 256x256 v4
+    2-5 LDS-DMA 128x128 v2 variants, 6-10 large-tile v3 variants, 11 pipelined 256x256 v4, 12 256x256 ping-pong v5
     (table at the dispatcher, ``csrc/gemm.hip``)."""
     global forced_gemm_impl
     forced_gemm_impl = int(impl)

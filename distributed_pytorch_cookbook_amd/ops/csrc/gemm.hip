@@ -966,9 +966,241 @@ __global__ __launch_bounds__(512, 1) void gemm4_kernel(GemmArgs p, unsigned long
   }
 }
 
+// =====================================================================================
+// v5: 256x256 ping-pong.  Same 4-slot ring of 32-deep k-slices and LDS images as v4, but the
+// two wave groups of the workgroup (waves 0-3 = rows 0-127, waves 4-7 = rows 128-255; waves
+// w and w+4 share a SIMD) run one barrier interval apart: while one group's MFMA segment
+// (16 x v_mfma_f32_16x16x32_bf16 = 256 cycles) runs, its SIMD partner is in a read segment
+// (fragment ds_reads, LDS-DMA issue, counted vmcnt, lgkmcnt(0)) and vice versa, so the
+// matrix pipe of every SIMD alternates between two waves instead of stalling on one wave's
+// reads.  Per k-slice s each wave runs two phases:
+//   phase (s,0): read B(s) + A rows 0-63 (s)                        | MFMA rows 0-63
+//   phase (s,1): read A rows 64-127 (s); DMA slice s+3; wait slice s+1 | MFMA rows 64-127
+// A read segment only issues its ds_reads; they are retired by lgkmcnt waits at the start of
+// the following MFMA segment.  RAW: slice s+1 is read in phase (s+1,0), after every wave's
+// counted vmcnt in its phase (s,1) read segment and the barrier that ends it (the lagging
+// group's wait precedes the barrier before the leading group's next read segment).  WAR:
+// slot (s+3)%4 last held slice s-1, last read in phase (s-1,1) -- two phases before the DMA,
+// so even the lagging group's reads were retired (start of its MFMA segment) before a barrier
+// the issuing wave has passed.  Slices past the end are issued with an empty descriptor (they
+// land as zeros in a slot nobody reads) so every vmcnt in the loop is the same constant.
+template <int NL>
+__device__ __forceinline__ void issue_tile_v(const void* base, unsigned long long total, unsigned long long off,
+                                             bool valid, const int* voff, bf16_t* lds_tile, int wave) {
+  const unsigned long long left = (valid && off < total) ? total - off : 0ull;
+  const unsigned nrec = left > 0xffffffffull ? 0xffffffffu : (unsigned)left;
+  const __amdgpu_buffer_rsrc_t rs =
+      __builtin_amdgcn_make_buffer_rsrc((void*)((const char*)base + (valid ? off : 0ull)), 0, nrec, 0x00020000);
+#pragma unroll
+  for (int i = 0; i < NL; ++i) {
+    const int j = wave * NL + i;
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void_t)(lds_tile + j * 512), 16, voff[i], 0, 0, 0);
+  }
+}
+
+__device__ __forceinline__ void seg_barrier() {
+  __builtin_amdgcn_sched_barrier(0);
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+}
+
+template <bool AK, bool BK>
+__global__ __launch_bounds__(512, 1) void gemm5_kernel(GemmArgs p, unsigned long long a_bytes,
+                                                       unsigned long long b_bytes) {
+  using Cfg = V3Cfg<256, 256, 2, 4, 32, 4>;
+  constexpr int NS = 4, SLOT = Cfg::TA + Cfg::TB;
+  constexpr int NLA = Cfg::NLA, NLB = Cfg::NLB;  // 2 + 2 DMA instructions per wave per slice
+  __shared__ __attribute__((aligned(16))) bf16_t smem[Cfg::SMEM];
+  const int tiles_m = (p.M + 255) / 256, tiles_n = (p.N + 255) / 256;
+  const int nwg = tiles_m * tiles_n;
+  const TileSlot ts = tile_slot(p, nwg);
+  const int bid = ts.bid;
+  const int group = GROUP_M * tiles_n;
+  const int gid = bid / group, first_m = gid * GROUP_M;
+  const int gsz = min(tiles_m - first_m, GROUP_M);
+  const int tm = first_m + (bid % group) % gsz;
+  const int tn = (bid % group) / gsz;
+  const int m0 = tm * 256, n0 = tn * 256;
+
+  const int lane = threadIdx.x & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wr = wid >> 2, wc = wid & 3;
+  const int ar = wr * 128, bc = wc * 64;
+
+  int va[NLA], vb[NLB];
+  dma_offsets3<32, AK, NLA>(va, p.lda, wid, lane);
+  dma_offsets3<32, BK, NLB>(vb, p.ldb, wid, lane);
+  const unsigned long long a_org = AK ? (unsigned long long)m0 * p.lda * 2 : (unsigned long long)m0 * 2;
+  const unsigned long long b_org = BK ? (unsigned long long)n0 * p.ldb * 2 : (unsigned long long)n0 * 2;
+  const unsigned long long a_step = AK ? 64ull : 32ull * p.lda * 2;
+  const unsigned long long b_step = BK ? 64ull : 32ull * p.ldb * 2;
+  floatx4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+
+  const int nk_all = (p.K + 31) / 32;
+  const int splits = ts.splits;
+  const int per = (nk_all + splits - 1) / splits;
+  const int kt0 = ts.split * per;
+  const int nk = max(0, min(nk_all, kt0 + per) - kt0);
+#define DPC_ISSUE5A(s_)                                                                              \
+  issue_tile_v<NLA>(p.A, a_bytes, a_org + a_step * (unsigned long long)(kt0 + (s_)), (s_) < nk, va,  \
+                    smem + ((s_) % NS) * SLOT, wid)
+#define DPC_ISSUE5B(s_)                                                                              \
+  issue_tile_v<NLB>(p.B, b_bytes, b_org + b_step * (unsigned long long)(kt0 + (s_)), (s_) < nk, vb,  \
+                    smem + ((s_) % NS) * SLOT + Cfg::TA, wid)
+
+  if (nk > 0) {
+    DPC_ISSUE5A(0); DPC_ISSUE5B(0);
+    DPC_ISSUE5A(1); DPC_ISSUE5B(1);
+    DPC_ISSUE5A(2); DPC_ISSUE5B(2);
+    wait_vm<2 * (NLA + NLB)>();  // slice 0 landed (slices 1, 2 in flight)
+    seg_barrier();
+    if (wr == 1) seg_barrier();  // the second group runs one barrier interval behind
+    bf16x8 alo[4], ahi[4], b[4];
+    for (int s = 0; s < nk; ++s) {
+      const bf16_t* la = smem + (s % NS) * SLOT;
+      const bf16_t* lb = la + Cfg::TA;
+      // ---- phase (s,0): read segment
+#pragma unroll
+      for (int j = 0; j < 4; ++j) b[j] = frag3<32, BK>(lb, bc + j * 16, 0, lane);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) alo[i] = frag3<32, AK>(la, ar + i * 16, 0, lane);
+      seg_barrier();
+      // ---- phase (s,0): MFMA segment (the compiler's counted lgkmcnt waits retire the reads)
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(alo[i], b[j], acc[i][j], 0, 0, 0);
+      __builtin_amdgcn_s_setprio(0);
+      seg_barrier();
+      // ---- phase (s,1): read segment
+#pragma unroll
+      for (int i = 0; i < 4; ++i) ahi[i] = frag3<32, AK>(la, ar + 64 + i * 16, 0, lane);
+      DPC_ISSUE5A(s + 3);
+      DPC_ISSUE5B(s + 3);
+      wait_vm<2 * (NLA + NLB)>();  // slice s+1 landed for this wave
+      seg_barrier();
+      // ---- phase (s,1): MFMA segment
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          acc[4 + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ahi[i], b[j], acc[4 + i][j], 0, 0, 0);
+      __builtin_amdgcn_s_setprio(0);
+      seg_barrier();
+    }
+    if (wr == 0) seg_barrier();  // rebalance the barrier count of the two groups
+  }
+#undef DPC_ISSUE5A
+#undef DPC_ISSUE5B
+
+  // ---------------- epilogue: four passes of 32 rows per wave through LDS (as v4)
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  float alpha = p.alpha;
+  if (p.alpha_ptr) alpha *= *p.alpha_ptr;
+  float* ct = reinterpret_cast<float*>(smem) + wid * 32 * 64;
+  const int c4 = lane & 15;
+  const int n = n0 + bc + c4 * 4;
+  const bool nok = n < p.N;
+  float4 bias4 = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (p.bias && nok) bias4 = *reinterpret_cast<const float4*>(p.bias + n);
+  float cs[4] = {0.f, 0.f, 0.f, 0.f};
+  const bf16_t* aux_in = static_cast<const bf16_t*>(p.aux_in);
+  bf16_t* aux_out = static_cast<bf16_t*>(p.aux_out);
+#pragma unroll
+  for (int h = 0; h < 4; ++h) {
+    __syncthreads();
+#pragma unroll
+    for (int ii = 0; ii < 2; ++ii)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int row = ii * 16 + (lane >> 4) * 4 + r;
+          const int col = (j * 16 + (lane & 15)) ^ (((row >> 2) & 3) << 4);
+          ct[row * 64 + col] = acc[2 * h + ii][j][r] * alpha;
+        }
+    __syncthreads();
+    if (splits > 1) {
+      split_rows_atomic(ct, static_cast<float*>(p.C), p.ldc, m0 + ar + h * 32, n0 + bc, p.M, p.N, lane);
+      continue;
+    }
+#pragma unroll 2
+    for (int t = 0; t < 8; ++t) {
+      const int row = (lane >> 4) + 4 * t;
+      const int m = m0 + ar + h * 32 + row;
+      const int col = (c4 * 4) ^ (((row >> 2) & 3) << 4);
+      float4 v4 = *reinterpret_cast<const float4*>(ct + row * 64 + col);
+      if (m >= p.M || !nok) continue;
+      float v[4] = {v4.x + bias4.x, v4.y + bias4.y, v4.z + bias4.z, v4.w + bias4.w};
+      if (p.act_bwd) {
+        const uint2 z = *reinterpret_cast<const uint2*>(aux_in + (long long)m * p.ld_aux_in + n);
+        v[0] *= act_grad(__uint_as_float(z.x << 16), p.act_bwd);
+        v[1] *= act_grad(__uint_as_float(z.x & 0xffff0000u), p.act_bwd);
+        v[2] *= act_grad(__uint_as_float(z.y << 16), p.act_bwd);
+        v[3] *= act_grad(__uint_as_float(z.y & 0xffff0000u), p.act_bwd);
+      }
+#pragma unroll
+      for (int e = 0; e < 4; ++e) cs[e] += v[e];
+      if (aux_out) {
+        uint2 w;
+        w.x = pack2bf(v[0], v[1]);
+        w.y = pack2bf(v[2], v[3]);
+        *reinterpret_cast<uint2*>(aux_out + (long long)m * p.ld_aux_out + n) = w;
+      }
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[e] = act_fwd(v[e], p.act);
+      if (p.residual) {
+        const float4 r4 = *reinterpret_cast<const float4*>(p.residual + (long long)m * p.ldr + n);
+        v[0] += r4.x; v[1] += r4.y; v[2] += r4.z; v[3] += r4.w;
+      }
+      const long long ci = (long long)m * p.ldc + n;
+      if (p.out_f32) {
+        float4* C = reinterpret_cast<float4*>(static_cast<float*>(p.C) + ci);
+        if (p.accumulate) {
+          const float4 o = *C;
+          v[0] += o.x; v[1] += o.y; v[2] += o.z; v[3] += o.w;
+        }
+        *C = make_float4(v[0], v[1], v[2], v[3]);
+      } else {
+        uint2 w;
+        w.x = pack2bf(v[0], v[1]);
+        w.y = pack2bf(v[2], v[3]);
+        *reinterpret_cast<uint2*>(static_cast<bf16_t*>(p.C) + ci) = w;
+      }
+    }
+  }
+  if (p.colsum) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      cs[e] += __shfl_xor(cs[e], 16, 64);
+      cs[e] += __shfl_xor(cs[e], 32, 64);
+    }
+    if ((lane >> 4) == 0 && nok) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) atomicAdd(p.colsum + n + e, cs[e]);
+    }
+  }
+}
+
 }  // namespace dpc
 
 using namespace dpc;
+
+static void launch_v5(const GemmArgs* a, dim3 grid, hipStream_t stream, unsigned long long ab,
+                      unsigned long long bb) {
+  if (a->a_kmaj && a->b_kmaj) hipLaunchKernelGGL((gemm5_kernel<true, true>), grid, dim3(512), 0, stream, *a, ab, bb);
+  else if (a->a_kmaj) hipLaunchKernelGGL((gemm5_kernel<true, false>), grid, dim3(512), 0, stream, *a, ab, bb);
+  else if (!a->b_kmaj) hipLaunchKernelGGL((gemm5_kernel<false, false>), grid, dim3(512), 0, stream, *a, ab, bb);
+  else hipLaunchKernelGGL((gemm5_kernel<false, true>), grid, dim3(512), 0, stream, *a, ab, bb);
+}
 
 static void launch_v4(const GemmArgs* a, dim3 grid, hipStream_t stream, unsigned long long ab,
                       unsigned long long bb) {
@@ -1009,7 +1241,7 @@ static void launch_v2(const GemmArgs* a, dim3 grid, hipStream_t stream, unsigned
 
 // -1: auto; 1: v1; 2: v2 KB64 x2 stages; 3: KB64 x3; 4: KB32 x3; 5: KB32 x4;
 // 6-10: v3 (6: 256x256 KB64 x2, 7: 256x256 KB32 x4, 8: 256x128 KB64 x2, 9: 256x128 KB32 x4,
-// 10: 256x128 KB32 x3); 11: v4 (256x256, pipelined k32 ring)
+// 10: 256x128 KB32 x3); 11: v4 (256x256, pipelined k32 ring); 12: v5 (256x256 ping-pong)
 static int g_gemm_impl = -1;
 // XCD-aligned split-K mapping (tile_slot): measured ~6 % slower than the default mapping on
 // the GPT-2 weight gradients, so off unless requested (sweeps)
@@ -1085,10 +1317,11 @@ DPC_API int dpc_gemm(const GemmArgs* a, hipStream_t stream) {
   const bool plain = a->out_f32 && !a->bias && !a->residual && !a->aux_in && !a->aux_out &&
                      !a->colsum && !a->act && !a->act_bwd;
   if (g_gemm_impl < 0 && v2_ok && plain && !a->a_kmaj && !a->b_kmaj && policy_impl(a) <= 0) {
-    // weight gradient: the 3-deep 32-k ring (3 workgroups per CU) once there are enough
-    // 128x128 tiles to spread over the k-splits, else the 2-stage 64-k kernel
+    // weight gradient: the 256x256 ping-pong kernel (v5) once there are enough 128x128 tiles
+    // to spread over the k-splits (2304x768 and up: 780-880 TF/s vs 720 for the 3-deep
+    // 128x128 ring, bench/kernels.py on MI355X), else the 2-stage 64-k kernel
     const int t128 = ((a->M + BM - 1) / BM) * ((a->N + BN - 1) / BN);
-    impl = t128 >= 100 ? 4 : 2;
+    impl = t128 >= 100 ? 12 : 2;
   }
   if (impl >= 2 && !v2_ok) impl = 1;
   GemmArgs b = *a;  // dispatcher-owned copy: split-K mode is decided here
@@ -1108,7 +1341,7 @@ DPC_API int dpc_gemm(const GemmArgs* a, hipStream_t stream) {
       // rounds = ceil(tiles * s / resident workgroups) (wave quantisation of the grid) and
       // beta * s the split-K partial-sum atomics relative to the K-proportional MFMA work.
       // resident workgroups per launch round: 256 CUs x workgroups per CU (LDS-bound, V2Cfg::WGS)
-      const int slots = impl >= 6 || impl == 3 ? 256 : (impl == 4 ? 768 : 512);
+      const int slots = impl >= 6 || impl == 3 ? 256 : (impl == 4 ? 768 : 512);  // (v3-v5: 1 WG/CU)
       const double beta = 0.0056 * 32768.0 / (double)a->K;
       double best = 1e30;
       for (int s = 1; s <= 16 && (s == 1 || nk / s >= 8); ++s) {
@@ -1136,6 +1369,7 @@ DPC_API int dpc_gemm(const GemmArgs* a, hipStream_t stream) {
       case 9: launch_v3<256, 128, 4, 2, 32, 4>(&b, g, stream, ab, bb); break;
       case 10: launch_v3<256, 128, 4, 2, 32, 3>(&b, g, stream, ab, bb); break;
       case 11: launch_v4(&b, g, stream, ab, bb); break;
+      case 12: launch_v5(&b, g, stream, ab, bb); break;
       default: launch_v2<64, 2>(&b, g, stream, ab, bb); break;
     }
     return (int)hipGetLastError();

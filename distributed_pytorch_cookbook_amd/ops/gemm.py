@@ -59,13 +59,14 @@ def act_grad_ref(z: torch.Tensor, act: int) -> torch.Tensor:
     return torch.ones_like(z)
 
 
-# Optional vendor path for plain products (no epilogue beyond a scale: the logits GEMM, the
-# f32 input gradients of the QKV / up / lm_head projections): DPC_BLAS_PLAIN=1 sends them to
-# hipBLASLt through torch.mm.  Off by default: in isolation hipBLASLt runs those shapes
-# 10-30 % faster (profiles/kernels_r1_v4_b32.json), but in the full GPT-2 step the
-# sustained-load clock absorbs it -- 2.3 ms/step less kernel time, identical step time
-# (profiles/r1_blas_plain_ab.txt) -- so every product stays on the hand-written dpc_gemm.
-_BLAS_PLAIN = os.environ.get("DPC_BLAS_PLAIN", "0") == "1"
+# Vendor path for PLAIN products only (no epilogue beyond a scale: the QKV and logits
+# GEMMs, the input gradients of the QKV / out / up / lm_head projections): hipBLASLt through
+# torch.mm.  Every product with a fused epilogue (bias, activation, act', residual, aux,
+# column sums) and every weight gradient stays on the hand-written dpc_gemm.  On by default
+# (DPC_BLAS_PLAIN=0 turns it off): GPT-2 small dp1 B=32 on one MI355X, 48.4 -> 46.2 ms/step
+# (676K -> 709K tok/s, profiles/r1_v8_blas_ab.txt); in isolation hipBLASLt runs those plain
+# shapes 10-45 % faster than dpc_gemm's best tile (bench/kernels.py).
+_BLAS_PLAIN = os.environ.get("DPC_BLAS_PLAIN", "1") == "1"
 _BLAS_MIN_FLOP = 2 ** 34  # below ~17 GFLOP the choice does not matter: keep dpc_gemm
 
 
