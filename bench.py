@@ -28,6 +28,7 @@ sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 
 from distributed_pytorch_cookbook_amd.config import apply_preset, build_parser  # noqa: E402
 from distributed_pytorch_cookbook_amd.parallel import comm  # noqa: E402
+from distributed_pytorch_cookbook_amd.utils.metrics import mfu, train_flops_per_token  # noqa: E402
 
 METRIC = "tokens/sec (node) GPT-2 training per recipe (DDP/FSDP/PP) at 1/2/4/8 MI355X"
 # The reference publishes no numbers.  vs_baseline compares against the
@@ -147,6 +148,8 @@ def main():
         "config": {"model": model_name, "global_batch": B * engine.dp_world, "seq_len": S,
                    "parallelism": par, "recipe": f"main-{a.recipe.replace('_', '-')}.py",
                    "tokens_per_step": tokens_per_step, "final_loss": round(loss_v, 4),
+                   "mfu_per_gpu": round(mfu(value / n, train_flops_per_token(
+                       args.dim, args.heads, args.head_dim, args.num_layers, vocab, S)), 4),
                    "baseline": ("stock PyTorch reference-default recipe (manual attention + torch.compile)"
                                 " x n_gpus" if base else None)},
     }

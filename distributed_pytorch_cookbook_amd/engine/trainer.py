@@ -24,6 +24,7 @@ from ..parallel import comm
 from ..utils.batch import generate, prepare_batch
 from ..utils.checkpoint import (latest_checkpoint, load_model_state, load_train_state, rng_state,
                                 save_model_state, save_train_state, set_rng_state)
+from ..utils.metrics import mfu, peak_memory_gib, train_flops_per_token
 from ..utils.profiling import StepProfiler, mark, maybe_inject_fault
 
 PRINT_FREQ = 8
@@ -70,6 +71,9 @@ class Trainer:
         self.log = engine.is_logger
         self.start_epoch = 0
         self.history = []
+        vocab = getattr(tokenizer, "vocab_size", 50257)
+        self.flops_per_token = train_flops_per_token(args.dim, args.heads, args.head_dim, args.num_layers,
+                                                     vocab, args.sequence_length)
 
     # ------------------------------------------------------------------ helpers
     def _jsonl(self, rec):
@@ -172,8 +176,12 @@ class Trainer:
                     torch.cuda.synchronize()
                 dt = time.perf_counter() - t0
                 tps = tokens / dt if dt > 0 else 0.0
-                pb.set_description(f"[training] Epoch {ei+1}/{a.epochs} | loss: {avg:.3f} | tok/s: {tps:,.0f}")
-                rec = {"epoch": ei + 1, "step": e.step_count, "loss": avg, "tokens_per_s": tps}
+                util = mfu(tps / max(comm.world_size(), 1), self.flops_per_token)
+                pb.set_description(f"[training] Epoch {ei+1}/{a.epochs} | loss: {avg:.3f} | tok/s: {tps:,.0f}"
+                                   f" | MFU {100 * util:.1f}%")
+                rec = {"epoch": ei + 1, "step": e.step_count, "loss": avg, "tokens_per_s": tps,
+                       "tokens_per_s_per_gpu": tps / max(comm.world_size(), 1), "mfu": util,
+                       "step_ms": 1000.0 * dt / PRINT_FREQ, "peak_mem_gib": peak_memory_gib(self.device)}
                 self.history.append(rec)
                 self._jsonl(rec)
                 window, nwin, tokens, t0 = None, 0, 0, time.perf_counter()

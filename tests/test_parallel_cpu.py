@@ -1,5 +1,7 @@
 """DDP / FSDP / pipeline / pipeline x DDP engines on CPU (gloo, multi-process) must produce
 the same parameters as the single-process engine on the same global batch."""
+import os
+
 import pytest
 import torch
 
@@ -77,3 +79,21 @@ def test_1f1b_order_counts():
             inflight += 1 if k == "F" else -1
             mx = max(mx, inflight)
         assert mx <= 4 - st
+
+
+def test_comm_bw_bench_runs_on_gloo(tmp_path):
+    """bench/comm_bw.py: every collective of the engines, 2 ranks over gloo."""
+    import json
+    import subprocess
+    import sys
+
+    from dist_helpers import ROOT, free_port
+
+    out = tmp_path / "bw.json"
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes", "1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(free_port()), f"{ROOT}/bench/comm_bw.py",
+           "--cpu", "--sizes_mb", "0.25", "--iters", "2", "--warmup", "1", "--json", str(out)]
+    subprocess.run(cmd, check=True, timeout=180, capture_output=True, env={**os.environ, "OMP_NUM_THREADS": "1"})
+    rows = json.loads(out.read_text())
+    assert {r["op"] for r in rows} == {"all_reduce", "all_gather", "reduce_scatter", "broadcast", "sendrecv"}
+    assert all(r["busbw_GBps"] > 0 and r["world"] == 2 for r in rows)

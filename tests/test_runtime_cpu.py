@@ -69,3 +69,12 @@ def test_recipe_with_native_token_file(tmp_path, monkeypatch):
                                    "--cpu"])
     assert ckpt is not None and ckpt.exists()
     assert any("val_loss" in h for h in trainer.history)
+
+
+def test_train_flops_per_token_matches_survey_table():
+    """GPT-2 small 0.86, XL 10.28 GFLOP per trained token."""
+    from distributed_pytorch_cookbook_amd.utils.metrics import mfu, train_flops_per_token
+
+    assert abs(train_flops_per_token(768, 12, 64, 12, 50257, 1024) / 1e9 - 0.86) < 0.01
+    assert abs(train_flops_per_token(1600, 25, 64, 48, 50257, 1024) / 1e9 - 10.28) < 0.05
+    assert abs(mfu(1e6, 1e9) - 0.4) < 1e-9
