@@ -37,6 +37,9 @@ def build_parser(recipe: str = "single") -> argparse.ArgumentParser:
     p.add_argument("--model", type=str, default=None, choices=sorted(PRESETS),
                    help="architecture preset (overrides dim/head_dim/heads/num_layers/sequence_length)")
     p.add_argument("--activation", type=str, default=None, choices=["relu", "gelu"])
+    p.add_argument("--grad_scaler", action="store_true",
+                   help="dynamic loss scaling as the reference's GradScaler (fused non-finite check, "
+                        "skip + back-off on device); unnecessary for bf16, off by default")
     p.add_argument("--dropout", type=float, default=0.0)
     p.add_argument("--recompute", action="store_true",
                    help="activation recompute: keep only each layer's input, re-run its forward in backward")

@@ -18,6 +18,17 @@ class Engine:
     dp_world = 1
     collective_generate = False  # True if generate must run on every rank
     is_logger = True          # this rank prints / saves
+    scaler = None             # ops.amp.GradScaler when --grad_scaler (reference GradScaler)
+
+    def _scaled(self, loss):
+        return self.scaler.scale(loss) if self.scaler is not None else loss
+
+    def _scaler_state(self) -> dict:
+        return {"scaler": self.scaler.state_dict()} if self.scaler is not None else {}
+
+    def _load_scaler_state(self, st: dict) -> None:
+        if self.scaler is not None and st.get("scaler") is not None:
+            self.scaler.load_state_dict(st["scaler"])
 
     def train_step(self, batch: dict, targets: torch.Tensor) -> torch.Tensor:
         """One optimizer step; returns the (local) mean loss as a 0-dim device tensor,

@@ -25,7 +25,7 @@ class DataParallelEngine(Engine):
 
     def __init__(self, model, device, lr: float, group=None, bucket_mb: float = 128.0,
                  reduce_dtype=torch.float32, overlap: bool = True, compute_dtype=None,
-                 graph: bool = False, native_comm: bool = False):
+                 graph: bool = False, native_comm: bool = False, grad_scaler: bool = False):
         self.device = torch.device(device)
         self.model = model
         self.dp_group = group
@@ -39,6 +39,10 @@ class DataParallelEngine(Engine):
         else:
             self.store = LocalStore(model, device, compute_dtype=compute_dtype)
         self.opt = FlatAdamW(self.store.master, self.store.grads, lr=lr, shadow=self.store.shadow)
+        if grad_scaler:
+            from ..ops.amp import GradScaler
+
+            self.scaler = GradScaler(self.device)
         self.graph = graph and self.device.type == "cuda" and self.dp_world == 1
         self._graph = None
         self._gkey = None
@@ -47,7 +51,16 @@ class DataParallelEngine(Engine):
     def _step_body(self, batch, targets):
         self.store.zero_grad()
         out = self.model(**batch, targets=targets)
-        out.loss.backward()
+        self._scaled(out.loss).backward()
+        if self.scaler is not None:
+            # the non-finite check needs every bucket reduced before any parameter moves;
+            # all-reduced gradients are identical on every rank, so is the flag
+            if self.dp_world > 1:
+                self.store.finish_grads()
+            self.scaler.check(self.store.grads)
+            self.opt.step(grad_scale=1.0 / self.dp_world, **self.scaler.opt_kwargs(self.opt))
+            self.scaler.update()
+            return out.loss.detach()
         if self.dp_world > 1 and self.store.master.is_cuda:
             # bucket by bucket: AdamW of the buckets already reduced runs on the compute stream
             # while the last ones (the embeddings, whose backward comes last) are still being
@@ -130,11 +143,12 @@ class DataParallelEngine(Engine):
 
     def train_state(self):
         return {"optimizer": {k: (v.detach().cpu() if torch.is_tensor(v) else v)
-                              for k, v in self.opt.state_dict().items()}}
+                              for k, v in self.opt.state_dict().items()}, **self._scaler_state()}
 
     def load_train_state(self, st):
         self.opt.load_state_dict({k: (v.to(self.device) if torch.is_tensor(v) else v)
                                   for k, v in st["optimizer"].items()})
+        self._load_scaler_state(st)
 
     @property
     def step_count(self):

@@ -22,7 +22,7 @@ class FSDPEngine(Engine):
 
     def __init__(self, model, device, lr: float, group=None, prefetch: int = 1,
                  reshard_after_forward: bool = True, cpu_offload: bool = False, compute_dtype=None,
-                 reduce_dtype=torch.float32):
+                 reduce_dtype=torch.float32, grad_scaler: bool = False):
         self.device = torch.device(device)
         self.model = model
         self.dp_group = group
@@ -36,15 +36,29 @@ class FSDPEngine(Engine):
         grad = st.grads_host if st.cpu_offload else st.grads
         self.opt = FlatAdamW(st.master, grad, lr=lr, shadow=st.shadow)
         self.opt_rep = FlatAdamW(st.rep_master, st.rep_grads, lr=lr)  # replicated 1-D params
+        if grad_scaler:
+            from ..ops.amp import GradScaler
+
+            self.scaler = GradScaler(self.device)
 
     def train_step(self, batch, targets):
         st = self.store
         st.zero_grad()
         out = self.model(**batch, targets=targets)
-        out.loss.backward()
+        self._scaled(out.loss).backward()
         st.finish_grads()
         if st.cpu_offload:
             torch.cuda.current_stream().synchronize()  # grads_host D2H landed
+        if self.scaler is not None:
+            # shards differ per rank: the skip decision is reduced over the group
+            sc = self.scaler
+            sc.check(self.opt.grad)
+            sc.check(self.opt_rep.grad)
+            sc.reduce_flag(self.dp_group)
+            self.opt.step(grad_scale=1.0 / self.dp_world, **sc.opt_kwargs(self.opt))
+            self.opt_rep.step(grad_scale=1.0 / self.dp_world, **sc.opt_kwargs(self.opt_rep))
+            sc.update()
+            return out.loss.detach()
         self.opt.step(grad_scale=1.0 / self.dp_world)
         self.opt_rep.step(grad_scale=1.0 / self.dp_world)
         return out.loss.detach()
@@ -69,7 +83,7 @@ class FSDPEngine(Engine):
         m = st.gather_full(self.opt.exp_avg, dst_rank=0, rep_flat=self.opt_rep.exp_avg)
         v = st.gather_full(self.opt.exp_avg_sq, dst_rank=0, rep_flat=self.opt_rep.exp_avg_sq)
         return {"optimizer": {"step": self.opt.step_count, "exp_avg": m, "exp_avg_sq": v,
-                              "format": "canonical"}}
+                              "format": "canonical"}, **self._scaler_state()}
 
     def load_train_state(self, st):
         o = st["optimizer"]
@@ -78,6 +92,7 @@ class FSDPEngine(Engine):
         if isinstance(o.get("exp_avg"), dict):
             self.store.load_full(o["exp_avg"], self.opt.exp_avg, rep_flat=self.opt_rep.exp_avg)
             self.store.load_full(o["exp_avg_sq"], self.opt.exp_avg_sq, rep_flat=self.opt_rep.exp_avg_sq)
+        self._load_scaler_state(st)
 
     @property
     def step_count(self):

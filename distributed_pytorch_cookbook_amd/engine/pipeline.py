@@ -33,9 +33,13 @@ class PipelineEngine(Engine):
 
     def __init__(self, model, device, lr: float, pp: int, dp: int = 1, num_microbatches: int = 0,
                  schedule: str = "1f1b", bucket_mb: float = 128.0, compute_dtype=None,
-                 seq_len: int | None = None):
+                 seq_len: int | None = None, grad_scaler: bool = False):
         self.device = torch.device(device)
         self.model = model
+        if grad_scaler:
+            from ..ops.amp import GradScaler
+
+            self.scaler = GradScaler(self.device)
         world = comm.world_size()
         if pp * dp != world:
             raise ValueError(f"pp ({pp}) x dp ({dp}) must equal the world size ({world})")
@@ -146,7 +150,7 @@ class PipelineEngine(Engine):
         def backward(m, g):
             y = outputs.pop(m)
             if self.last:
-                y.backward()
+                self._scaled(y).backward()
             else:
                 torch.autograd.backward(y, g)
             x = inputs.pop(m)
@@ -190,6 +194,13 @@ class PipelineEngine(Engine):
                 p2p.exchange(send_prev=dx)
         if self.dp > 1:
             st.finish_grads()
+        if self.scaler is not None:
+            # every stage holds different gradients: one skip decision for the whole job
+            self.scaler.check(self.opt.grad)
+            self.scaler.reduce_flag(None)
+            self.opt.step(grad_scale=1.0 / self.dp, **self.scaler.opt_kwargs(self.opt))
+            self.scaler.update()
+            return acc.get("loss")
         self.opt.step(grad_scale=1.0 / self.dp)
         return acc.get("loss")
 
@@ -273,7 +284,7 @@ class PipelineEngine(Engine):
         m = self._gather_named(self._named_flat(self.opt.exp_avg))
         v = self._gather_named(self._named_flat(self.opt.exp_avg_sq))
         return {"optimizer": {"step": self.opt.step_count, "exp_avg": m, "exp_avg_sq": v,
-                              "format": "canonical"}}
+                              "format": "canonical"}, **self._scaler_state()}
 
     def load_train_state(self, st):
         o = st["optimizer"]
@@ -284,6 +295,7 @@ class PipelineEngine(Engine):
                 for e in self.store.entries:
                     if e.name in d:
                         self.store._view(flat, e).copy_(d[e.name])
+        self._load_scaler_state(st)
 
     @property
     def step_count(self):

@@ -87,8 +87,17 @@ class AdamArgs(ctypes.Structure):
         ("lr", c_float), ("beta1", c_float), ("beta2", c_float), ("eps", c_float),
         ("weight_decay", c_float), ("bias_correction1", c_float),
         ("bias_correction2_sqrt", c_float), ("grad_scale", c_float),
-        ("step_ptr", P),
+        ("step_ptr", P), ("skip_ptr", P),
     ]
+
+
+class AmpCheckArgs(ctypes.Structure):
+    _fields_ = [("g", P), ("n", LL), ("found_inf", P)]
+
+
+class AmpUpdateArgs(ctypes.Structure):
+    _fields_ = [("scale", P), ("inv_scale", P), ("found_inf", P), ("tracker", P),
+                ("growth", c_float), ("backoff", c_float), ("interval", c_int)]
 
 
 class CastArgs(ctypes.Structure):
@@ -125,6 +134,8 @@ _FUNCS = {
     "dpc_embedding_bwd": EmbArgs,
     "dpc_cross_entropy": CEArgs,
     "dpc_adamw": AdamArgs,
+    "dpc_amp_check": AmpCheckArgs,
+    "dpc_amp_update": AmpUpdateArgs,
     "dpc_cast_f32_bf16": CastArgs,
     "dpc_bias_act_bwd": BiasActArgs,
     "dpc_dropout_residual": DropResArgs,

@@ -172,9 +172,12 @@ struct AdamArgs {
   float grad_scale;
   const float* step_ptr;  // optional device step counter (HIP-graph replay): bias corrections
                           // are then computed on the device from it
+  const float* skip_ptr;  // optional device flag: != 0 -> leave everything untouched (the loss
+                          // scaler found a non-finite gradient this step)
 };
 
 __global__ __launch_bounds__(256) void adamw_kernel(AdamArgs a) {
+  if (a.skip_ptr && *a.skip_ptr != 0.f) return;
   const long long n4 = a.n >> 2;
   float gs = a.grad_scale;
   if (a.grad_scale_ptr) gs *= *a.grad_scale_ptr;
@@ -231,6 +234,60 @@ __global__ __launch_bounds__(256) void cast_kernel(CastArgs a) {
     w.y = pack2bf(v.z, v.w);
     reinterpret_cast<uint2*>(a.dst)[i] = w;
   }
+}
+
+// ------------------------------------------------------------------ dynamic loss scaling
+// Reference: torch.cuda.amp.GradScaler (main-single.py:78,99-101): _amp_foreach_non_finite_
+// check_and_unscale_ + _amp_update_scale_.  Here the unscale is folded into AdamW (its
+// grad_scale_ptr reads 1/scale), so the check only reads the flat gradient buffer once and
+// raises a device flag that AdamW (skip_ptr) and the scale update consume -- no host sync,
+// HIP-graph replayable.  Non-finite = exponent bits all ones (independent of fast-math flags).
+struct AmpCheckArgs {
+  const float* g;
+  long long n;
+  float* found_inf;
+};
+
+__device__ __forceinline__ bool nonfinite(float x) { return (__float_as_uint(x) & 0x7f800000u) == 0x7f800000u; }
+
+__global__ __launch_bounds__(256) void amp_check_kernel(AmpCheckArgs a) {
+  const long long n4 = a.n >> 2;
+  bool bad = false;
+  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n4; i += (long long)gridDim.x * 256) {
+    const float4 v = reinterpret_cast<const float4*>(a.g)[i];
+    bad |= nonfinite(v.x) | nonfinite(v.y) | nonfinite(v.z) | nonfinite(v.w);
+  }
+  if (blockIdx.x == 0 && threadIdx.x < (a.n & 3)) bad |= nonfinite(a.g[(n4 << 2) + threadIdx.x]);
+  if (__any(bad) && (threadIdx.x & 63) == 0) *a.found_inf = 1.f;  // every writer stores 1
+}
+
+struct AmpUpdateArgs {
+  float* scale;
+  float* inv_scale;
+  float* found_inf;  // consumed and cleared
+  float* tracker;    // consecutive finite steps
+  float growth, backoff;
+  int interval;
+};
+
+__global__ void amp_update_kernel(AmpUpdateArgs a) {
+  if (threadIdx.x != 0) return;
+  float s = *a.scale;
+  if (*a.found_inf != 0.f) {
+    s *= a.backoff;
+    *a.tracker = 0.f;
+  } else {
+    const float t = *a.tracker + 1.f;
+    if (t >= (float)a.interval) {
+      s *= a.growth;
+      *a.tracker = 0.f;
+    } else {
+      *a.tracker = t;
+    }
+  }
+  *a.scale = s;
+  *a.inv_scale = 1.f / s;
+  *a.found_inf = 0.f;
 }
 
 // ------------------------------------------------------------------ dropout
@@ -380,6 +437,17 @@ DPC_API int dpc_adamw(const AdamArgs* a, hipStream_t stream) {
   if (a->n <= 0) return 0;
   if (a->n % 4) return (int)hipErrorInvalidValue;
   hipLaunchKernelGGL(adamw_kernel, dim3(grid_for(a->n >> 2)), dim3(256), 0, stream, *a);
+  return (int)hipGetLastError();
+}
+
+DPC_API int dpc_amp_check(const AmpCheckArgs* a, hipStream_t stream) {
+  if (a->n <= 0) return 0;
+  hipLaunchKernelGGL(amp_check_kernel, dim3(grid_for((a->n + 3) >> 2)), dim3(256), 0, stream, *a);
+  return (int)hipGetLastError();
+}
+
+DPC_API int dpc_amp_update(const AmpUpdateArgs* a, hipStream_t stream) {
+  hipLaunchKernelGGL(amp_update_kernel, dim3(1), dim3(64), 0, stream, *a);
   return (int)hipGetLastError();
 }
 

@@ -41,23 +41,31 @@ class FlatAdamW:
         self.exp_avg_sq.copy_(sd["exp_avg_sq"])
 
     @torch.no_grad()
-    def step(self, grad_scale: float = 1.0, grad_scale_t: torch.Tensor | None = None) -> None:
-        self.begin_step()
-        self.update(0, self.param.numel(), grad_scale, grad_scale_t)
+    def step(self, grad_scale: float = 1.0, grad_scale_t: torch.Tensor | None = None,
+             skip_t: torch.Tensor | None = None) -> None:
+        self.begin_step(skip_t)
+        self.update(0, self.param.numel(), grad_scale, grad_scale_t, skip_t)
 
-    def begin_step(self) -> None:
-        """Advance the step count (host and, for HIP-graph replay, device counter)."""
+    def begin_step(self, skip_t: torch.Tensor | None = None) -> None:
+        """Advance the step count (host and, for HIP-graph replay, device counter).  With a
+        loss scaler, ``skip_t`` (device flag) keeps a skipped step out of the device count
+        that the bias corrections read (torch's GradScaler skips ``optimizer.step``)."""
         self.step_count += 1
         p = self.param
         if p.is_cuda and p.numel() % 4 == 0:
-            if self.device_step:
+            if skip_t is not None:
+                self.device_step = True
+                self.step_t.add_(1.0).sub_(skip_t.to(self.step_t.dtype))
+            elif self.device_step:
                 self.step_t.add_(1.0)
             else:
                 self.step_t.fill_(float(self.step_count))
+        elif skip_t is not None:
+            self.step_t.add_(1.0).sub_(skip_t.to(self.step_t.device, self.step_t.dtype))
 
     @torch.no_grad()
     def update(self, lo: int, hi: int, grad_scale: float = 1.0,
-               grad_scale_t: torch.Tensor | None = None) -> None:
+               grad_scale_t: torch.Tensor | None = None, skip_t: torch.Tensor | None = None) -> None:
         """Apply the current step to elements [lo, hi) of the flat buffers -- lets DDP update
         the buckets whose all-reduce has finished while the last one is still on the links."""
         b1, b2 = self.betas
@@ -76,11 +84,20 @@ class FlatAdamW:
                 beta2=b2, eps=self.eps, weight_decay=self.weight_decay, bias_correction1=bc1,
                 bias_correction2_sqrt=bc2s, grad_scale=grad_scale,
                 step_ptr=self.step_t.data_ptr() if self.device_step else None,
+                skip_ptr=_lib.ptr(skip_t),
             )
             _lib.call("dpc_adamw", args, p.device)
             return
         if lo != 0 or hi != p.numel():
             raise ValueError("FlatAdamW.update: sub-ranges need the HIP path (4-aligned)")
+        if skip_t is not None:
+            # non-HIP paths: a host-read flag (the CPU / offload paths synchronise anyway)
+            if float(skip_t) != 0.0:
+                return
+            t = float(self.step_t)  # counted without the skipped steps
+            bc1, bc2s = 1.0 - b1 ** t, math.sqrt(1.0 - b2 ** t)
+        if p.device.type == "cpu" and grad_scale_t is not None and grad_scale_t.numel() == 1:
+            grad_scale, grad_scale_t = grad_scale * float(grad_scale_t), None  # host path: a scalar
         if p.device.type == "cpu" and grad_scale_t is None and g.device.type == "cpu":
             # host path (FSDP --cpu_offload): one fused native pass (runtime/csrc/runtime.cpp)
             try:
@@ -93,8 +110,9 @@ class FlatAdamW:
                         self._host_shadow = torch.empty(p.numel(), dtype=torch.bfloat16,
                                                         pin_memory=torch.cuda.is_available())
                     host_shadow = self._host_shadow
+                hstep = int(round(float(self.step_t))) if skip_t is not None else self.step_count
                 runtime.adamw_host(p, g, self.exp_avg, self.exp_avg_sq, self.lr, b1, b2, self.eps,
-                                   self.weight_decay, self.step_count, grad_scale, host_shadow)
+                                   self.weight_decay, hstep, grad_scale, host_shadow)
                 if bf16_shadow:
                     self.shadow.copy_(host_shadow, non_blocking=True)
                 elif self.shadow is not None:

@@ -47,13 +47,15 @@ def build_engine(recipe: str, model, info, args):
             # (dropout masks are drawn per step on the host: not graph-replayable)
             graph=not args.disable_compile and not args.disable_amp and not args.dropout,
             native_comm=getattr(args, "comm", "torch") == "native",
+            grad_scaler=getattr(args, "grad_scaler", False),
         )
     if recipe == "fsdp":
         from .engine.fsdp import FSDPEngine
 
         return FSDPEngine(model, info.device, lr=args.learning_rate, prefetch=args.prefetch,
                           reshard_after_forward=not args.no_reshard_after_forward,
-                          cpu_offload=args.cpu_offload, compute_dtype=compute_dtype)
+                          cpu_offload=args.cpu_offload, compute_dtype=compute_dtype,
+                          grad_scaler=getattr(args, "grad_scaler", False))
     if recipe in ("pipe", "pipe_ddp"):
         from .engine.pipeline import PipelineEngine
 
@@ -64,7 +66,7 @@ def build_engine(recipe: str, model, info, args):
         return PipelineEngine(model, info.device, lr=args.learning_rate, pp=pp, dp=dp,
                               num_microbatches=args.num_microbatches or 2 * pp,
                               schedule=args.schedule, bucket_mb=args.bucket_mb,
-                              compute_dtype=compute_dtype)
+                              compute_dtype=compute_dtype, grad_scaler=getattr(args, "grad_scaler", False))
     raise ValueError(recipe)
 
 

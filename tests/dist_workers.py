@@ -101,3 +101,30 @@ def worker_pipe(rank, world, out, steps, pp, dp, micro, schedule):
     f(input_ids=ids, position_ids=torch.arange(5).unsqueeze(0))
     if rank == 0:
         torch.save({"sd": sd, "groups": eng.groups}, out)
+
+
+def worker_scaled(rank, world, out, kind):
+    """--grad_scaler on each engine kind (DDP / FSDP / pipeline): a 2^16-scaled backward with
+    the unscale folded into AdamW must land on the unscaled result."""
+    from distributed_pytorch_cookbook_amd.engine.data_parallel import DataParallelEngine
+    from distributed_pytorch_cookbook_amd.engine.fsdp import FSDPEngine
+    from distributed_pytorch_cookbook_amd.engine.pipeline import PipelineEngine
+    from distributed_pytorch_cookbook_amd.parallel import comm
+
+    comm.init_dist(force_cpu=True)
+    m = make_model()
+    if kind == "ddp":
+        eng = DataParallelEngine(m, "cpu", lr=LR, bucket_mb=0.05, grad_scaler=True)
+    elif kind == "fsdp":
+        eng = FSDPEngine(m, "cpu", lr=LR, grad_scaler=True)
+    else:
+        eng = PipelineEngine(m, "cpu", lr=LR, pp=world, dp=1, num_microbatches=2, bucket_mb=0.01, seq_len=S,
+                             grad_scaler=True)
+    dp, idx = (1, 0) if kind == "pipe" else (world, rank)
+    for s in range(2):
+        b, t = shard(*full_batch(step=s), idx, dp)
+        eng.train_step(b, t)
+    assert float(eng.scaler.tracker) == 2.0
+    sd = eng.full_state_dict()
+    if rank == 0:
+        torch.save({k: v.clone() for k, v in sd.items()}, out)

@@ -69,3 +69,37 @@ def test_pipeline_single_stage_microbatched(ref, schedule):
     # batch (and split-K adds partials atomically): Adam turns near-zero gradients of the
     # small 1-D tensors into +-lr moves of either sign, so allow a wider band here
     close(sd, ref[1], tol=5e-2)
+
+
+@pytest.mark.parametrize("graph", [False, True])
+def test_grad_scaler_matches_unscaled(ref, graph):
+    """--grad_scaler: 2^16-scaled backward, unscale folded into AdamW, same result."""
+    eng = DataParallelEngine(make(), "cuda", lr=1e-3, graph=graph, grad_scaler=True)
+    losses, sd = run(eng)
+    assert float(eng.scaler.scale_t) == 2.0 ** 16 and float(eng.scaler.tracker) == 3.0
+    assert abs(losses[-1] - ref[0][-1]) < 2e-2
+    close(sd, ref[1], tol=1e-2)
+
+
+def test_grad_scaler_skips_nonfinite_step():
+    """A non-finite gradient: parameters and moments untouched, scale halved, the skipped
+    step left out of the bias-correction count (torch GradScaler semantics)."""
+    eng = DataParallelEngine(make(), "cuda", lr=1e-3, grad_scaler=True)
+    eng.train_step(*batch(0))
+    before = eng.store.master.clone()
+    m_before = eng.opt.exp_avg.clone()
+    real_check = eng.scaler.check
+
+    def poisoned(grad):
+        grad[7] = float("inf")
+        real_check(grad)
+
+    eng.scaler.check = poisoned
+    eng.train_step(*batch(1))
+    torch.cuda.synchronize()
+    assert torch.equal(eng.store.master, before) and torch.equal(eng.opt.exp_avg, m_before)
+    assert float(eng.scaler.scale_t) == 2.0 ** 15 and float(eng.scaler.found_inf) == 0.0
+    assert float(eng.opt.step_t) == 1.0
+    eng.scaler.check = real_check
+    eng.train_step(*batch(2))
+    assert float(eng.opt.step_t) == 2.0 and not torch.equal(eng.store.master, before)

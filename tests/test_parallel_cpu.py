@@ -6,7 +6,7 @@ import pytest
 import torch
 
 from dist_helpers import run_workers
-from dist_workers import (reference_state, worker_ddp, worker_fsdp, worker_pipe)
+from dist_workers import (reference_state, worker_ddp, worker_fsdp, worker_pipe, worker_scaled)
 
 from distributed_pytorch_cookbook_amd.parallel.pipeline import partition, schedule_1f1b
 
@@ -57,6 +57,13 @@ def test_pipe_ddp_mesh_matches_single(tmp_path, ref):
     out = tmp_path / "ppdp.pt"
     run_workers(worker_pipe, 4, str(out), 2, 2, 2, 2, "1f1b")
     assert_close_sd(torch.load(out, weights_only=True)["sd"], ref[0])
+
+
+@pytest.mark.parametrize("kind", ["ddp", "fsdp", "pipe"])
+def test_grad_scaler_engines_match_single(tmp_path, ref, kind):
+    out = tmp_path / f"scaled_{kind}.pt"
+    run_workers(worker_scaled, 2, str(out), kind)
+    assert_close_sd(torch.load(out, weights_only=True), ref[0])
 
 
 def test_partition_balanced_and_contiguous():

@@ -78,3 +78,35 @@ def test_train_flops_per_token_matches_survey_table():
     assert abs(train_flops_per_token(768, 12, 64, 12, 50257, 1024) / 1e9 - 0.86) < 0.01
     assert abs(train_flops_per_token(1600, 25, 64, 48, 50257, 1024) / 1e9 - 10.28) < 0.05
     assert abs(mfu(1e6, 1e9) - 0.4) < 1e-9
+
+
+def test_grad_scaler_cpu_semantics():
+    """GradScaler on the host path: check / back-off / growth / skip (reference GradScaler)."""
+    import torch
+
+    from distributed_pytorch_cookbook_amd.ops.amp import GradScaler
+    from distributed_pytorch_cookbook_amd.ops.optim import FlatAdamW
+
+    sc = GradScaler("cpu", init_scale=8.0, growth_interval=2)
+    p = torch.ones(16)
+    g = torch.full((16,), 8.0)  # a scaled gradient of 1.0
+    opt = FlatAdamW(p, g, lr=0.1, weight_decay=0.0)
+    ref_p = torch.ones(16)
+    ref = FlatAdamW(ref_p, torch.ones(16), lr=0.1, weight_decay=0.0)
+    sc.check(g)
+    opt.step(**sc.opt_kwargs(opt))
+    sc.update()
+    ref.step()
+    assert torch.allclose(p, ref_p)
+    g[3] = float("nan")
+    sc.check(g)
+    before = p.clone()
+    opt.step(**sc.opt_kwargs(opt))
+    sc.update()
+    assert torch.equal(p, before) and float(sc.scale_t) == 4.0 and float(opt.step_t) == 1.0
+    g[3] = 4.0
+    for _ in range(2):
+        sc.check(g)
+        opt.step(**sc.opt_kwargs(opt))
+        sc.update()
+    assert float(sc.scale_t) == 8.0 and float(opt.step_t) == 3.0
