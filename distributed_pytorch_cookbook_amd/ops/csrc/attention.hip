@@ -129,13 +129,27 @@ __device__ __forceinline__ bf16x8 load_row8(const bf16_t* p) {
 
 #define MFMA32(a, b, c) __builtin_amdgcn_mfma_f32_32x32x16_bf16((a), (b), (c), 0, 0, 0)
 
+// XCD-aware work id (1-D grid of nblk * N * H workgroups): workgroup b runs on XCD b % 8, and
+// the bijective remap gives every XCD a contiguous run of ids, so all the q- (or key-) blocks
+// of one (batch, head) -- which read the same K/V (Q/dO) rows -- share one XCD's L2 instead of
+// being spread over all eight (the 2-D grid put block i of every head on XCD i: each head's
+// K/V was fetched into eight L2s).  Returns (bh, i): i = block index within the head.
+__device__ __forceinline__ void xcd_work(int nblk, int& bh, int& i) {
+  const int b = blockIdx.x, nwg = gridDim.x, xcd = b & 7, q = nwg >> 3, r = nwg & 7;
+  const int t = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (b >> 3);
+  bh = t / nblk;
+  i = t - bh * nblk;
+}
+
 // ------------------------------------------------------------------ forward
 __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(AttnArgs p) {
   __shared__ __attribute__((aligned(16))) bf16_t smem[2 * 2 * KT * HD];  // [stage][K|V]
   const int S = p.S, H = p.H;
   const int nqb = (S + QB - 1) / QB;
-  const int qb = nqb - 1 - (int)blockIdx.x;  // heaviest causal blocks first
-  const int bh = blockIdx.y, n = bh / H, h = bh % H;
+  int bh, bi;
+  xcd_work(nqb, bh, bi);
+  const int qb = nqb - 1 - bi;  // heaviest causal blocks of a head first
+  const int n = bh / H, h = bh % H;
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, hh = lane >> 5;
   const int q0 = qb * QB + wid * 32;
   const int q = q0 + (lane & 31);
@@ -302,9 +316,9 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_kernel(AttnArgs p) {
   __shared__ __attribute__((aligned(16))) float srow[2][2][KT];                                    // [stage][lse2|delta]
   const int S = p.S, H = p.H;
   const int nkb = (S + QB - 1) / QB;
-  const int kb = blockIdx.x;
-  (void)nkb;
-  const int bh = blockIdx.y, n = bh / H, h = bh % H;
+  int bh, kb;
+  xcd_work(nkb, bh, kb);  // kb = 0 (the most queries under the causal mask) first
+  const int n = bh / H, h = bh % H;
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, hh = lane >> 5;
   const int k0 = kb * QB + wid * 32;
   const int key = k0 + (lane & 31);
@@ -445,8 +459,10 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(AttnArgs p) {
   __shared__ __attribute__((aligned(16))) bf16_t smem[2 * 2 * KT * HD];  // [stage][K|V]
   const int S = p.S, H = p.H;
   const int nqb = (S + QB - 1) / QB;
-  const int qb = nqb - 1 - (int)blockIdx.x;
-  const int bh = blockIdx.y, n = bh / H, h = bh % H;
+  int bh, bi;
+  xcd_work(nqb, bh, bi);
+  const int qb = nqb - 1 - bi;
+  const int n = bh / H, h = bh % H;
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, hh = lane >> 5;
   const int q0 = qb * QB + wid * 32;
   const int q = q0 + (lane & 31);
@@ -557,7 +573,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(AttnArgs p) {
 using namespace dpc;
 
 DPC_API int dpc_attn_fwd(const AttnArgs* a, hipStream_t stream) {
-  dim3 grid((a->S + QB - 1) / QB, a->N * a->H);
+  dim3 grid((unsigned)(((a->S + QB - 1) / QB) * a->N * a->H));  // 1-D: xcd_work() maps it
   hipLaunchKernelGGL(attn_fwd_kernel, grid, dim3(256), 0, stream, *a);
   return (int)hipGetLastError();
 }
@@ -566,7 +582,7 @@ DPC_API int dpc_attn_bwd(const AttnArgs* a, hipStream_t stream) {
   const long long rows = (long long)a->N * a->S * a->H;
   dim3 gpre((unsigned)((rows * 8 + 255) / 256));
   hipLaunchKernelGGL(attn_bwd_pre_kernel, gpre, dim3(256), 0, stream, *a);
-  dim3 grid((a->S + QB - 1) / QB, a->N * a->H);
+  dim3 grid((unsigned)(((a->S + QB - 1) / QB) * a->N * a->H));
   hipLaunchKernelGGL(attn_bwd_dkdv_kernel, grid, dim3(256), 0, stream, *a);
   hipLaunchKernelGGL(attn_bwd_dq_kernel, grid, dim3(256), 0, stream, *a);
   return (int)hipGetLastError();
