@@ -96,6 +96,24 @@ __device__ __forceinline__ void split_rows_atomic(const float* ct, float* C, lon
     atomicAdd(c + (long long)row * ldc, ct[row * 64 + (lane ^ (((row >> 2) & 3) << 4))]);
 }
 
+// Bias-gradient column sums of a wave's 64 columns [nb, nb + 64): lane l & 15 holds columns
+// nb + 4 (l & 15) + e in cs[e], summed over its row group l >> 4.  Reduce over the four row
+// groups, then hand column nb + l to lane l so ONE atomic instruction covers 256 contiguous
+// bytes (four lane-owns-4-columns instructions hit every 64-B segment four times; with every
+// M-tile adding to the same N columns the serialised atomics cost ~20 % of a dgrad GEMM).
+__device__ __forceinline__ void colsum_flush(float (&cs)[4], float* colsum, int nb, int N, int lane) {
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    cs[e] += __shfl_xor(cs[e], 16, 64);
+    cs[e] += __shfl_xor(cs[e], 32, 64);
+  }
+  const int src = lane >> 2, e = lane & 3;
+  const float v0 = __shfl(cs[0], src, 64), v1 = __shfl(cs[1], src, 64);
+  const float v2 = __shfl(cs[2], src, 64), v3 = __shfl(cs[3], src, 64);
+  const float v = e == 0 ? v0 : (e == 1 ? v1 : (e == 2 ? v2 : v3));
+  if (nb + lane < N) atomicAdd(colsum + nb + lane, v);
+}
+
 constexpr int BM = 128, BN = 128, BKT = 64, NT = 256;
 constexpr int TILE_ELEMS = BM * BKT;  // 8192 bf16 = 16 KiB per operand per stage
 constexpr int GROUP_M = 8;
@@ -530,17 +548,7 @@ __global__ __launch_bounds__(NT, (V2Cfg<KB, STAGES>::WGS)) void gemm2_kernel(Gem
       }
     }
   }
-  if (p.colsum) {
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      cs[e] += __shfl_xor(cs[e], 16, 64);
-      cs[e] += __shfl_xor(cs[e], 32, 64);
-    }
-    if ((lane >> 4) == 0 && nok) {
-#pragma unroll
-      for (int e = 0; e < 4; ++e) atomicAdd(p.colsum + n + e, cs[e]);
-    }
-  }
+  if (p.colsum) colsum_flush(cs, p.colsum, n - c4 * 4, p.N, lane);
 }
 
 // =====================================================================================
@@ -744,17 +752,7 @@ __global__ __launch_bounds__((V3Cfg<BM_, BN_, WM, WN, KB, STAGES>::NTH), 1) void
       }
     }
   }
-  if (p.colsum) {
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      cs[e] += __shfl_xor(cs[e], 16, 64);
-      cs[e] += __shfl_xor(cs[e], 32, 64);
-    }
-    if ((lane >> 4) == 0 && nok) {
-#pragma unroll
-      for (int e = 0; e < 4; ++e) atomicAdd(p.colsum + n + e, cs[e]);
-    }
-  }
+  if (p.colsum) colsum_flush(cs, p.colsum, n - c4 * 4, p.N, lane);
 }
 
 // =====================================================================================
@@ -953,17 +951,7 @@ __global__ __launch_bounds__(512, 1) void gemm4_kernel(GemmArgs p, unsigned long
       }
     }
   }
-  if (p.colsum) {
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      cs[e] += __shfl_xor(cs[e], 16, 64);
-      cs[e] += __shfl_xor(cs[e], 32, 64);
-    }
-    if ((lane >> 4) == 0 && nok) {
-#pragma unroll
-      for (int e = 0; e < 4; ++e) atomicAdd(p.colsum + n + e, cs[e]);
-    }
-  }
+  if (p.colsum) colsum_flush(cs, p.colsum, n - c4 * 4, p.N, lane);
 }
 
 // =====================================================================================
@@ -1177,17 +1165,7 @@ __global__ __launch_bounds__(512, 1) void gemm5_kernel(GemmArgs p, unsigned long
       }
     }
   }
-  if (p.colsum) {
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      cs[e] += __shfl_xor(cs[e], 16, 64);
-      cs[e] += __shfl_xor(cs[e], 32, 64);
-    }
-    if ((lane >> 4) == 0 && nok) {
-#pragma unroll
-      for (int e = 0; e < 4; ++e) atomicAdd(p.colsum + n + e, cs[e]);
-    }
-  }
+  if (p.colsum) colsum_flush(cs, p.colsum, n - c4 * 4, p.N, lane);
 }
 
 }  // namespace dpc
@@ -1307,6 +1285,7 @@ DPC_API int dpc_gemm(const GemmArgs* a, hipStream_t stream) {
     if (v2_ok) {
       impl = 2;
       if (a->a_kmaj && a->b_kmaj && a->K <= 1024) impl = 10;
+      else if (a->a_kmaj && !a->b_kmaj && a->K <= 1024) impl = 10;  // dgrad + act' / colsum epilogue
       else if (a->a_kmaj && !a->b_kmaj && a->K <= 2304) impl = 4;
       else if (!a->a_kmaj && !a->b_kmaj && a->M > 2304 && a->M <= 4096) impl = 4;
       const int pol = policy_impl(a);
