@@ -21,6 +21,7 @@ Q, K, V weights are adjacent in the flat layout, so ``[Wq; Wk; Wv]`` is a view.
 """
 from __future__ import annotations
 
+import os
 from dataclasses import dataclass
 from typing import Optional
 
@@ -35,6 +36,13 @@ from ..ops.loss import cross_entropy_fused
 from ..ops.norm import layernorm_bwd, layernorm_fwd
 
 LN_EPS = 1e-5
+# input gradients feeding a LayerNorm backward: bf16 (as autocast makes them in the
+# reference) unless DPC_DH_F32=1
+_DH_F32 = os.environ.get("DPC_DH_F32", "0") == "1"
+
+
+def _dh_dtype(cdt):
+    return torch.float32 if _DH_F32 else cdt
 
 
 def vocab_ld(vocab: int) -> int:
@@ -190,7 +198,7 @@ def _layer_backward(dx3, x, mask, saved, layer, store, N, S, H, hd, act, drops):
     dz1 = linear_dgrad(dz2, w(fc.down_proj.weight), act_bwd=act, aux_in=zup, out_dtype=cdt,
                        colsum=g(fc.up_proj.bias))
     linear_wgrad(dz1, h2, out=g(fc.up_proj.weight))
-    dh2 = linear_dgrad(dz1, w(fc.up_proj.weight), out_dtype=torch.float32)
+    dh2 = linear_dgrad(dz1, w(fc.up_proj.weight), out_dtype=_dh_dtype(cdt))
     # LN2 backward with the attention output projection's bias/dropout backward fused in:
     # x2 = x + drop(o Wo^T + bo)  ->  dYo = bf16(dx2 * keep), dbo += colsum
     dyo = torch.empty(dx.shape, device=dx.device, dtype=cdt)
@@ -205,7 +213,7 @@ def _layer_backward(dx3, x, mask, saved, layer, store, N, S, H, hd, act, drops):
         n = split[0].shape[0]
         for i, gi in enumerate(split):
             gi.add_(gqkv[i * n:(i + 1) * n])
-    dh1 = linear_dgrad(dqkv, _qkv_weight(store, attn), out_dtype=torch.float32)
+    dh1 = linear_dgrad(dqkv, _qkv_weight(store, attn), out_dtype=_dh_dtype(cdt))
     layernorm_bwd(dh1, x, mu1, rs1, w(layer.norm1.weight), dx, g(layer.norm1.weight),
                   g(layer.norm1.bias))
     return dx
@@ -249,7 +257,7 @@ class _HeadFn(torch.autograd.Function):
         linear_wgrad(dl, hf, out=g(head.weight), alpha_t=scale)
         # K = padded vocab: the CE kernel zeroed dlogits' pad columns, W_lm rows >= V read as 0
         dhf = linear_dgrad(dlogits, _head_weight_padded(store, head, dlogits.shape[1]),
-                           out_dtype=torch.float32, alpha_t=scale)
+                           out_dtype=_dh_dtype(store.compute_dtype), alpha_t=scale)
         dx = torch.zeros_like(x)
         layernorm_bwd(dhf, x, mu, rs, w(norm.weight), dx, g(norm.weight), g(norm.bias))
         store.post_backward(unit)

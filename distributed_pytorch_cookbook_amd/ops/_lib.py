@@ -57,6 +57,7 @@ class LNArgs(ctypes.Structure):
         ("y_f32", c_int),
         ("gout", P), ("gsum", P), ("ld_gout", LL),
         ("drop_key", c_uint), ("drop_thresh", c_uint), ("drop_scale", c_float),
+        ("dy_bf16", c_int),
     ]
 
 

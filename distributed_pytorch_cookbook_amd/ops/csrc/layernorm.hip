@@ -37,6 +37,7 @@ struct LNArgs {
   long long ld_gout;
   unsigned drop_key, drop_thresh;
   float drop_scale;
+  int dy_bf16;  // bwd: dy is bf16 (the input gradient of the next Linear, as autocast makes it)
 };
 
 template <int NV>
@@ -110,6 +111,7 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(LNArgs p) {
   for (long long row = (long long)blockIdx.x * 4 + w; row < p.T; row += (long long)gridDim.x * 4) {
     const float4* xr = reinterpret_cast<const float4*>(p.x + row * p.ldx);
     const float4* dyr = reinterpret_cast<const float4*>(p.dy + row * p.lddy);
+    const uint2* dyb = reinterpret_cast<const uint2*>(static_cast<const bf16_t*>((const void*)p.dy) + row * p.lddy);
     const float mu = p.mean[row], rs = p.rstd[row];
     float4 xh[NV], dg[NV];
     float s1 = 0.f, s2 = 0.f;
@@ -117,7 +119,15 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(LNArgs p) {
     for (int i = 0; i < NV; ++i) {
       const int c = lane + i * 64;
       if (c < nv4) {
-        const float4 xv = xr[c], d = dyr[c];
+        const float4 xv = xr[c];
+        float4 d;
+        if (p.dy_bf16) {
+          const uint2 z = dyb[c];
+          d = make_float4(__uint_as_float(z.x << 16), __uint_as_float(z.x & 0xffff0000u),
+                          __uint_as_float(z.y << 16), __uint_as_float(z.y & 0xffff0000u));
+        } else {
+          d = dyr[c];
+        }
         xh[i] = make_float4((xv.x - mu) * rs, (xv.y - mu) * rs, (xv.z - mu) * rs, (xv.w - mu) * rs);
         dg[i] = make_float4(d.x * gam[i].x, d.y * gam[i].y, d.z * gam[i].z, d.w * gam[i].w);
         s1 += dg[i].x + dg[i].y + dg[i].z + dg[i].w;

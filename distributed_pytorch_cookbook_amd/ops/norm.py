@@ -52,7 +52,9 @@ def layernorm_bwd(dy: torch.Tensor, x: torch.Tensor, mean: torch.Tensor, rstd: t
                   gamma: torch.Tensor, dx: torch.Tensor, dgamma: torch.Tensor, dbeta: torch.Tensor,
                   gout: torch.Tensor | None = None, gsum: torch.Tensor | None = None,
                   drop=None):
-    """dx += LN'(dy); dgamma += sum dy*xhat; dbeta += sum dy.  dy, x, dx f32 [T, D].
+    """dx += LN'(dy); dgamma += sum dy*xhat; dbeta += sum dy.  x, dx f32 [T, D]; dy f32 or
+    bf16 (the input gradient of the Linear that consumed the LayerNorm's output -- bf16 under
+    the reference's autocast too).
 
     Optional fused consumer of the updated dx (the backward of the bias + dropout of the
     projection whose output fed this LayerNorm's residual): ``gout = dx * keep`` (bf16,
@@ -60,7 +62,7 @@ def layernorm_bwd(dy: torch.Tensor, x: torch.Tensor, mean: torch.Tensor, rstd: t
     gradient), saving a separate pass over the f32 dx.
     """
     T, D = x.shape
-    if not (x.is_cuda and dy.dtype == torch.float32 and gamma.dtype == torch.float32
+    if not (x.is_cuda and dy.dtype in (torch.float32, torch.bfloat16) and gamma.dtype == torch.float32
             and (gout is None or gout.dtype == torch.bfloat16)):
         xh = (x.float() - mean[:, None]) * rstd[:, None]
         dyf = dy.float()
@@ -76,13 +78,16 @@ def layernorm_bwd(dy: torch.Tensor, x: torch.Tensor, mean: torch.Tensor, rstd: t
             if gsum is not None:
                 gsum.add_(g.sum(0))
         return dx
-    for t, nm in ((dy, "dy"), (x, "x"), (dx, "dx")):
+    for t, nm in ((x, "x"), (dx, "dx")):
         if t.dtype != torch.float32 or t.stride(1) != 1:
             raise ValueError(f"layernorm_bwd: {nm} must be f32 with contiguous rows")
+    if dy.stride(1) != 1 or (dy.dtype == torch.bfloat16 and (dy.stride(0) % 4 or dy.data_ptr() % 8)):
+        raise ValueError("layernorm_bwd: dy must have contiguous (8-B aligned for bf16) rows")
     args = _lib.LNArgs(
         x=x.data_ptr(), gamma=gamma.data_ptr(), mean=mean.data_ptr(), rstd=rstd.data_ptr(),
         dy=dy.data_ptr(), dx=dx.data_ptr(), dgamma=dgamma.data_ptr(), dbeta=dbeta.data_ptr(),
         ldx=x.stride(0), lddy=dy.stride(0), lddx=dx.stride(0), T=T, D=D, eps=0.0,
+        dy_bf16=int(dy.dtype == torch.bfloat16),
     )
     if gout is not None:
         if gout.dtype != torch.bfloat16 or gout.stride(1) != 1 or gout.stride(0) % 4 or D % 4:

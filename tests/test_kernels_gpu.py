@@ -220,6 +220,16 @@ def test_layernorm(D):
         ref = dx2 if drop is None else dx2 * keep_mask(drop, T, D, dev)
         assert rel_err(gout, ref) < 5e-3
         assert rel_err(gsum - 1, ref.sum(0)) < 1e-4
+    # bf16 dy (the input gradient of the next Linear): same math on the rounded values
+    dyb = dy.bfloat16()
+    dx3 = dres.clone()
+    dg3, db3 = torch.zeros(D, device=dev), torch.zeros(D, device=dev)
+    layernorm_bwd(dyb, x, mean, rstd, g, dx3, dg3, db3)
+    xx.grad, gg.grad, bb.grad = None, None, None
+    torch.nn.functional.layer_norm(xx, (D,), gg, bb, 1e-5).backward(dyb.float())
+    assert rel_err(dx3 - dres, xx.grad) < 1e-4
+    assert rel_err(dg3, gg.grad) < 1e-4
+    assert rel_err(db3, bb.grad) < 1e-4
 
 
 @pytest.mark.parametrize("tdt", [torch.float32, torch.bfloat16])
