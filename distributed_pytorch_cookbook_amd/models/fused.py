@@ -32,7 +32,7 @@ from ..ops.elementwise import bias_act_bwd
 from ..ops.dropout import dropout_residual
 from ..ops.embedding import embedding_bwd, embedding_fwd
 from ..ops.gemm import ACT_GELU, ACT_RELU, act_code, linear_dgrad, linear_fwd, linear_wgrad
-from ..ops.loss import cross_entropy_fused
+from ..ops.loss import cross_entropy_fused, cross_entropy_rows
 from ..ops.norm import layernorm_bwd, layernorm_fwd
 
 LN_EPS = 1e-5
@@ -43,6 +43,13 @@ _DH_F32 = os.environ.get("DPC_DH_F32", "0") == "1"
 
 def _dh_dtype(cdt):
     return torch.float32 if _DH_F32 else cdt
+
+
+# rows per chunk of the logits GEMM + cross-entropy (0 = whole batch at once).  Off by
+# default: on GPT-2 small (B=32) chunks of 1024 / 2048 / 4096 rows ran 751K / 757K / 762K
+# tok/s against 775-781K unchunked -- the smaller logits GEMMs lose more than the
+# cache-resident cross-entropy pass gains.
+_HEAD_CHUNK = int(os.environ.get("DPC_HEAD_CHUNK", "0"))
 
 
 def vocab_ld(vocab: int) -> int:
@@ -233,9 +240,27 @@ class _HeadFn(torch.autograd.Function):
         ld = vocab_ld(V) if x.is_cuda else V
         buf = torch.empty(T, ld, device=x.device, dtype=cdt)
         # padded columns come out 0 (B rows >= V are the layout's zero rows / read as 0)
-        linear_fwd(hf, _head_weight_padded(store, head, ld), out=buf)
-        loss, n_valid, n_correct = cross_entropy_fused(buf, targets, V, write_grad=training,
-                                                       want_correct=want_correct)
+        wpad = _head_weight_padded(store, head, ld)
+        chunk = _HEAD_CHUNK if (x.is_cuda and cdt == torch.bfloat16) else 0
+        if chunk and T > chunk:
+            # row chunks: each chunk's bf16 logits (chunk x Vp x 2 B) are still in the 256 MB
+            # Infinity Cache when the cross-entropy pass reads them back
+            tg = targets.reshape(-1)
+            n_valid = (tg != -100).sum().float()
+            inv = 1.0 / n_valid.clamp_min(1.0)
+            row_loss = torch.empty(T, device=x.device, dtype=torch.float32)
+            row_corr = torch.empty(T, device=x.device, dtype=torch.float32) if want_correct else None
+            for c0 in range(0, T, chunk):
+                c1 = min(T, c0 + chunk)
+                linear_fwd(hf[c0:c1], wpad, out=buf[c0:c1])
+                cross_entropy_rows(buf[c0:c1], tg[c0:c1], V, inv, row_loss[c0:c1],
+                                   None if row_corr is None else row_corr[c0:c1], write_grad=training)
+            loss = row_loss.sum() * inv
+            n_correct = row_corr.sum() if want_correct else None
+        else:
+            linear_fwd(hf, wpad, out=buf)
+            loss, n_valid, n_correct = cross_entropy_fused(buf, targets, V, write_grad=training,
+                                                           want_correct=want_correct)
         store.post_forward(unit, training)
         if training:
             ctx.save_for_backward(x, hf, mu, rs, buf)

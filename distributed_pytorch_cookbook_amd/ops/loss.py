@@ -19,6 +19,26 @@ from . import _lib
 IGNORE_INDEX = -100
 
 
+def cross_entropy_rows(logits: torch.Tensor, targets: torch.Tensor, vocab: int, inv_count: torch.Tensor,
+                       row_loss: torch.Tensor, row_correct: torch.Tensor | None = None,
+                       write_grad: bool = True, ignore_index: int = IGNORE_INDEX) -> None:
+    """HIP kernel on a block of rows: per-row loss (and argmax hit) into ``row_loss`` /
+    ``row_correct``, dlogits = (softmax - onehot) * inv_count in place.  ``inv_count`` is the
+    device scalar 1 / n_valid of the WHOLE batch, so a batch can be processed in row chunks
+    (the chunked head keeps each chunk's logits resident in the Infinity Cache between the
+    logits GEMM and this pass)."""
+    T = logits.shape[0]
+    if logits.stride(1) != 1 or logits.stride(0) % 8 or logits.data_ptr() % 16:
+        raise ValueError("cross_entropy_rows: rows must be contiguous, 16-B aligned, ld % 8 == 0")
+    tg = targets.reshape(-1).to(torch.int64).contiguous()
+    args = _lib.CEArgs(
+        logits=logits.data_ptr(), dlogits=logits.data_ptr(), targets=tg.data_ptr(),
+        inv_count=inv_count.data_ptr(), row_loss=row_loss.data_ptr(), row_correct=_lib.ptr(row_correct),
+        ld=logits.stride(0), T=T, V=vocab, write_grad=int(write_grad), ignore_index=ignore_index,
+    )
+    _lib.call("dpc_cross_entropy", args, logits.device)
+
+
 def cross_entropy_fused(logits: torch.Tensor, targets: torch.Tensor, vocab: int,
                         write_grad: bool = True, want_correct: bool = False,
                         ignore_index: int = IGNORE_INDEX):

@@ -93,3 +93,38 @@ def test_main_single_recipe_gpu(tmp_path, monkeypatch):
     assert path is not None and path.exists()
     sd = torch.load(path, weights_only=True)
     assert len(sd) == 13 * 2 + 5
+
+
+@pytest.mark.parametrize("want_correct", [False, True])
+def test_chunked_head_matches_whole_batch(monkeypatch, want_correct):
+    """Row-chunked logits GEMM + cross-entropy (ragged last chunk, ignored targets) gives the
+    same loss, accuracy and gradients as one pass over the whole batch."""
+    import distributed_pytorch_cookbook_amd.models.fused as fused
+
+    N, S, V = 3, 129, 1000
+    g = torch.Generator().manual_seed(3)
+    ids = torch.randint(0, V, (N, S), generator=g).cuda()
+    tg = torch.randint(0, V, (N, S), generator=g)
+    tg[2, 50:70] = -100
+    tg = tg.cuda()
+    pos = torch.arange(S).repeat(N, 1).cuda()
+    res = []
+    for chunk in (0, 100):
+        monkeypatch.setattr(fused, "_HEAD_CHUNK", chunk)
+        m = make("gelu").cuda()
+        store = LocalStore(m, "cuda")
+        store.zero_grad()
+        if want_correct:
+            with torch.no_grad():
+                out = m(ids, pos, None, targets=tg, want_correct=True)
+            res.append((out.loss.item(), out.n_correct.item(), None))
+            continue
+        out = m(ids, pos, None, targets=tg)
+        out.loss.backward()
+        torch.cuda.synchronize()
+        res.append((out.loss.item(), None, store.grads.clone()))
+    assert abs(res[0][0] - res[1][0]) < 1e-5 * abs(res[0][0])
+    if want_correct:
+        assert res[0][1] == res[1][1]
+    else:
+        assert torch.allclose(res[0][2], res[1][2], rtol=1e-3, atol=1e-6)
