@@ -54,30 +54,32 @@ struct GemmArgs {
   int ksplit;
 };
 
-// Which output tile and k-range a workgroup computes.
-//  * default: an XCD-aware bijective remap (blocks b, b+8, ... share an XCD: each XCD gets a
-//    contiguous run of tile ids, walked in GROUP_M supertiles for L2 reuse); split-K, if
-//    any, on blockIdx.y.
-//  * ksplit > 1 (small outputs with a long K, i.e. weight gradients): block L runs on XCD
-//    L % 8, so split = L % ksplit pins every k-range to its own XCD(s) -- an XCD streams only
-//    its 1/ksplit of both operands, once, shared in its L2 by all the tiles it computes.
-//    (With the default mapping the same shapes hit L2 only ~53 % of the time: PMC
-//    TCC_HIT/MISS on the 3072x768x32736 weight gradient, profiles/r1_pmc_*.)
+// Which output tile and k-range a workgroup computes.  The grid is 1-D, ntiles x splits
+// workgroups (splits = |ksplit|, set by the dispatcher; 0 = 1), and block b runs on XCD b % 8.
+//  * default (ksplit >= 0): a bijective remap gives every XCD a contiguous run of work ids,
+//    split-major (id = split * ntiles + tile), walked in GROUP_M supertiles: the workgroups
+//    that share an XCD's L2 compute the SAME k-range of neighbouring tiles, so each k-slice of
+//    both operands is fetched into that L2 once and read by all of them.  (A 2-D grid with the
+//    split on blockIdx.y put block (x, y) on XCD (x + ntiles * y) % 8 -- every XCD mixed all
+//    k-ranges, and the weight gradients streamed their operands from beyond L2.)
+//  * ksplit < 0: split = b % splits pins each k-range to its own XCD(s) (sweeps only).
 struct TileSlot {
   int bid, split, splits;
 };
-__device__ __forceinline__ TileSlot tile_slot(const GemmArgs& p, int nwg) {
+__device__ __forceinline__ TileSlot tile_slot(const GemmArgs& p, int ntiles) {
   TileSlot t;
-  if (p.ksplit > 1) {
-    t.splits = p.ksplit;
-    t.split = blockIdx.x % p.ksplit;
-    t.bid = blockIdx.x / p.ksplit;
-  } else {
-    const int b = blockIdx.x, xcd = b & 7, q = nwg >> 3, r = nwg & 7;
-    t.bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (b >> 3);
-    t.splits = gridDim.y;
-    t.split = blockIdx.y;
+  if (p.ksplit < -1) {
+    t.splits = -p.ksplit;
+    t.split = blockIdx.x % t.splits;
+    t.bid = blockIdx.x / t.splits;
+    return t;
   }
+  t.splits = p.ksplit > 1 ? p.ksplit : 1;
+  const int nwg = ntiles * t.splits;
+  const int b = blockIdx.x, xcd = b & 7, q = nwg >> 3, r = nwg & 7;
+  const int w = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (b >> 3);
+  t.split = w / ntiles;
+  t.bid = w - t.split * ntiles;
   return t;
 }
 
@@ -426,7 +428,7 @@ __global__ __launch_bounds__(NT, (V2Cfg<KB, STAGES>::WGS)) void gemm2_kernel(Gem
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
 
-  // split-K: blockIdx.y owns a contiguous run of k-tiles (the host only splits plain
+  // split-K: each split owns a contiguous run of k-tiles (the host only splits plain
   // f32-accumulating products, whose partial tiles are combined with f32 atomics)
   const int nk_all = (p.K + KB - 1) / KB;
   const int splits = ts.splits;
@@ -1330,14 +1332,10 @@ DPC_API int dpc_gemm(const GemmArgs* a, hipStream_t stream) {
       }
       if (g_force_splits > 0) splits = g_force_splits;
     }
-    const bool xcd_split = g_xcd_split && splits > 1;
     if (splits > 1 && !a->accumulate)
       hipMemset2DAsync(a->C, (size_t)a->ldc * 4, 0, (size_t)a->N * 4, (size_t)a->M, stream);
-    dim3 g(t, splits);
-    if (xcd_split) {
-      g = dim3(t * splits, 1);
-      b.ksplit = splits;
-    }
+    dim3 g(t * splits);  // 1-D: tile_slot() maps block -> (split, tile)
+    b.ksplit = splits > 1 ? (g_xcd_split ? -splits : splits) : 0;
     switch (impl) {
       case 3: launch_v2<64, 3>(&b, g, stream, ab, bb); break;
       case 4: launch_v2<32, 3>(&b, g, stream, ab, bb); break;
