@@ -90,6 +90,10 @@ def main():
         res_row = {"case": name, "M": M, "N": N, "K": K}
         _lib.set_gemm_impl(-1)
         res_row["default_tflops"] = round(fl / timeit(fn) / 1e9)
+        # speed-of-light reference: the same M x N x K as a plain hipBLASLt product
+        pa, pb = r(M, K), r(K, N)
+        res_row["blas_plain"] = round(fl / timeit(lambda: torch.mm(pa, pb)) / 1e9)
+        del pa, pb
         for impl in a.impls:
             _lib.set_gemm_impl(impl)
             try:

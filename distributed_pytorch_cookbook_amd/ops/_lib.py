@@ -33,6 +33,7 @@ class GemmArgs(ctypes.Structure):
         ("a_kmaj", c_int), ("b_kmaj", c_int),
         ("a_r", c_int), ("a_c", c_int), ("b_r", c_int), ("b_c", c_int),
         ("ksplit", c_int),  # dispatcher-owned (pass 0)
+        ("impl", c_int),    # 0 = dispatcher policy, else a measured per-shape choice
     ]
 
 

@@ -52,6 +52,10 @@ struct GemmArgs {
   int a_r, a_c, b_r, b_c;
   // set by the dispatcher (callers pass 0): > 1 = XCD-aligned split-K into this many k-ranges
   int ksplit;
+  // caller's implementation choice (0 = the dispatcher's shape policy), e.g. from the
+  // measured per-shape table of ops/gemm.py (autotuned on MI355X); a forced global impl
+  // (dpc_gemm_set_impl, sweeps / tests) takes precedence
+  int impl;
 };
 
 // Which output tile and k-range a workgroup computes.  The grid is 1-D, ntiles x splits
@@ -114,6 +118,136 @@ __device__ __forceinline__ void colsum_flush(float (&cs)[4], float* colsum, int 
   const float v2 = __shfl(cs[2], src, 64), v3 = __shfl(cs[3], src, 64);
   const float v = e == 0 ? v0 : (e == 1 ? v1 : (e == 2 ? v2 : v3));
   if (nb + lane < N) atomicAdd(colsum + nb + lane, v);
+}
+
+// ---- Shared epilogue of the LDS-DMA kernels (v2-v5).  A wave owns FM x 4 fragments of
+// 16x16 (FM/2 passes of 32 rows x 64 columns).  Each pass stages its f32 rows through LDS
+// ([32][64] per wave, columns XOR-swizzled by ((row >> 2) & 3) << 4) so that bias /
+// residual / aux / C move 16 B (f32) or 8 B (bf16) per lane along rows.  Every global READ
+// of a pass (aux_in for act', the f32 residual or the accumulated C) is issued as one batch
+// one pass AHEAD, into a double buffer: one HBM round trip per pass overlapped with the
+// previous pass, instead of one exposed round trip per 4 rows (the v12 epilogue waited on
+// each row group's aux load before issuing the next: act' dgrad ran at ~65 % of the plain
+// product's rate).  DB = false (kernels that need their registers: several workgroups per CU,
+// or 128-row wave tiles) issues a pass's reads right after staging it instead, overlapping
+// only the barrier and LDS re-read.
+struct EpiIn {
+  // per row group t: the f32 residual (or accumulated C) when there is one, else the act'
+  // operand (bf16 x 4 in .x/.y) -- one 16-B slot, so the prefetch costs 32 VGPRs not 48
+  // (no caller combines act' with a residual; if one did, its aux is read late)
+  uint4 v[8];
+};
+
+__device__ __forceinline__ const float* epi_fsrc(const GemmArgs& p) {
+  return p.residual ? p.residual : (p.out_f32 && p.accumulate ? static_cast<const float*>(p.C) : nullptr);
+}
+
+__device__ __forceinline__ void epi_load(const GemmArgs& p, EpiIn& e, int mb, int n, bool nok, int lane) {
+  const bf16_t* aux_in = static_cast<const bf16_t*>(p.aux_in);
+  const float* fsrc = epi_fsrc(p);
+  const long long ldf = p.residual ? p.ldr : p.ldc;
+#pragma unroll
+  for (int t = 0; t < 8; ++t) {
+    const int m = mb + (lane >> 4) + 4 * t;
+    const bool ok = nok && m < p.M;
+    e.v[t] = make_uint4(0u, 0u, 0u, 0u);
+    if (ok && fsrc) {
+      e.v[t] = *reinterpret_cast<const uint4*>(fsrc + (long long)m * ldf + n);
+    } else if (ok && p.act_bwd) {
+      const uint2 z = *reinterpret_cast<const uint2*>(aux_in + (long long)m * p.ld_aux_in + n);
+      e.v[t].x = z.x;
+      e.v[t].y = z.y;
+    }
+  }
+}
+
+template <int FM, bool DB>
+__device__ __forceinline__ void epi_tile(const GemmArgs& p, floatx4 (&acc)[FM][4], float* ct, int splits,
+                                         int mw, int nw, int lane) {
+  constexpr int NP = FM / 2;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  float alpha = p.alpha;
+  if (p.alpha_ptr) alpha *= *p.alpha_ptr;
+  const int c4 = lane & 15;
+  const int n = nw + c4 * 4;
+  const bool nok = n < p.N;  // N % 4 == 0 is required by the host for v2+
+  float4 bias4 = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (p.bias && nok) bias4 = *reinterpret_cast<const float4*>(p.bias + n);
+  float cs[4] = {0.f, 0.f, 0.f, 0.f};
+  bf16_t* aux_out = static_cast<bf16_t*>(p.aux_out);
+  const float* fsrc = epi_fsrc(p);
+  EpiIn e[DB ? 2 : 1];
+  if (DB && splits <= 1) epi_load(p, e[0], mw, n, nok, lane);
+#pragma unroll
+  for (int h = 0; h < NP; ++h) {
+    __syncthreads();  // the ring (h = 0) / previous pass (h > 0) fully consumed
+#pragma unroll
+    for (int ii = 0; ii < 2; ++ii)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int row = ii * 16 + (lane >> 4) * 4 + r;
+          const int col = (j * 16 + (lane & 15)) ^ (((row >> 2) & 3) << 4);
+          ct[row * 64 + col] = acc[2 * h + ii][j][r] * alpha;
+        }
+    // (after the staging writes, so this pass's accumulators are dead before the loads land)
+    if (!DB && splits <= 1) epi_load(p, e[0], mw + h * 32, n, nok, lane);
+    __syncthreads();
+    if (splits > 1) {  // f32 partial sums: atomics (no epilogue operands)
+      split_rows_atomic(ct, static_cast<float*>(p.C), p.ldc, mw + h * 32, nw, p.M, p.N, lane);
+      continue;
+    }
+    if (DB && h + 1 < NP) epi_load(p, e[(h + 1) & 1], mw + (h + 1) * 32, n, nok, lane);
+    const EpiIn& cur = e[DB ? (h & 1) : 0];
+#pragma unroll
+    for (int t = 0; t < 8; ++t) {
+      const int row = (lane >> 4) + 4 * t;
+      const int m = mw + h * 32 + row;
+      const int col = (c4 * 4) ^ (((row >> 2) & 3) << 4);
+      const float4 v4 = *reinterpret_cast<const float4*>(ct + row * 64 + col);
+      if (m >= p.M || !nok) continue;
+      float v[4] = {v4.x + bias4.x, v4.y + bias4.y, v4.z + bias4.z, v4.w + bias4.w};
+      if (p.act_bwd) {
+        const uint2 z = fsrc ? *reinterpret_cast<const uint2*>(static_cast<const bf16_t*>(p.aux_in) +
+                                                              (long long)m * p.ld_aux_in + n)
+                             : make_uint2(cur.v[t].x, cur.v[t].y);
+        v[0] *= act_grad(__uint_as_float(z.x << 16), p.act_bwd);
+        v[1] *= act_grad(__uint_as_float(z.x & 0xffff0000u), p.act_bwd);
+        v[2] *= act_grad(__uint_as_float(z.y << 16), p.act_bwd);
+        v[3] *= act_grad(__uint_as_float(z.y & 0xffff0000u), p.act_bwd);
+      }
+#pragma unroll
+      for (int q = 0; q < 4; ++q) cs[q] += v[q];
+      if (aux_out) {
+        uint2 w;
+        w.x = pack2bf(v[0], v[1]);
+        w.y = pack2bf(v[2], v[3]);
+        *reinterpret_cast<uint2*>(aux_out + (long long)m * p.ld_aux_out + n) = w;
+      }
+#pragma unroll
+      for (int q = 0; q < 4; ++q) v[q] = act_fwd(v[q], p.act);
+      const long long ci = (long long)m * p.ldc + n;
+      if (fsrc) {
+        v[0] += __uint_as_float(cur.v[t].x); v[1] += __uint_as_float(cur.v[t].y);
+        v[2] += __uint_as_float(cur.v[t].z); v[3] += __uint_as_float(cur.v[t].w);
+      }
+      if (p.out_f32) {
+        float4* C = reinterpret_cast<float4*>(static_cast<float*>(p.C) + ci);
+        if (p.accumulate && p.residual) {  // (no caller does both; C read late)
+          const float4 o = *C;
+          v[0] += o.x; v[1] += o.y; v[2] += o.z; v[3] += o.w;
+        }
+        *C = make_float4(v[0], v[1], v[2], v[3]);
+      } else {
+        uint2 w;
+        w.x = pack2bf(v[0], v[1]);
+        w.y = pack2bf(v[2], v[3]);
+        *reinterpret_cast<uint2*>(static_cast<bf16_t*>(p.C) + ci) = w;
+      }
+    }
+  }
+  if (p.colsum) colsum_flush(cs, p.colsum, nw, p.N, lane);
 }
 
 constexpr int BM = 128, BN = 128, BKT = 64, NT = 256;
@@ -475,82 +609,7 @@ __global__ __launch_bounds__(NT, (V2Cfg<KB, STAGES>::WGS)) void gemm2_kernel(Gem
 
   // ---------------- epilogue through LDS, two passes of 32 rows per wave: the f32 tile is
   // re-read row-contiguously so bias / residual / aux / C move 16 B per lane
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  float alpha = p.alpha;
-  if (p.alpha_ptr) alpha *= *p.alpha_ptr;
-  float* ct = reinterpret_cast<float*>(smem) + wid * 32 * 64;
-  const int c4 = lane & 15;
-  const int n = n0 + wc * 64 + c4 * 4;
-  const bool nok = n < p.N;  // N % 4 == 0 is required by the host for v2
-  float4 bias4 = make_float4(0.f, 0.f, 0.f, 0.f);
-  if (p.bias && nok) bias4 = *reinterpret_cast<const float4*>(p.bias + n);
-  float cs[4] = {0.f, 0.f, 0.f, 0.f};
-  const bf16_t* aux_in = static_cast<const bf16_t*>(p.aux_in);
-  bf16_t* aux_out = static_cast<bf16_t*>(p.aux_out);
-#pragma unroll
-  for (int h = 0; h < 2; ++h) {
-    __syncthreads();  // ring (h = 0) / previous pass (h = 1) fully consumed
-#pragma unroll
-    for (int ii = 0; ii < 2; ++ii)
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int row = ii * 16 + (lane >> 4) * 4 + r;
-          const int col = (j * 16 + (lane & 15)) ^ (((row >> 2) & 3) << 4);
-          ct[row * 64 + col] = acc[2 * h + ii][j][r] * alpha;
-        }
-    __syncthreads();
-    if (splits > 1) {
-      split_rows_atomic(ct, static_cast<float*>(p.C), p.ldc, m0 + wr * 64 + h * 32, n0 + wc * 64, p.M, p.N, lane);
-      continue;
-    }
-#pragma unroll 2
-    for (int t = 0; t < 8; ++t) {
-      const int row = (lane >> 4) + 4 * t;
-      const int m = m0 + wr * 64 + h * 32 + row;
-      const int col = (c4 * 4) ^ (((row >> 2) & 3) << 4);
-      float4 v4 = *reinterpret_cast<const float4*>(ct + row * 64 + col);
-      if (m >= p.M || !nok) continue;
-      float v[4] = {v4.x + bias4.x, v4.y + bias4.y, v4.z + bias4.z, v4.w + bias4.w};
-      if (p.act_bwd) {
-        const uint2 z = *reinterpret_cast<const uint2*>(aux_in + (long long)m * p.ld_aux_in + n);
-        v[0] *= act_grad(__uint_as_float(z.x << 16), p.act_bwd);
-        v[1] *= act_grad(__uint_as_float(z.x & 0xffff0000u), p.act_bwd);
-        v[2] *= act_grad(__uint_as_float(z.y << 16), p.act_bwd);
-        v[3] *= act_grad(__uint_as_float(z.y & 0xffff0000u), p.act_bwd);
-      }
-#pragma unroll
-      for (int e = 0; e < 4; ++e) cs[e] += v[e];
-      if (aux_out) {
-        uint2 w;
-        w.x = pack2bf(v[0], v[1]);
-        w.y = pack2bf(v[2], v[3]);
-        *reinterpret_cast<uint2*>(aux_out + (long long)m * p.ld_aux_out + n) = w;
-      }
-#pragma unroll
-      for (int e = 0; e < 4; ++e) v[e] = act_fwd(v[e], p.act);
-      if (p.residual) {
-        const float4 r4 = *reinterpret_cast<const float4*>(p.residual + (long long)m * p.ldr + n);
-        v[0] += r4.x; v[1] += r4.y; v[2] += r4.z; v[3] += r4.w;
-      }
-      const long long ci = (long long)m * p.ldc + n;
-      if (p.out_f32) {  // (split-K partials were added by split_rows_atomic)
-        float4* C = reinterpret_cast<float4*>(static_cast<float*>(p.C) + ci);
-        if (p.accumulate) {
-          const float4 o = *C;
-          v[0] += o.x; v[1] += o.y; v[2] += o.z; v[3] += o.w;
-        }
-        *C = make_float4(v[0], v[1], v[2], v[3]);
-      } else {
-        uint2 w;
-        w.x = pack2bf(v[0], v[1]);
-        w.y = pack2bf(v[2], v[3]);
-        *reinterpret_cast<uint2*>(static_cast<bf16_t*>(p.C) + ci) = w;
-      }
-    }
-  }
-  if (p.colsum) colsum_flush(cs, p.colsum, n - c4 * 4, p.N, lane);
+  epi_tile<4, (Cfg::WGS <= 2)>(p, acc, reinterpret_cast<float*>(smem) + wid * 32 * 64, splits, m0 + wr * 64, n0 + wc * 64, lane);
 }
 
 // =====================================================================================
@@ -602,7 +661,7 @@ __device__ __forceinline__ bf16x8 frag3(const bf16_t* lds, int r0, int kstep, in
 }
 
 template <int BM_, int BN_, int WM, int WN, int KB, int STAGES, bool AK, bool BK>
-__global__ __launch_bounds__((V3Cfg<BM_, BN_, WM, WN, KB, STAGES>::NTH), 1) void gemm3_kernel(
+__global__ __launch_bounds__((V3Cfg<BM_, BN_, WM, WN, KB, STAGES>::NTH), (V3Cfg<BM_, BN_, WM, WN, KB, STAGES>::WGS)) void gemm3_kernel(
     GemmArgs p, unsigned long long a_bytes, unsigned long long b_bytes) {
   using Cfg = V3Cfg<BM_, BN_, WM, WN, KB, STAGES>;
   constexpr int FM = Cfg::FM, FN = Cfg::FN, NLA = Cfg::NLA, NLB = Cfg::NLB;
@@ -679,82 +738,7 @@ __global__ __launch_bounds__((V3Cfg<BM_, BN_, WM, WN, KB, STAGES>::NTH), 1) void
 #undef DPC_ISSUE3
 
   // ---------------- epilogue (as v2): WTM/32 passes of 32 rows per wave through LDS
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  float alpha = p.alpha;
-  if (p.alpha_ptr) alpha *= *p.alpha_ptr;
-  float* ct = reinterpret_cast<float*>(smem) + wid * 32 * 64;
-  const int c4 = lane & 15;
-  const int n = n0 + wc * 64 + c4 * 4;
-  const bool nok = n < p.N;
-  float4 bias4 = make_float4(0.f, 0.f, 0.f, 0.f);
-  if (p.bias && nok) bias4 = *reinterpret_cast<const float4*>(p.bias + n);
-  float cs[4] = {0.f, 0.f, 0.f, 0.f};
-  const bf16_t* aux_in = static_cast<const bf16_t*>(p.aux_in);
-  bf16_t* aux_out = static_cast<bf16_t*>(p.aux_out);
-#pragma unroll
-  for (int h = 0; h < Cfg::WTM / 32; ++h) {
-    __syncthreads();
-#pragma unroll
-    for (int ii = 0; ii < 2; ++ii)
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int row = ii * 16 + (lane >> 4) * 4 + r;
-          const int col = (j * 16 + (lane & 15)) ^ (((row >> 2) & 3) << 4);
-          ct[row * 64 + col] = acc[2 * h + ii][j][r] * alpha;
-        }
-    __syncthreads();
-    if (splits > 1) {
-      split_rows_atomic(ct, static_cast<float*>(p.C), p.ldc, m0 + wr * Cfg::WTM + h * 32, n0 + wc * 64, p.M, p.N, lane);
-      continue;
-    }
-#pragma unroll 2
-    for (int t = 0; t < 8; ++t) {
-      const int row = (lane >> 4) + 4 * t;
-      const int m = m0 + wr * Cfg::WTM + h * 32 + row;
-      const int col = (c4 * 4) ^ (((row >> 2) & 3) << 4);
-      float4 v4 = *reinterpret_cast<const float4*>(ct + row * 64 + col);
-      if (m >= p.M || !nok) continue;
-      float v[4] = {v4.x + bias4.x, v4.y + bias4.y, v4.z + bias4.z, v4.w + bias4.w};
-      if (p.act_bwd) {
-        const uint2 z = *reinterpret_cast<const uint2*>(aux_in + (long long)m * p.ld_aux_in + n);
-        v[0] *= act_grad(__uint_as_float(z.x << 16), p.act_bwd);
-        v[1] *= act_grad(__uint_as_float(z.x & 0xffff0000u), p.act_bwd);
-        v[2] *= act_grad(__uint_as_float(z.y << 16), p.act_bwd);
-        v[3] *= act_grad(__uint_as_float(z.y & 0xffff0000u), p.act_bwd);
-      }
-#pragma unroll
-      for (int e = 0; e < 4; ++e) cs[e] += v[e];
-      if (aux_out) {
-        uint2 w;
-        w.x = pack2bf(v[0], v[1]);
-        w.y = pack2bf(v[2], v[3]);
-        *reinterpret_cast<uint2*>(aux_out + (long long)m * p.ld_aux_out + n) = w;
-      }
-#pragma unroll
-      for (int e = 0; e < 4; ++e) v[e] = act_fwd(v[e], p.act);
-      if (p.residual) {
-        const float4 r4 = *reinterpret_cast<const float4*>(p.residual + (long long)m * p.ldr + n);
-        v[0] += r4.x; v[1] += r4.y; v[2] += r4.z; v[3] += r4.w;
-      }
-      const long long ci = (long long)m * p.ldc + n;
-      if (p.out_f32) {  // (split-K partials were added by split_rows_atomic)
-        float4* C = reinterpret_cast<float4*>(static_cast<float*>(p.C) + ci);
-        if (p.accumulate) {
-          const float4 o = *C;
-          v[0] += o.x; v[1] += o.y; v[2] += o.z; v[3] += o.w;
-        }
-        *C = make_float4(v[0], v[1], v[2], v[3]);
-      } else {
-        uint2 w;
-        w.x = pack2bf(v[0], v[1]);
-        w.y = pack2bf(v[2], v[3]);
-        *reinterpret_cast<uint2*>(static_cast<bf16_t*>(p.C) + ci) = w;
-      }
-    }
-  }
-  if (p.colsum) colsum_flush(cs, p.colsum, n - c4 * 4, p.N, lane);
+  epi_tile<FM, (FM == 4 && Cfg::WGS == 1)>(p, acc, reinterpret_cast<float*>(smem) + wid * 32 * 64, splits, m0 + wr * Cfg::WTM, n0 + wc * 64, lane);
 }
 
 // =====================================================================================
@@ -878,82 +862,7 @@ __global__ __launch_bounds__(512, 1) void gemm4_kernel(GemmArgs p, unsigned long
 #undef DPC_ISSUE4
 
   // ---------------- epilogue: four passes of 32 rows per wave through LDS (as v3)
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  float alpha = p.alpha;
-  if (p.alpha_ptr) alpha *= *p.alpha_ptr;
-  float* ct = reinterpret_cast<float*>(smem) + wid * 32 * 64;
-  const int c4 = lane & 15;
-  const int n = n0 + bc + c4 * 4;
-  const bool nok = n < p.N;
-  float4 bias4 = make_float4(0.f, 0.f, 0.f, 0.f);
-  if (p.bias && nok) bias4 = *reinterpret_cast<const float4*>(p.bias + n);
-  float cs[4] = {0.f, 0.f, 0.f, 0.f};
-  const bf16_t* aux_in = static_cast<const bf16_t*>(p.aux_in);
-  bf16_t* aux_out = static_cast<bf16_t*>(p.aux_out);
-#pragma unroll
-  for (int h = 0; h < 4; ++h) {
-    __syncthreads();
-#pragma unroll
-    for (int ii = 0; ii < 2; ++ii)
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int row = ii * 16 + (lane >> 4) * 4 + r;
-          const int col = (j * 16 + (lane & 15)) ^ (((row >> 2) & 3) << 4);
-          ct[row * 64 + col] = acc[2 * h + ii][j][r] * alpha;
-        }
-    __syncthreads();
-    if (splits > 1) {
-      split_rows_atomic(ct, static_cast<float*>(p.C), p.ldc, m0 + ar + h * 32, n0 + bc, p.M, p.N, lane);
-      continue;
-    }
-#pragma unroll 2
-    for (int t = 0; t < 8; ++t) {
-      const int row = (lane >> 4) + 4 * t;
-      const int m = m0 + ar + h * 32 + row;
-      const int col = (c4 * 4) ^ (((row >> 2) & 3) << 4);
-      float4 v4 = *reinterpret_cast<const float4*>(ct + row * 64 + col);
-      if (m >= p.M || !nok) continue;
-      float v[4] = {v4.x + bias4.x, v4.y + bias4.y, v4.z + bias4.z, v4.w + bias4.w};
-      if (p.act_bwd) {
-        const uint2 z = *reinterpret_cast<const uint2*>(aux_in + (long long)m * p.ld_aux_in + n);
-        v[0] *= act_grad(__uint_as_float(z.x << 16), p.act_bwd);
-        v[1] *= act_grad(__uint_as_float(z.x & 0xffff0000u), p.act_bwd);
-        v[2] *= act_grad(__uint_as_float(z.y << 16), p.act_bwd);
-        v[3] *= act_grad(__uint_as_float(z.y & 0xffff0000u), p.act_bwd);
-      }
-#pragma unroll
-      for (int e = 0; e < 4; ++e) cs[e] += v[e];
-      if (aux_out) {
-        uint2 w;
-        w.x = pack2bf(v[0], v[1]);
-        w.y = pack2bf(v[2], v[3]);
-        *reinterpret_cast<uint2*>(aux_out + (long long)m * p.ld_aux_out + n) = w;
-      }
-#pragma unroll
-      for (int e = 0; e < 4; ++e) v[e] = act_fwd(v[e], p.act);
-      if (p.residual) {
-        const float4 r4 = *reinterpret_cast<const float4*>(p.residual + (long long)m * p.ldr + n);
-        v[0] += r4.x; v[1] += r4.y; v[2] += r4.z; v[3] += r4.w;
-      }
-      const long long ci = (long long)m * p.ldc + n;
-      if (p.out_f32) {  // (split-K partials were added by split_rows_atomic)
-        float4* C = reinterpret_cast<float4*>(static_cast<float*>(p.C) + ci);
-        if (p.accumulate) {
-          const float4 o = *C;
-          v[0] += o.x; v[1] += o.y; v[2] += o.z; v[3] += o.w;
-        }
-        *C = make_float4(v[0], v[1], v[2], v[3]);
-      } else {
-        uint2 w;
-        w.x = pack2bf(v[0], v[1]);
-        w.y = pack2bf(v[2], v[3]);
-        *reinterpret_cast<uint2*>(static_cast<bf16_t*>(p.C) + ci) = w;
-      }
-    }
-  }
-  if (p.colsum) colsum_flush(cs, p.colsum, n - c4 * 4, p.N, lane);
+  epi_tile<8, false>(p, acc, reinterpret_cast<float*>(smem) + wid * 32 * 64, splits, m0 + ar, n0 + bc, lane);
 }
 
 // =====================================================================================
@@ -1092,82 +1001,7 @@ __global__ __launch_bounds__(512, 1) void gemm5_kernel(GemmArgs p, unsigned long
 #undef DPC_ISSUE5B
 
   // ---------------- epilogue: four passes of 32 rows per wave through LDS (as v4)
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  float alpha = p.alpha;
-  if (p.alpha_ptr) alpha *= *p.alpha_ptr;
-  float* ct = reinterpret_cast<float*>(smem) + wid * 32 * 64;
-  const int c4 = lane & 15;
-  const int n = n0 + bc + c4 * 4;
-  const bool nok = n < p.N;
-  float4 bias4 = make_float4(0.f, 0.f, 0.f, 0.f);
-  if (p.bias && nok) bias4 = *reinterpret_cast<const float4*>(p.bias + n);
-  float cs[4] = {0.f, 0.f, 0.f, 0.f};
-  const bf16_t* aux_in = static_cast<const bf16_t*>(p.aux_in);
-  bf16_t* aux_out = static_cast<bf16_t*>(p.aux_out);
-#pragma unroll
-  for (int h = 0; h < 4; ++h) {
-    __syncthreads();
-#pragma unroll
-    for (int ii = 0; ii < 2; ++ii)
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int row = ii * 16 + (lane >> 4) * 4 + r;
-          const int col = (j * 16 + (lane & 15)) ^ (((row >> 2) & 3) << 4);
-          ct[row * 64 + col] = acc[2 * h + ii][j][r] * alpha;
-        }
-    __syncthreads();
-    if (splits > 1) {
-      split_rows_atomic(ct, static_cast<float*>(p.C), p.ldc, m0 + ar + h * 32, n0 + bc, p.M, p.N, lane);
-      continue;
-    }
-#pragma unroll 2
-    for (int t = 0; t < 8; ++t) {
-      const int row = (lane >> 4) + 4 * t;
-      const int m = m0 + ar + h * 32 + row;
-      const int col = (c4 * 4) ^ (((row >> 2) & 3) << 4);
-      float4 v4 = *reinterpret_cast<const float4*>(ct + row * 64 + col);
-      if (m >= p.M || !nok) continue;
-      float v[4] = {v4.x + bias4.x, v4.y + bias4.y, v4.z + bias4.z, v4.w + bias4.w};
-      if (p.act_bwd) {
-        const uint2 z = *reinterpret_cast<const uint2*>(aux_in + (long long)m * p.ld_aux_in + n);
-        v[0] *= act_grad(__uint_as_float(z.x << 16), p.act_bwd);
-        v[1] *= act_grad(__uint_as_float(z.x & 0xffff0000u), p.act_bwd);
-        v[2] *= act_grad(__uint_as_float(z.y << 16), p.act_bwd);
-        v[3] *= act_grad(__uint_as_float(z.y & 0xffff0000u), p.act_bwd);
-      }
-#pragma unroll
-      for (int e = 0; e < 4; ++e) cs[e] += v[e];
-      if (aux_out) {
-        uint2 w;
-        w.x = pack2bf(v[0], v[1]);
-        w.y = pack2bf(v[2], v[3]);
-        *reinterpret_cast<uint2*>(aux_out + (long long)m * p.ld_aux_out + n) = w;
-      }
-#pragma unroll
-      for (int e = 0; e < 4; ++e) v[e] = act_fwd(v[e], p.act);
-      if (p.residual) {
-        const float4 r4 = *reinterpret_cast<const float4*>(p.residual + (long long)m * p.ldr + n);
-        v[0] += r4.x; v[1] += r4.y; v[2] += r4.z; v[3] += r4.w;
-      }
-      const long long ci = (long long)m * p.ldc + n;
-      if (p.out_f32) {
-        float4* C = reinterpret_cast<float4*>(static_cast<float*>(p.C) + ci);
-        if (p.accumulate) {
-          const float4 o = *C;
-          v[0] += o.x; v[1] += o.y; v[2] += o.z; v[3] += o.w;
-        }
-        *C = make_float4(v[0], v[1], v[2], v[3]);
-      } else {
-        uint2 w;
-        w.x = pack2bf(v[0], v[1]);
-        w.y = pack2bf(v[2], v[3]);
-        *reinterpret_cast<uint2*>(static_cast<bf16_t*>(p.C) + ci) = w;
-      }
-    }
-  }
-  if (p.colsum) colsum_flush(cs, p.colsum, n - c4 * 4, p.N, lane);
+  epi_tile<8, false>(p, acc, reinterpret_cast<float*>(smem) + wid * 32 * 64, splits, m0 + ar, n0 + bc, lane);
 }
 
 }  // namespace dpc
@@ -1277,6 +1111,7 @@ DPC_API int dpc_gemm(const GemmArgs* a, hipStream_t stream) {
                      al(a->C, a->out_f32 ? 16 : 8) && al(a->bias, 16) && al(a->residual, 16) &&
                      al(a->aux_in, 8) && al(a->aux_out, 8) && al(a->colsum, 4);
   int impl = g_gemm_impl;
+  if (impl < 0 && a->impl > 0) impl = a->impl;
   if (impl < 0) {
     // Default per operand layout and depth, from the GPT-2 shape sweep on MI355X
     // (bench/kernels.py, profiles/kernels_r1_*.json): forward products with a short K
@@ -1297,7 +1132,7 @@ DPC_API int dpc_gemm(const GemmArgs* a, hipStream_t stream) {
   // plain f32 products (weight gradients: small M x N, K = tokens) are split along K
   const bool plain = a->out_f32 && !a->bias && !a->residual && !a->aux_in && !a->aux_out &&
                      !a->colsum && !a->act && !a->act_bwd;
-  if (g_gemm_impl < 0 && v2_ok && plain && !a->a_kmaj && !a->b_kmaj && policy_impl(a) <= 0) {
+  if (g_gemm_impl < 0 && a->impl <= 0 && v2_ok && plain && !a->a_kmaj && !a->b_kmaj && policy_impl(a) <= 0) {
     // weight gradient: the 256x256 ping-pong kernel (v5) once there are enough 128x128 tiles
     // to spread over the k-splits (2304x768 and up: 780-880 TF/s vs 720 for the 3-deep
     // 128x128 ring, bench/kernels.py on MI355X), else the 2-stage 64-k kernel

@@ -21,6 +21,8 @@ same math with torch ops -- that expression is also the numerics oracle of the t
 """
 from __future__ import annotations
 
+import atexit
+import json
 import math
 import os
 
@@ -91,6 +93,93 @@ def _blas_plain(a, b, a_kmaj, b_kmaj, out, M, N, K, alpha, alpha_t) -> bool:
     if alpha_t is not None:
         out.mul_(alpha_t)
     return True
+
+
+# ---------------------------------------------------------------- measured per-shape choices
+# The dispatcher's built-in policy (csrc/gemm.hip) was fitted to GPT-2 small; on other shapes
+# the best tile / pipeline depends on wave quantisation (tiles vs 256 CUs), the epilogue's
+# traffic and K.  ``gemm_tuned.json`` (next to this file) maps a product's signature to the
+# implementation measured fastest for it on MI355X; ``DPC_GEMM_TUNE=1`` measures every
+# signature missing from the table the first time it runs eagerly (never inside a HIP-graph
+# capture: outputs are cloned, candidates timed with HIP events, best of 3 x 5 launches) and
+# writes the merged table to ``DPC_GEMM_TUNE_OUT`` (default: the in-package file) at exit.
+_TUNE_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "gemm_tuned.json")
+_TUNE = os.environ.get("DPC_GEMM_TUNE", "0") == "1"
+_USE_TABLE = os.environ.get("DPC_GEMM_TABLE", "1") == "1"
+_CANDIDATES = (0, 2, 4, 6, 10, 12)  # 0 = the dispatcher policy
+_TUNE_MAX_OUT_BYTES = 1 << 30
+
+
+def _load_table(path: str = _TUNE_PATH) -> dict:
+    try:
+        with open(path) as f:
+            return {k: int(v) for k, v in json.load(f).get("impl", {}).items()}
+    except (OSError, ValueError):
+        return {}
+
+
+_table: dict = _load_table() if _USE_TABLE else {}
+_tuned_new: dict = {}
+
+
+def _save_table() -> None:
+    if not _tuned_new:
+        return
+    path = os.environ.get("DPC_GEMM_TUNE_OUT", _TUNE_PATH)
+    merged = _load_table(path) if os.path.exists(path) else _load_table()
+    merged.update(_tuned_new)
+    os.makedirs(os.path.dirname(os.path.abspath(path)), exist_ok=True)
+    with open(path, "w") as f:
+        json.dump({"device": "MI355X (gfx950)", "impl": dict(sorted(merged.items()))}, f, indent=1)
+
+
+if _TUNE:
+    atexit.register(_save_table)
+
+
+def _sig(M, N, K, a_kmaj, b_kmaj, out_f32, bias, act, act_bwd, aux_out, residual, colsum,
+         accumulate) -> str:
+    flags = "".join(c for c, on in (("b", bias is not None), ("x", aux_out is not None),
+                                     ("r", residual is not None), ("c", colsum is not None),
+                                     ("a", accumulate)) if on)
+    return (f"{M}x{N}x{K}:{'k' if a_kmaj else 'm'}{'k' if b_kmaj else 'm'}:"
+            f"{'f' if out_f32 else 'h'}:{act}{act_bwd}:{flags}")
+
+
+def _tune(args, out, aux_out, colsum, device) -> int:
+    """Time every candidate implementation on clones of the outputs; return the fastest."""
+    scratch = {"C": out.clone()}
+    if aux_out is not None:
+        scratch["aux_out"] = aux_out.clone()
+    if colsum is not None:
+        scratch["colsum"] = colsum.clone()
+    saved = {k: getattr(args, k) for k in scratch}
+    for k, t in scratch.items():
+        setattr(args, k, t.data_ptr())
+    best, best_t = 0, float("inf")
+    try:
+        for impl in _CANDIDATES:
+            args.impl = impl
+            try:
+                _lib.call("dpc_gemm", args, device)
+                torch.cuda.synchronize(device)
+            except RuntimeError:
+                continue
+            t_min = float("inf")
+            for _ in range(3):
+                s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                s.record()
+                for _ in range(5):
+                    _lib.call("dpc_gemm", args, device)
+                e.record()
+                e.synchronize()
+                t_min = min(t_min, s.elapsed_time(e))
+            if t_min < best_t:
+                best, best_t = impl, t_min
+    finally:
+        for k, v in saved.items():
+            setattr(args, k, v)
+    return best
 
 
 def _check_operand(t: torch.Tensor, rows: int, cols: int, name: str) -> None:
@@ -176,6 +265,15 @@ def gemm(
             a_kmaj=int(a_kmaj), b_kmaj=int(b_kmaj),
             a_r=a.shape[0], a_c=a.shape[1], b_r=b.shape[0], b_c=b.shape[1],
         )
+        if (_table or _TUNE) and _lib.forced_gemm_impl < 0:
+            key = _sig(M, N, K, a_kmaj, b_kmaj, out.dtype == torch.float32, bias, act, act_bwd,
+                       aux_out, residual, colsum, accumulate)
+            impl = _table.get(key)
+            if (impl is None and _TUNE and not torch.cuda.is_current_stream_capturing()
+                    and out.numel() * out.element_size() <= _TUNE_MAX_OUT_BYTES):
+                impl = _tune(args, out, aux_out, colsum, a.device)
+                _table[key] = _tuned_new[key] = impl
+            args.impl = impl or 0
         _lib.call("dpc_gemm", args, a.device)
         return out
     return _gemm_ref(a, b, a_kmaj, b_kmaj, out, bias, act, act_bwd, aux_in, aux_out, residual,

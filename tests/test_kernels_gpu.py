@@ -75,8 +75,16 @@ def test_gemm_impls_with_epilogue(impl, a_kmaj, b_kmaj, M, N, K):
         acc = acc0.clone()
         gemm(A, B, a_kmaj=a_kmaj, b_kmaj=b_kmaj, out=acc, accumulate=True)
         ob = gemm(A, B, a_kmaj=a_kmaj, b_kmaj=b_kmaj)  # bf16 out
+        # act' without a residual: the aux operand rides the epilogue's prefetch slot
+        cs2 = torch.zeros(N, device=dev)
+        od = gemm(A, B, a_kmaj=a_kmaj, b_kmaj=b_kmaj, act_bwd=2, aux_in=z, colsum=cs2)
     finally:
         _lib.set_gemm_impl(-1)
+    od_r = torch.empty(M, N, device=dev)
+    cs2_r = torch.zeros(N, device=dev)
+    _gemm_ref(a, b, True, True, od_r, None, 0, 2, z, None, None, 1.0, None, False, cs2_r)
+    assert rel_err(od, od_r) < 1e-2
+    assert rel_err(cs2, cs2_r) < 2e-3
     ref_out = torch.empty(M, N, device=dev)
     aux_r = torch.empty_like(aux)
     cs_r = torch.zeros(N, device=dev)
