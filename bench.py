@@ -33,10 +33,15 @@ from distributed_pytorch_cookbook_amd.utils.metrics import mfu, train_flops_per_
 METRIC = "tokens/sec (node) GPT-2 training per recipe (DDP/FSDP/PP) at 1/2/4/8 MI355X"
 # The reference publishes no numbers.  vs_baseline compares against the
 # stock-PyTorch run of the reference's own default recipe (manual attention + torch.compile,
-# bf16 autocast, fused AdamW) measured on one MI355X at 32 x 1024 tokens per GPU
+# bf16 autocast, fused AdamW) measured on one MI355X at the same per-GPU batch x 1024 tokens
 # (bench/baseline_torch.py --compile; profiles/r1_stock_pytorch_baselines.jsonl), scaled
 # linearly with the GPU count.
-BASELINE_TOKS_PER_GPU = {("ddp", "gpt2-small", 32, 1024): 276672.6}
+BASELINE_TOKS_PER_GPU = {("ddp", "gpt2-small", 32, 1024): 276672.6,
+                         ("ddp", "gpt2-small", 64, 1024): 300633.0}
+# Per-GPU batch (sequences) per recipe when --batch_size is not given: the DDP recipe runs
+# the reference's own default per-rank batch (--batch_size 64, main-ddp.py argparse, SURVEY.md
+# §5.6); the larger models use what fits their activations comfortably in one GPU's HBM.
+DEFAULT_BATCH = {"ddp": 64, "fsdp": 16, "pipe": 32, "pipe_ddp": 16}
 
 
 def main():
@@ -46,7 +51,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--recipe", default="ddp", choices=["ddp", "fsdp", "pipe", "pipe_ddp"])
     ap.add_argument("--model", default=None)
-    ap.add_argument("--batch_size", type=int, default=32, help="sequences per GPU (per DP replica for PP)")
+    ap.add_argument("--batch_size", type=int, default=None,
+                    help="sequences per GPU (per DP replica for PP); default per recipe (DEFAULT_BATCH)")
     ap.add_argument("--seq_len", type=int, default=1024)
     ap.add_argument("--bucket_mb", type=float, default=128.0)
     ap.add_argument("--reduce_dtype", default="fp32", choices=["fp32", "bf16"])
@@ -57,6 +63,8 @@ def main():
     ap.add_argument("--json", default=None, help="also write the result line to this file")
     a = ap.parse_args()
 
+    if a.batch_size is None:
+        a.batch_size = DEFAULT_BATCH[a.recipe]
     default_model = {"ddp": "gpt2-small", "fsdp": "gpt2-xl", "pipe": "gpt2-medium",
                      "pipe_ddp": "gpt2-large"}[a.recipe]
     model_name = a.model or default_model

@@ -220,11 +220,20 @@ DPC_API int dpc_layernorm_fwd(const LNArgs* a, hipStream_t stream) {
   return (int)hipGetLastError();
 }
 
+// Workgroups of the persistent backward grid.  Each workgroup ends with 2 D column atomics
+// (dgamma / dbeta), so the best grid shrinks as D grows: bench/ln_grid.py on MI355X, 1024 at
+// D = 768 (5.2 TB/s; 512: 4.6, 2048: 4.3) and 512 at D = 1600 (4.4 TB/s; 1024: 4.1) -- i.e.
+// ~786K column-atomics per launch.  0 = that rule; > 0 forces a size (sweeps).
+static int g_ln_bwd_blocks = 0;
+DPC_API void dpc_layernorm_set_bwd_blocks(int n) { g_ln_bwd_blocks = n > 0 ? n : 0; }
+
 DPC_API int dpc_layernorm_bwd(const LNArgs* a, hipStream_t stream) {
   if (a->T <= 0) return 0;
   if (a->D % 4) return (int)hipErrorInvalidValue;
   const long long blocks = (a->T + 3) / 4;
-  dim3 grid((unsigned)(blocks < 1024 ? blocks : 1024));
+  long long cap = g_ln_bwd_blocks > 0 ? g_ln_bwd_blocks : 786432 / a->D;
+  cap = cap < 256 ? 256 : (cap > 1024 && g_ln_bwd_blocks <= 0 ? 1024 : cap);
+  dim3 grid((unsigned)(blocks < cap ? blocks : cap));
   LN_DISPATCH(ln_bwd_kernel, grid);
   return (int)hipGetLastError();
 }
