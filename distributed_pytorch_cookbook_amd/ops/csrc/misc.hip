@@ -91,34 +91,13 @@ __device__ __forceinline__ void ms_combine(float& m, float& s, float m2, float s
   m = mn;
 }
 
-__global__ __launch_bounds__(256) void ce_kernel(CEArgs p) {
-  __shared__ float sm[4], ss[4], sv[4];
-  __shared__ int si[4];
-  const long long row = blockIdx.x;
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const bf16_t* x = static_cast<const bf16_t*>(p.logits) + row * p.ld;
-  const long long tgt = p.targets[row];
-  const bool valid = tgt != p.ignore_index && tgt >= 0 && tgt < p.V;
-  const int nch = (p.V + 7) >> 3;
-  float m = -INFINITY, s = 0.f, bv = -INFINITY;
-  int bi = 0x7fffffff;
-  for (int c = tid; c < nch; c += 256) {
-    float f[8];
-    unpack8(reinterpret_cast<const uint4*>(x)[c], f);
-    float cm = -INFINITY;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const int idx = c * 8 + j;
-      if (idx >= p.V) f[j] = -INFINITY;
-      cm = fmaxf(cm, f[j]);
-      if (f[j] > bv) { bv = f[j]; bi = idx; }
-    }
-    float cs = 0.f;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) cs += __expf(f[j] - cm);
-    ms_combine(m, s, cm, cs);
-  }
-  // wave combine
+// One workgroup per row.  The block reduction of (max, sum-exp, argmax) and the row's target
+// logit; the target logit is captured in the first pass by the thread that owns its chunk
+// (dlogits may alias logits, so it must not be re-read once the gradient pass has started).
+template <int NW>
+__device__ __forceinline__ void ce_block_reduce(float& m, float& s, float& bv, int& bi, float* red_m, float* red_s,
+                                                float* red_v, int* red_i) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) {
     const float m2 = __shfl_xor(m, o, 64), s2 = __shfl_xor(s, o, 64);
@@ -127,34 +106,147 @@ __global__ __launch_bounds__(256) void ce_kernel(CEArgs p) {
     const int i2 = __shfl_xor(bi, o, 64);
     if (v2 > bv || (v2 == bv && i2 < bi)) { bv = v2; bi = i2; }
   }
-  if (lane == 0) { sm[w] = m; ss[w] = s; sv[w] = bv; si[w] = bi; }
+  if (lane == 0) { red_m[w] = m; red_s[w] = s; red_v[w] = bv; red_i[w] = bi; }
   __syncthreads();
-  m = sm[0]; s = ss[0]; bv = sv[0]; bi = si[0];
+  m = red_m[0]; s = red_s[0]; bv = red_v[0]; bi = red_i[0];
 #pragma unroll
-  for (int i = 1; i < 4; ++i) {
-    ms_combine(m, s, sm[i], ss[i]);
-    if (sv[i] > bv || (sv[i] == bv && si[i] < bi)) { bv = sv[i]; bi = si[i]; }
+  for (int i = 1; i < NW; ++i) {
+    ms_combine(m, s, red_m[i], red_s[i]);
+    if (red_v[i] > bv || (red_v[i] == bv && red_i[i] < bi)) { bv = red_v[i]; bi = red_i[i]; }
   }
+}
+
+__device__ __forceinline__ void ce_chunk_stats(const uint4& raw, int c, int V, long long tgt, float& m, float& s,
+                                               float& bv, int& bi, float* tval) {
+  float f[8];
+  unpack8(raw, f);
+  float cm = -INFINITY;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int idx = c * 8 + j;
+    if (idx >= V) f[j] = -INFINITY;
+    if (idx == tgt) *tval = f[j];
+    cm = fmaxf(cm, f[j]);
+    if (f[j] > bv) { bv = f[j]; bi = idx; }
+  }
+  if (cm == -INFINITY) return;  // past the row end
+  float cs = 0.f;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) cs += __expf(f[j] - cm);
+  ms_combine(m, s, cm, cs);
+}
+
+__device__ __forceinline__ uint4 ce_chunk_grad(const uint4& raw, int c, int V, long long tgt, float lse, float scale) {
+  float f[8];
+  unpack8(raw, f);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int idx = c * 8 + j;
+    f[j] = idx < V ? (__expf(f[j] - lse) - (idx == tgt ? 1.f : 0.f)) * scale : 0.f;
+  }
+  return pack8(f);
+}
+
+// Register-resident row (the GPT-2 head: V = 50257 -> 6283 16-B chunks, NC = 16 per thread
+// of 512): every chunk is loaded once, all NC loads in flight per thread before any math,
+// and the gradient pass runs from registers -- one HBM read of the logits and one write of
+// dlogits (the earlier two-pass form re-read each 100 KB row and kept one load in flight per
+// wave: 4.3 TB/s).
+constexpr int CE_NT = 512;
+
+template <int NC>
+__global__ __launch_bounds__(CE_NT) void ce_kernel(CEArgs p) {
+  __shared__ float red_m[CE_NT / 64], red_s[CE_NT / 64], red_v[CE_NT / 64], tv;
+  __shared__ int red_i[CE_NT / 64];
+  const long long row = blockIdx.x;
+  const int tid = threadIdx.x;
+  const bf16_t* x = static_cast<const bf16_t*>(p.logits) + row * p.ld;
+  const uint4* xv = reinterpret_cast<const uint4*>(x);
+  const long long tgt = p.targets[row];
+  const bool valid = tgt != p.ignore_index && tgt >= 0 && tgt < p.V;
+  const int nch = (p.V + 7) >> 3;
+  uint4 raw[NC];
+#pragma unroll
+  for (int u = 0; u < NC; ++u) {
+    const int c = tid + u * CE_NT;
+    raw[u] = c < nch ? xv[c] : make_uint4(0u, 0u, 0u, 0u);
+  }
+  float m = -INFINITY, s = 0.f, bv = -INFINITY, tval = 0.f;
+  int bi = 0x7fffffff;
+#pragma unroll
+  for (int u = 0; u < NC; ++u) {
+    const int c = tid + u * CE_NT;
+    if (c < nch) ce_chunk_stats(raw[u], c, p.V, tgt, m, s, bv, bi, &tval);
+  }
+  if (valid && tgt / 8 % CE_NT == tid) tv = tval;
+  ce_block_reduce<CE_NT / 64>(m, s, bv, bi, red_m, red_s, red_v, red_i);  // (its barrier publishes tv)
   const float lse = m + __logf(s);
   if (tid == 0) {
-    p.row_loss[row] = valid ? lse - bf2f(x[tgt]) : 0.f;
+    p.row_loss[row] = valid ? lse - tv : 0.f;
     if (p.row_correct) p.row_correct[row] = (valid && bi == tgt) ? 1.f : 0.f;
   }
   if (!p.write_grad) return;
   const float scale = valid ? *p.inv_count : 0.f;
-  bf16_t* g = static_cast<bf16_t*>(p.dlogits) + row * p.ld;
+  uint4* g = reinterpret_cast<uint4*>(static_cast<bf16_t*>(p.dlogits) + row * p.ld);
   const int nchl = (int)(p.ld >> 3);
-  for (int c = tid; c < nchl; c += 256) {
-    float f[8];
-    if (c < nch) unpack8(reinterpret_cast<const uint4*>(x)[c], f);
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const int idx = c * 8 + j;
-      float v = 0.f;
-      if (idx < p.V) v = (__expf(f[j] - lse) - (idx == tgt ? 1.f : 0.f)) * scale;
-      f[j] = v;
+  for (int u = 0; u < NC; ++u) {
+    const int c = tid + u * CE_NT;
+    if (c < nchl) g[c] = ce_chunk_grad(raw[u], c, p.V, tgt, lse, scale);
+  }
+}
+
+// Streaming fallback for rows longer than CE_NT * 16 chunks (V > 65536): CE_UNROLL chunks in
+// flight per thread per trip, the gradient pass re-reads the row.
+template <int CE_UNROLL>
+__global__ __launch_bounds__(256) void ce_stream_kernel(CEArgs p) {
+  __shared__ float red_m[4], red_s[4], red_v[4], tv;
+  __shared__ int red_i[4];
+  const long long row = blockIdx.x;
+  const int tid = threadIdx.x;
+  const bf16_t* x = static_cast<const bf16_t*>(p.logits) + row * p.ld;
+  const uint4* xv = reinterpret_cast<const uint4*>(x);
+  const long long tgt = p.targets[row];
+  const bool valid = tgt != p.ignore_index && tgt >= 0 && tgt < p.V;
+  const int nch = (p.V + 7) >> 3;
+  float m = -INFINITY, s = 0.f, bv = -INFINITY, tval = 0.f;
+  int bi = 0x7fffffff;
+  for (int c0 = tid; c0 < nch; c0 += 256 * CE_UNROLL) {
+    uint4 raw[CE_UNROLL];
+#pragma unroll
+    for (int u = 0; u < CE_UNROLL; ++u) {
+      const int c = c0 + u * 256;
+      raw[u] = c < nch ? xv[c] : make_uint4(0u, 0u, 0u, 0u);
     }
-    reinterpret_cast<uint4*>(g)[c] = pack8(f);
+#pragma unroll
+    for (int u = 0; u < CE_UNROLL; ++u) {
+      const int c = c0 + u * 256;
+      if (c < nch) ce_chunk_stats(raw[u], c, p.V, tgt, m, s, bv, bi, &tval);
+    }
+  }
+  if (valid && tgt / 8 % 256 == tid) tv = tval;
+  ce_block_reduce<4>(m, s, bv, bi, red_m, red_s, red_v, red_i);
+  const float lse = m + __logf(s);
+  if (tid == 0) {
+    p.row_loss[row] = valid ? lse - tv : 0.f;
+    if (p.row_correct) p.row_correct[row] = (valid && bi == tgt) ? 1.f : 0.f;
+  }
+  if (!p.write_grad) return;
+  const float scale = valid ? *p.inv_count : 0.f;
+  uint4* g = reinterpret_cast<uint4*>(static_cast<bf16_t*>(p.dlogits) + row * p.ld);
+  const int nchl = (int)(p.ld >> 3);
+  for (int c0 = tid; c0 < nchl; c0 += 256 * CE_UNROLL) {
+    uint4 raw[CE_UNROLL];
+#pragma unroll
+    for (int u = 0; u < CE_UNROLL; ++u) {
+      const int c = c0 + u * 256;
+      raw[u] = c < nch ? xv[c] : make_uint4(0u, 0u, 0u, 0u);
+    }
+#pragma unroll
+    for (int u = 0; u < CE_UNROLL; ++u) {
+      const int c = c0 + u * 256;
+      if (c < nchl) g[c] = ce_chunk_grad(raw[u], c, p.V, tgt, lse, scale);
+    }
   }
 }
 
@@ -426,10 +518,25 @@ DPC_API int dpc_embedding_bwd(const EmbArgs* a, hipStream_t stream) {
   return (int)hipGetLastError();
 }
 
+// 0: register-resident rows when they fit (default); 1 / 2: streaming with 1 / 4 chunks in
+// flight per thread (A/B sweeps: bench/ce_one.py)
+static int g_ce_mode = 0;
+DPC_API void dpc_ce_set_mode(int m) { g_ce_mode = m; }
+
 DPC_API int dpc_cross_entropy(const CEArgs* a, hipStream_t stream) {
   if (a->T <= 0) return 0;
   if (a->ld % 8) return (int)hipErrorInvalidValue;
-  hipLaunchKernelGGL(ce_kernel, dim3((unsigned)a->T), dim3(256), 0, stream, *a);
+  const long long nc = ((a->ld >> 3) + CE_NT - 1) / CE_NT;  // chunks per thread (ld >= V)
+  const dim3 grid((unsigned)a->T);
+  if (g_ce_mode == 1) hipLaunchKernelGGL(ce_stream_kernel<1>, grid, dim3(256), 0, stream, *a);
+  else if (g_ce_mode == 2) hipLaunchKernelGGL(ce_stream_kernel<4>, grid, dim3(256), 0, stream, *a);
+  else if (nc <= 1) hipLaunchKernelGGL(ce_kernel<1>, grid, dim3(CE_NT), 0, stream, *a);
+  else if (nc <= 2) hipLaunchKernelGGL(ce_kernel<2>, grid, dim3(CE_NT), 0, stream, *a);
+  else if (nc <= 4) hipLaunchKernelGGL(ce_kernel<4>, grid, dim3(CE_NT), 0, stream, *a);
+  else if (nc <= 8) hipLaunchKernelGGL(ce_kernel<8>, grid, dim3(CE_NT), 0, stream, *a);
+  else if (nc <= 13) hipLaunchKernelGGL(ce_kernel<13>, grid, dim3(CE_NT), 0, stream, *a);
+  else if (nc <= 16) hipLaunchKernelGGL(ce_kernel<16>, grid, dim3(CE_NT), 0, stream, *a);
+  else hipLaunchKernelGGL(ce_stream_kernel<4>, grid, dim3(256), 0, stream, *a);
   return (int)hipGetLastError();
 }
 
