@@ -63,8 +63,12 @@ def main():
     ap.add_argument("--json", default=None, help="also write the result line to this file")
     a = ap.parse_args()
 
-    if a.batch_size is None:
+    batch_given = a.batch_size is not None
+    if not batch_given:
         a.batch_size = DEFAULT_BATCH[a.recipe]
+    if a.recipe == "pipe_ddp" and not a.dp_size:
+        # the BASELINE.json hybrid: 2 pipeline stages x (N / 2) data-parallel replicas
+        a.dp_size = max(1, int(os.environ.get("WORLD_SIZE", a.gpus)) // 2)
     default_model = {"ddp": "gpt2-small", "fsdp": "gpt2-xl", "pipe": "gpt2-medium",
                      "pipe_ddp": "gpt2-large"}[a.recipe]
     model_name = a.model or default_model
@@ -93,6 +97,12 @@ def main():
     # synthetic batches: a small pool of distinct random token batches per DP replica
     S = a.seq_len
     B = a.batch_size
+    pp = max(1, info.world_size // max(engine.dp_world, 1))
+    if not batch_given and a.recipe in ("pipe", "pipe_ddp"):
+        # weak scaling for pipelines too: each pipeline replica gets pp x the per-GPU batch,
+        # so every GPU still processes DEFAULT_BATCH sequences per step (2 pp micro-batches
+        # of DEFAULT_BATCH / 2 sequences each, as at N = 1)
+        B = a.batch_size * pp
     g = torch.Generator(device="cpu").manual_seed(1000 + engine.dp_rank)
     pool = []
     for _ in range(4):

@@ -24,4 +24,6 @@ run ddp2_bf16 2 --batch_size 8 --reduce_dtype bf16 &&
 run fsdp2 2 --recipe fsdp --model gpt2-medium --batch_size 4 &&
 run pipe2 2 --recipe pipe --batch_size 8 &&
 run pipe4_gpipe 4 --recipe pipe --batch_size 8 --schedule gpipe &&
-run pipeddp4 4 --recipe pipe_ddp --model gpt2-medium --batch_size 4 --dp_size 2
+run pipeddp4 4 --recipe pipe_ddp --model gpt2-medium --batch_size 4 --dp_size 2 &&
+run pipe4_default 4 --recipe pipe --model gpt2-small &&
+run pipeddp4_default 4 --recipe pipe_ddp --model gpt2-small
