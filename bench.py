@@ -38,10 +38,13 @@ METRIC = "tokens/sec (node) GPT-2 training per recipe (DDP/FSDP/PP) at 1/2/4/8 M
 # linearly with the GPU count.
 BASELINE_TOKS_PER_GPU = {("ddp", "gpt2-small", 32, 1024): 276672.6,
                          ("ddp", "gpt2-small", 64, 1024): 300633.0}
-# Per-GPU batch (sequences) per recipe when --batch_size is not given: the DDP recipe runs
-# the reference's own default per-rank batch (--batch_size 64, main-ddp.py argparse, SURVEY.md
-# §5.6); the larger models use what fits their activations comfortably in one GPU's HBM.
-DEFAULT_BATCH = {"ddp": 64, "fsdp": 16, "pipe": 32, "pipe_ddp": 16}
+# Per-GPU batch (sequences) per recipe when --batch_size is not given: DDP and the pipeline
+# run the reference's own default per-rank batch (--batch_size 64, main-*.py argparse,
+# SURVEY.md §5.6); GPT-2 XL (FSDP) and GPT-2 large (PP x DP) take 32, which keeps their saved
+# activations well inside one GPU's 288 GB.  Larger batches are faster per token on one MI355X
+# (profiles/r1_v17_recipe_batch_sweep.jsonl): FSDP XL 16 -> 32 +8 %, PP x DP large +15 %,
+# pipeline medium 32 -> 64 +7 %.
+DEFAULT_BATCH = {"ddp": 64, "fsdp": 32, "pipe": 64, "pipe_ddp": 32}
 
 
 def main():
