@@ -259,25 +259,61 @@ def test_embedding(tdt):
     assert torch.allclose(dt, rt, atol=1e-4) and torch.allclose(dp, rp, atol=1e-4)
 
 
-def test_cross_entropy():
+@pytest.mark.parametrize("V,mode", [(50257, 0), (1000, 0), (9000, 0), (40000, 0), (70001, 0),
+                                    (50257, 1), (50257, 2)])
+def test_cross_entropy(V, mode):
+    """Register-resident rows (ce_kernel<1..16>: V = 1000 .. 50257), the streaming fallback
+    (V = 70001 > 64K columns) and the forced streaming modes, all in place."""
     torch.manual_seed(6)
-    T, V = 300, 50257
+    T = 300
     ld = (V + 63) // 64 * 64
+    _lib.lib().dpc_ce_set_mode(mode)
     buf = torch.zeros(T, ld, device=dev, dtype=torch.bfloat16)
     buf[:, :V] = (torch.randn(T, V, device=dev) * 2).bfloat16()
     logits = buf.clone()
     tg = torch.randint(0, V, (T,), device=dev)
     tg[::7] = -100
-    loss, n, correct = cross_entropy_fused(buf, tg, V, write_grad=True, want_correct=True)
+    try:
+        loss, n, correct = cross_entropy_fused(buf, tg, V, write_grad=True, want_correct=True)
+    finally:
+        _lib.lib().dpc_ce_set_mode(0)
     lf = logits[:, :V].float().requires_grad_(True)
     lr = torch.nn.functional.cross_entropy(lf, tg, ignore_index=-100)
     lr.backward()
     assert abs(loss.item() - lr.item()) < 1e-3 * abs(lr.item())
     assert rel_err(buf[:, :V], lf.grad) < 1e-2
-    assert buf[:, V:].abs().max().item() == 0
+    assert ld == V or buf[:, V:].abs().max().item() == 0
     valid = tg != -100
     rc = (lf.argmax(-1) == tg)[valid].sum().item()
     assert abs(correct.item() - rc) <= 1
+
+
+def test_gemm_autotune_leaves_outputs_intact():
+    """The autotuner times candidates on CLONES of the outputs: an accumulating weight
+    gradient and a column-sum epilogue must come out exactly as one untuned call makes them."""
+    from distributed_pytorch_cookbook_amd.ops import gemm as G
+    torch.manual_seed(12)
+    T, N, K = 4096, 384, 256
+    dy = torch.randn(T, N, device=dev).bfloat16()
+    x = torch.randn(T, K, device=dev).bfloat16()
+    g0 = torch.randn(N, K, device=dev)
+    z = torch.randn(T, K, device=dev).bfloat16()
+    w = torch.randn(N, K, device=dev).bfloat16()
+    saved = (G._TUNE, dict(G._table), dict(G._tuned_new))
+    try:
+        G._TUNE, G._table, G._tuned_new = True, {}, {}
+        g = g0.clone()
+        G.gemm(dy, x, a_kmaj=False, b_kmaj=False, out=g, accumulate=True)
+        cs = torch.zeros(K, device=dev)
+        d = G.gemm(dy, w, a_kmaj=True, b_kmaj=False, act_bwd=2, aux_in=z, colsum=cs)
+        assert len(G._tuned_new) == 2 and all(v in G._CANDIDATES for v in G._tuned_new.values())
+    finally:
+        G._TUNE, G._table, G._tuned_new = saved
+    assert rel_err(g - g0, dy.float().t() @ x.float()) < 2e-3
+    d_r = torch.empty(T, K, device=dev)
+    cs_r = torch.zeros(K, device=dev)
+    _gemm_ref(dy, w.t().contiguous(), True, True, d_r, None, 0, 2, z, None, None, 1.0, None, False, cs_r)
+    assert rel_err(d, d_r) < 1e-2 and rel_err(cs, cs_r) < 2e-3
 
 
 def test_adamw_matches_torch():

@@ -110,3 +110,18 @@ def test_grad_scaler_cpu_semantics():
         opt.step(**sc.opt_kwargs(opt))
         sc.update()
     assert float(sc.scale_t) == 8.0 and float(opt.step_t) == 3.0
+
+
+def test_gemm_table_signature_and_file():
+    """The measured GEMM table: signature format, and every entry names a real implementation."""
+    import json
+    import os
+
+    from distributed_pytorch_cookbook_amd.ops import gemm as G
+    sig = G._sig(65472, 3072, 768, True, False, False, None, 0, 2, None, None, object(), False)
+    assert sig == "65472x3072x768:km:h:02:c"
+    with open(G._TUNE_PATH) as f:
+        table = json.load(f)["impl"]
+    assert table and all(v in G._CANDIDATES for v in table.values())
+    assert all(k.count(":") == 4 for k in table)
+    assert os.path.dirname(G._TUNE_PATH).endswith("ops")
