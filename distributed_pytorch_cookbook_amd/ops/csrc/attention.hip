@@ -74,6 +74,35 @@ __device__ __forceinline__ void tile_store(const uint4 (&r)[2], bf16_t* lds) {
   }
 }
 
+// LDS-DMA staging of a 64-row x 64-col bf16 tile (buffer_load_dwordx4 ... lds: no VGPR round
+// trip, no ds_write).  The DMA writes lane-linearly -- wave-instruction j fills rows 8j..8j+7,
+// lane l slot (l & 7) of row 8j + (l >> 3) -- so the chunk swizzle of aoff() moves to the
+// SOURCE address: the lane fetches chunk (l & 7) ^ aswz(row).  dma_voff: the lane's byte
+// offset for the wave's two instructions (4 waves x 2 x 1 KiB = the 8 KiB tile), relative to
+// the tile's first row.  num_records ends the descriptor at the sequence end (rows >= S land
+// as zeros, as the register-staged path zero-filled them).
+typedef __attribute__((address_space(3))) void* lds_void_t;
+
+__device__ __forceinline__ void dma_voff(int (&v)[2], long long ld, int wid, int lane) {
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int row = 8 * (wid * 2 + i) + (lane >> 3);
+    const int chunk = (lane & 7) ^ aswz(row);
+    v[i] = (int)((long long)row * ld * 2 + chunk * 16);
+  }
+}
+
+__device__ __forceinline__ void tile_dma(const bf16_t* base, long long ld, int row0, int S, const int (&v)[2],
+                                         bf16_t* lds, int wid) {
+  const long long left = (long long)(S - row0) * ld * 2;
+  const unsigned nrec = left <= 0 ? 0u : (left > 0xffffffffll ? 0xffffffffu : (unsigned)left);
+  const __amdgpu_buffer_rsrc_t rs =
+      __builtin_amdgcn_make_buffer_rsrc((void*)(base + (long long)row0 * ld), 0, nrec, 0x00020000);
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void_t)(lds + (wid * 2 + i) * 512), 16, v[i], 0, 0, 0);
+}
+
 // Row fragment (A or B operand of 32x32x16): lane holds X[row0 + (lane & 31)][16 st + 8 h .. +7]
 __device__ __forceinline__ bf16x8 row_frag(const bf16_t* lds, int row0, int st, int lane) {
   const int row = row0 + (lane & 31);
@@ -142,7 +171,11 @@ __device__ __forceinline__ void xcd_work(int nblk, int& bh, int& i) {
 }
 
 // ------------------------------------------------------------------ forward
-__global__ __launch_bounds__(256, 2) void attn_fwd_kernel(AttnArgs p) {
+// Three workgroups (12 waves) per CU: with the K/V tiles staged by LDS-DMA the kernel fits
+// 168 VGPRs (7 spilled); a third wave per SIMD hides more of the softmax / MFMA alternation.
+// bench/attn_one.py N=64 S=1023 H=12 on one MI355X: register staging at 2 WG/CU 285.7 us,
+// DMA at 2 WG/CU 277.2 us, DMA at 3 WG/CU 264.5 us (profiles/r1_v18_attn_fwd_dma_ab.txt).
+__global__ __launch_bounds__(256, 3) void attn_fwd_kernel(AttnArgs p) {
   __shared__ __attribute__((aligned(16))) bf16_t smem[2 * 2 * KT * HD];  // [stage][K|V]
   const int S = p.S, H = p.H;
   const int nqb = (S + QB - 1) / QB;
@@ -174,19 +207,24 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(AttnArgs p) {
 #pragma unroll
   for (int i = 0; i < 16; ++i) { o[0][i] = 0.f; o[1][i] = 0.f; }
 
-  uint4 rk[2], rv[2];
-  tile_load(rk, K, p.ld_qkv, 0, S);
-  tile_load(rv, V, p.ld_qkv, 0, S);
-  tile_store(rk, smem);
-  tile_store(rv, smem + KT * HD);
+  // K/V tiles stream into the LDS double buffer by DMA: tile t+1 is issued at the top of
+  // iteration t into the stage iteration t-1 read (released by its closing barrier), and
+  // lands under this iteration's MFMAs; no staging registers (16 VGPRs) as the
+  // register-staged copy needed.
+  int dv[2];
+  dma_voff(dv, p.ld_qkv, wid, lane);
+  tile_dma(K, p.ld_qkv, 0, S, dv, smem, wid);
+  tile_dma(V, p.ld_qkv, 0, S, dv, smem + KT * HD, wid);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
 
   for (int t = 0; t < ntiles; ++t) {
     const int cur = t & 1;
     const bool more = t + 1 < ntiles;
     if (more) {
-      tile_load(rk, K, p.ld_qkv, (t + 1) * KT, S);
-      tile_load(rv, V, p.ld_qkv, (t + 1) * KT, S);
+      bf16_t* nx = smem + (cur ^ 1) * 2 * KT * HD;
+      tile_dma(K, p.ld_qkv, (t + 1) * KT, S, dv, nx, wid);
+      tile_dma(V, p.ld_qkv, (t + 1) * KT, S, dv, nx + KT * HD, wid);
     }
     const bf16_t* lk = smem + cur * 2 * KT * HD;
     const bf16_t* lv = lk + KT * HD;
@@ -255,12 +293,8 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(AttnArgs p) {
           for (int dt = 0; dt < 2; ++dt) o[dt] = MFMA32(tr_frag(lv, kb * 32, ss, dt * 32, lane), pb, o[dt]);
         }
     }
-    if (more) {
-      bf16_t* nx = smem + (cur ^ 1) * 2 * KT * HD;
-      tile_store(rk, nx);
-      tile_store(rv, nx + KT * HD);
-    }
-    __syncthreads();
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's DMA of tile t+1 landed
+    __syncthreads();  // ... every wave's, and stage cur is free for tile t+2
   }
 
   if (q < S) {
@@ -493,19 +527,24 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(AttnArgs p) {
 
   const int kend = p.causal ? min(S, qb * QB + QB) : S;
   const int ntiles = (kend + KT - 1) / KT;
-  uint4 rk[2], rv[2];
-  tile_load(rk, K, p.ld_qkv, 0, S);
-  tile_load(rv, V, p.ld_qkv, 0, S);
-  tile_store(rk, smem);
-  tile_store(rv, smem + KT * HD);
+  // K/V tiles stream into the LDS double buffer by DMA: tile t+1 is issued at the top of
+  // iteration t into the stage iteration t-1 read (released by its closing barrier), and
+  // lands under this iteration's MFMAs; no staging registers (16 VGPRs) as the
+  // register-staged copy needed.
+  int dv[2];
+  dma_voff(dv, p.ld_qkv, wid, lane);
+  tile_dma(K, p.ld_qkv, 0, S, dv, smem, wid);
+  tile_dma(V, p.ld_qkv, 0, S, dv, smem + KT * HD, wid);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
 
   for (int t = 0; t < ntiles; ++t) {
     const int cur = t & 1;
     const bool more = t + 1 < ntiles;
     if (more) {
-      tile_load(rk, K, p.ld_qkv, (t + 1) * KT, S);
-      tile_load(rv, V, p.ld_qkv, (t + 1) * KT, S);
+      bf16_t* nx = smem + (cur ^ 1) * 2 * KT * HD;
+      tile_dma(K, p.ld_qkv, (t + 1) * KT, S, dv, nx, wid);
+      tile_dma(V, p.ld_qkv, (t + 1) * KT, S, dv, nx + KT * HD, wid);
     }
     const bf16_t* lk = smem + cur * 2 * KT * HD;
     const bf16_t* lv = lk + KT * HD;
@@ -545,12 +584,8 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(AttnArgs p) {
         }
       }
     }
-    if (more) {
-      bf16_t* nx = smem + (cur ^ 1) * 2 * KT * HD;
-      tile_store(rk, nx);
-      tile_store(rv, nx + KT * HD);
-    }
-    __syncthreads();
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's DMA of tile t+1 landed
+    __syncthreads();  // ... every wave's, and stage cur is free for tile t+2
   }
 
   if (q < S) {
