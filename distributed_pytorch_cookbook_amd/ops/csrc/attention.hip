@@ -384,11 +384,15 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_kernel(AttnArgs p) {
   const int qt_begin = p.causal ? (kb * QB) / KT : 0;
   const int nqt = (S + KT - 1) / KT;
 
-  uint4 rq[2], rd[2];
+  // Q / dO tiles by LDS-DMA (as the forward's K / V); the per-query (lse, delta) pairs still
+  // go through two registers of the first 64 threads
+  int vq[2], vd[2];
+  dma_voff(vq, p.ld_qkv, wid, lane);
+  dma_voff(vd, p.ld_o, wid, lane);
   float rl = 0.f, rdl = 0.f;
-  auto load_rows = [&](int qt) {
-    tile_load(rq, Q, p.ld_qkv, qt * KT, S);
-    tile_load(rd, dO, p.ld_o, qt * KT, S);
+  auto load_rows = [&](int qt, int stg) {
+    tile_dma(Q, p.ld_qkv, qt * KT, S, vq, smem + stg * 2 * KT * HD, wid);
+    tile_dma(dO, p.ld_o, qt * KT, S, vd, smem + stg * 2 * KT * HD + KT * HD, wid);
     if (threadIdx.x < KT) {
       const int qq = qt * KT + threadIdx.x;
       rl = qq < S ? lse[qq] * LOG2E : INFINITY;
@@ -396,17 +400,16 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_kernel(AttnArgs p) {
     }
   };
   auto store_rows = [&](int stg) {
-    tile_store(rq, smem + stg * 2 * KT * HD);
-    tile_store(rd, smem + stg * 2 * KT * HD + KT * HD);
     if (threadIdx.x < KT) { srow[stg][0][threadIdx.x] = rl; srow[stg][1][threadIdx.x] = rdl; }
   };
-  if (qt_begin < nqt) { load_rows(qt_begin); store_rows(0); }
+  if (qt_begin < nqt) { load_rows(qt_begin, 0); store_rows(0); }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
 
   for (int qt = qt_begin; qt < nqt; ++qt) {
     const int cur = (qt - qt_begin) & 1;
     const bool more = qt + 1 < nqt;
-    if (more) load_rows(qt + 1);
+    if (more) load_rows(qt + 1, cur ^ 1);
     const bf16_t* lq = smem + cur * 2 * KT * HD;
     const bf16_t* ld = lq + KT * HD;
     const int qt0 = qt * KT;
@@ -464,6 +467,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_kernel(AttnArgs p) {
       }
     }
     if (more) store_rows(cur ^ 1);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's DMA of tile qt+1 landed
     __syncthreads();
   }
 

@@ -2,7 +2,8 @@
 # A/B kernel-library builds on one box: for each bench/ab_*.so.bak (and the in-tree build,
 # "cur"), run the attention microbenches and a short bench.py.  The in-tree .so is restored.
 run_set() {
-  scripts/gpu_step.sh "60:${1}_f:python bench/attn_one.py --N 64 --iters 20" \
+  scripts/gpu_step.sh "200:${1}_t:python -u -m pytest tests/test_kernels_gpu.py -x -q --timeout 120 --timeout-method thread -k attention" \
+    "60:${1}_f:python bench/attn_one.py --N 64 --iters 20" \
     "60:${1}_b:python bench/attn_one.py --N 64 --iters 10 --bwd" \
     "150:${1}_bench:python -u bench.py --steps 10"
 }
