@@ -72,6 +72,34 @@ _BLAS_PLAIN = os.environ.get("DPC_BLAS_PLAIN", "1") == "1"
 _BLAS_MIN_FLOP = 2 ** 34  # below ~17 GFLOP the choice does not matter: keep dpc_gemm
 
 
+# hipBLASLt / rocBLAS solution choice for those plain products: PyTorch TunableOp tuned on
+# MI355X over the bench recipes (``scripts/tunableop.sh``), shipped as ``hipblaslt_tuned.csv``
+# and used read-only (no tuning at run time; shapes missing from it use the library default).
+# The file's validator lines pin torch / HIP / hipBLASLt / rocBLAS versions and gfx950, so on
+# any other stack TunableOp ignores it.  GPT-2 small B=64: +0.7 % tokens/s
+# (profiles/r1_v18_tunableop_ab.txt).  DPC_TUNABLEOP=0 disables.
+_TUNABLEOP_CSV = os.path.join(os.path.dirname(os.path.abspath(__file__)), "hipblaslt_tuned.csv")
+_tunableop_done = False
+
+
+def enable_vendor_tuning() -> bool:
+    """Turn on TunableOp with the shipped MI355X results (read-only).  Idempotent; a no-op
+    without a GPU, with DPC_TUNABLEOP=0, or when the environment already configures
+    TunableOp (e.g. a tuning run of scripts/tunableop.sh)."""
+    global _tunableop_done
+    if _tunableop_done:
+        return torch.cuda.tunable.is_enabled()
+    _tunableop_done = True
+    if (os.environ.get("DPC_TUNABLEOP", "1") != "1" or not torch.cuda.is_available()
+            or "PYTORCH_TUNABLEOP_ENABLED" in os.environ or not os.path.exists(_TUNABLEOP_CSV)):
+        return False
+    torch.cuda.tunable.enable(True)
+    torch.cuda.tunable.tuning_enable(False)
+    torch.cuda.tunable.record_untuned_enable(False)
+    torch.cuda.tunable.set_filename(_TUNABLEOP_CSV, insert_device_ordinal=False)
+    return bool(torch.cuda.tunable.read_file(_TUNABLEOP_CSV))
+
+
 def set_blas_plain(on: bool) -> None:
     global _BLAS_PLAIN
     _BLAS_PLAIN = bool(on)

@@ -36,6 +36,10 @@ def build_model(args, vocab_size: int, device) -> TransformerDecoderLM:
 
 def build_engine(recipe: str, model, info, args):
     compute_dtype = torch.float32 if args.disable_amp else None
+    if info.device.type == "cuda":
+        from .ops.gemm import enable_vendor_tuning
+
+        enable_vendor_tuning()  # tuned hipBLASLt solutions for the plain products (read-only)
     if recipe in ("single", "ddp"):
         from .engine.data_parallel import DataParallelEngine
 
