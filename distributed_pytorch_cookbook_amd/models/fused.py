@@ -119,6 +119,10 @@ class _EmbedFn(torch.autograd.Function):
         return None, None, None, None, None, None
 
 
+# DPC_FUSE_OUT_LN=0: out-projection with the bias + residual GEMM epilogue and a separate LN2
+_FUSE_OUT_LN = os.environ.get("DPC_FUSE_OUT_LN", "1") == "1"
+
+
 def _layer_forward(x, mask, layer, store, N, S, act, training, drops):
     """Decoder-layer forward on the store's compute weights (no store hooks).
 
@@ -133,13 +137,23 @@ def _layer_forward(x, mask, layer, store, N, S, act, training, drops):
     h1, mu1, rs1 = layernorm_fwd(x, w(layer.norm1.weight), w(layer.norm1.bias), LN_EPS, cdt)
     qkv = linear_fwd(h1, _qkv_weight(store, attn), out_dtype=cdt)
     o, lse = attention_fwd(qkv, N, S, H, hd, mask, causal=True)
-    if drop_attn is None:
-        x2 = linear_fwd(o, w(attn.to_out.weight), bias=w(attn.to_out.bias), residual=x,
-                        out_dtype=torch.float32)
+    if x.is_cuda and cdt == torch.bfloat16 and _FUSE_OUT_LN:
+        # out-projection as a plain product (hipBLASLt, bf16 out -- the reference's autocast
+        # Linear output dtype) and its bias / dropout / residual add fused into LN2, which
+        # writes the new f32 residual stream x2: the residual is read and written once,
+        # instead of by a memory-bound GEMM epilogue and again by LN2
+        yo = linear_fwd(o, w(attn.to_out.weight), out_dtype=cdt)
+        x2 = torch.empty(T, D, device=x.device, dtype=torch.float32)
+        h2, mu2, rs2 = layernorm_fwd(x, w(layer.norm2.weight), w(layer.norm2.bias), LN_EPS, cdt,
+                                     add=(yo, w(attn.to_out.bias), drop_attn), x_out=x2)
     else:
-        x2 = linear_fwd(o, w(attn.to_out.weight), bias=w(attn.to_out.bias), out_dtype=torch.float32)
-        dropout_residual(x2, x, drop_attn, out=x2)
-    h2, mu2, rs2 = layernorm_fwd(x2, w(layer.norm2.weight), w(layer.norm2.bias), LN_EPS, cdt)
+        if drop_attn is None:
+            x2 = linear_fwd(o, w(attn.to_out.weight), bias=w(attn.to_out.bias), residual=x,
+                            out_dtype=torch.float32)
+        else:
+            x2 = linear_fwd(o, w(attn.to_out.weight), bias=w(attn.to_out.bias), out_dtype=torch.float32)
+            dropout_residual(x2, x, drop_attn, out=x2)
+        h2, mu2, rs2 = layernorm_fwd(x2, w(layer.norm2.weight), w(layer.norm2.bias), LN_EPS, cdt)
     F4 = w(fc.up_proj.weight).shape[0]
     z1 = torch.empty(T, F4, device=x.device, dtype=cdt) if (training and act == ACT_GELU) else None
     uact = linear_fwd(h2, w(fc.up_proj.weight), bias=w(fc.up_proj.bias), act=act, aux_out=z1,

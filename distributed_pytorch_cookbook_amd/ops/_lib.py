@@ -59,6 +59,7 @@ class LNArgs(ctypes.Structure):
         ("gout", P), ("gsum", P), ("ld_gout", LL),
         ("drop_key", c_uint), ("drop_thresh", c_uint), ("drop_scale", c_float),
         ("dy_bf16", c_int),
+        ("add_y", P), ("add_bias", P), ("x_out", P), ("ld_add", LL), ("ld_xout", LL),
     ]
 
 

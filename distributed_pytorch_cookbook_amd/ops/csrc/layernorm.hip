@@ -38,6 +38,13 @@ struct LNArgs {
   unsigned drop_key, drop_thresh;
   float drop_scale;
   int dy_bf16;  // bwd: dy is bf16 (the input gradient of the next Linear, as autocast makes it)
+  // fwd, optional fused producer (the residual add of the projection feeding this LayerNorm):
+  // the normalised row is  xs = x + keep * (add_y + add_bias)  (add_y bf16, the plain GEMM's
+  // output; keep as in the backward's drop_factor), and xs is written to x_out (f32).
+  const void* add_y;
+  const float* add_bias;
+  float* x_out;
+  long long ld_add, ld_xout;
 };
 
 template <int NV>
@@ -49,11 +56,42 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(LNArgs p) {
   const int nv4 = p.D >> 2;
   float4 v[NV];
   float s = 0.f;
+  if (p.add_y) {
+    // all loads of the row first (x f32, y bf16, bias), then the fused residual add
+    const uint2* yr = reinterpret_cast<const uint2*>(static_cast<const bf16_t*>(p.add_y) + row * p.ld_add);
+    const float4* b4 = reinterpret_cast<const float4*>(p.add_bias);
+    uint2 yv[NV];
 #pragma unroll
-  for (int i = 0; i < NV; ++i) {
-    const int c = lane + i * 64;
-    v[i] = c < nv4 ? xr[c] : make_float4(0.f, 0.f, 0.f, 0.f);
-    s += v[i].x + v[i].y + v[i].z + v[i].w;
+    for (int i = 0; i < NV; ++i) {
+      const int c = lane + i * 64;
+      v[i] = c < nv4 ? xr[c] : make_float4(0.f, 0.f, 0.f, 0.f);
+      yv[i] = c < nv4 ? yr[c] : make_uint2(0u, 0u);
+    }
+    float4* xo = reinterpret_cast<float4*>(p.x_out + row * p.ld_xout);
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      const int c = lane + i * 64;
+      if (c < nv4) {
+        const float4 b = p.add_bias ? b4[c] : make_float4(0.f, 0.f, 0.f, 0.f);
+        float a[4] = {__uint_as_float(yv[i].x << 16) + b.x, __uint_as_float(yv[i].x & 0xffff0000u) + b.y,
+                      __uint_as_float(yv[i].y << 16) + b.z, __uint_as_float(yv[i].y & 0xffff0000u) + b.w};
+        if (p.drop_scale != 0.f) {
+          const uint32_t idx = (uint32_t)(row * p.D + 4 * c);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) a[e] *= drop_factor(idx + e, p.drop_key, p.drop_thresh, p.drop_scale);
+        }
+        v[i].x += a[0]; v[i].y += a[1]; v[i].z += a[2]; v[i].w += a[3];
+        xo[c] = v[i];
+      }
+      s += v[i].x + v[i].y + v[i].z + v[i].w;
+    }
+  } else {
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      const int c = lane + i * 64;
+      v[i] = c < nv4 ? xr[c] : make_float4(0.f, 0.f, 0.f, 0.f);
+      s += v[i].x + v[i].y + v[i].z + v[i].w;
+    }
   }
   const float mu = wave_sum(s) / p.D;
   float ss = 0.f;

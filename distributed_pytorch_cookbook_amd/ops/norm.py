@@ -18,10 +18,26 @@ def _use_hip(x: torch.Tensor, y_dtype: torch.dtype) -> bool:
 
 
 def layernorm_fwd(x: torch.Tensor, gamma: torch.Tensor, beta: torch.Tensor, eps: float = 1e-5,
-                  out_dtype: torch.dtype = torch.bfloat16, out: torch.Tensor | None = None):
-    """x [T, D] f32 -> (y [T, D] out_dtype, mean [T], rstd [T])."""
+                  out_dtype: torch.dtype = torch.bfloat16, out: torch.Tensor | None = None,
+                  add=None, x_out: torch.Tensor | None = None):
+    """x [T, D] f32 -> (y [T, D] out_dtype, mean [T], rstd [T]).
+
+    ``add=(y, bias, drop)`` fuses the residual add of the projection that feeds this
+    LayerNorm: the row normalised is ``xs = x + drop(y + bias)`` (y the plain GEMM output,
+    bf16 on the HIP path; drop a ``dropout.Drop`` or None), and ``xs`` is written to
+    ``x_out`` (f32 [T, D]) -- the new residual stream, read once and written once instead of
+    the GEMM epilogue writing it and this kernel reading it back."""
     T, D = x.shape
+    if add is not None and x_out is None:
+        raise ValueError("layernorm_fwd: add= needs x_out")
     if not _use_hip(x, out_dtype):
+        if add is not None:
+            y_add, b_add, drop = add
+            a = y_add.float() + (b_add.float() if b_add is not None else 0.0)
+            if drop is not None:
+                a = a * keep_mask(drop, T, D, x.device)
+            x_out.copy_(x.float() + a)
+            x = x_out
         xf = x.float()
         mean = xf.mean(-1)
         var = xf.var(-1, unbiased=False)
@@ -44,6 +60,19 @@ def layernorm_fwd(x: torch.Tensor, gamma: torch.Tensor, beta: torch.Tensor, eps:
         mean=mean.data_ptr(), rstd=rstd.data_ptr(), ldx=x.stride(0), ldy=out.stride(0),
         T=T, D=D, eps=float(eps), y_f32=int(out.dtype == torch.float32),
     )
+    if add is not None:
+        y_add, b_add, drop = add
+        if (y_add.dtype != torch.bfloat16 or y_add.stride(1) != 1 or y_add.stride(0) % 4
+                or x_out.dtype != torch.float32 or x_out.stride(1) != 1 or x_out.stride(0) % 4
+                or tuple(y_add.shape) != (T, D) or tuple(x_out.shape) != (T, D)
+                or (b_add is not None and (b_add.dtype != torch.float32 or not b_add.is_contiguous()))):
+            raise ValueError("layernorm_fwd: add= needs bf16 y [T, D], f32 bias [D], f32 x_out [T, D]")
+        args.add_y, args.add_bias, args.x_out = y_add.data_ptr(), _lib.ptr(b_add), x_out.data_ptr()
+        args.ld_add, args.ld_xout = y_add.stride(0), x_out.stride(0)
+        if drop is not None:
+            if T * D >= 2 ** 32:
+                raise ValueError("layernorm_fwd: dropout needs T * D < 2^32")
+            args.drop_key, args.drop_thresh, args.drop_scale = drop.key, drop.thresh, drop.scale
     _lib.call("dpc_layernorm_fwd", args, x.device)
     return out, mean, rstd
 

@@ -436,3 +436,27 @@ def test_plain_gemm_vendor_path_matches_kernel(out_dtype, b_kmaj):
             set_blas_plain(True)
     ref = 2.0 * 0.37 * (a.float() @ (b.float().t() if b_kmaj else b.float()))
     assert rel_err(outs[0], ref) < 1e-2 and rel_err(outs[1], ref) < 1e-2
+
+
+@pytest.mark.parametrize("D,p_drop", [(768, 0.0), (1600, 0.0), (768, 0.1)])
+def test_layernorm_fwd_fused_residual_add(D, p_drop):
+    """LN forward with the projection's bias + dropout + residual add fused in:
+    xs = x + keep * (y + b) written to x_out, LN(xs) vs the torch expression."""
+    from distributed_pytorch_cookbook_amd.ops.dropout import DropSpec, keep_mask
+    torch.manual_seed(13)
+    T = 1000
+    x = torch.randn(T, D, device=dev)
+    y = torch.randn(T, D, device=dev).bfloat16()
+    b = torch.randn(D, device=dev)
+    g, be = torch.randn(D, device=dev), torch.randn(D, device=dev)
+    drop = DropSpec.make(p_drop, seed=5, site=3) if p_drop else None
+    xs = torch.empty(T, D, device=dev)
+    h, mu, rs = layernorm_fwd(x, g, be, 1e-5, torch.bfloat16, add=(y, b, drop), x_out=xs)
+    a = y.float() + b
+    if drop is not None:
+        a = a * keep_mask(drop, T, D, dev)
+    xs_r = x + a
+    assert rel_err(xs, xs_r) < 1e-6
+    h_r = torch.nn.functional.layer_norm(xs_r, (D,), g, be, 1e-5)
+    assert rel_err(h, h_r) < 1e-2
+    assert rel_err(mu, xs_r.mean(-1)) < 1e-5
