@@ -204,6 +204,44 @@ class _LayerFn(torch.autograd.Function):
         return dx, None, None, None, None, None, None, None, None, None
 
 
+# Weight gradients of a layer run on a side HIP stream, concurrently with the input-gradient
+# chain (bias/act backward -> dgrad -> LayerNorm backward -> attention backward) they do not
+# feed: each wgrad waits for the main stream (its dY is ready), the main stream joins the side
+# stream once at the end of the layer's backward, before the store's post_backward hook (DDP
+# bucket all-reduce / FSDP reduce-scatter) reads the gradients.  Both run inside the HIP-graph
+# capture as a fork / join.  Off by default (DPC_WGRAD_STREAM=1 turns it on): on one MI355X
+# the GEMMs already fill the chip, and GPT-2 small B=64 measured 822.5 / 822.8K tok/s with
+# the side stream against 825.2 / 824.2K without; FSDP GPT-2 XL 68.6K vs 68.8K
+# (profiles/r1_v19_wgrad_stream_ab.txt).
+_WGRAD_STREAM = os.environ.get("DPC_WGRAD_STREAM", "0") == "1"
+_side_streams: dict = {}
+
+
+class _SideWork:
+    def __init__(self, device: torch.device):
+        self.on = _WGRAD_STREAM and device.type == "cuda"
+        self.stream = None
+        if self.on:
+            key = torch.cuda.current_stream(device).cuda_stream
+            if key not in _side_streams:
+                _side_streams[key] = torch.cuda.Stream(device=device)
+            self.stream = _side_streams[key]
+
+    def run(self, fn, *tensors):
+        if not self.on:
+            fn()
+            return
+        self.stream.wait_stream(torch.cuda.current_stream(self.stream.device))
+        with torch.cuda.stream(self.stream):
+            fn()
+        for t in tensors:  # temporaries freed by the main stream: not reused before the side reads
+            t.record_stream(self.stream)
+
+    def join(self):
+        if self.on:
+            torch.cuda.current_stream(self.stream.device).wait_stream(self.stream)
+
+
 def _layer_backward(dx3, x, mask, saved, layer, store, N, S, H, hd, act, drops):
     """Hand-written backward of ``_layer_forward``; weight grads go into the store."""
     (h1, mu1, rs1, qkv, o, lse, x2, h2, mu2, rs2, zup, uact, z2) = saved
@@ -213,30 +251,36 @@ def _layer_backward(dx3, x, mask, saved, layer, store, N, S, H, hd, act, drops):
     drop_attn, drop_ffn = drops
     dx = dx3.contiguous()  # becomes dx2 then dx (in place)
     # FFN down projection: x3 = x2 + drop(act(z2)), z2 = u W2^T + b2
+    side = _SideWork(dx.device)
     dz2 = bias_act_bwd(dx, z2, act, g(fc.down_proj.bias), out_dtype=cdt, drop=drop_ffn)
-    linear_wgrad(dz2, uact, out=g(fc.down_proj.weight))
+    side.run(lambda: linear_wgrad(dz2, uact, out=g(fc.down_proj.weight)), dz2, uact)
     # up projection gradient with act' fused (relu' from its output, gelu' from z1)
     dz1 = linear_dgrad(dz2, w(fc.down_proj.weight), act_bwd=act, aux_in=zup, out_dtype=cdt,
                        colsum=g(fc.up_proj.bias))
-    linear_wgrad(dz1, h2, out=g(fc.up_proj.weight))
+    side.run(lambda: linear_wgrad(dz1, h2, out=g(fc.up_proj.weight)), dz1, h2)
     dh2 = linear_dgrad(dz1, w(fc.up_proj.weight), out_dtype=_dh_dtype(cdt))
     # LN2 backward with the attention output projection's bias/dropout backward fused in:
     # x2 = x + drop(o Wo^T + bo)  ->  dYo = bf16(dx2 * keep), dbo += colsum
     dyo = torch.empty(dx.shape, device=dx.device, dtype=cdt)
     layernorm_bwd(dh2, x2, mu2, rs2, w(layer.norm2.weight), dx, g(layer.norm2.weight),
                   g(layer.norm2.bias), gout=dyo, gsum=g(attn.to_out.bias), drop=drop_attn)
-    linear_wgrad(dyo, o, out=g(attn.to_out.weight))
+    side.run(lambda: linear_wgrad(dyo, o, out=g(attn.to_out.weight)), dyo, o)
     do = linear_dgrad(dyo, w(attn.to_out.weight), out_dtype=cdt)
     dqkv = attention_bwd(do, qkv, o, lse, N, S, H, hd, mask, causal=True)
     gqkv, split = _qkv_grad(store, attn)
-    linear_wgrad(dqkv, h1, out=gqkv)
-    if split is not None:
-        n = split[0].shape[0]
-        for i, gi in enumerate(split):
-            gi.add_(gqkv[i * n:(i + 1) * n])
+
+    def qkv_wgrad():
+        linear_wgrad(dqkv, h1, out=gqkv)
+        if split is not None:
+            n = split[0].shape[0]
+            for i, gi in enumerate(split):
+                gi.add_(gqkv[i * n:(i + 1) * n])
+
+    side.run(qkv_wgrad, dqkv, h1, gqkv)
     dh1 = linear_dgrad(dqkv, _qkv_weight(store, attn), out_dtype=_dh_dtype(cdt))
     layernorm_bwd(dh1, x, mu1, rs1, w(layer.norm1.weight), dx, g(layer.norm1.weight),
                   g(layer.norm1.bias))
+    side.join()
     return dx
 
 
