@@ -128,3 +128,24 @@ def test_chunked_head_matches_whole_batch(monkeypatch, want_correct):
         assert res[0][1] == res[1][1]
     else:
         assert torch.allclose(res[0][2], res[1][2], rtol=1e-3, atol=1e-6)
+
+
+def test_side_stream_wgrad_matches_single_stream(monkeypatch):
+    """DPC_WGRAD_STREAM: weight gradients on a side stream give the same gradients as the
+    single-stream backward (same kernels; split-K f32 atomics make the last bits run-dependent)."""
+    from distributed_pytorch_cookbook_amd.models import fused
+    N, S, V = 3, 129, 1000
+    g = torch.Generator().manual_seed(2)
+    ids = torch.randint(0, V, (N, S), generator=g).cuda()
+    tg = torch.randint(0, V, (N, S), generator=g).cuda()
+    pos = torch.arange(S).repeat(N, 1).cuda()
+    grads = []
+    for on in (False, True):
+        monkeypatch.setattr(fused, "_WGRAD_STREAM", on)
+        m = make("gelu").cuda()
+        store = LocalStore(m, "cuda")
+        store.zero_grad()
+        m(ids, pos, None, targets=tg).loss.backward()
+        torch.cuda.synchronize()
+        grads.append(store.grads.clone())
+    assert ((grads[0] - grads[1]).norm() / grads[0].norm()).item() < 1e-5
