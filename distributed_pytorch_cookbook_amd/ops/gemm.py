@@ -134,7 +134,7 @@ def _blas_plain(a, b, a_kmaj, b_kmaj, out, M, N, K, alpha, alpha_t) -> bool:
 _TUNE_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "gemm_tuned.json")
 _TUNE = os.environ.get("DPC_GEMM_TUNE", "0") == "1"
 _USE_TABLE = os.environ.get("DPC_GEMM_TABLE", "1") == "1"
-_CANDIDATES = (0, 2, 4, 6, 10, 12)  # 0 = the dispatcher policy
+_CANDIDATES = (0, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12)  # 0 = the dispatcher policy
 _TUNE_MAX_OUT_BYTES = 1 << 30
 
 
