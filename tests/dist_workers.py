@@ -128,3 +128,21 @@ def worker_scaled(rank, world, out, kind):
     sd = eng.full_state_dict()
     if rank == 0:
         torch.save({k: v.clone() for k, v in sd.items()}, out)
+
+
+def worker_coll_mismatch(rank, world):
+    """DPC_COLL_CHECK: a rank issuing a differently shaped collective is caught by the
+    fingerprint exchange (on every rank) instead of hanging or corrupting the reduction."""
+    import os
+
+    os.environ["DPC_COLL_CHECK"] = "1"
+    from distributed_pytorch_cookbook_amd.parallel import comm
+
+    comm.init_dist(force_cpu=True)
+    comm.all_reduce(torch.ones(4))  # matched: passes
+    try:
+        comm.all_reduce(torch.ones(4 + rank))  # rank 1 differs
+    except RuntimeError as exc:
+        assert "collective mismatch" in str(exc), exc
+        return
+    raise AssertionError("mismatched collective was not detected")

@@ -1,0 +1,46 @@
+"""Auxiliary subsystems on CPU: collective fingerprints, fault injection,
+checkpoint layout and --resume."""
+import os
+import subprocess
+import sys
+
+import torch
+
+from dist_helpers import ROOT, run_workers
+from dist_workers import worker_coll_mismatch
+
+TINY = ["--synthetic_data", "--batch_size", "4", "--epochs", "1", "--sequence_length", "32",
+        "--dim", "32", "--heads", "2", "--head_dim", "16", "--num_layers", "2",
+        "--train_samples", "64", "--val_samples", "8", "--num_workers", "0", "--no_generate", "--cpu"]
+
+
+def test_collective_fingerprint_catches_mismatch():
+    run_workers(worker_coll_mismatch, 2)
+
+
+def test_fault_injection_then_resume(tmp_path):
+    """DPC_FAULT_STEP kills the run mid-epoch; --save_every left a checkpoint behind, and
+    --resume latest restores weights, AdamW moments and the step count from it."""
+    ck = tmp_path / "ckpt"
+    env = dict(os.environ, DPC_FAULT_STEP="5", PYTHONPATH=ROOT)
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "main-single.py"), *TINY, "--max_steps", "8",
+                        "--save_every", "2", "--checkpoint_dir", str(ck)],
+                       cwd=tmp_path, env=env, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 13, (r.returncode, r.stdout[-2000:], r.stderr[-2000:])
+    assert "[fault-injection]" in r.stdout
+
+    from distributed_pytorch_cookbook_amd.recipes import run
+    from distributed_pytorch_cookbook_amd.utils.checkpoint import latest_checkpoint, load_model_state, load_train_state
+
+    path = latest_checkpoint(str(ck))
+    assert path is not None
+    sd = load_model_state(path)
+    assert len(sd) == 13 * 2 + 5 and not any(k.startswith(("module.", "_orig_mod.")) for k in sd)
+    st = load_train_state(path)
+    assert st is not None and int(st["optimizer"]["step"]) == 4  # saved at steps 2 and 4
+    assert st["optimizer"]["exp_avg"].abs().sum() > 0 and "rng" in st
+    trainer, _ = run("single", [*TINY, "--max_steps", "2", "--resume", "latest", "--checkpoint_dir", str(ck),
+                                "--no_save"])
+    assert trainer.engine.step_count == 4 + 2
+    w = dict(trainer.engine.lm().state_dict())["lm_head.weight"]
+    assert torch.isfinite(w).all()
