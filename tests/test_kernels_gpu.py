@@ -180,6 +180,25 @@ def test_attention_fwd_bwd(S, with_pad):
         assert rel_err(dqkv[:, sl], g[:, sl]) < 2e-2, name
 
 
+@pytest.mark.parametrize("S", [4096, 8191])
+def test_attention_long_context(S):
+    """O(S) flash attention at 4-8x GPT-2's context, vs the f32 O(S^2) reference."""
+    torch.manual_seed(5)
+    N, H, hd = 1, 2, 64
+    qkv = torch.randn(N * S, 3 * H * hd, device=dev).bfloat16()
+    o, lse = attention_fwd(qkv, N, S, H, hd, None, causal=True)
+    o_r, lse_r = attention_ref(qkv, N, S, H, hd, None, causal=True)
+    assert rel_err(o, o_r) < 1e-2
+    assert torch.allclose(lse, lse_r, atol=2e-2, rtol=1e-3)
+    do = torch.randn_like(o)
+    dqkv = attention_bwd(do, qkv, o, lse, N, S, H, hd, None, causal=True)
+    x = qkv.float().requires_grad_(True)
+    (g,) = torch.autograd.grad(attention_ref(x, N, S, H, hd, None, causal=True)[0], x, do.float())
+    for i, name in enumerate("qkv"):
+        sl = slice(i * H * hd, (i + 1) * H * hd)
+        assert rel_err(dqkv[:, sl], g[:, sl]) < 2e-2, name
+
+
 def test_attention_head_dim_32_padded():
     torch.manual_seed(3)
     N, S, H, hd = 2, 100, 4, 32

@@ -1,5 +1,6 @@
 """End-to-end fused model on the GPU (bf16 kernels) vs the f32 CPU reference."""
 import copy
+import math
 
 import pytest
 import torch
@@ -79,6 +80,19 @@ def test_gpt2_small_step_and_generate():
     assert 10.0 < l0 < 12.0 and l1 < l0
     s = generate(m, "One day, ", ByteTokenizer(), torch.device("cuda"), max_new_tokens=4)
     assert s.startswith("One day, ")
+
+
+def test_long_context_train_step():
+    """a full fused train step at S = 8191 (8x GPT-2's context) stays finite and learns."""
+    torch.manual_seed(0)
+    S = 8191
+    with torch.device("cuda"):
+        m = TransformerDecoderLM(256, 64, 4, 2, 50257, S + 1, activation="gelu")
+    eng = DataParallelEngine(m, "cuda", lr=1e-3)
+    ids = torch.randint(0, 50257, (1, S + 1), device="cuda")
+    b = dict(input_ids=ids[:, :-1], position_ids=torch.arange(S, device="cuda").expand(1, -1), mask=None)
+    losses = [eng.train_step(b, ids[:, 1:]).item() for _ in range(3)]
+    assert all(math.isfinite(l) for l in losses) and losses[-1] < losses[0], losses
 
 
 def test_main_single_recipe_gpu(tmp_path, monkeypatch):
