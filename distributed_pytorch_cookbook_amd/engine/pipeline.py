@@ -228,7 +228,7 @@ class PipelineEngine(Engine):
 
         @torch.no_grad()
         def forward(input_ids, position_ids, mask=None):
-            from ..models.fused import head_logits
+            from ..models.fused import head_logits, last_rows
 
             N, S = input_ids.shape
             shape = (N * S, eng.D)
@@ -240,8 +240,7 @@ class PipelineEngine(Engine):
             V = eng.model.vocab_size
             tok = torch.zeros(1, dtype=torch.int64, device=eng.device)
             if eng.last:
-                logits = head_logits(eng.model, x, st).reshape(N, S, -1)
-                tok[0] = logits[0, -1].argmax()
+                tok[0] = head_logits(eng.model, last_rows(x, N, S), st)[0].argmax()
             else:
                 eng.p2p.exchange(send_next=x)
             if eng.pp > 1:

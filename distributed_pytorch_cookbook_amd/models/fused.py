@@ -21,6 +21,7 @@ Q, K, V weights are adjacent in the flat layout, so ``[Wq; Wk; Wv]`` is a view.
 """
 from __future__ import annotations
 
+import math
 import os
 from dataclasses import dataclass
 from typing import Optional
@@ -123,10 +124,12 @@ class _EmbedFn(torch.autograd.Function):
 _FUSE_OUT_LN = os.environ.get("DPC_FUSE_OUT_LN", "1") == "1"
 
 
-def _layer_forward(x, mask, layer, store, N, S, act, training, drops):
+def _layer_forward(x, mask, layer, store, N, S, act, training, drops, attend=None):
     """Decoder-layer forward on the store's compute weights (no store hooks).
 
     Returns ``(x3, saved)``; ``saved`` holds what the backward needs when ``training``.
+    ``attend(qkv) -> (o, lse)`` replaces the causal self-attention over these S tokens
+    (the KV-cache decode attends over the cached keys instead).
     """
     drop_attn, drop_ffn = drops
     attn, fc = layer.attn, layer.fc
@@ -136,7 +139,7 @@ def _layer_forward(x, mask, layer, store, N, S, act, training, drops):
     cdt = store.compute_dtype
     h1, mu1, rs1 = layernorm_fwd(x, w(layer.norm1.weight), w(layer.norm1.bias), LN_EPS, cdt)
     qkv = linear_fwd(h1, _qkv_weight(store, attn), out_dtype=cdt)
-    o, lse = attention_fwd(qkv, N, S, H, hd, mask, causal=True)
+    o, lse = attention_fwd(qkv, N, S, H, hd, mask, causal=True) if attend is None else attend(qkv)
     if x.is_cuda and cdt == torch.bfloat16 and _FUSE_OUT_LN:
         # out-projection as a plain product (hipBLASLt, bf16 out -- the reference's autocast
         # Linear output dtype) and its bias / dropout / residual add fused into LN2, which
@@ -397,8 +400,13 @@ def run_head(model, store, x, targets, training, want_correct):
                          model._head_unit_id, training, want_correct)
 
 
+def last_rows(x, N, S):
+    """[N*S, D] -> [N, D]: the last position of every sequence (all a greedy decode step needs)."""
+    return x.view(N, S, -1)[:, -1].contiguous()
+
+
 def fused_lm_forward(model, input_ids, position_ids, mask=None, targets=None, want_correct=False,
-                     dropout_seed=None):
+                     dropout_seed=None, last_only=False):
     store = ensure_store(model)
     N, S = input_ids.shape
     training = torch.is_grad_enabled()
@@ -407,6 +415,135 @@ def fused_lm_forward(model, input_ids, position_ids, mask=None, targets=None, wa
     x = run_embeddings(model, store, input_ids, position_ids, training)
     x = run_layers(model, store, x, mask, N, S, model.decoder.layers, training, dropout_seed)
     if targets is None:
+        if last_only:  # decode: LM head on the last position only ([N, 1, V]; T x fewer FLOPs)
+            return head_logits(model, last_rows(x, N, S), store).reshape(N, 1, -1)
         return head_logits(model, x, store).reshape(N, S, -1)
     loss, n_valid, n_correct = run_head(model, store, x, targets, training, want_correct)
     return LMOutput(loss, n_valid, n_correct if want_correct else None)
+
+
+class KVCache:
+    """Keys / values of every layer for the tokens decoded so far: ``[N, S_max, H*hd]`` each
+    in the compute dtype (GPT-2 XL at S_max = 1024: 2 x 48 x 1024 x 1600 x 2 B = 315 MB per
+    sequence)."""
+
+    def __init__(self, model, N, S_max, device, dtype):
+        self.k, self.v = [], []
+        for layer in model.decoder.layers:
+            E = layer.attn.heads * layer.attn.head_dim
+            # zeroed: the graphed step reads the whole capacity (masked, but 0 * NaN = NaN)
+            self.k.append(torch.zeros(N, S_max, E, device=device, dtype=dtype))
+            self.v.append(torch.zeros(N, S_max, E, device=device, dtype=dtype))
+        self.len = 0
+        self.capacity = S_max
+        self.len_t = torch.zeros(1, device=device, dtype=torch.int64)  # device copy for the graph
+
+
+def _cached_attention(qkv, cache, li, N, n, H, hd):
+    """Append the n new tokens' K/V to layer li's cache and attend to every cached key.
+
+    Prefill (empty cache) is the flash-attention kernel over the n tokens; a decode step is
+    n queries against ``start + n`` keys -- a memory-bound read of the cache (GEMV-shaped,
+    no tiles to fill), done as two batched products in f32."""
+    E = H * hd
+    start = cache.len
+    L = start + n
+    q3 = qkv.view(N, n, 3, E)
+    cache.k[li][:, start:L] = q3[:, :, 1]
+    cache.v[li][:, start:L] = q3[:, :, 2]
+    if start == 0:
+        return attention_fwd(qkv, N, n, H, hd, None, causal=True)
+    q = q3[:, :, 0].float().reshape(N, n, H, hd).transpose(1, 2)             # [N, H, n, hd]
+    k = cache.k[li][:, :L].float().reshape(N, L, H, hd).transpose(1, 2)     # [N, H, L, hd]
+    v = cache.v[li][:, :L].float().reshape(N, L, H, hd).transpose(1, 2)
+    sc = (q @ k.transpose(-1, -2)) * (1.0 / math.sqrt(hd))                  # [N, H, n, L]
+    if n > 1:  # causal inside the new block: query i sees keys < start + i + 1
+        qi = torch.arange(n, device=qkv.device)[:, None] + start
+        sc = sc.masked_fill(torch.arange(L, device=qkv.device)[None, :] > qi, float("-inf"))
+    o = torch.softmax(sc, -1) @ v                                            # [N, H, n, hd]
+    return o.transpose(1, 2).reshape(N * n, E).to(qkv.dtype), None
+
+
+def kv_decode_forward(model, input_ids, position_ids, cache):
+    """Incremental forward for greedy decoding: runs only the new tokens (the whole prompt
+    on the first call, then one token per call) through the layers, extends ``cache`` and
+    returns the logits of the last new token, ``[N, 1, V]``.  Same kernels as the training
+    forward (LayerNorm, QKV / FFN GEMMs with fused epilogues, the LM head); the reference
+    recomputes the whole sequence for every token (``/root/reference/utils.py:57-65``)."""
+    store = ensure_store(model)
+    N, n = input_ids.shape
+    if cache.len + n > cache.capacity:
+        raise ValueError(f"KV cache full ({cache.len} + {n} > {cache.capacity})")
+    act = act_code(model.activation)
+    x = run_embeddings(model, store, input_ids, position_ids, False)
+    for li, layer in enumerate(model.decoder.layers):
+        H, hd = layer.attn.heads, layer.attn.head_dim
+        u = layer._unit_id
+        store.pre_forward(u)
+        x, _ = _layer_forward(x, None, layer, store, N, n, act, False, (None, None),
+                              attend=lambda qkv, li=li, H=H, hd=hd: _cached_attention(qkv, cache, li, N, n, H, hd))
+        store.post_forward(u, False)
+    cache.len += n
+    cache.len_t.fill_(cache.len)
+    return head_logits(model, last_rows(x, N, n), store).reshape(N, 1, -1)
+
+
+def _static_attention(qkv, cache, li, N, H, hd):
+    """One query per sequence against the cache's whole capacity, keys at or past the
+    device-side length masked: no shape depends on the length, so the step can be graphed."""
+    E, Smax = H * hd, cache.capacity
+    q3 = qkv.view(N, 1, 3, E)
+    cache.k[li].index_copy_(1, cache.len_t, q3[:, :, 1])
+    cache.v[li].index_copy_(1, cache.len_t, q3[:, :, 2])
+    q = q3[:, 0, 0].float().reshape(N, H, 1, hd)
+    k = cache.k[li].float().reshape(N, Smax, H, hd).transpose(1, 2)
+    v = cache.v[li].float().reshape(N, Smax, H, hd).transpose(1, 2)
+    sc = (q @ k.transpose(-1, -2)) * (1.0 / math.sqrt(hd))                  # [N, H, 1, Smax]
+    sc = sc.masked_fill(torch.arange(Smax, device=qkv.device) > cache.len_t, float("-inf"))
+    o = torch.softmax(sc, -1) @ v
+    return o.reshape(N, E).to(qkv.dtype), None
+
+
+class GraphDecoder:
+    """The one-token decode step (embedding, every layer, LM head, cache append) captured
+    once as a HIP graph and replayed per token: a GPT-2 decode step is a few hundred small
+    launches, so eager decoding is launch-bound (measured in ``bench/generate.py``).  Needs
+    a non-sharded parameter store (single GPU / DDP); FSDP decodes eagerly."""
+
+    def __init__(self, model, cache):
+        self.model, self.cache = model, cache
+        self.store = ensure_store(model)
+        N = cache.k[0].shape[0]
+        self.tok = torch.zeros(N, 1, device=cache.len_t.device, dtype=torch.int64)
+        self.graph = None
+        self.out = None
+
+    def _step(self):
+        model, store, cache = self.model, self.store, self.cache
+        N = self.tok.shape[0]
+        act = act_code(model.activation)
+        x = run_embeddings(model, store, self.tok, cache.len_t.expand(N, 1), False)
+        for li, layer in enumerate(model.decoder.layers):
+            H, hd = layer.attn.heads, layer.attn.head_dim
+            x, _ = _layer_forward(x, None, layer, store, N, 1, act, False, (None, None),
+                                  attend=lambda qkv, li=li, H=H, hd=hd: _static_attention(qkv, cache, li, N, H, hd))
+        cache.len_t.add_(1)
+        return head_logits(model, x, store).reshape(N, 1, -1)
+
+    def step(self, tok):
+        """Append ``tok`` [N, 1] at the cache's current length; logits [N, 1, V] (a view of the
+        graph's output buffer, overwritten by the next step)."""
+        cache = self.cache
+        if cache.len + 1 > cache.capacity:
+            raise ValueError(f"KV cache full ({cache.len} + 1 > {cache.capacity})")
+        self.tok.copy_(tok)
+        if self.graph is None:
+            self._step()                 # eager warm-up (lazy library init), then undo it
+            cache.len_t.sub_(1)
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                self.out = self._step()
+            self.graph = g
+        self.graph.replay()
+        cache.len += 1
+        return self.out

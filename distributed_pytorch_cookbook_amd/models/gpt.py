@@ -244,10 +244,30 @@ class TransformerDecoderLM(nn.Module):
                     layer.attn.dropout.spec = layer.fc.dropout.spec = None
 
     def forward(self, input_ids, position_ids, mask=None, targets=None, want_correct=False,
-                dropout_seed=None):
+                dropout_seed=None, last_only=False):
         from .fused import fused_lm_forward
 
-        return fused_lm_forward(self, input_ids, position_ids, mask, targets, want_correct, dropout_seed)
+        return fused_lm_forward(self, input_ids, position_ids, mask, targets, want_correct, dropout_seed,
+                                last_only)
+
+    def new_kv_cache(self, batch_size: int, max_len: int):
+        from .fused import KVCache, ensure_store
+
+        return KVCache(self, batch_size, max_len, next(self.parameters()).device,
+                       ensure_store(self).compute_dtype)
+
+    def decode(self, input_ids, position_ids, cache):
+        """Logits ``[N, 1, V]`` of the last of the new tokens, attending over ``cache`` (extended)."""
+        from .fused import kv_decode_forward
+
+        return kv_decode_forward(self, input_ids, position_ids, cache)
+
+    def graph_decoder(self, cache):
+        """HIP-graph one-token decode step over ``cache`` (None for a sharded store)."""
+        from ..parallel.store import LocalStore
+        from .fused import GraphDecoder, ensure_store
+
+        return GraphDecoder(self, cache) if isinstance(ensure_store(self), LocalStore) else None
 
 
 PRESETS = {

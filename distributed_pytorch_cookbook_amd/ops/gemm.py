@@ -348,8 +348,33 @@ def _gemm_ref(a, b, a_kmaj, b_kmaj, out, bias, act, act_bwd, aux_in, aux_out, re
 def linear_fwd(x, w, *, bias=None, act=None, residual=None, aux_out=None, out=None,
                out_dtype=torch.bfloat16):
     """y = act(x @ w^T + bias) (+ residual); x [M, K], w [N, K] (nn.Linear layout)."""
+    if (x.is_cuda and x.shape[0] <= _GEMV_ROWS and aux_out is None and x.dtype == torch.bfloat16
+            and w.dtype == torch.bfloat16):
+        return _linear_fwd_few_rows(x, w, bias, act_code(act), residual, out, out_dtype)
     return gemm(x, w, a_kmaj=True, b_kmaj=True, bias=bias, act=act, residual=residual,
                 aux_out=aux_out, out=out, out_dtype=out_dtype)
+
+
+# decode-shaped products (a handful of rows): the MFMA tile kernels would launch N / 256
+# workgroups on a 256-CU chip; the weight stream is the whole cost, so these go to the
+# library's GEMV-shaped kernels with the (tiny) epilogue as elementwise ops
+_GEMV_ROWS = 16
+
+
+def _linear_fwd_few_rows(x, w, bias, act, residual, out, out_dtype):
+    v = torch.mm(x, w.t()).float()
+    if bias is not None:
+        v += bias.float()
+    v = act_fwd_ref(v, act)
+    if residual is not None:
+        v += residual.float()
+    if out is None:
+        return v.to(out_dtype)
+    n = v.shape[1]
+    out[:, :n].copy_(v)
+    if out.shape[1] > n:
+        out[:, n:].zero_()
+    return out
 
 
 def linear_dgrad(dy, w, *, act_bwd=None, aux_in=None, out=None, out_dtype=torch.bfloat16,
