@@ -28,7 +28,7 @@ from typing import Optional
 
 import torch
 
-from ..ops.attention import attention_bwd, attention_fwd
+from ..ops.attention import DECODE_MAX_S, attention_bwd, attention_fwd, decode_attention
 from ..ops.elementwise import bias_act_bwd
 from ..ops.dropout import dropout_residual
 from ..ops.embedding import embedding_bwd, embedding_fwd
@@ -489,19 +489,10 @@ def kv_decode_forward(model, input_ids, position_ids, cache):
 
 
 def _static_attention(qkv, cache, li, N, H, hd):
-    """One query per sequence against the cache's whole capacity, keys at or past the
-    device-side length masked: no shape depends on the length, so the step can be graphed."""
-    E, Smax = H * hd, cache.capacity
-    q3 = qkv.view(N, 1, 3, E)
-    cache.k[li].index_copy_(1, cache.len_t, q3[:, :, 1])
-    cache.v[li].index_copy_(1, cache.len_t, q3[:, :, 2])
-    q = q3[:, 0, 0].float().reshape(N, H, 1, hd)
-    k = cache.k[li].float().reshape(N, Smax, H, hd).transpose(1, 2)
-    v = cache.v[li].float().reshape(N, Smax, H, hd).transpose(1, 2)
-    sc = (q @ k.transpose(-1, -2)) * (1.0 / math.sqrt(hd))                  # [N, H, 1, Smax]
-    sc = sc.masked_fill(torch.arange(Smax, device=qkv.device) > cache.len_t, float("-inf"))
-    o = torch.softmax(sc, -1) @ v
-    return o.reshape(N, E).to(qkv.dtype), None
+    """One query per sequence against the cache, the new key / value appended at the
+    device-side length by the decode kernel: no shape depends on the length, so the step
+    can be graphed."""
+    return decode_attention(qkv, cache.k[li], cache.v[li], cache.len_t, H, hd), None
 
 
 class GraphDecoder:

@@ -265,9 +265,12 @@ class TransformerDecoderLM(nn.Module):
     def graph_decoder(self, cache):
         """HIP-graph one-token decode step over ``cache`` (None for a sharded store)."""
         from ..parallel.store import LocalStore
+        from ..ops.attention import DECODE_MAX_S
         from .fused import GraphDecoder, ensure_store
 
-        return GraphDecoder(self, cache) if isinstance(ensure_store(self), LocalStore) else None
+        if not isinstance(ensure_store(self), LocalStore) or cache.capacity > DECODE_MAX_S:
+            return None
+        return GraphDecoder(self, cache)
 
 
 PRESETS = {

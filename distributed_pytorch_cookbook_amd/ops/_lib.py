@@ -127,7 +127,17 @@ class DropResArgs(ctypes.Structure):
     ]
 
 
+class DecodeAttnArgs(ctypes.Structure):
+    _fields_ = [
+        ("qkv", P), ("kc", P), ("vc", P), ("o", P), ("len", P),
+        ("ldqkv", LL), ("ldo", LL),
+        ("N", c_int), ("H", c_int), ("hd", c_int), ("Smax", c_int),
+        ("scale", c_float),
+    ]
+
+
 _FUNCS = {
+    "dpc_decode_attn": DecodeAttnArgs,
     "dpc_gemm": GemmArgs,
     "dpc_attn_fwd": AttnArgs,
     "dpc_attn_bwd": AttnArgs,

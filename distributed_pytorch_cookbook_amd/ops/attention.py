@@ -178,3 +178,39 @@ def _attn_bwd_hip(dout, qkv, o, lse, N, S, heads, pad_mask, causal, scale, dqkv)
     )
     _lib.call("dpc_attn_bwd", args, qkv.device)
     return dqkv
+
+
+DECODE_MAX_S = 16384  # csrc/decode.hip: LDS score buffer
+
+
+def decode_attention(qkv, kc, vc, length, heads, head_dim, scale=None):
+    """One new token per sequence against a KV cache: appends its key / value at
+    ``length`` (device int64 [1], cached tokens so far) and returns o [N, H*hd].
+
+    qkv [N, 3*H*hd]; kc, vc [N, S_max, H*hd].  HIP path: ``dpc_decode_attn``
+    (``csrc/decode.hip``); reads the length on the device, so it can be graph-captured.
+    """
+    scale = 1.0 / math.sqrt(head_dim) if scale is None else scale
+    N, E = qkv.shape[0], heads * head_dim
+    Smax = kc.shape[1]
+    if not _use_hip(qkv):
+        pos = int(length)
+        q, k, v = split_qkv(qkv, heads, head_dim)
+        kc[:, pos] = k
+        vc[:, pos] = v
+        qf = q.float().reshape(N, heads, 1, head_dim)
+        kf = kc[:, :pos + 1].float().reshape(N, pos + 1, heads, head_dim).transpose(1, 2)
+        vf = vc[:, :pos + 1].float().reshape(N, pos + 1, heads, head_dim).transpose(1, 2)
+        p = torch.softmax((qf @ kf.transpose(-1, -2)) * scale, -1)
+        return (p @ vf).reshape(N, E).to(qkv.dtype)
+    if (qkv.stride(1) != 1 or kc.shape != (N, Smax, E) or vc.shape != kc.shape or not kc.is_contiguous()
+            or not vc.is_contiguous() or kc.dtype != torch.bfloat16 or vc.dtype != torch.bfloat16
+            or head_dim % 8 or head_dim > 256 or 256 % (head_dim // 8) or Smax > DECODE_MAX_S
+            or qkv.stride(0) % 8 or qkv.data_ptr() % 16 or length.dtype != torch.int64):
+        raise ValueError("decode_attention: unsupported layout")
+    o = torch.empty(N, E, device=qkv.device, dtype=torch.bfloat16)
+    args = _lib.DecodeAttnArgs(qkv=qkv.data_ptr(), kc=kc.data_ptr(), vc=vc.data_ptr(), o=o.data_ptr(),
+                               len=length.data_ptr(), ldqkv=qkv.stride(0), ldo=E, N=N, H=heads,
+                               hd=head_dim, Smax=Smax, scale=scale)
+    _lib.call("dpc_decode_attn", args, qkv.device)
+    return o

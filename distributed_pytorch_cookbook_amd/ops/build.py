@@ -28,7 +28,7 @@ BUILD_DIR = HERE / "_build"
 LIB_PATH = HERE / "libdpc_kernels.so"
 ARCH = os.environ.get("DPC_OFFLOAD_ARCH", "gfx950")
 
-SOURCES = ["gemm.hip", "attention.hip", "layernorm.hip", "misc.hip"]
+SOURCES = ["gemm.hip", "attention.hip", "layernorm.hip", "misc.hip", "decode.hip"]
 HEADERS = ["common.h"]
 
 # code-object v5 keeps the library loadable by torch's bundled ROCm 7.0 runtime as

@@ -362,14 +362,14 @@ _GEMV_ROWS = 16
 
 
 def _linear_fwd_few_rows(x, w, bias, act, residual, out, out_dtype):
-    v = torch.mm(x, w.t()).float()
-    if bias is not None:
-        v += bias.float()
-    v = act_fwd_ref(v, act)
+    # bias in the library epilogue (f32 accumulate), then at most two elementwise launches
+    v = torch.mm(x, w.t()) if bias is None else torch.addmm(bias.to(x.dtype), x, w.t())
+    if act:
+        v = act_fwd_ref(v, act)
     if residual is not None:
-        v += residual.float()
+        v = residual + v  # f32 residual stream: promotes
     if out is None:
-        return v.to(out_dtype)
+        return v if v.dtype == out_dtype else v.to(out_dtype)
     n = v.shape[1]
     out[:, :n].copy_(v)
     if out.shape[1] > n:

@@ -479,3 +479,32 @@ def test_layernorm_fwd_fused_residual_add(D, p_drop):
     h_r = torch.nn.functional.layer_norm(xs_r, (D,), g, be, 1e-5)
     assert rel_err(h, h_r) < 1e-2
     assert rel_err(mu, xs_r.mean(-1)) < 1e-5
+
+
+@pytest.mark.parametrize("hd", [64, 32])
+@pytest.mark.parametrize("pos", [0, 37, 299])
+def test_decode_attention(hd, pos):
+    """Single-query KV-cache attention kernel (appends the new K/V at the device length) vs
+    the f32 softmax over the cached keys."""
+    from distributed_pytorch_cookbook_amd.ops.attention import decode_attention
+
+    torch.manual_seed(7)
+    N, H, Smax = 2, 3, 300
+    E = H * hd
+    kc = torch.randn(N, Smax, E, device=dev).bfloat16()
+    vc = torch.randn(N, Smax, E, device=dev).bfloat16()
+    kc[:, pos:] = 0  # not yet written
+    vc[:, pos:] = 0
+    qkv = torch.randn(N, 3 * E, device=dev).bfloat16()
+    length = torch.full((1,), pos, device=dev, dtype=torch.int64)
+    k_ref, v_ref = kc.clone(), vc.clone()
+    o = decode_attention(qkv, kc, vc, length, H, hd)
+    k_ref[:, pos] = qkv[:, E:2 * E]
+    v_ref[:, pos] = qkv[:, 2 * E:]
+    assert torch.equal(kc, k_ref) and torch.equal(vc, v_ref)
+    L = pos + 1
+    q = qkv[:, :E].float().reshape(N, H, 1, hd)
+    k = k_ref[:, :L].float().reshape(N, L, H, hd).transpose(1, 2)
+    v = v_ref[:, :L].float().reshape(N, L, H, hd).transpose(1, 2)
+    ref = (torch.softmax(q @ k.transpose(-1, -2) / math.sqrt(hd), -1) @ v).reshape(N, E)
+    assert rel_err(o, ref) < 1e-2
