@@ -1,0 +1,119 @@
+"""A/B the hand-written GEMM implementations against hipBLASLt (torch.mm) on random data.
+
+    python bench/gemm_ab.py [--impls 12 13 14] [--shapes square|gpt2s|all] [--rounds 3]
+
+Every variant of a shape is timed in interleaved rounds inside one process (HIP events over
+``--iters`` back-to-back launches, median over rounds), and checked once against an f32
+product of the same bf16 operands (max |err| relative to max |ref|).
+Layouts: nt = A, B k-major (forward), nn = B n-major (input gradient), tn = both mn-major
+(weight gradient, f32 accumulate).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import statistics
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from distributed_pytorch_cookbook_amd.ops import _lib  # noqa: E402
+from distributed_pytorch_cookbook_amd.ops.gemm import gemm, set_blas_plain  # noqa: E402
+
+set_blas_plain(False)
+
+SQUARE = [("sq8k_nt", 8192, 8192, 8192, "nt"), ("sq8k_nn", 8192, 8192, 8192, "nn"),
+          ("sq8k_tn", 8192, 8192, 8192, "tn"), ("sq4k_nt", 4096, 4096, 4096, "nt")]
+T = 64 * 1023
+GPT2S = [("qkv_fwd", T, 2304, 768, "nt"), ("out_fwd", T, 768, 768, "nt"),
+         ("lm_fwd", T, 50304, 768, "nt"), ("qkv_dgrad", T, 768, 2304, "nn"),
+         ("out_dgrad", T, 768, 768, "nn"), ("up_dgrad", T, 768, 3072, "nn"),
+         ("lm_dgrad", T, 768, 50304, "nn"), ("up_fwd", T, 3072, 768, "nt"),
+         ("down_fwd", T, 768, 3072, "nt")]
+
+
+def operands(M, N, K, lay, dev="cuda"):
+    r = lambda *s: (torch.rand(*s, device=dev) * 2 - 1).bfloat16()  # noqa: E731
+    if lay == "nt":
+        return r(M, K), r(N, K), dict(a_kmaj=True, b_kmaj=True), torch.bfloat16
+    if lay == "nn":
+        return r(M, K), r(K, N), dict(a_kmaj=True, b_kmaj=False), torch.bfloat16
+    return r(K, M), r(K, N), dict(a_kmaj=False, b_kmaj=False), torch.float32
+
+
+def torch_fn(A, B, lay, out):
+    if lay == "nt":
+        return lambda: torch.mm(A, B.t(), out=out)
+    if lay == "nn":
+        return lambda: torch.mm(A, B, out=out)
+    return lambda: torch.ops.aten.mm.dtype_out(A.t(), B, torch.float32, out=out)
+
+
+def time_ms(fn, iters):
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(iters):
+        fn()
+    e.record()
+    e.synchronize()
+    return s.elapsed_time(e) / iters
+
+
+def check(A, B, lay, out):
+    am = A.float() if lay != "tn" else A.float().t()
+    bm = B.float().t() if lay == "nt" else B.float()
+    ref = am @ bm
+    return float((out.float() - ref).abs().max() / ref.abs().max())
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--impls", type=int, nargs="+", default=[12, 13, 14])
+    ap.add_argument("--shapes", default="all", choices=["square", "gpt2s", "all"])
+    ap.add_argument("--only", nargs="*", default=None)
+    ap.add_argument("--rounds", type=int, default=3)
+    ap.add_argument("--iters", type=int, default=10)
+    ap.add_argument("--json", default=None)
+    a = ap.parse_args()
+    shapes = (SQUARE if a.shapes in ("square", "all") else []) + (GPT2S if a.shapes in ("gpt2s", "all") else [])
+    if a.only:
+        shapes = [s for s in shapes if s[0] in a.only]
+    rows = []
+    for name, M, N, K, lay in shapes:
+        torch.manual_seed(0)
+        A, B, kw, odt = operands(M, N, K, lay)
+        out = torch.empty(M, N, device="cuda", dtype=odt)
+        variants = {"blas": torch_fn(A, B, lay, out)}
+        for impl in a.impls:
+            variants[f"i{impl}"] = (lambda impl=impl: (_lib.set_gemm_impl(impl), gemm(A, B, out=out, **kw)))
+        errs = {}
+        for k, fn in variants.items():
+            fn()
+            torch.cuda.synchronize()
+            if M * N * K <= 8192 ** 3:
+                errs[k] = check(A, B, lay, out)
+            fn()
+        times = {k: [] for k in variants}
+        for _ in range(a.rounds):
+            for k, fn in variants.items():
+                times[k].append(time_ms(fn, a.iters))
+        _lib.set_gemm_impl(-1)
+        fl = 2.0 * M * N * K
+        row = dict(case=name, M=M, N=N, K=K, layout=lay)
+        for k in variants:
+            ms = statistics.median(times[k])
+            row[k] = dict(ms=round(ms, 4), tflops=round(fl / ms / 1e9, 1), err=errs.get(k))
+        rows.append(row)
+        print(json.dumps(row), flush=True)
+        del A, B, out
+        torch.cuda.empty_cache()
+    if a.json:
+        os.makedirs(os.path.dirname(a.json) or ".", exist_ok=True)
+        with open(a.json, "w") as f:
+            json.dump(rows, f, indent=1)
+
+
+if __name__ == "__main__":
+    main()

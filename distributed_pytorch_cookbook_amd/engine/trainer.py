@@ -70,6 +70,7 @@ class Trainer:
         self.device = engine.device
         self.log = engine.is_logger
         self.start_epoch = 0
+        self.skip_batches = 0  # batches of start_epoch already trained (mid-epoch resume)
         self.history = []
         vocab = getattr(tokenizer, "vocab_size", 50257)
         self.flops_per_token = train_flops_per_token(args.dim, args.heads, args.head_dim, args.num_layers,
@@ -94,10 +95,14 @@ class Trainer:
         if st is not None:
             self.engine.load_train_state(st)
             self.start_epoch = int(st.get("epoch", 0))
-            if "rng" in st:
+            self.skip_batches = int(st.get("batch", 0))
+            rng = st.get("rng_per_rank")
+            if rng is not None and len(rng) == comm.world_size():
+                set_rng_state(rng[comm.rank()])  # each rank its own stream
+            elif "rng" in st and comm.world_size() == 1:
                 set_rng_state(st["rng"])
         if self.log:
-            print(f"[resume] loaded {path} (epoch {self.start_epoch})")
+            print(f"[resume] loaded {path} (epoch {self.start_epoch}, batch {self.skip_batches})")
 
     # ------------------------------------------------------------------ main loop
     def fit(self, train_ds, val_ds):
@@ -136,7 +141,11 @@ class Trainer:
         for ei in range(self.start_epoch, a.epochs):
             if sampler is not None:
                 sampler.set_epoch(ei)
-            self.train_epoch(ei, train_loader)
+            elif getattr(train_loader, "generator", None) is not None:
+                # the shuffle order is a function of (seed, epoch) alone, so a resumed run sees
+                # the same batches as an uninterrupted one
+                train_loader.generator.manual_seed(a.seed + ei)
+            self.train_epoch(ei, train_loader, skip=self.skip_batches if ei == self.start_epoch else 0)
             self.validate(ei, val_loader)
             if not a.no_generate:
                 self.sample()
@@ -147,7 +156,7 @@ class Trainer:
             path = self.save(a.epochs)
         return path
 
-    def train_epoch(self, ei, loader):
+    def train_epoch(self, ei, loader, skip: int = 0):
         a, e = self.args, self.engine
         e.model.train()  # reference main-single.py:35 / main-ddp.py:109 (dropout on)
         pb = _tqdm(loader, self.log) if self.log else _NoBar(loader)
@@ -159,13 +168,15 @@ class Trainer:
         for i, batch in enumerate(pb):
             if a.max_steps and i >= a.max_steps:
                 break
+            if i < skip:  # trained before the checkpoint this run resumed from
+                continue
             maybe_inject_fault(e.step_count, comm.rank())
             inputs, targets = prepare_batch(batch, self.pad_id, self.device)
             with mark("train_step"):
                 loss = e.train_step(inputs, targets)
             prof.step()
             if getattr(a, "save_every", 0) and e.step_count % a.save_every == 0:
-                self.save(ei)  # resume restarts this epoch with the saved weights/moments
+                self.save(ei, batch=i + 1)  # resume continues this epoch after batch i
             tokens += targets.numel() * e.dp_world
             if loss is not None:
                 window = loss if window is None else window + loss
@@ -229,14 +240,15 @@ class Trainer:
             if self.log:
                 print(s)
 
-    def save(self, epoch):
+    def save(self, epoch, batch: int = 0):
         sd = self.engine.full_state_dict()
         path = None
         tstate = self.engine.train_state()
+        rngs = comm.gather_objects(rng_state())  # every rank's RNG streams (collective)
         if self.log and sd is not None:
             path = save_model_state(sd, self.args.checkpoint_dir)
             tstate = dict(tstate or {})
-            tstate.update({"epoch": epoch, "rng": rng_state()})
+            tstate.update({"epoch": epoch, "batch": batch, "rng": rng_state(), "rng_per_rank": rngs})
             save_train_state(path, tstate)
             print(f"saved {path}")
         comm.barrier()

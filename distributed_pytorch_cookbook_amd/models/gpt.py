@@ -265,10 +265,17 @@ class TransformerDecoderLM(nn.Module):
     def graph_decoder(self, cache):
         """HIP-graph one-token decode step over ``cache`` (None for a sharded store)."""
         from ..parallel.store import LocalStore
-        from ..ops.attention import DECODE_MAX_S
+        from ..ops.attention import DECODE_MAX_S, decode_supported
         from .fused import GraphDecoder, ensure_store
 
-        if not isinstance(ensure_store(self), LocalStore) or cache.capacity > DECODE_MAX_S:
+        store = ensure_store(self)
+        # the graphed step runs the HIP decode kernel, which reads the cache length on the
+        # device; anything it does not take (an f32 store under --disable_amp, a head size it
+        # does not handle) decodes eagerly instead -- the torch fallback reads the length on
+        # the host, which a graph capture does not allow
+        attn = self.decoder.layers[0].attn
+        if (not isinstance(store, LocalStore) or cache.capacity > DECODE_MAX_S
+                or store.compute_dtype != torch.bfloat16 or not decode_supported(attn.head_dim)):
             return None
         return GraphDecoder(self, cache)
 

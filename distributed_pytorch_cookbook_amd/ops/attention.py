@@ -183,6 +183,11 @@ def _attn_bwd_hip(dout, qkv, o, lse, N, S, heads, pad_mask, causal, scale, dqkv)
 DECODE_MAX_S = 16384  # csrc/decode.hip: LDS score buffer
 
 
+def decode_supported(head_dim: int) -> bool:
+    """Head sizes the decode kernel takes (16-B chunks of a row, at most one per thread)."""
+    return head_dim > 0 and head_dim % 8 == 0 and head_dim <= 256
+
+
 def decode_attention(qkv, kc, vc, length, heads, head_dim, scale=None):
     """One new token per sequence against a KV cache: appends its key / value at
     ``length`` (device int64 [1], cached tokens so far) and returns o [N, H*hd].
@@ -205,7 +210,7 @@ def decode_attention(qkv, kc, vc, length, heads, head_dim, scale=None):
         return (p @ vf).reshape(N, E).to(qkv.dtype)
     if (qkv.stride(1) != 1 or kc.shape != (N, Smax, E) or vc.shape != kc.shape or not kc.is_contiguous()
             or not vc.is_contiguous() or kc.dtype != torch.bfloat16 or vc.dtype != torch.bfloat16
-            or head_dim % 8 or head_dim > 256 or 256 % (head_dim // 8) or Smax > DECODE_MAX_S
+            or not decode_supported(head_dim) or Smax > DECODE_MAX_S
             or qkv.stride(0) % 8 or qkv.data_ptr() % 16 or length.dtype != torch.int64):
         raise ValueError("decode_attention: unsupported layout")
     o = torch.empty(N, E, device=qkv.device, dtype=torch.bfloat16)

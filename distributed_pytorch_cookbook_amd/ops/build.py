@@ -28,8 +28,8 @@ BUILD_DIR = HERE / "_build"
 LIB_PATH = HERE / "libdpc_kernels.so"
 ARCH = os.environ.get("DPC_OFFLOAD_ARCH", "gfx950")
 
-SOURCES = ["gemm.hip", "attention.hip", "layernorm.hip", "misc.hip", "decode.hip"]
-HEADERS = ["common.h"]
+SOURCES = ["gemm.hip", "gemm7.hip", "attention.hip", "layernorm.hip", "misc.hip", "decode.hip"]
+HEADERS = ["common.h", "gemm.h"]
 
 # code-object v5 keeps the library loadable by torch's bundled ROCm 7.0 runtime as
 # well as by the 7.2 toolchain in /opt/rocm.

@@ -40,8 +40,10 @@ __global__ __launch_bounds__(DA_NT) void decode_attn_kernel(DecodeAttnArgs p) {
   bf16_t* kc = static_cast<bf16_t*>(p.kc) + (long long)n * p.Smax * E + h * hd;
   bf16_t* vc = static_cast<bf16_t*>(p.vc) + (long long)n * p.Smax * E + h * hd;
   // append the new row (the score / PV loops read it from qkv, not back from the cache)
-  if (tid < hd) kc[pos * E + tid] = knew[tid];
-  else if (tid < 2 * hd) vc[pos * E + tid - hd] = vnew[tid - hd];
+  for (int i = tid; i < 2 * hd; i += DA_NT) {  // (strided: hd may reach DA_NT)
+    if (i < hd) kc[pos * E + i] = knew[i];
+    else vc[pos * E + i - hd] = vnew[i - hd];
+  }
   if (tid < hd) qs[tid] = bf2f(qrow[tid]) * p.scale;
   __syncthreads();
 
@@ -81,11 +83,12 @@ __global__ __launch_bounds__(DA_NT) void decode_attn_kernel(DecodeAttnArgs p) {
   }
   const float inv_l = 1.f / red[0];
 
-  // P.V: thread = (key group g, 8-dim chunk c), tid = g * nc + c
+  // P.V: thread = (key group g, 8-dim chunk c), tid = g * nc + c; with nc not dividing
+  // DA_NT (e.g. hd 24, 40, 48, 56) the last DA_NT - G nc threads sit out
   const int G = DA_NT / nc;
   const int c = tid % nc, g = tid / nc;
   float a[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-  for (int j = g; j < L; j += G) {
+  for (int j = g; g < G && j < L; j += G) {
     const uint4* vr = reinterpret_cast<const uint4*>(j == pos ? vnew : vc + (long long)j * E);
     float f[8];
     unpack8(vr[c], f);
@@ -93,8 +96,10 @@ __global__ __launch_bounds__(DA_NT) void decode_attn_kernel(DecodeAttnArgs p) {
 #pragma unroll
     for (int e = 0; e < 8; ++e) a[e] += pj * f[e];
   }
+  if (g < G) {
 #pragma unroll
-  for (int e = 0; e < 8; ++e) acc[tid * 8 + e] = a[e];  // = acc[g][c * 8 + e]
+    for (int e = 0; e < 8; ++e) acc[tid * 8 + e] = a[e];  // = acc[g][c * 8 + e]
+  }
   __syncthreads();
   if (tid < hd) {
     float s = 0.f;
@@ -109,7 +114,7 @@ using namespace dpc;
 
 DPC_API int dpc_decode_attn(const DecodeAttnArgs* a, hipStream_t stream) {
   if (a->N <= 0) return 0;
-  if (a->hd % 8 || a->hd > 256 || DA_NT % (a->hd / 8) || a->Smax > DA_MAX_S || a->ldqkv % 8)
+  if (a->hd <= 0 || a->hd % 8 || a->hd > 256 || a->Smax > DA_MAX_S || a->ldqkv % 8)
     return (int)hipErrorInvalidValue;
   hipLaunchKernelGGL(decode_attn_kernel, dim3((unsigned)(a->N * a->H)), dim3(DA_NT), 0, stream, *a);
   return (int)hipGetLastError();

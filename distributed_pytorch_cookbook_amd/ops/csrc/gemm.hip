@@ -21,7 +21,7 @@
 //     CDNA4 transposing LDS read, which yields the k-run per lane that MFMA wants.
 //   * workgroup ids are remapped so consecutive tiles share an XCD (private L2), then
 //     walked in GROUP_M-row supertiles for operand reuse.
-#include "common.h"
+#include "gemm.h"
 
 #include <cstdio>
 #include <cstdlib>
@@ -29,34 +29,6 @@
 
 namespace dpc {
 
-struct GemmArgs {
-  const void* A;
-  const void* B;
-  void* C;
-  const float* bias;      // [N] f32, optional
-  const float* residual;  // [M][ldr] f32, optional (may alias C)
-  const void* aux_in;     // [M][ld_aux_in] bf16, optional: multiply by act'(aux_in)
-  void* aux_out;          // [M][ld_aux_out] bf16, optional: store pre-activation
-  const float* alpha_ptr; // device scalar multiplier, optional
-  float* colsum;          // [N] f32, optional: colsum[n] += sum_m v (v after act_bwd, before act)
-  long long lda, ldb, ldc, ldr, ld_aux_in, ld_aux_out;
-  int M, N, K;
-  float alpha;
-  int act;         // activation applied after bias (Act)
-  int act_bwd;     // multiply by act'(aux_in) (Act)
-  int out_f32;     // C is f32 (else bf16)
-  int accumulate;  // C += result (f32 output only)
-  int a_kmaj, b_kmaj;
-  // stored extents of the operands ([rows][cols] as laid out in memory); reads beyond them
-  // return zeros.  k-major: rows = M or N, cols = K;  mn-major: rows = K, cols = M or N.
-  int a_r, a_c, b_r, b_c;
-  // set by the dispatcher (callers pass 0): > 1 = XCD-aligned split-K into this many k-ranges
-  int ksplit;
-  // caller's implementation choice (0 = the dispatcher's shape policy), e.g. from the
-  // measured per-shape table of ops/gemm.py (autotuned on MI355X); a forced global impl
-  // (dpc_gemm_set_impl, sweeps / tests) takes precedence
-  int impl;
-};
 
 // Which output tile and k-range a workgroup computes.  The grid is 1-D, ntiles x splits
 // workgroups (splits = |ksplit|, set by the dispatcher; 0 = 1), and block b runs on XCD b % 8.
@@ -250,19 +222,7 @@ __device__ __forceinline__ void epi_tile(const GemmArgs& p, floatx4 (&acc)[FM][4
   if (p.colsum) colsum_flush(cs, p.colsum, nw, p.N, lane);
 }
 
-constexpr int BM = 128, BN = 128, BKT = 64, NT = 256;
-constexpr int TILE_ELEMS = BM * BKT;  // 8192 bf16 = 16 KiB per operand per stage
-constexpr int GROUP_M = 8;
 
-// ---- LDS addressing (element offsets inside one operand tile) ----
-__device__ __forceinline__ int kmaj_off(int row, int chunk) {  // chunk = 8 k-elements
-  return row * 64 + ((chunk ^ ((row >> 1) & 7)) << 3);
-}
-__device__ __forceinline__ int mn_swz(int k) { return (k & 3) | (((k >> 3) & 1) << 2); }
-__device__ __forceinline__ int mnmaj_off(int k, int col) {      // col multiple of 4
-  const int blk = col >> 4, within = col & 15;
-  return k * 128 + (((blk ^ mn_swz(k)) << 4) | within);
-}
 
 // Load this thread's 4 x 16 B of a 128x64 (k-major) or 64x128 (mn-major) tile.
 template <bool KMAJ>
@@ -303,26 +263,6 @@ __device__ __forceinline__ void s_store(const uint4 (&r)[4], bf16_t* lds) {
     if (KMAJ) off = kmaj_off(c >> 3, c & 7);
     else      off = mnmaj_off(c >> 4, (c & 15) * 8);
     *reinterpret_cast<uint4*>(lds + off) = r[i];
-  }
-}
-
-// Fragment for v_mfma_f32_16x16x32_bf16: lane l holds X[r = l & 15][k = 8 (l >> 4) + j].
-template <bool KMAJ>
-__device__ __forceinline__ bf16x8 frag(const bf16_t* lds, int r0, int kstep, int lane) {
-  if (KMAJ) {
-    const int row = r0 + (lane & 15);
-    const int chunk = kstep * 4 + (lane >> 4);
-    return *reinterpret_cast<const bf16x8*>(lds + kmaj_off(row, chunk));
-  } else {
-    const int g = lane >> 4, i16 = lane & 15, q = i16 >> 2, pp = i16 & 3;
-    const int k = kstep * 32 + 8 * g + q;
-    const int col = r0 + 4 * pp;
-    typedef short4_t __attribute__((address_space(3))) * lptr;
-    short4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lptr)(lds + mnmaj_off(k, col)));
-    short4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lptr)(lds + mnmaj_off(k + 4, col)));
-    typedef short short8_t __attribute__((ext_vector_type(8)));
-    short8_t s = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-    return __builtin_bit_cast(bf16x8, s);
   }
 }
 
@@ -443,49 +383,8 @@ __global__ __launch_bounds__(NT, 2) void gemm_kernel(GemmArgs p) {
 // with the same involution.  Epilogue: the f32 tile goes through LDS so that bias / residual /
 // aux / C traffic is 16-B-per-lane row-contiguous.
 // =====================================================================================
-typedef __attribute__((address_space(3))) void* lds_void_t;
 
-// ---- v2 geometry, templated on the k-depth KB of a stage (64 or 32)
-template <int KB>
-__device__ __forceinline__ int swz_k(int row) {  // 16-B chunk swizzle of a k-major [row][KB] tile
-  if (KB == 64) return (row >> 1) & 7;
-  const int q = (row >> 2) & 3;  // KB == 32: 4 chunks per 64-B row, 4 rows per bank row
-  return (0x1320 >> (q * 4)) & 3;  // {0, 2, 3, 1}[q]
-}
-template <int KB>
-__device__ __forceinline__ int kmaj_off_k(int row, int chunk) {
-  return row * KB + ((chunk ^ swz_k<KB>(row)) << 3);
-}
 
-template <int KB, bool KMAJ>
-__device__ __forceinline__ bf16x8 frag_k(const bf16_t* lds, int r0, int kstep, int lane) {
-  if (KMAJ) {
-    const int row = r0 + (lane & 15);
-    const int chunk = kstep * 4 + (lane >> 4);
-    return *reinterpret_cast<const bf16x8*>(lds + kmaj_off_k<KB>(row, chunk));
-  }
-  return frag<false>(lds, r0, kstep, lane);  // [KB][128] mn-major image, 256-B rows
-}
-
-// per-thread DMA source offsets of one operand tile (relative to the tile origin)
-template <int KB, bool KMAJ>
-__device__ __forceinline__ void dma_offsets(int (&v)[KB / 16], long long ld, int wid, int lane) {
-  constexpr int NL = KB / 16;  // 1-KiB wave-instructions per wave per operand tile
-#pragma unroll
-  for (int i = 0; i < NL; ++i) {
-    const int j = wid * NL + i;
-    if (KMAJ) {
-      constexpr int LPR = KB / 8;       // lanes per row (16 B each)
-      constexpr int RPI = 64 / LPR;     // rows per wave-instruction
-      const int row = RPI * j + lane / LPR, pos = lane % LPR, c = pos ^ swz_k<KB>(row);
-      v[i] = (int)(((long long)row * ld + c * 8) * 2);
-    } else {
-      const int kr = 4 * j + (lane >> 4), pos = lane & 15;
-      const int c = (((pos >> 1) ^ mn_swz(kr)) << 1) | (pos & 1);
-      v[i] = (int)(((long long)kr * ld + c * 8) * 2);
-    }
-  }
-}
 
 template <int NL>
 __device__ __forceinline__ void issue_tile(const void* base, unsigned long long total, unsigned long long off,
@@ -510,10 +409,6 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, un
   return __builtin_amdgcn_make_buffer_rsrc((void*)((const char*)base + off), 0, nrec, 0x00020000);
 }
 
-template <int N>
-__device__ __forceinline__ void wait_vm() {
-  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
-}
 
 template <int KB, int STAGES>
 struct V2Cfg {
@@ -636,29 +531,7 @@ struct V3Cfg {
   static_assert(SMEM * 2 <= 160 * 1024, "LDS");
 };
 
-template <int KB, bool KMAJ, int NL>
-__device__ __forceinline__ void dma_offsets3(int (&v)[NL], long long ld, int wid, int lane) {
-#pragma unroll
-  for (int i = 0; i < NL; ++i) {
-    const int j = wid * NL + i;
-    if (KMAJ) {
-      constexpr int LPR = KB / 8, RPI = 64 / LPR;
-      const int row = RPI * j + lane / LPR, pos = lane % LPR, c = pos ^ swz_k<KB>(row);
-      v[i] = (int)(((long long)row * ld + c * 8) * 2);
-    } else {
-      constexpr int IPH = KB / 4;  // wave-instructions per 128-column half
-      const int h = j / IPH, kr = 4 * (j % IPH) + (lane >> 4), pos = lane & 15;
-      const int c = (((pos >> 1) ^ mn_swz(kr)) << 1) | (pos & 1);
-      v[i] = (int)(((long long)kr * ld + h * 128 + c * 8) * 2);
-    }
-  }
-}
 
-template <int KB, bool KMAJ>
-__device__ __forceinline__ bf16x8 frag3(const bf16_t* lds, int r0, int kstep, int lane) {
-  if (KMAJ) return frag_k<KB, true>(lds, r0, kstep, lane);
-  return frag<false>(lds + (r0 >> 7) * KB * 128, r0 & 127, kstep, lane);
-}
 
 template <int BM_, int BN_, int WM, int WN, int KB, int STAGES, bool AK, bool BK>
 __global__ __launch_bounds__((V3Cfg<BM_, BN_, WM, WN, KB, STAGES>::NTH), (V3Cfg<BM_, BN_, WM, WN, KB, STAGES>::WGS)) void gemm3_kernel(
@@ -883,19 +756,6 @@ __global__ __launch_bounds__(512, 1) void gemm4_kernel(GemmArgs p, unsigned long
 // so even the lagging group's reads were retired (start of its MFMA segment) before a barrier
 // the issuing wave has passed.  Slices past the end are issued with an empty descriptor (they
 // land as zeros in a slot nobody reads) so every vmcnt in the loop is the same constant.
-template <int NL>
-__device__ __forceinline__ void issue_tile_v(const void* base, unsigned long long total, unsigned long long off,
-                                             bool valid, const int* voff, bf16_t* lds_tile, int wave) {
-  const unsigned long long left = (valid && off < total) ? total - off : 0ull;
-  const unsigned nrec = left > 0xffffffffull ? 0xffffffffu : (unsigned)left;
-  const __amdgpu_buffer_rsrc_t rs =
-      __builtin_amdgcn_make_buffer_rsrc((void*)((const char*)base + (valid ? off : 0ull)), 0, nrec, 0x00020000);
-#pragma unroll
-  for (int i = 0; i < NL; ++i) {
-    const int j = wave * NL + i;
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void_t)(lds_tile + j * 512), 16, voff[i], 0, 0, 0);
-  }
-}
 
 __device__ __forceinline__ void seg_barrier() {
   __builtin_amdgcn_sched_barrier(0);
@@ -1004,6 +864,126 @@ __global__ __launch_bounds__(512, 1) void gemm5_kernel(GemmArgs p, unsigned long
   epi_tile<8, false>(p, acc, reinterpret_cast<float*>(smem) + wid * 32 * 64, splits, m0 + ar, n0 + bc, lane);
 }
 
+// =====================================================================================
+// v6: the v5 ping-pong with the LDS-DMA issue spread over BOTH read segments of a k-slice
+// and an NS-slot ring (NS = 4: 128 KiB, NS = 5: the whole 160 KiB LDS, one more slice in
+// flight).  In v5 the (s,1) read segment issued all four 1-KiB DMA pieces of slice s+3 on
+// top of its fragment reads; a DMA piece costs ~60-185 issue cycles beside MFMA traffic
+// (MI355X_MICROARCH.md cycle constants), so that segment outlasted the partner group's
+// 256-cycle MFMA segment and the matrix pipe idled every other phase.  Here
+//   R(s,0): fragment reads B(s) + A rows 0-63 (s), then the B part of slice s+NS-1
+//   R(s,1): fragment reads A rows 64-127 (s), then the A part of slice s+NS-1, counted vmcnt
+// WAR (slot (s+NS-1)%NS last held slice s-1): B(s-1) was read in R(s-1,0) by both groups and
+// retired at the start of each group's M(s-1,0) -- at least two barriers before either group's
+// R(s,0).  A(s-1) rows 64-127 were read in R(s-1,1), retired at the start of M(s-1,1); the
+// lagging group's M(s-1,1) starts at the barrier that opens the leading group's R(s,0), so the
+// A part waits until R(s,1), which both groups enter after that barrier's successor.
+// RAW: slice s+1 is read in R(s+1,0); the youngest loads a wave may leave in flight after its
+// R(s,1) issue are slices s+2 .. s+NS-1 (4 pieces each) -> vmcnt(4 (NS-2)), then the barrier
+// (and for the leading group the lagging group's vmcnt precedes the barrier before R(s+1,0)).
+template <int NS, bool AK, bool BK>
+__global__ __launch_bounds__(512, 1) void gemm6_kernel(GemmArgs p, unsigned long long a_bytes,
+                                                       unsigned long long b_bytes) {
+  using Cfg = V3Cfg<256, 256, 2, 4, 32, 4>;
+  constexpr int SLOT = Cfg::TA + Cfg::TB;
+  constexpr int NLA = Cfg::NLA, NLB = Cfg::NLB;  // 2 + 2 DMA instructions per wave per slice
+  constexpr int SMEM = NS * SLOT > Cfg::SMEM ? NS * SLOT : Cfg::SMEM;
+  static_assert(SMEM * 2 <= 160 * 1024, "LDS");
+  __shared__ __attribute__((aligned(16))) bf16_t smem[SMEM];
+  const int tiles_m = (p.M + 255) / 256, tiles_n = (p.N + 255) / 256;
+  const int nwg = tiles_m * tiles_n;
+  const TileSlot ts = tile_slot(p, nwg);
+  const int bid = ts.bid;
+  const int group = GROUP_M * tiles_n;
+  const int gid = bid / group, first_m = gid * GROUP_M;
+  const int gsz = min(tiles_m - first_m, GROUP_M);
+  const int tm = first_m + (bid % group) % gsz;
+  const int tn = (bid % group) / gsz;
+  const int m0 = tm * 256, n0 = tn * 256;
+
+  const int lane = threadIdx.x & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wr = wid >> 2, wc = wid & 3;
+  const int ar = wr * 128, bc = wc * 64;
+
+  int va[NLA], vb[NLB];
+  dma_offsets3<32, AK, NLA>(va, p.lda, wid, lane);
+  dma_offsets3<32, BK, NLB>(vb, p.ldb, wid, lane);
+  const unsigned long long a_org = AK ? (unsigned long long)m0 * p.lda * 2 : (unsigned long long)m0 * 2;
+  const unsigned long long b_org = BK ? (unsigned long long)n0 * p.ldb * 2 : (unsigned long long)n0 * 2;
+  const unsigned long long a_step = AK ? 64ull : 32ull * p.lda * 2;
+  const unsigned long long b_step = BK ? 64ull : 32ull * p.ldb * 2;
+  floatx4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+
+  const int nk_all = (p.K + 31) / 32;
+  const int splits = ts.splits;
+  const int per = (nk_all + splits - 1) / splits;
+  const int kt0 = ts.split * per;
+  const int nk = max(0, min(nk_all, kt0 + per) - kt0);
+#define DPC_ISSUE6A(s_)                                                                              \
+  issue_tile_v<NLA>(p.A, a_bytes, a_org + a_step * (unsigned long long)(kt0 + (s_)), (s_) < nk, va,  \
+                    smem + ((s_) % NS) * SLOT, wid)
+#define DPC_ISSUE6B(s_)                                                                              \
+  issue_tile_v<NLB>(p.B, b_bytes, b_org + b_step * (unsigned long long)(kt0 + (s_)), (s_) < nk, vb,  \
+                    smem + ((s_) % NS) * SLOT + Cfg::TA, wid)
+
+  if (nk > 0) {
+#pragma unroll
+    for (int s = 0; s < NS - 1; ++s) {
+      DPC_ISSUE6B(s);
+      DPC_ISSUE6A(s);
+    }
+    wait_vm<(NS - 2) * (NLA + NLB)>();  // slice 0 landed (slices 1 .. NS-2 in flight)
+    seg_barrier();
+    if (wr == 1) seg_barrier();  // the second group runs one barrier interval behind
+    bf16x8 alo[4], ahi[4], b[4];
+    for (int s = 0; s < nk; ++s) {
+      const bf16_t* la = smem + (s % NS) * SLOT;
+      const bf16_t* lb = la + Cfg::TA;
+      // ---- R(s,0)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) b[j] = frag3<32, BK>(lb, bc + j * 16, 0, lane);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) alo[i] = frag3<32, AK>(la, ar + i * 16, 0, lane);
+      DPC_ISSUE6B(s + NS - 1);
+      seg_barrier();
+      // ---- M(s,0)
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(alo[i], b[j], acc[i][j], 0, 0, 0);
+      __builtin_amdgcn_s_setprio(0);
+      seg_barrier();
+      // ---- R(s,1)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) ahi[i] = frag3<32, AK>(la, ar + 64 + i * 16, 0, lane);
+      DPC_ISSUE6A(s + NS - 1);
+      wait_vm<(NS - 2) * (NLA + NLB)>();  // slice s+1 landed for this wave
+      seg_barrier();
+      // ---- M(s,1)
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          acc[4 + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ahi[i], b[j], acc[4 + i][j], 0, 0, 0);
+      __builtin_amdgcn_s_setprio(0);
+      seg_barrier();
+    }
+    if (wr == 0) seg_barrier();  // rebalance the barrier count of the two groups
+  }
+#undef DPC_ISSUE6A
+#undef DPC_ISSUE6B
+
+  epi_tile<8, false>(p, acc, reinterpret_cast<float*>(smem) + wid * 32 * 64, splits, m0 + ar, n0 + bc, lane);
+}
+
 }  // namespace dpc
 
 using namespace dpc;
@@ -1014,6 +994,15 @@ static void launch_v5(const GemmArgs* a, dim3 grid, hipStream_t stream, unsigned
   else if (a->a_kmaj) hipLaunchKernelGGL((gemm5_kernel<true, false>), grid, dim3(512), 0, stream, *a, ab, bb);
   else if (!a->b_kmaj) hipLaunchKernelGGL((gemm5_kernel<false, false>), grid, dim3(512), 0, stream, *a, ab, bb);
   else hipLaunchKernelGGL((gemm5_kernel<false, true>), grid, dim3(512), 0, stream, *a, ab, bb);
+}
+
+template <int NS>
+static void launch_v6(const GemmArgs* a, dim3 grid, hipStream_t stream, unsigned long long ab,
+                      unsigned long long bb) {
+  if (a->a_kmaj && a->b_kmaj) hipLaunchKernelGGL((gemm6_kernel<NS, true, true>), grid, dim3(512), 0, stream, *a, ab, bb);
+  else if (a->a_kmaj) hipLaunchKernelGGL((gemm6_kernel<NS, true, false>), grid, dim3(512), 0, stream, *a, ab, bb);
+  else if (!a->b_kmaj) hipLaunchKernelGGL((gemm6_kernel<NS, false, false>), grid, dim3(512), 0, stream, *a, ab, bb);
+  else hipLaunchKernelGGL((gemm6_kernel<NS, false, true>), grid, dim3(512), 0, stream, *a, ab, bb);
 }
 
 static void launch_v4(const GemmArgs* a, dim3 grid, hipStream_t stream, unsigned long long ab,
@@ -1055,7 +1044,10 @@ static void launch_v2(const GemmArgs* a, dim3 grid, hipStream_t stream, unsigned
 
 // -1: auto; 1: v1; 2: v2 KB64 x2 stages; 3: KB64 x3; 4: KB32 x3; 5: KB32 x4;
 // 6-10: v3 (6: 256x256 KB64 x2, 7: 256x256 KB32 x4, 8: 256x128 KB64 x2, 9: 256x128 KB32 x4,
-// 10: 256x128 KB32 x3); 11: v4 (256x256, pipelined k32 ring); 12: v5 (256x256 ping-pong)
+// 10: 256x128 KB32 x3); 11: v4 (256x256, pipelined k32 ring); 12: v5 (256x256 ping-pong);
+// 13 / 14: v6 (v5 with the DMA spread over both read segments; 4- / 5-slot ring);
+// 15 / 16: v7 (gemm7.hip: persistent one-wave-per-SIMD 256x256, 4- / 5-slot ring);
+// 17 / 18: v7 with one tile per workgroup (4- / 5-slot ring)
 static int g_gemm_impl = -1;
 // XCD-aligned split-K mapping (tile_slot): measured ~6 % slower than the default mapping on
 // the GPT-2 weight gradients, so off unless requested (sweeps)
@@ -1094,6 +1086,8 @@ static int policy_impl(const GemmArgs* a) {
   else return 0;
   return g_policy[c];
 }
+
+extern "C" int dpc_gemm7(const GemmArgs* a, int ns, int persistent, int sched, hipStream_t stream);
 
 DPC_API int dpc_gemm(const GemmArgs* a, hipStream_t stream) {
   if (a->M <= 0 || a->N <= 0) return 0;
@@ -1139,13 +1133,21 @@ DPC_API int dpc_gemm(const GemmArgs* a, hipStream_t stream) {
     const int t128 = ((a->M + BM - 1) / BM) * ((a->N + BN - 1) / BN);
     impl = t128 >= 100 ? 12 : 2;
   }
+  if (impl >= 15 && impl <= 22) {  // v7 (gemm7.hip): 4-wave 256x256, no split-K
+    GemmArgs c = *a;
+    c.ksplit = 0;
+    const int rc = impl >= 19 ? dpc_gemm7(&c, 5, 1, impl - 18, stream)
+                              : dpc_gemm7(&c, (impl & 1) ? 4 : 5, impl <= 16, 0, stream);
+    if (rc >= 0) return rc;
+    impl = v2_ok ? 2 : 1;  // requirements not met: the 128x128 kernels
+  }
   if (impl >= 2 && !v2_ok) impl = 1;
   GemmArgs b = *a;  // dispatcher-owned copy: split-K mode is decided here
   b.ksplit = 0;
   if (impl >= 2) {
     int bm = BM, bn = BN;
     if (impl >= 6) {
-      bm = 256;
+      bm = 256;  // (v3-v6)
       bn = (impl == 8 || impl == 9 || impl == 10) ? 128 : 256;
     }
     const int t = ((a->M + bm - 1) / bm) * ((a->N + bn - 1) / bn);
@@ -1157,7 +1159,7 @@ DPC_API int dpc_gemm(const GemmArgs* a, hipStream_t stream) {
       // rounds = ceil(tiles * s / resident workgroups) (wave quantisation of the grid) and
       // beta * s the split-K partial-sum atomics relative to the K-proportional MFMA work.
       // resident workgroups per launch round: 256 CUs x workgroups per CU (LDS-bound, V2Cfg::WGS)
-      const int slots = impl >= 6 || impl == 3 ? 256 : (impl == 4 ? 768 : 512);  // (v3-v5: 1 WG/CU)
+      const int slots = impl >= 6 || impl == 3 ? 256 : (impl == 4 ? 768 : 512);  // (v3-v6: 1 WG/CU)
       const double beta = 0.0056 * 32768.0 / (double)a->K;
       double best = 1e30;
       for (int s = 1; s <= 16 && (s == 1 || nk / s >= 8); ++s) {
@@ -1182,6 +1184,8 @@ DPC_API int dpc_gemm(const GemmArgs* a, hipStream_t stream) {
       case 10: launch_v3<256, 128, 4, 2, 32, 3>(&b, g, stream, ab, bb); break;
       case 11: launch_v4(&b, g, stream, ab, bb); break;
       case 12: launch_v5(&b, g, stream, ab, bb); break;
+      case 13: launch_v6<4>(&b, g, stream, ab, bb); break;
+      case 14: launch_v6<5>(&b, g, stream, ab, bb); break;
       default: launch_v2<64, 2>(&b, g, stream, ab, bb); break;
     }
     return (int)hipGetLastError();

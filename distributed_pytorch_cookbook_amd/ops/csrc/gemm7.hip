@@ -1,0 +1,456 @@
+// v7: persistent 256x256 bf16 MFMA GEMM, one 4-wave workgroup per CU, one wave per SIMD.
+//
+// Why this shape (MI355X, measured with bench/gemm_ab.py): the 8-wave ping-pong kernels
+// (v5/v6) pay two workgroup barriers per 16 MFMAs and re-read 12 fragments per 32 MFMAs; on
+// short-K products (K = 768: the QKV / out / up / LM-head forward products of GPT-2 small) they
+// also drain the whole pipeline at every tile -- prologue latency + a 128 KiB store burst per
+// CU with the matrix pipe idle -- and ran at ~680 TF/s against hipBLASLt's ~1,200.  Here:
+//   * each wave owns a 128x128 output tile: 8 x 8 accumulators of v_mfma_f32_16x16x32_bf16
+//     (256 accumulator registers; a 512-register wave, one per SIMD), i.e. 16 fragment reads
+//     per 64 MFMAs (0.25 / MFMA vs 0.375) and ONE workgroup barrier per 32-deep k-slice
+//     (1,024 MFMA cycles per SIMD);
+//   * the k-slices of all the tiles a workgroup owns form one stream: an NS-slot LDS ring
+//     (32 KiB per slot: A 256x32 + B 256x32) filled by LDS-DMA (buffer_load ... lds) DIST =
+//     NS-1 slices ahead, never drained at a tile boundary, so the next tile's first slices are
+//     in flight while the previous tile's epilogue runs;
+//   * fragments of slice q+1 are read into a second register set while the MFMAs of slice q
+//     run (two named sets, the loop unrolled by two);
+//   * the MFMA operands are swapped (C^T = B A^T): lane l of a 16x16 accumulator holds output
+//     row l & 15 and four CONSECUTIVE columns 4 (l >> 4) + r, so the epilogue works straight
+//     from registers -- no LDS staging, no barrier: 16-B f32 stores, and for bf16 outputs
+//     v_permlane16_swap pairs two fragments' 8-B halves into one 16-B store per lane.
+// LDS images and fragment reads are the v3 ones (gemm.h): k-major [rows][32] with the 16-B
+// chunk swizzle, mn-major [k][128-column halves] read with ds_read_b64_tr_b16.
+//
+// Synchronisation (per slice q, every wave):  body(q) = MFMAs on frags(q) | reads of frags(q+1)
+// from slot (q+1) % NS | DMA of slice q+DIST into slot (q+DIST) % NS | epilogue if q ends a
+// tile;  then vmcnt(slice q+2 landed) + s_barrier.
+//   RAW: slot (q+2) is read in body(q+1), after this barrier, which every wave enters after its
+//        own counted vmcnt for slice q+2 (its DMA pieces are older than the count).
+//   WAR: slot (q+DIST) % NS held slice q-1, read in body(q-2) and consumed by the MFMAs of
+//        body(q-1), i.e. retired before every wave passed barrier(q-1) -- before any wave
+//        can be in body(q).
+// Reference: every nn.Linear of /root/reference/models/gpt.py:29-30,60-64,219.
+#include "gemm.h"
+
+#include <cstdlib>
+
+namespace dpc {
+
+constexpr int G7_KB = 32;              // k depth of a slice
+constexpr int G7_TA = 256 * G7_KB;     // bf16 elements per operand per slice (16 KiB)
+constexpr int G7_SLOT = 2 * G7_TA;     // A + B
+constexpr int G7_NL = G7_TA / 512 / 4; // 1-KiB DMA pieces per wave per operand per slice (4)
+
+struct G7Plan {
+  int tiles_m, tiles_n;
+  int units;   // tiles (no split-K in this kernel)
+  int grid;    // workgroups launched (<= 256: one per CU)
+  int nk;      // k-slices per tile
+  int store_cnt;  // vector-memory ops the epilogue issues per wave-lane (0: unknown -> no credit)
+  int debug;      // experiments only (DPC_G7_DEBUG): 1 = no epilogue stores, 2 = no in-loop DMA
+};
+
+// XCD-aware assignment: round i covers units [i*grid, (i+1)*grid); inside a round the blocks
+// that share an XCD (b % 8) get a contiguous run of unit ids (bijective for any grid), and unit
+// ids walk GROUP_M-row supertiles, so an XCD's concurrent tiles share A/B panels in its L2.
+__device__ __forceinline__ int g7_local(int b, int grid) {
+  const int xcd = b & 7, q = grid >> 3, r = grid & 7;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (b >> 3);
+}
+
+__device__ __forceinline__ void g7_tile(const G7Plan& pl, int u, int& m0, int& n0) {
+  const int group = GROUP_M * pl.tiles_n;
+  const int gid = u / group, first_m = gid * GROUP_M;
+  const int gsz = min(pl.tiles_m - first_m, GROUP_M);
+  const int w = u - gid * group;
+  m0 = (first_m + w % gsz) * 256;
+  n0 = (w / gsz) * 256;
+}
+
+// One 1-KiB LDS-DMA piece (buffer_load_dwordx4 ... lds: 64 lanes x 16 B, lane-linear at M0).
+// Issued from inline asm ON PURPOSE: hipcc (ROCm 7.2) answers a compiler-visible LDS-DMA with an
+// s_waitcnt vmcnt(0) in front of every later ds_read_b64_tr_b16 (the transposing read of the
+// mn-major images), which drained the whole prefetch ring once per fragment and held the
+// B-n-major / weight-gradient layouts at ~380 TF/s.  Hidden in asm the DMA is ordered only by
+// this kernel's own counted vmcnt + barrier (see the synchronisation notes above); the compiler
+// never counts these loads, so every vmcnt it emits for its own loads over-waits (safe).
+// M0 (the LDS destination base) is saved and restored around the piece.
+__device__ __forceinline__ void g7_piece(__amdgpu_buffer_rsrc_t rs, int voff, const bf16_t* lds) {
+  const unsigned la = (unsigned)(uintptr_t)(lds_void_t)lds;
+  unsigned keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(voff), "s"(rs), "s"(la)
+      : "memory");
+}
+
+template <int N>
+__device__ __forceinline__ void g7_wait() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+// ---- epilogue straight from the swapped accumulators.  Lane l, accumulator (i, j), register
+// r holds C[mw + 16 i + (l & 15)][nw + 16 j + 4 (l >> 4) + r].  Same semantics and order as
+// epi_tile (gemm.hip) / ops/gemm.py:_gemm_ref.
+// GEN = false: plain products only (alpha, bf16 or f32 C, no accumulate) -- the hot path,
+// with the register budget of the main loop untouched; GEN = true: every fused operation.
+template <bool GEN>
+__device__ __forceinline__ void g7_epilogue(const GemmArgs& p, floatx4 (&acc)[8][8], int mw, int nw, int lane) {
+  float alpha = p.alpha;
+  if (p.alpha_ptr) alpha *= *p.alpha_ptr;
+  const int g = lane >> 4, rl = lane & 15;
+  if (!GEN && p.out_f32) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int m = mw + 16 * i + rl;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int n = nw + 16 * j + 4 * g;
+        if (m < p.M && n < p.N)
+          *reinterpret_cast<float4*>(static_cast<float*>(p.C) + (long long)m * p.ldc + n) =
+              make_float4(acc[i][j][0] * alpha, acc[i][j][1] * alpha, acc[i][j][2] * alpha, acc[i][j][3] * alpha);
+      }
+    }
+    return;
+  }
+  if (!GEN) {
+    // bf16 C, 16-B stores: after v_permlane16_swap of fragments (j, j+1) lane group g holds
+    // columns 16 j + {0, 16, 8, 24}[g] .. +7 (host: N % 8 == 0, ldc % 8 == 0, C 16-B aligned)
+    const int coff = 16 * (g & 1) + 8 * (g >> 1);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int m = mw + 16 * i + rl;
+#pragma unroll
+      for (int j = 0; j < 8; j += 2) {
+        unsigned x0 = pack2bf(acc[i][j][0] * alpha, acc[i][j][1] * alpha);
+        unsigned x1 = pack2bf(acc[i][j][2] * alpha, acc[i][j][3] * alpha);
+        unsigned y0 = pack2bf(acc[i][j + 1][0] * alpha, acc[i][j + 1][1] * alpha);
+        unsigned y1 = pack2bf(acc[i][j + 1][2] * alpha, acc[i][j + 1][3] * alpha);
+        const auto s0 = __builtin_amdgcn_permlane16_swap(x0, y0, false, false);
+        const auto s1 = __builtin_amdgcn_permlane16_swap(x1, y1, false, false);
+        const int n = nw + 16 * j + coff;
+        if (m < p.M && n < p.N)
+          *reinterpret_cast<uint4*>(static_cast<bf16_t*>(p.C) + (long long)m * p.ldc + n) =
+              make_uint4(s0[0], s1[0], s0[1], s1[1]);
+      }
+    }
+    return;
+  }
+  if (!GEN) return;
+  float4 bias4[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int n = nw + 16 * j + 4 * g;
+    bias4[j] = (p.bias && n < p.N) ? *reinterpret_cast<const float4*>(p.bias + n) : make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+  float cs[8][4];
+#pragma unroll
+  for (int j = 0; j < 8; ++j)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) cs[j][r] = 0.f;
+  const bf16_t* aux_in = static_cast<const bf16_t*>(p.aux_in);
+  bf16_t* aux_out = static_cast<bf16_t*>(p.aux_out);
+  const float* fsrc = p.residual ? p.residual : (p.out_f32 && p.accumulate ? static_cast<const float*>(p.C) : nullptr);
+  const long long ldf = p.residual ? p.ldr : p.ldc;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int m = mw + 16 * i + rl;
+    const bool mok = m < p.M;
+    // this row's operand reads, all in flight before the first use
+    uint2 z[8];
+    float4 f[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int n = nw + 16 * j + 4 * g;
+      const bool ok = mok && n < p.N;
+      z[j] = make_uint2(0u, 0u);
+      f[j] = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (ok && p.act_bwd) z[j] = *reinterpret_cast<const uint2*>(aux_in + (long long)m * p.ld_aux_in + n);
+      if (ok && fsrc) f[j] = *reinterpret_cast<const float4*>(fsrc + (long long)m * ldf + n);
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int n = nw + 16 * j + 4 * g;
+      if (!mok || n >= p.N) continue;
+      float v[4] = {acc[i][j][0] * alpha + bias4[j].x, acc[i][j][1] * alpha + bias4[j].y,
+                    acc[i][j][2] * alpha + bias4[j].z, acc[i][j][3] * alpha + bias4[j].w};
+      if (p.act_bwd) {
+        v[0] *= act_grad(__uint_as_float(z[j].x << 16), p.act_bwd);
+        v[1] *= act_grad(__uint_as_float(z[j].x & 0xffff0000u), p.act_bwd);
+        v[2] *= act_grad(__uint_as_float(z[j].y << 16), p.act_bwd);
+        v[3] *= act_grad(__uint_as_float(z[j].y & 0xffff0000u), p.act_bwd);
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) cs[j][r] += v[r];
+      if (aux_out)
+        *reinterpret_cast<uint2*>(aux_out + (long long)m * p.ld_aux_out + n) =
+            make_uint2(pack2bf(v[0], v[1]), pack2bf(v[2], v[3]));
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v[r] = act_fwd(v[r], p.act);
+      if (fsrc) {
+        v[0] += f[j].x; v[1] += f[j].y; v[2] += f[j].z; v[3] += f[j].w;
+      }
+      const long long ci = (long long)m * p.ldc + n;
+      if (p.out_f32) {
+        float4* C = reinterpret_cast<float4*>(static_cast<float*>(p.C) + ci);
+        if (p.accumulate && p.residual) {  // (no caller does both; C read late)
+          const float4 o = *C;
+          v[0] += o.x; v[1] += o.y; v[2] += o.z; v[3] += o.w;
+        }
+        *C = make_float4(v[0], v[1], v[2], v[3]);
+      } else {
+        *reinterpret_cast<uint2*>(static_cast<bf16_t*>(p.C) + ci) = make_uint2(pack2bf(v[0], v[1]), pack2bf(v[2], v[3]));
+      }
+    }
+  }
+  if (p.colsum) {
+    // sum over the 16 rows of a lane group, then lane t of group g adds columns 2t, 2t+1 of the
+    // group's 32 (j = e >> 2, r = e & 3 -> column 16 j + 4 g + r)
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        float v = cs[j][r];
+        v += __shfl_xor(v, 1, 64);
+        v += __shfl_xor(v, 2, 64);
+        v += __shfl_xor(v, 4, 64);
+        v += __shfl_xor(v, 8, 64);
+        cs[j][r] = v;
+      }
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int e = 2 * rl + h;
+      float v = 0.f;
+#pragma unroll
+      for (int k = 0; k < 32; ++k) v = (e == k) ? cs[k >> 2][k & 3] : v;
+      const int n = nw + 16 * (e >> 2) + 4 * g + (e & 3);
+      if (n < p.N) atomicAdd(p.colsum + n, v);
+    }
+  }
+}
+
+template <int NS, bool GEN, int SCHED, bool AK, bool BK>
+__global__ __launch_bounds__(256, 1) void gemm7_kernel(GemmArgs p, unsigned long long a_bytes,
+                                                       unsigned long long b_bytes, G7Plan pl) {
+  constexpr int DIST = NS - 1;
+  static_assert(NS * G7_SLOT * 2 <= 160 * 1024, "LDS");
+  __shared__ __attribute__((aligned(16))) bf16_t smem[NS * G7_SLOT];
+
+  const int lane = threadIdx.x & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wr = wid >> 1, wc = wid & 1;
+  const int ar = wr * 128, bc = wc * 128;
+
+  const int local = g7_local(blockIdx.x, pl.grid);
+  const int nmine = local < pl.units ? (pl.units - local + pl.grid - 1) / pl.grid : 0;
+  if (nmine == 0) return;
+
+  int va[G7_NL], vb[G7_NL];
+  dma_offsets3<32, AK, G7_NL>(va, p.lda, wid, lane);
+  dma_offsets3<32, BK, G7_NL>(vb, p.ldb, wid, lane);
+  const unsigned long long a_step = AK ? 64ull : 32ull * p.lda * 2;
+  const unsigned long long b_step = BK ? 64ull : 32ull * p.ldb * 2;
+
+  // ---- DMA issue cursor (unit, slice, ring slot, byte offsets), all wave-uniform.  The
+  // descriptor of a slice starts at its k-offset and ends with the operand (host: < 4 GiB), so
+  // rows beyond the stored extent land in LDS as zeros.
+  int is_u = 0, is_k = 0, is_slot = 0;
+  unsigned long long is_aoff = 0, is_boff = 0;
+  auto set_org = [&](int ui) {
+    int m0, n0;
+    g7_tile(pl, local + ui * pl.grid, m0, n0);
+    is_aoff = AK ? (unsigned long long)m0 * p.lda * 2 : (unsigned long long)m0 * 2;
+    is_boff = BK ? (unsigned long long)n0 * p.ldb * 2 : (unsigned long long)n0 * 2;
+  };
+  set_org(0);
+  __amdgpu_buffer_rsrc_t rsa, rsb;
+  const bf16_t* is_lds = smem;
+  auto prep = [&]() {  // descriptors + LDS slot of the slice the cursor points at
+    const bool valid = is_u < nmine;
+    const unsigned long long la = a_bytes - is_aoff, lb = b_bytes - is_boff;
+    const unsigned na = valid ? ((la >> 32) ? 0xffffffffu : (unsigned)la) : 0u;
+    const unsigned nb = valid ? ((lb >> 32) ? 0xffffffffu : (unsigned)lb) : 0u;
+    rsa = __builtin_amdgcn_make_buffer_rsrc((void*)((const char*)p.A + is_aoff), 0, na, 0x00020000);
+    rsb = __builtin_amdgcn_make_buffer_rsrc((void*)((const char*)p.B + is_boff), 0, nb, 0x00020000);
+    is_lds = smem + is_slot * G7_SLOT;
+  };
+  auto piece = [&](int i) {  // the pieces of one slice: A then B, NL each
+    if (i < G7_NL) g7_piece(rsa, va[i], is_lds + (wid * G7_NL + i) * 512);
+    else g7_piece(rsb, vb[i - G7_NL], is_lds + G7_TA + (wid * G7_NL + i - G7_NL) * 512);
+  };
+  auto advance = [&]() {
+    is_slot = is_slot + 1 == NS ? 0 : is_slot + 1;
+    is_aoff += a_step;
+    is_boff += b_step;
+    if (++is_k == pl.nk) {
+      is_k = 0;
+      ++is_u;
+      if (is_u < nmine) set_org(is_u);
+    }
+  };
+
+  // prologue: slices 0 .. DIST-1, then the descriptors of slice DIST for body 0
+#pragma unroll
+  for (int s = 0; s < DIST; ++s) {
+    prep();
+#pragma unroll
+    for (int i = 0; i < 2 * G7_NL; ++i) piece(i);
+    advance();
+  }
+  prep();
+
+  floatx4 acc[8][8];  // written first by each tile's FIRST body
+
+  // slice 0 landed (DIST-1 slices younger) -> frags(0)
+  g7_wait<(DIST - 1) * 2 * G7_NL>();
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+  bf16x8 a0[8], b0[8], a1[8], b1[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) a0[i] = frag3<32, AK>(smem, ar + 16 * i, 0, lane);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) b0[j] = frag3<32, BK>(smem + G7_TA, bc + 16 * j, 0, lane);
+  // slice 1 landed -> its slot may be read in body(0)
+  g7_wait<(DIST - 2) * 2 * G7_NL>();
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+
+  int rd_slot = 1;          // slot of slice q+1
+  int credit = 0;           // bodies left during which the last epilogue's stores may stay in flight
+
+  // one slice: MFMAs on (ac, bcur), reads of slice q+1 into (an, bn), DMA of slice q+DIST,
+  // then slice q+2 landed (younger: slices q+3 .. q+DIST, plus a recent epilogue's stores) +
+  // barrier.  nk is even (host: K % 64 == 0), so every tile starts on register set 0.
+#define G7_MFMA_ROW(i_, ac, bcur, FIRST)                                                            \
+  _Pragma("unroll") for (int j = 0; j < 8; ++j) acc[i_][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(  \
+      bcur[j], ac[i_], (FIRST) ? floatx4{0.f, 0.f, 0.f, 0.f} : acc[i_][j], 0, 0, 0)
+  // DMA piece placement inside a body (SCHED): 0 = piece g at the head of group g, 1 = four
+  // pieces at the head of groups 0 and 4, 2 = two pieces at the head of every even group,
+  // 3 = piece g at the tail of group g, 4 = all eight at the head of group 0
+  auto piece_sched = [&](int g, bool tail) {
+    if (pl.debug & 2) return;
+    if (SCHED == 0 && !tail) piece(g);
+    if (SCHED == 3 && tail) piece(g);
+    if (SCHED == 2 && !tail && !(g & 1)) { piece(g); piece(g + 1); }
+    if (SCHED == 1 && !tail && !(g & 3)) { piece(g); piece(g + 1); piece(g + 2); piece(g + 3); }
+    if (SCHED == 4 && !tail && g == 0) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) piece(i);
+    }
+  };
+  // one slice: MFMAs on (ac, bcur) -- FIRST: a tile's first slice, accumulating onto zero (an
+  // inline-constant C operand: no accumulator clearing between tiles) --, reads of slice q+1
+  // into (an, bn), DMA of slice q+DIST, then slice q+2 landed (younger: slices q+3 .. q+DIST,
+  // plus a recent epilogue's stores) + barrier.  nk is even (host: K % 64 == 0), so every tile
+  // starts on register set 0.
+#define G7_BODY(ac, bcur, an, bn, FIRST)                                                            \
+  do {                                                                                              \
+    const bf16_t* la_ = smem + rd_slot * G7_SLOT;                                                   \
+    _Pragma("unroll") for (int i = 0; i < 8; ++i) {                                                 \
+      piece_sched(i, false);                                                                        \
+      an[i] = frag3<32, AK>(la_, ar + 16 * i, 0, lane);                                             \
+      bn[i] = frag3<32, BK>(la_ + G7_TA, bc + 16 * i, 0, lane);                                     \
+      G7_MFMA_ROW(i, ac, bcur, FIRST);                                                              \
+      piece_sched(i, true);                                                                         \
+      if (i == 7) { /* next body's descriptors, in the shadow of this group's MFMAs */           \
+        advance();                                                                                  \
+        prep();                                                                                     \
+      }                                                                                             \
+      __builtin_amdgcn_sched_barrier(0);                                                            \
+    }                                                                                               \
+    rd_slot = rd_slot + 1 == NS ? 0 : rd_slot + 1;                                                  \
+    if (credit > 0) {                                                                               \
+      --credit;                                                                                     \
+      if (pl.store_cnt >= 48) g7_wait<(DIST - 2) * 2 * G7_NL + 47>();                               \
+      else g7_wait<(DIST - 2) * 2 * G7_NL + 31>();                                                  \
+    } else {                                                                                        \
+      g7_wait<(DIST - 2) * 2 * G7_NL>();                                                            \
+    }                                                                                               \
+    __builtin_amdgcn_s_barrier();                                                                   \
+    asm volatile("" ::: "memory");                                                                  \
+  } while (0)
+
+  for (int u = 0; u < nmine; ++u) {
+    G7_BODY(a0, b0, a1, b1, true);
+    G7_BODY(a1, b1, a0, b0, false);
+    for (int k = 2; k < pl.nk; k += 2) {
+      G7_BODY(a0, b0, a1, b1, false);
+      G7_BODY(a1, b1, a0, b0, false);
+    }
+    int m0, n0;
+    g7_tile(pl, local + u * pl.grid, m0, n0);
+    if (!(pl.debug & 1)) g7_epilogue<GEN>(p, acc, m0 + ar, n0 + bc, lane);
+    // the stores were issued after this tile's last wait: the next DIST-2 waits (slices whose
+    // DMA is older than the stores) may leave them in flight -- full tiles only (an edge tile
+    // skips stores, and the credit must not exceed what was issued)
+    credit = (pl.store_cnt > 0 && m0 + 256 <= p.M && n0 + 256 <= p.N) ? DIST - 2 : 0;
+  }
+#undef G7_MFMA_ROW
+#undef G7_BODY
+  g7_wait<0>();  // empty-descriptor DMA of the slices past the end: drained before exit
+}
+
+}  // namespace dpc
+
+using namespace dpc;
+
+static inline long long g7_operand_bytes(long long rows, long long cols, long long ld) {
+  if (rows <= 0 || cols <= 0) return 0;
+  return ((rows - 1) * ld + ((cols + 7) / 8) * 8) * 2;
+}
+
+template <int NS, bool GEN, int SCHED>
+static void g7_launch(const GemmArgs* a, const G7Plan& pl, hipStream_t stream, unsigned long long ab,
+                      unsigned long long bb) {
+  dim3 grid(pl.grid), block(256);
+  if (a->a_kmaj && a->b_kmaj) hipLaunchKernelGGL((gemm7_kernel<NS, GEN, SCHED, true, true>), grid, block, 0, stream, *a, ab, bb, pl);
+  else if (a->a_kmaj) hipLaunchKernelGGL((gemm7_kernel<NS, GEN, SCHED, true, false>), grid, block, 0, stream, *a, ab, bb, pl);
+  else if (!a->b_kmaj) hipLaunchKernelGGL((gemm7_kernel<NS, GEN, SCHED, false, false>), grid, block, 0, stream, *a, ab, bb, pl);
+  else hipLaunchKernelGGL((gemm7_kernel<NS, GEN, SCHED, false, true>), grid, block, 0, stream, *a, ab, bb, pl);
+}
+
+// Returns -1 if the product does not meet v7's requirements (caller falls back), else the
+// hipError_t of the launch.  Requirements: k-major operands hold exactly K (% 64 == 0) columns,
+// K % 64 == 0 (an even slice count), N % 8 == 0, 16-B aligned C / bias / residual, 8-B aligned aux, no split-K.
+DPC_API int dpc_gemm7(const GemmArgs* a, int ns, int persistent, int sched, hipStream_t stream) {
+  if (a->M <= 0 || a->N <= 0) return 0;
+  const long long ab = g7_operand_bytes(a->a_r, a->a_c, a->lda);
+  const long long bb = g7_operand_bytes(a->b_r, a->b_c, a->ldb);
+  auto al = [](const void* q, int b) { return ((uintptr_t)q % b) == 0; };
+  const bool kmaj_ok = (!a->a_kmaj || (a->a_c == a->K && a->K % 64 == 0)) &&
+                       (!a->b_kmaj || (a->b_c == a->K && a->K % 64 == 0));
+  const bool ok = kmaj_ok && a->K > 0 && a->K % 64 == 0 && ab > 0 && bb > 0 && a->N % 8 == 0 && a->ldc % 8 == 0 &&
+                  a->ldr % 4 == 0 && a->ld_aux_in % 4 == 0 && a->ld_aux_out % 4 == 0 && al(a->C, 16) &&
+                  al(a->bias, 16) && al(a->residual, 16) && al(a->aux_in, 8) && al(a->aux_out, 8) &&
+                  al(a->colsum, 4);
+  if (!ok) return -1;
+  G7Plan pl;
+  pl.tiles_m = (a->M + 255) / 256;
+  pl.tiles_n = (a->N + 255) / 256;
+  pl.units = pl.tiles_m * pl.tiles_n;
+  // persistent: one workgroup per CU streams its tiles through one ring; otherwise one tile per
+  // workgroup (a finished workgroup's stores drain while its successor on the CU starts)
+  pl.grid = (persistent && pl.units > 256) ? 256 : pl.units;
+  pl.nk = (a->K + G7_KB - 1) / G7_KB;
+  const bool plain = !a->bias && !a->act_bwd && !a->aux_out && !a->act && !a->residual && !a->colsum && !a->accumulate;
+  pl.store_cnt = plain ? (a->out_f32 ? 64 : 32) : 0;
+  static int dbg = -1;
+  if (dbg < 0) dbg = getenv("DPC_G7_DEBUG") ? atoi(getenv("DPC_G7_DEBUG")) : 0;
+  pl.debug = dbg;
+  if (dbg & 1) pl.store_cnt = 0;
+  if (plain) {
+    if (sched == 1) g7_launch<5, false, 1>(a, pl, stream, ab, bb);
+    else if (sched == 2) g7_launch<5, false, 2>(a, pl, stream, ab, bb);
+    else if (sched == 3) g7_launch<5, false, 3>(a, pl, stream, ab, bb);
+    else if (sched == 4) g7_launch<5, false, 4>(a, pl, stream, ab, bb);
+    else if (ns == 4) g7_launch<4, false, 0>(a, pl, stream, ab, bb);
+    else g7_launch<5, false, 0>(a, pl, stream, ab, bb);
+  } else {
+    if (ns == 4) g7_launch<4, true, 0>(a, pl, stream, ab, bb);
+    else g7_launch<5, true, 0>(a, pl, stream, ab, bb);
+  }
+  return (int)hipGetLastError();
+}

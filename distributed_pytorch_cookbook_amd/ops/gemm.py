@@ -131,10 +131,12 @@ def _blas_plain(a, b, a_kmaj, b_kmaj, out, M, N, K, alpha, alpha_t) -> bool:
 # signature missing from the table the first time it runs eagerly (never inside a HIP-graph
 # capture: outputs are cloned, candidates timed with HIP events, best of 3 x 5 launches) and
 # writes the merged table to ``DPC_GEMM_TUNE_OUT`` (default: the in-package file) at exit.
-_TUNE_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "gemm_tuned.json")
+_TUNE_PATH = os.environ.get("DPC_GEMM_TABLE_PATH") or os.path.join(
+    os.path.dirname(os.path.abspath(__file__)), "gemm_tuned.json")
 _TUNE = os.environ.get("DPC_GEMM_TUNE", "0") == "1"
 _USE_TABLE = os.environ.get("DPC_GEMM_TABLE", "1") == "1"
-_CANDIDATES = (0, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12)  # 0 = the dispatcher policy
+# 0 = the dispatcher policy; 16 / 19 / 20 = the persistent 4-wave 256x256 kernel (gemm7.hip)
+_CANDIDATES = (0, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 16, 19, 20)
 _TUNE_MAX_OUT_BYTES = 1 << 30
 
 

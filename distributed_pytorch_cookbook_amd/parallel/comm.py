@@ -133,6 +133,16 @@ def reduce_scatter_into(out, inp, op=dist.ReduceOp.SUM, group=None, async_op=Fal
     return dist.reduce_scatter_tensor(out, inp, op=op, group=group, async_op=async_op)
 
 
+def gather_objects(obj):
+    """Every rank's ``obj`` as a list indexed by rank (a single-element list without a
+    process group).  Collective: call on every rank."""
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+        return [obj]
+    out = [None] * dist.get_world_size()
+    dist.all_gather_object(out, obj)
+    return out
+
+
 def all_reduce_scalars(values: list[float | torch.Tensor], device, group=None, op="sum"):
     """Reduce several scalars in ONE collective (reference issues one per metric,
     main-ddp.py:159-160)."""

@@ -39,8 +39,30 @@ def test_fault_injection_then_resume(tmp_path):
     st = load_train_state(path)
     assert st is not None and int(st["optimizer"]["step"]) == 4  # saved at steps 2 and 4
     assert st["optimizer"]["exp_avg"].abs().sum() > 0 and "rng" in st
-    trainer, _ = run("single", [*TINY, "--max_steps", "2", "--resume", "latest", "--checkpoint_dir", str(ck),
+    # --max_steps counts batches of the epoch: the resumed run skips the 4 already trained
+    trainer, _ = run("single", [*TINY, "--max_steps", "6", "--resume", "latest", "--checkpoint_dir", str(ck),
                                 "--no_save"])
     assert trainer.engine.step_count == 4 + 2
     w = dict(trainer.engine.lm().state_dict())["lm_head.weight"]
     assert torch.isfinite(w).all()
+
+
+def test_resume_mid_epoch_matches_uninterrupted(tmp_path):
+    """A run killed mid-epoch and resumed from its --save_every checkpoint trains the same
+    batches, in the same order, as an uninterrupted run: identical final weights."""
+    from distributed_pytorch_cookbook_amd.recipes import run
+
+    full, _ = run("single", [*TINY, "--max_steps", "8", "--no_save"])
+    w_full = {k: v.detach().clone() for k, v in full.engine.lm().state_dict().items()}
+    ck = tmp_path / "ckpt"
+    env = dict(os.environ, DPC_FAULT_STEP="5", PYTHONPATH=ROOT)
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "main-single.py"), *TINY, "--max_steps", "8",
+                        "--save_every", "2", "--checkpoint_dir", str(ck)],
+                       cwd=tmp_path, env=env, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 13, (r.returncode, r.stdout[-2000:], r.stderr[-2000:])
+    resumed, _ = run("single", [*TINY, "--max_steps", "8", "--resume", "latest", "--checkpoint_dir", str(ck),
+                                "--no_save"])
+    assert resumed.skip_batches == 4 and resumed.engine.step_count == 8
+    w_res = resumed.engine.lm().state_dict()
+    for k, v in w_full.items():
+        assert torch.equal(v, w_res[k]), k

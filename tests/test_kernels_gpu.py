@@ -96,6 +96,70 @@ def test_gemm_impls_with_epilogue(impl, a_kmaj, b_kmaj, M, N, K):
     assert rel_err(ob, a.float() @ b.float().t()) < 1e-2
 
 
+def _store(x, kmaj):
+    """Operand storage as the model lays it out: k-major rows (or mn-major columns) padded
+    to a multiple of 8 elements."""
+    r, c = x.shape
+    if kmaj:
+        buf = torch.zeros(r, (c + 7) // 8 * 8, device=dev, dtype=x.dtype)
+        buf[:, :c] = x
+        return buf[:, :c]
+    buf = torch.zeros(c, (r + 7) // 8 * 8, device=dev, dtype=x.dtype)
+    buf[:, :r] = x.t()
+    return buf[:, :r]
+
+
+@pytest.mark.parametrize("impl", [13, 14, 15, 16])
+@pytest.mark.parametrize("a_kmaj,b_kmaj", [(True, True), (True, False), (False, False), (False, True)])
+@pytest.mark.parametrize("M,N,K", [(300, 264, 128), (1023, 768, 768), (4096, 4352, 256), (513, 2304, 1536)])
+def test_gemm_v6_v7(impl, a_kmaj, b_kmaj, M, N, K):
+    """The 256x256 kernels on the shapes they serve: ragged M, N % 8 == 0, K % 64 == 0, and
+    (4096 x 4352: 272 tiles) more tiles than CUs, so a persistent v7 workgroup streams two
+    tiles through one ring -- plain bf16 / f32 outputs, accumulate and every fused epilogue."""
+    torch.manual_seed(3)
+    a = torch.randn(M, K, device=dev).bfloat16()
+    b = torch.randn(N, K, device=dev).bfloat16()
+    A, B = _store(a, a_kmaj), _store(b, b_kmaj)
+    ref = a.float() @ b.float().t()
+    bias = torch.randn(N, device=dev)
+    res = torch.randn(M, N, device=dev)
+    z = torch.randn(M, N, device=dev).bfloat16()
+    aux = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+    cs = torch.zeros(N, device=dev)
+    acc0 = torch.randn(M, N, device=dev)
+    acc = acc0.clone()
+    _lib.set_gemm_impl(impl)
+    try:
+        ob = gemm(A, B, a_kmaj=a_kmaj, b_kmaj=b_kmaj)
+        of = gemm(A, B, a_kmaj=a_kmaj, b_kmaj=b_kmaj, out_dtype=torch.float32, alpha=0.5)
+        gemm(A, B, a_kmaj=a_kmaj, b_kmaj=b_kmaj, out=acc, accumulate=True)
+        out = gemm(A, B, a_kmaj=a_kmaj, b_kmaj=b_kmaj, bias=bias, act=2, act_bwd=1, aux_in=z,
+                   aux_out=aux, residual=res, colsum=cs, out_dtype=torch.float32)
+        cs2 = torch.zeros(N, device=dev)
+        od = gemm(A, B, a_kmaj=a_kmaj, b_kmaj=b_kmaj, act_bwd=2, aux_in=z, colsum=cs2)
+        og = gemm(A, B, a_kmaj=a_kmaj, b_kmaj=b_kmaj, bias=bias, act=2, aux_out=torch.empty_like(aux))
+    finally:
+        _lib.set_gemm_impl(-1)
+    assert rel_err(ob, ref) < 1e-2
+    assert rel_err(of, 0.5 * ref) < 2e-3
+    assert rel_err(acc - acc0, ref) < 2e-3
+    ref_out = torch.empty(M, N, device=dev)
+    aux_r = torch.empty_like(aux)
+    cs_r = torch.zeros(N, device=dev)
+    _gemm_ref(a, b, True, True, ref_out, bias, 2, 1, z, aux_r, res, 1.0, None, False, cs_r)
+    assert rel_err(out, ref_out) < 2e-3
+    assert rel_err(aux, aux_r) < 1e-2
+    assert rel_err(cs, cs_r) < 2e-3
+    od_r = torch.empty(M, N, device=dev)
+    cs2_r = torch.zeros(N, device=dev)
+    _gemm_ref(a, b, True, True, od_r, None, 0, 2, z, None, None, 1.0, None, False, cs2_r)
+    assert rel_err(od, od_r) < 1e-2
+    assert rel_err(cs2, cs2_r) < 2e-3
+    og_r = torch.empty(M, N, device=dev)
+    _gemm_ref(a, b, True, True, og_r, bias, 2, 0, None, torch.empty_like(aux), None, 1.0, None, False)
+    assert rel_err(og, og_r) < 1e-2
+
+
 @pytest.mark.parametrize("impl", [2, 4, 7, 10, 11, 12])
 @pytest.mark.parametrize("splits", [2, 3, 8])
 @pytest.mark.parametrize("M,N,K", [(77, 1000, 4160), (600, 520, 8192), (2304, 136, 4096)])
