@@ -62,18 +62,21 @@ def build_parser(recipe: str = "single") -> argparse.ArgumentParser:
     p.add_argument("--bucket_mb", type=float, default=128.0, help="DDP gradient bucket size")
     p.add_argument("--reduce_dtype", type=str, default="fp32", choices=["fp32", "bf16"])
     p.add_argument("--no_overlap", action="store_true", help="all-reduce after backward instead of during")
-    p.add_argument("--comm", default=os.environ.get("DPC_COMM", "torch"), choices=["torch", "native"],
-                   help="gradient all-reduce through torch's nccl process group or the native C++ RCCL "
-                        "communicator (parallel/native_comm.py)")
+    p.add_argument("--comm", default=os.environ.get("DPC_COMM", "auto"), choices=["auto", "torch", "native"],
+                   help="collective transport of every engine (parallel/transport.py): the native C++ RCCL "
+                        "communicator on its own HIP stream (auto = on a GPU), or torch.distributed")
     p.add_argument("--profile", type=str, default=None, help="write a torch.profiler trace here")
     p.add_argument("--log_jsonl", type=str, default=None, help="append step metrics as JSON lines")
     p.add_argument("--cpu", action="store_true", help="force CPU (gloo) even if a GPU is present")
     if recipe in ("pipe", "pipe_ddp"):
         p.add_argument("--pp_size", type=int, default=0, help="pipeline stages (0 = world size / dp)")
-        p.add_argument("--num_microbatches", type=int, default=0, help="0 = 2 x stages")
+        p.add_argument("--num_microbatches", type=int, default=0, help="0 = 4 x stages")
         p.add_argument("--schedule", type=str, default="1f1b", choices=["1f1b", "gpipe"])
+        p.add_argument("--pp_comm_dtype", type=str, default="fp32", choices=["fp32", "bf16"],
+                       help="wire format of the stage-boundary activations and their gradients")
     if recipe == "pipe_ddp":
-        p.add_argument("--dp_size", type=int, default=0, help="data-parallel replicas per stage")
+        p.add_argument("--dp_size", type=int, default=0,
+                       help="data-parallel replicas per stage (0 = world size / 2: PP = 2 x DP = N / 2)")
     if recipe == "fsdp":
         p.add_argument("--prefetch", type=int, default=1, help="units all-gathered ahead")
         p.add_argument("--no_reshard_after_forward", action="store_true")

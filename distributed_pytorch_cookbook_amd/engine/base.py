@@ -60,3 +60,69 @@ class Engine:
     @property
     def step_count(self) -> int:
         return 0
+
+
+class GraphedStep:
+    """The whole training step of an engine -- memset of the gradients, forward, backward with
+    its collectives, optimizer -- captured once into ONE HIP graph and replayed: the
+    cookbook's meaning of the reference's ``torch.compile`` (``/root/reference/main-ddp.py:60-61``,
+    ``main-fsdp.py:74-75``, ``main-pipe.py:108-109``), without Inductor / Triton.
+
+    Call 1 for an input signature runs eagerly (lazy init, allocator and communicator
+    warm-up); call 2 captures the step against static input buffers and replays it; later
+    calls copy the batch into the static buffers and replay.  The optimizers read their step
+    count from a device counter (``FlatAdamW.device_step``), so a replay applies the right
+    bias corrections.  Collectives must be capturable (native RCCL transport, or none at one
+    rank).  If capture fails the engine stays eager and says so."""
+
+    def __init__(self, engine, optimizers):
+        self.engine = engine
+        self.opts = list(optimizers)
+        self.enabled = True
+        self.graph = None
+        self.key = None
+        self.static = None
+        self.loss = None
+
+    def __call__(self, body, batch, targets):
+        if not self.enabled:
+            return body(batch, targets)
+        mask = batch.get("mask")
+        key = (tuple(batch["input_ids"].shape), mask is None)
+        if self.graph is not None and key == self.key:
+            st = self.static
+            st["ids"].copy_(batch["input_ids"], non_blocking=True)
+            st["pos"].copy_(batch["position_ids"], non_blocking=True)
+            st["tg"].copy_(targets, non_blocking=True)
+            if mask is not None:
+                st["mask"].copy_(mask, non_blocking=True)
+            self.graph.replay()
+            for o in self.opts:
+                o.step_count += 1
+            return None if self.loss is None else self.loss.clone()
+        if self.key != key:  # first call for this signature: eager (warm-up)
+            self.key = key
+            self.graph = None
+            return body(batch, targets)
+        st = {"ids": batch["input_ids"].clone(), "pos": batch["position_ids"].clone(),
+              "tg": targets.clone(), "mask": None if mask is None else mask.clone()}
+        self.static = st
+        for o in self.opts:
+            o.device_step = True
+        g = torch.cuda.CUDAGraph()
+        torch.cuda.synchronize()
+        try:
+            with torch.cuda.graph(g):
+                b = {"input_ids": st["ids"], "position_ids": st["pos"], "mask": st["mask"]}
+                self.loss = body(b, st["tg"])
+        except Exception as exc:  # capture not possible: stay eager
+            for o in self.opts:
+                o.device_step = False
+            self.enabled = False
+            if self.engine.is_logger:
+                print(f"[hip-graph] capture failed ({exc!r}); running eagerly")
+            torch.cuda.synchronize()
+            return body(batch, targets)
+        self.graph = g
+        g.replay()
+        return None if self.loss is None else self.loss.clone()

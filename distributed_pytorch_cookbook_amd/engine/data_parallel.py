@@ -17,7 +17,7 @@ from ..ops.optim import FlatAdamW
 from ..parallel import comm
 from ..parallel.ddp import DDPStore
 from ..parallel.store import LocalStore
-from .base import Engine
+from .base import Engine, GraphedStep
 
 
 class DataParallelEngine(Engine):
@@ -25,17 +25,19 @@ class DataParallelEngine(Engine):
 
     def __init__(self, model, device, lr: float, group=None, bucket_mb: float = 128.0,
                  reduce_dtype=torch.float32, overlap: bool = True, compute_dtype=None,
-                 graph: bool = False, native_comm: bool = False, grad_scaler: bool = False):
+                 graph: bool = False, comm_kind: str | None = None, grad_scaler: bool = False,
+                 force_ddp_store: bool = False):
         self.device = torch.device(device)
         self.model = model
         self.dp_group = group
         self.dp_world = comm.world_size(group)
         self.dp_rank = comm.rank(group)
         self.is_logger = comm.rank() == 0
-        if self.dp_world > 1:
+        if self.dp_world > 1 or force_ddp_store:
+            # (force_ddp_store: the bucketed store and its transport at one rank -- tests)
             self.store = DDPStore(model, device, group=group, bucket_mb=bucket_mb,
                                   reduce_dtype=reduce_dtype, overlap=overlap, compute_dtype=compute_dtype,
-                                  native=native_comm)
+                                  comm_kind=comm_kind)
         else:
             self.store = LocalStore(model, device, compute_dtype=compute_dtype)
         self.opt = FlatAdamW(self.store.master, self.store.grads, lr=lr, shadow=self.store.shadow)
@@ -43,9 +45,11 @@ class DataParallelEngine(Engine):
             from ..ops.amp import GradScaler
 
             self.scaler = GradScaler(self.device)
-        self.graph = graph and self.device.type == "cuda" and self.dp_world == 1
-        self._graph = None
-        self._gkey = None
+        # HIP-graph "compile": at one rank, or across ranks when the gradient all-reduces ride
+        # the capturable native RCCL transport
+        tp = getattr(self.store, "tp", None)
+        self.graph = graph and self.device.type == "cuda" and (self.dp_world == 1 or (tp is not None and tp.capturable()))
+        self._stepper = GraphedStep(self, [self.opt])
 
     # ------------------------------------------------------------------ training
     def _step_body(self, batch, targets):
@@ -55,13 +59,13 @@ class DataParallelEngine(Engine):
         if self.scaler is not None:
             # the non-finite check needs every bucket reduced before any parameter moves;
             # all-reduced gradients are identical on every rank, so is the flag
-            if self.dp_world > 1:
+            if isinstance(self.store, DDPStore):
                 self.store.finish_grads()
             self.scaler.check(self.store.grads)
             self.opt.step(grad_scale=1.0 / self.dp_world, **self.scaler.opt_kwargs(self.opt))
             self.scaler.update()
             return out.loss.detach()
-        if self.dp_world > 1 and self.store.master.is_cuda:
+        if isinstance(self.store, DDPStore) and self.store.tp.active and self.store.master.is_cuda:
             # bucket by bucket: AdamW of the buckets already reduced runs on the compute stream
             # while the last ones (the embeddings, whose backward comes last) are still being
             # all-reduced on the comm stream
@@ -74,7 +78,7 @@ class DataParallelEngine(Engine):
                 self.opt.update(lo, hi, grad_scale=1.0 / self.dp_world)
             st.reset_buckets()
             return out.loss.detach()
-        if self.dp_world > 1:
+        if isinstance(self.store, DDPStore):
             self.store.finish_grads()
         self.opt.step(grad_scale=1.0 / self.dp_world)
         return out.loss.detach()
@@ -82,49 +86,7 @@ class DataParallelEngine(Engine):
     def train_step(self, batch, targets):
         if not self.graph:
             return self._step_body(batch, targets)
-        return self._graph_step(batch, targets)
-
-    def _graph_step(self, batch, targets):
-        """The whole step (memset of the grads, forward, backward, AdamW) as ONE HIP graph.
-
-        Call 1 for a given input signature runs eagerly (lazy init, allocator warm-up), call 2
-        captures the step into a graph against static input buffers and replays it, later
-        calls copy the batch into the static buffers and replay.  AdamW reads its step count
-        from a device counter, so replays apply the right bias corrections."""
-        mask = batch.get("mask")
-        key = (tuple(batch["input_ids"].shape), mask is None)
-        if self._graph is not None and key == self._gkey:
-            self._static["ids"].copy_(batch["input_ids"], non_blocking=True)
-            self._static["pos"].copy_(batch["position_ids"], non_blocking=True)
-            self._static["tg"].copy_(targets, non_blocking=True)
-            if mask is not None:
-                self._static["mask"].copy_(mask, non_blocking=True)
-            self._graph.replay()
-            self.opt.step_count += 1
-            return self._static_loss.clone()
-        if self._gkey != key:  # first call for this signature: eager (warm-up)
-            self._gkey = key
-            self._graph = None
-            return self._step_body(batch, targets)
-        st = {"ids": batch["input_ids"].clone(), "pos": batch["position_ids"].clone(),
-              "tg": targets.clone(), "mask": None if mask is None else mask.clone()}
-        self._static = st
-        self.opt.device_step = True
-        g = torch.cuda.CUDAGraph()
-        torch.cuda.synchronize()
-        try:
-            with torch.cuda.graph(g):
-                b = {"input_ids": st["ids"], "position_ids": st["pos"], "mask": st["mask"]}
-                self._static_loss = self._step_body(b, st["tg"])
-        except Exception as exc:  # capture not possible: stay eager
-            self.opt.device_step = False
-            self.graph = False
-            if self.is_logger:
-                print(f"[hip-graph] capture failed ({exc!r}); running eagerly")
-            return self._step_body(batch, targets)
-        self._graph = g
-        self._graph.replay()
-        return self._static_loss.clone()
+        return self._stepper(self._step_body, batch, targets)
 
     @torch.no_grad()
     def eval_step(self, batch, targets):

@@ -13,7 +13,7 @@ import torch
 from ..ops.optim import FlatAdamW
 from ..parallel import comm
 from ..parallel.fsdp import FSDPStore
-from .base import Engine
+from .base import Engine, GraphedStep
 
 
 class FSDPEngine(Engine):
@@ -22,7 +22,8 @@ class FSDPEngine(Engine):
 
     def __init__(self, model, device, lr: float, group=None, prefetch: int = 1,
                  reshard_after_forward: bool = True, cpu_offload: bool = False, compute_dtype=None,
-                 reduce_dtype=torch.float32, grad_scaler: bool = False):
+                 reduce_dtype=torch.float32, grad_scaler: bool = False, graph: bool = False,
+                 comm_kind: str | None = None):
         self.device = torch.device(device)
         self.model = model
         self.dp_group = group
@@ -31,7 +32,7 @@ class FSDPEngine(Engine):
         self.is_logger = comm.rank() == 0
         self.store = FSDPStore(model, device, group=group, compute_dtype=compute_dtype,
                                prefetch=prefetch, reshard_after_forward=reshard_after_forward,
-                               cpu_offload=cpu_offload, reduce_dtype=reduce_dtype)
+                               cpu_offload=cpu_offload, reduce_dtype=reduce_dtype, comm_kind=comm_kind)
         st = self.store
         grad = st.grads_host if st.cpu_offload else st.grads
         self.opt = FlatAdamW(st.master, grad, lr=lr, shadow=st.shadow)
@@ -40,8 +41,18 @@ class FSDPEngine(Engine):
             from ..ops.amp import GradScaler
 
             self.scaler = GradScaler(self.device)
+        # HIP-graph "compile" of the whole sharded step (gathers, reduce-scatters, AdamW);
+        # not with --cpu_offload, whose host optimizer synchronises mid-step
+        self.graph = (graph and self.device.type == "cuda" and not st.cpu_offload
+                      and (st.W == 1 or st.tp.capturable()))
+        self._stepper = GraphedStep(self, [self.opt, self.opt_rep])
 
     def train_step(self, batch, targets):
+        if self.graph:
+            return self._stepper(self._step_body, batch, targets)
+        return self._step_body(batch, targets)
+
+    def _step_body(self, batch, targets):
         st = self.store
         st.zero_grad()
         out = self.model(**batch, targets=targets)

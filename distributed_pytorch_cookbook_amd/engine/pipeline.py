@@ -4,10 +4,13 @@
 Reference: ``/root/reference/main-pipe.py:85-221`` (GPipe via torch Pipe, chunks =
 stages, single process) and ``main-pipe-ddp.py`` (an empty stub).  Here: one process per
 GPU on a (pp, dp) mesh -- rank = stage * dp + replica -- each stage owning a contiguous,
-cost-balanced run of units (``parallel/pipeline.py``), micro-batches scheduled 1F1B
-(default) or GPipe, activations exchanged by grouped RCCL send/recv between neighbouring
-stages, and, for dp > 1, each stage's gradients all-reduced across its replicas with the
-bucketed DDP store once the last micro-batch's backward has produced them.
+cost-balanced run of units (``parallel/pipeline.py``), micro-batches (default 4 x stages)
+executed in exactly the order ``schedule_1f1b`` (default) or ``schedule_gpipe`` gives,
+activations exchanged by asynchronous grouped RCCL send/recv between neighbouring stages
+(``run_schedule``; optional bf16 wire format), and, for dp > 1, each stage's gradients
+all-reduced across its replicas with the bucketed DDP store once the last micro-batch's
+backward has produced them.  The pipeline and replica communicators are ONE native RCCL
+communicator split with ncclCommSplit (``parallel/transport.py``).
 
 The loss is the exact mean over all valid tokens of the batch: micro-batch losses are
 weighted by their share of valid targets (computed on device, no sync).
@@ -22,9 +25,10 @@ from ..ops.optim import FlatAdamW
 from ..parallel import comm
 from ..parallel.ddp import DDPStore
 from ..parallel.fsdp import _placeholder
-from ..parallel.pipeline import P2P, partition, schedule_1f1b, schedule_gpipe, unit_costs
+from ..parallel.pipeline import P2P, partition, run_schedule, schedule_1f1b, schedule_gpipe, unit_costs
 from ..parallel.store import LocalStore
-from .base import Engine
+from ..parallel.transport import TorchTransport, make_mesh_transports
+from .base import Engine, GraphedStep
 
 
 class PipelineEngine(Engine):
@@ -33,7 +37,8 @@ class PipelineEngine(Engine):
 
     def __init__(self, model, device, lr: float, pp: int, dp: int = 1, num_microbatches: int = 0,
                  schedule: str = "1f1b", bucket_mb: float = 128.0, compute_dtype=None,
-                 seq_len: int | None = None, grad_scaler: bool = False):
+                 seq_len: int | None = None, grad_scaler: bool = False, comm_kind: str | None = None,
+                 wire_dtype=None, graph: bool = False):
         self.device = torch.device(device)
         self.model = model
         if grad_scaler:
@@ -46,15 +51,19 @@ class PipelineEngine(Engine):
         self.pp, self.dp = pp, dp
         if world > 1:
             self.pp_group, self.dp_group, self.stage, self.replica, pp_ranks = comm.make_mesh(pp, dp)
+            self.pp_tp, self.dp_tp = make_mesh_transports(self.pp_group, self.dp_group, self.stage,
+                                                          self.replica, self.device, comm_kind)
         else:
             self.pp_group = self.dp_group = None
             self.stage, self.replica, pp_ranks = 0, 0, [0]
+            self.pp_tp = self.dp_tp = TorchTransport(None)
         self.dp_world = dp
         self.dp_rank = self.replica
         self.first = self.stage == 0
         self.last = self.stage == pp - 1
         self.is_logger = comm.rank() == 0
-        self.n_micro = max(1, num_microbatches or 2 * pp)
+        # 4 x stages micro-batches: the 1F1B bubble is (pp - 1) / (M + pp - 1) -- 18 % at pp 8
+        self.n_micro = max(1, num_microbatches or 4 * pp)
         self.schedule = schedule
         S = seq_len or model.max_position_embeddings
         groups = partition(unit_costs(model, S), pp)
@@ -71,22 +80,26 @@ class PipelineEngine(Engine):
                         p.data = _placeholder(p.shape, self.device)
         if dp > 1:
             self.store = DDPStore(model, device, group=self.dp_group, bucket_mb=bucket_mb,
-                                  compute_dtype=compute_dtype, units=self.my_units)
+                                  compute_dtype=compute_dtype, units=self.my_units, transport=self.dp_tp)
         else:
             self.store = LocalStore(model, device, compute_dtype=compute_dtype, units=self.my_units)
         self.store.accum_steps = self.n_micro
         self.opt = FlatAdamW(self.store.master, self.store.grads, lr=lr, shadow=self.store.shadow)
-        self.p2p = P2P(pp_ranks, self.stage, self.device)
+        self.p2p = P2P(self.pp_tp, self.stage, pp, self.device, wire_dtype=wire_dtype)
         self.pp_ranks = pp_ranks
         self.D = model.dim
         assert nunits == len(model.units())
         if world > 1:
             # bring up the communicators before the first (grouped) p2p
             t = torch.zeros(1, device=self.device)
-            if self.pp_group is not None:
-                dist.all_reduce(t, group=self.pp_group)
-            if self.dp_group is not None:
-                dist.all_reduce(t, group=self.dp_group)
+            self.pp_tp.all_reduce(t)
+            self.dp_tp.all_reduce(t)
+        # HIP-graph "compile": the whole step -- every micro-batch's forward / backward, the
+        # asynchronous p2p and the replica all-reduces -- as one graph (single stage, or
+        # capturable native transports)
+        self.graph = graph and self.device.type == "cuda" and (
+            world == 1 or (self.pp_tp.capturable() and (dp == 1 or self.dp_tp.capturable())))
+        self._stepper = GraphedStep(self, [self.opt])
 
     # ------------------------------------------------------------------ pieces
     def _split(self, batch, targets):
@@ -123,6 +136,11 @@ class PipelineEngine(Engine):
 
     # ------------------------------------------------------------------ training
     def train_step(self, batch, targets):
+        if self.graph:
+            return self._stepper(self._step_body, batch, targets)
+        return self._step_body(batch, targets)
+
+    def _step_body(self, batch, targets):
         st = self.store
         st.zero_grad()
         micro, mb = self._split(batch, targets)
@@ -131,7 +149,6 @@ class PipelineEngine(Engine):
         n_total = (targets != -100).sum().float().clamp_min(1.0) if self.last else None
         inputs, outputs = {}, {}
         acc = {"loss": torch.zeros((), device=self.device)} if self.last else {}
-        p2p = self.p2p
 
         def forward(m, x):
             if x is not None:
@@ -156,42 +173,8 @@ class PipelineEngine(Engine):
             x = inputs.pop(m)
             return None if x is None else x.grad
 
-        first, last = self.first, self.last
-        rp = None if first else shape
-        rn = None if last else shape
-        M = self.n_micro
-        if self.schedule == "gpipe":
-            for m in range(M):
-                x, _ = p2p.exchange(recv_prev_shape=rp)
-                y = forward(m, x)
-                p2p.exchange(send_next=y)
-            for m in range(M):
-                _, g = p2p.exchange(recv_next_shape=rn)
-                dx = backward(m, g)
-                p2p.exchange(send_prev=dx)
-        else:
-            warm = min(self.pp - self.stage - 1, M)
-            rem = M - warm
-            for m in range(warm):
-                x, _ = p2p.exchange(recv_prev_shape=rp)
-                y = forward(m, x)
-                p2p.exchange(send_next=y)
-            x = None
-            if rem > 0:
-                x, _ = p2p.exchange(recv_prev_shape=rp)
-            for i in range(rem):
-                y = forward(warm + i, x)
-                _, g = p2p.exchange(send_next=y, recv_next_shape=rn)
-                dx = backward(i, g)
-                if i == rem - 1:
-                    p2p.exchange(send_prev=dx)
-                    x = None
-                else:
-                    x, _ = p2p.exchange(send_prev=dx, recv_prev_shape=rp)
-            for i in range(warm):
-                _, g = p2p.exchange(recv_next_shape=rn)
-                dx = backward(rem + i, g)
-                p2p.exchange(send_prev=dx)
+        order = (schedule_gpipe if self.schedule == "gpipe" else schedule_1f1b)(self.n_micro, self.stage, self.pp)
+        run_schedule(order, self.first, self.last, forward, backward, self.p2p, shape)
         if self.dp > 1:
             st.finish_grads()
         if self.scaler is not None:
@@ -244,7 +227,7 @@ class PipelineEngine(Engine):
             else:
                 eng.p2p.exchange(send_next=x)
             if eng.pp > 1:
-                dist.broadcast(tok, src=eng.pp_ranks[-1], group=eng.pp_group)
+                eng.pp_tp.broadcast(tok, src=eng.pp - 1)
             out = torch.zeros(1, 1, V, device=eng.device)
             out[0, 0, tok[0]] = 1.0
             return out

@@ -1046,8 +1046,8 @@ static void launch_v2(const GemmArgs* a, dim3 grid, hipStream_t stream, unsigned
 // 6-10: v3 (6: 256x256 KB64 x2, 7: 256x256 KB32 x4, 8: 256x128 KB64 x2, 9: 256x128 KB32 x4,
 // 10: 256x128 KB32 x3); 11: v4 (256x256, pipelined k32 ring); 12: v5 (256x256 ping-pong);
 // 13 / 14: v6 (v5 with the DMA spread over both read segments; 4- / 5-slot ring);
-// 15 / 16: v7 (gemm7.hip: persistent one-wave-per-SIMD 256x256, 4- / 5-slot ring);
-// 17 / 18: v7 with one tile per workgroup (4- / 5-slot ring)
+// 16 / 19 / 20: v7 (gemm7.hip: persistent one-wave-per-SIMD 256x256, 5-slot ring; DMA
+// placement 0 / 1 / 2); 17: v7, one unit per workgroup; plain f32 products split K
 static int g_gemm_impl = -1;
 // XCD-aligned split-K mapping (tile_slot): measured ~6 % slower than the default mapping on
 // the GPT-2 weight gradients, so off unless requested (sweeps)
@@ -1087,7 +1087,8 @@ static int policy_impl(const GemmArgs* a) {
   return g_policy[c];
 }
 
-extern "C" int dpc_gemm7(const GemmArgs* a, int ns, int persistent, int sched, hipStream_t stream);
+extern "C" int dpc_gemm7(const GemmArgs* a, int persistent, int sched, int splits, hipStream_t stream);
+extern "C" int dpc_gemm7_ok(const GemmArgs* a);
 
 DPC_API int dpc_gemm(const GemmArgs* a, hipStream_t stream) {
   if (a->M <= 0 || a->N <= 0) return 0;
@@ -1106,6 +1107,15 @@ DPC_API int dpc_gemm(const GemmArgs* a, hipStream_t stream) {
                      al(a->aux_in, 8) && al(a->aux_out, 8) && al(a->colsum, 4);
   int impl = g_gemm_impl;
   if (impl < 0 && a->impl > 0) impl = a->impl;
+  const bool plain_any = !a->bias && !a->residual && !a->aux_in && !a->aux_out && !a->colsum && !a->act &&
+                         !a->act_bwd;
+  if (impl < 0 && plain_any && policy_impl(a) <= 0 && dpc_gemm7_ok(a)) {
+    // products without a fused epilogue -- the QKV / out / LM-head forward, every input
+    // gradient without act', the weight gradients (split K) -- run the persistent 4-wave
+    // kernel (v7); GPT-2 small B=64 shapes on MI355X: 940-1,220 TF/s vs 640-940 for the
+    // 8-wave / 128-wide kernels (bench/gemm_ab.py, profiles/r2_gemm/)
+    impl = 20;
+  }
   if (impl < 0) {
     // Default per operand layout and depth, from the GPT-2 shape sweep on MI355X
     // (bench/kernels.py, profiles/kernels_r1_*.json): forward products with a short K
@@ -1127,17 +1137,18 @@ DPC_API int dpc_gemm(const GemmArgs* a, hipStream_t stream) {
   const bool plain = a->out_f32 && !a->bias && !a->residual && !a->aux_in && !a->aux_out &&
                      !a->colsum && !a->act && !a->act_bwd;
   if (g_gemm_impl < 0 && a->impl <= 0 && v2_ok && plain && !a->a_kmaj && !a->b_kmaj && policy_impl(a) <= 0) {
-    // weight gradient: the 256x256 ping-pong kernel (v5) once there are enough 128x128 tiles
-    // to spread over the k-splits (2304x768 and up: 780-880 TF/s vs 720 for the 3-deep
-    // 128x128 ring, bench/kernels.py on MI355X), else the 2-stage 64-k kernel
+    // weight gradient: the split-K persistent kernel (v7, chosen above when K % 64 == 0) or the
+    // 256x256 ping-pong kernel (v5) once there are enough 128x128 tiles to spread over the
+    // k-splits, else the 2-stage 64-k kernel (768 x 768)
     const int t128 = ((a->M + BM - 1) / BM) * ((a->N + BN - 1) / BN);
-    impl = t128 >= 100 ? 12 : 2;
+    if (t128 < 100) impl = 2;
+    else if (impl != 20) impl = 12;
   }
-  if (impl >= 15 && impl <= 22) {  // v7 (gemm7.hip): 4-wave 256x256, no split-K
+  if (impl >= 15 && impl <= 22) {  // v7 (gemm7.hip): 4-wave 256x256, split-K f32 products
     GemmArgs c = *a;
     c.ksplit = 0;
-    const int rc = impl >= 19 ? dpc_gemm7(&c, 5, 1, impl - 18, stream)
-                              : dpc_gemm7(&c, (impl & 1) ? 4 : 5, impl <= 16, 0, stream);
+    const int sched = impl == 19 ? 1 : (impl == 20 || impl == 17 ? 2 : 0);
+    const int rc = dpc_gemm7(&c, impl != 17, sched, g_force_splits > 0 ? g_force_splits : 0, stream);
     if (rc >= 0) return rc;
     impl = v2_ok ? 2 : 1;  // requirements not met: the 128x128 kernels
   }

@@ -44,9 +44,11 @@ constexpr int G7_NL = G7_TA / 512 / 4; // 1-KiB DMA pieces per wave per operand 
 
 struct G7Plan {
   int tiles_m, tiles_n;
-  int units;   // tiles (no split-K in this kernel)
-  int grid;    // workgroups launched (<= 256: one per CU)
-  int nk;      // k-slices per tile
+  int units;   // tiles x splits (split-major: unit = split * tiles + tile)
+  int grid;    // workgroups launched
+  int nk;      // k-slices per unit (even)
+  int nk_all;  // k-slices of the whole product (slices of a unit past it read zeros)
+  int splits;
   int store_cnt;  // vector-memory ops the epilogue issues per wave-lane (0: unknown -> no credit)
   int debug;      // experiments only (DPC_G7_DEBUG): 1 = no epilogue stores, 2 = no in-loop DMA
 };
@@ -232,10 +234,33 @@ __device__ __forceinline__ void g7_epilogue(const GemmArgs& p, floatx4 (&acc)[8]
   }
 }
 
-template <int NS, bool GEN, int SCHED, bool AK, bool BK>
+// split-K partial tile (non-swapped accumulators: lane l, register r of accumulator (i, j) holds
+// C[mw + 16 i + 4 (l >> 4) + r][nw + 16 j + (l & 15)]): f32 atomic adds, each wave-instruction
+// four rows x 64 contiguous bytes.  The host zeroes C first unless the product accumulates.
+__device__ __forceinline__ void g7_epilogue_atomic(const GemmArgs& p, floatx4 (&acc)[8][8], int mw, int nw,
+                                                   int lane) {
+  float alpha = p.alpha;
+  if (p.alpha_ptr) alpha *= *p.alpha_ptr;
+  float* C = static_cast<float*>(p.C);
+  const int g = lane >> 4, cl = lane & 15;
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int n = nw + 16 * j + cl;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int m = mw + 16 * i + 4 * g + r;
+        if (m < p.M && n < p.N) atomicAdd(C + (long long)m * p.ldc + n, acc[i][j][r] * alpha);
+      }
+    }
+}
+
+// EPI: 0 = plain products (bf16 / f32 C), 1 = every fused epilogue, 2 = split-K f32 atomics.
+template <int EPI, int SCHED, bool AK, bool BK>
 __global__ __launch_bounds__(256, 1) void gemm7_kernel(GemmArgs p, unsigned long long a_bytes,
                                                        unsigned long long b_bytes, G7Plan pl) {
-  constexpr int DIST = NS - 1;
+  constexpr int NS = 5, DIST = NS - 1;
   static_assert(NS * G7_SLOT * 2 <= 160 * 1024, "LDS");
   __shared__ __attribute__((aligned(16))) bf16_t smem[NS * G7_SLOT];
 
@@ -259,17 +284,22 @@ __global__ __launch_bounds__(256, 1) void gemm7_kernel(GemmArgs p, unsigned long
   // rows beyond the stored extent land in LDS as zeros.
   int is_u = 0, is_k = 0, is_slot = 0;
   unsigned long long is_aoff = 0, is_boff = 0;
+  int is_kt0 = 0;  // first k-slice of the cursor's unit
+  const int ntiles = pl.tiles_m * pl.tiles_n;
   auto set_org = [&](int ui) {
+    const int uu = local + ui * pl.grid;
+    const int sp = uu / ntiles;
     int m0, n0;
-    g7_tile(pl, local + ui * pl.grid, m0, n0);
-    is_aoff = AK ? (unsigned long long)m0 * p.lda * 2 : (unsigned long long)m0 * 2;
-    is_boff = BK ? (unsigned long long)n0 * p.ldb * 2 : (unsigned long long)n0 * 2;
+    g7_tile(pl, uu - sp * ntiles, m0, n0);
+    is_kt0 = sp * pl.nk;
+    is_aoff = (AK ? (unsigned long long)m0 * p.lda * 2 : (unsigned long long)m0 * 2) + a_step * is_kt0;
+    is_boff = (BK ? (unsigned long long)n0 * p.ldb * 2 : (unsigned long long)n0 * 2) + b_step * is_kt0;
   };
   set_org(0);
   __amdgpu_buffer_rsrc_t rsa, rsb;
   const bf16_t* is_lds = smem;
   auto prep = [&]() {  // descriptors + LDS slot of the slice the cursor points at
-    const bool valid = is_u < nmine;
+    const bool valid = is_u < nmine && is_kt0 + is_k < pl.nk_all;
     const unsigned long long la = a_bytes - is_aoff, lb = b_bytes - is_boff;
     const unsigned na = valid ? ((la >> 32) ? 0xffffffffu : (unsigned)la) : 0u;
     const unsigned nb = valid ? ((lb >> 32) ? 0xffffffffu : (unsigned)lb) : 0u;
@@ -323,28 +353,27 @@ __global__ __launch_bounds__(256, 1) void gemm7_kernel(GemmArgs p, unsigned long
 
   // one slice: MFMAs on (ac, bcur), reads of slice q+1 into (an, bn), DMA of slice q+DIST,
   // then slice q+2 landed (younger: slices q+3 .. q+DIST, plus a recent epilogue's stores) +
-  // barrier.  nk is even (host: K % 64 == 0), so every tile starts on register set 0.
+  // barrier.  nk is even (padded with all-zero slices), so every unit starts on register set 0.
 #define G7_MFMA_ROW(i_, ac, bcur, FIRST)                                                            \
   _Pragma("unroll") for (int j = 0; j < 8; ++j) acc[i_][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(  \
-      bcur[j], ac[i_], (FIRST) ? floatx4{0.f, 0.f, 0.f, 0.f} : acc[i_][j], 0, 0, 0)
+      EPI == 2 ? ac[i_] : bcur[j], EPI == 2 ? bcur[j] : ac[i_],                                    \
+      (FIRST) ? floatx4{0.f, 0.f, 0.f, 0.f} : acc[i_][j], 0, 0, 0)
   // DMA piece placement inside a body (SCHED): 0 = piece g at the head of group g, 1 = four
-  // pieces at the head of groups 0 and 4, 2 = two pieces at the head of every even group,
-  // 3 = piece g at the tail of group g, 4 = all eight at the head of group 0
+  // pieces at the head of groups 0 and 4, 2 = two pieces at the head of every even group
+  // (measured on MI355X, bench/gemm_ab.py: 1 and 2 beat 0 by 2-6 %; all eight at the head
+  // of the body or one at the tail of each group lost)
   auto piece_sched = [&](int g, bool tail) {
     if (pl.debug & 2) return;
     if (SCHED == 0 && !tail) piece(g);
-    if (SCHED == 3 && tail) piece(g);
+
     if (SCHED == 2 && !tail && !(g & 1)) { piece(g); piece(g + 1); }
     if (SCHED == 1 && !tail && !(g & 3)) { piece(g); piece(g + 1); piece(g + 2); piece(g + 3); }
-    if (SCHED == 4 && !tail && g == 0) {
-#pragma unroll
-      for (int i = 0; i < 8; ++i) piece(i);
-    }
+
   };
   // one slice: MFMAs on (ac, bcur) -- FIRST: a tile's first slice, accumulating onto zero (an
   // inline-constant C operand: no accumulator clearing between tiles) --, reads of slice q+1
   // into (an, bn), DMA of slice q+DIST, then slice q+2 landed (younger: slices q+3 .. q+DIST,
-  // plus a recent epilogue's stores) + barrier.  nk is even (host: K % 64 == 0), so every tile
+  // plus a recent epilogue's stores) + barrier.  nk is even (padded with all-zero slices), so every unit
   // starts on register set 0.
 #define G7_BODY(ac, bcur, an, bn, FIRST)                                                            \
   do {                                                                                              \
@@ -380,13 +409,19 @@ __global__ __launch_bounds__(256, 1) void gemm7_kernel(GemmArgs p, unsigned long
       G7_BODY(a0, b0, a1, b1, false);
       G7_BODY(a1, b1, a0, b0, false);
     }
+    const int uu = local + u * pl.grid;
     int m0, n0;
-    g7_tile(pl, local + u * pl.grid, m0, n0);
-    if (!(pl.debug & 1)) g7_epilogue<GEN>(p, acc, m0 + ar, n0 + bc, lane);
+    g7_tile(pl, uu % ntiles, m0, n0);
+    if (pl.debug & 1) {
+    } else if (EPI == 2) {
+      g7_epilogue_atomic(p, acc, m0 + ar, n0 + bc, lane);
+    } else {
+      g7_epilogue<EPI == 1>(p, acc, m0 + ar, n0 + bc, lane);
+    }
     // the stores were issued after this tile's last wait: the next DIST-2 waits (slices whose
     // DMA is older than the stores) may leave them in flight -- full tiles only (an edge tile
     // skips stores, and the credit must not exceed what was issued)
-    credit = (pl.store_cnt > 0 && m0 + 256 <= p.M && n0 + 256 <= p.N) ? DIST - 2 : 0;
+    credit = (EPI == 0 && pl.store_cnt > 0 && m0 + 256 <= p.M && n0 + 256 <= p.N) ? DIST - 2 : 0;
   }
 #undef G7_MFMA_ROW
 #undef G7_BODY
@@ -402,55 +437,84 @@ static inline long long g7_operand_bytes(long long rows, long long cols, long lo
   return ((rows - 1) * ld + ((cols + 7) / 8) * 8) * 2;
 }
 
-template <int NS, bool GEN, int SCHED>
+template <int EPI, int SCHED>
 static void g7_launch(const GemmArgs* a, const G7Plan& pl, hipStream_t stream, unsigned long long ab,
                       unsigned long long bb) {
   dim3 grid(pl.grid), block(256);
-  if (a->a_kmaj && a->b_kmaj) hipLaunchKernelGGL((gemm7_kernel<NS, GEN, SCHED, true, true>), grid, block, 0, stream, *a, ab, bb, pl);
-  else if (a->a_kmaj) hipLaunchKernelGGL((gemm7_kernel<NS, GEN, SCHED, true, false>), grid, block, 0, stream, *a, ab, bb, pl);
-  else if (!a->b_kmaj) hipLaunchKernelGGL((gemm7_kernel<NS, GEN, SCHED, false, false>), grid, block, 0, stream, *a, ab, bb, pl);
-  else hipLaunchKernelGGL((gemm7_kernel<NS, GEN, SCHED, false, true>), grid, block, 0, stream, *a, ab, bb, pl);
+  if (a->a_kmaj && a->b_kmaj) hipLaunchKernelGGL((gemm7_kernel<EPI, SCHED, true, true>), grid, block, 0, stream, *a, ab, bb, pl);
+  else if (a->a_kmaj) hipLaunchKernelGGL((gemm7_kernel<EPI, SCHED, true, false>), grid, block, 0, stream, *a, ab, bb, pl);
+  else if (!a->b_kmaj) hipLaunchKernelGGL((gemm7_kernel<EPI, SCHED, false, false>), grid, block, 0, stream, *a, ab, bb, pl);
+  else hipLaunchKernelGGL((gemm7_kernel<EPI, SCHED, false, true>), grid, block, 0, stream, *a, ab, bb, pl);
 }
 
 // Returns -1 if the product does not meet v7's requirements (caller falls back), else the
 // hipError_t of the launch.  Requirements: k-major operands hold exactly K (% 64 == 0) columns,
-// K % 64 == 0 (an even slice count), N % 8 == 0, 16-B aligned C / bias / residual, 8-B aligned aux, no split-K.
-DPC_API int dpc_gemm7(const GemmArgs* a, int ns, int persistent, int sched, hipStream_t stream) {
-  if (a->M <= 0 || a->N <= 0) return 0;
+// those of dpc_gemm7_ok.
+// splits: 1 = none, > 1 forced, 0 = automatic (plain f32 products only: the tiles are too few to
+// fill the chip, e.g. weight gradients -- K = tokens, M x N = a weight).
+// Whether v7 takes this product: k-major operands hold exactly K columns with K % 32 == 0 (a
+// slice never straddles a row end; mn-major operands end at row K, so their last slice reads
+// zeros past it), N % 8 == 0, 16-B aligned C / bias / residual, 8-B aligned aux.
+DPC_API int dpc_gemm7_ok(const GemmArgs* a) {
   const long long ab = g7_operand_bytes(a->a_r, a->a_c, a->lda);
   const long long bb = g7_operand_bytes(a->b_r, a->b_c, a->ldb);
   auto al = [](const void* q, int b) { return ((uintptr_t)q % b) == 0; };
-  const bool kmaj_ok = (!a->a_kmaj || (a->a_c == a->K && a->K % 64 == 0)) &&
-                       (!a->b_kmaj || (a->b_c == a->K && a->K % 64 == 0));
-  const bool ok = kmaj_ok && a->K > 0 && a->K % 64 == 0 && ab > 0 && bb > 0 && a->N % 8 == 0 && a->ldc % 8 == 0 &&
-                  a->ldr % 4 == 0 && a->ld_aux_in % 4 == 0 && a->ld_aux_out % 4 == 0 && al(a->C, 16) &&
-                  al(a->bias, 16) && al(a->residual, 16) && al(a->aux_in, 8) && al(a->aux_out, 8) &&
-                  al(a->colsum, 4);
-  if (!ok) return -1;
+  const bool kmaj_ok = (!a->a_kmaj || (a->a_c == a->K && a->K % 32 == 0)) &&
+                       (!a->b_kmaj || (a->b_c == a->K && a->K % 32 == 0)) &&
+                       (a->a_kmaj || a->a_r == a->K) && (a->b_kmaj || a->b_r == a->K);
+  return kmaj_ok && a->K > 0 && ab > 0 && bb > 0 && a->N % 8 == 0 && a->ldc % 8 == 0 && a->ldr % 4 == 0 &&
+         a->ld_aux_in % 4 == 0 && a->ld_aux_out % 4 == 0 && al(a->C, 16) && al(a->bias, 16) &&
+         al(a->residual, 16) && al(a->aux_in, 8) && al(a->aux_out, 8) && al(a->colsum, 4);
+}
+
+// splits: 1 = none, > 1 forced, 0 = automatic (plain f32 products only: the tiles are too few to
+// fill the chip, e.g. weight gradients -- K = tokens, M x N = a weight).
+DPC_API int dpc_gemm7(const GemmArgs* a, int persistent, int sched, int splits, hipStream_t stream) {
+  if (a->M <= 0 || a->N <= 0) return 0;
+  if (!dpc_gemm7_ok(a)) return -1;
+  const long long ab = g7_operand_bytes(a->a_r, a->a_c, a->lda);
+  const long long bb = g7_operand_bytes(a->b_r, a->b_c, a->ldb);
   G7Plan pl;
   pl.tiles_m = (a->M + 255) / 256;
   pl.tiles_n = (a->N + 255) / 256;
-  pl.units = pl.tiles_m * pl.tiles_n;
-  // persistent: one workgroup per CU streams its tiles through one ring; otherwise one tile per
-  // workgroup (a finished workgroup's stores drain while its successor on the CU starts)
+  const int tiles = pl.tiles_m * pl.tiles_n;
+  pl.nk_all = (a->K + G7_KB - 1) / G7_KB;
+  const bool plain = !a->bias && !a->act_bwd && !a->aux_out && !a->act && !a->residual && !a->colsum;
+  const bool splittable = plain && a->out_f32;
+  int s = splits > 0 ? splits : 1;
+  if (splits <= 0 && splittable && tiles < 192) {
+    // fill the chip: time ~ rounds * slices per unit + an atomic epilogue per unit-round
+    // (256 KiB of f32 adds per CU, ~40 slices' worth at the chip's memory-side atomic rate)
+    double best = 1e30;
+    for (int c = 1; c <= 32; ++c) {
+      const int per = 2 * ((pl.nk_all + 2 * c - 1) / (2 * c));
+      if (c > 1 && per < 16) break;
+      const int rounds = (tiles * c + 255) / 256;
+      const double cost = (double)rounds * (per + (c > 1 ? 40.0 : 0.0));
+      if (cost < best - 1e-9) { best = cost; s = c; }
+    }
+  }
+  if (s > 1 && !splittable) return -1;
+  pl.splits = s;
+  pl.nk = 2 * ((pl.nk_all + 2 * s - 1) / (2 * s));  // even: a unit starts on register set 0
+  pl.units = tiles * s;
+  // persistent: one workgroup per CU streams its units through one ring; otherwise one unit
+  // per workgroup
   pl.grid = (persistent && pl.units > 256) ? 256 : pl.units;
-  pl.nk = (a->K + G7_KB - 1) / G7_KB;
-  const bool plain = !a->bias && !a->act_bwd && !a->aux_out && !a->act && !a->residual && !a->colsum && !a->accumulate;
-  pl.store_cnt = plain ? (a->out_f32 ? 64 : 32) : 0;
+  pl.store_cnt = (plain && !a->accumulate && s == 1) ? (a->out_f32 ? 64 : 32) : 0;
   static int dbg = -1;
   if (dbg < 0) dbg = getenv("DPC_G7_DEBUG") ? atoi(getenv("DPC_G7_DEBUG")) : 0;
   pl.debug = dbg;
   if (dbg & 1) pl.store_cnt = 0;
-  if (plain) {
-    if (sched == 1) g7_launch<5, false, 1>(a, pl, stream, ab, bb);
-    else if (sched == 2) g7_launch<5, false, 2>(a, pl, stream, ab, bb);
-    else if (sched == 3) g7_launch<5, false, 3>(a, pl, stream, ab, bb);
-    else if (sched == 4) g7_launch<5, false, 4>(a, pl, stream, ab, bb);
-    else if (ns == 4) g7_launch<4, false, 0>(a, pl, stream, ab, bb);
-    else g7_launch<5, false, 0>(a, pl, stream, ab, bb);
+  if (s > 1) {
+    if (!a->accumulate) hipMemset2DAsync(a->C, (size_t)a->ldc * 4, 0, (size_t)a->N * 4, (size_t)a->M, stream);
+    g7_launch<2, 2>(a, pl, stream, ab, bb);
+  } else if (plain && !a->accumulate) {
+    if (sched == 1) g7_launch<0, 1>(a, pl, stream, ab, bb);
+    else if (sched == 2) g7_launch<0, 2>(a, pl, stream, ab, bb);
+    else g7_launch<0, 0>(a, pl, stream, ab, bb);
   } else {
-    if (ns == 4) g7_launch<4, true, 0>(a, pl, stream, ab, bb);
-    else g7_launch<5, true, 0>(a, pl, stream, ab, bb);
+    g7_launch<1, 2>(a, pl, stream, ab, bb);
   }
   return (int)hipGetLastError();
 }

@@ -61,14 +61,12 @@ def act_grad_ref(z: torch.Tensor, act: int) -> torch.Tensor:
     return torch.ones_like(z)
 
 
-# Vendor path for PLAIN products only (no epilogue beyond a scale: the QKV and logits
-# GEMMs, the input gradients of the QKV / out / up / lm_head projections): hipBLASLt through
-# torch.mm.  Every product with a fused epilogue (bias, activation, act', residual, aux,
-# column sums) and every weight gradient stays on the hand-written dpc_gemm.  On by default
-# (DPC_BLAS_PLAIN=0 turns it off): GPT-2 small dp1 B=32 on one MI355X, 48.4 -> 46.2 ms/step
-# (676K -> 709K tok/s, profiles/r1_v8_blas_ab.txt); in isolation hipBLASLt runs those plain
-# shapes 10-45 % faster than dpc_gemm's best tile (bench/kernels.py).
-_BLAS_PLAIN = os.environ.get("DPC_BLAS_PLAIN", "1") == "1"
+# Optional vendor path for PLAIN products (no epilogue beyond a scale): hipBLASLt through
+# torch.mm.  OFF by default since round 2: the persistent 4-wave kernel (csrc/gemm7.hip) runs
+# every plain product of the training step -- QKV / out / LM-head forward, the input and weight
+# gradients -- and the GPT-2 small step is as fast without the library (profiles/r2_gemm/).
+# DPC_BLAS_PLAIN=1 restores the library path for comparisons.
+_BLAS_PLAIN = os.environ.get("DPC_BLAS_PLAIN", "0") == "1"
 _BLAS_MIN_FLOP = 2 ** 34  # below ~17 GFLOP the choice does not matter: keep dpc_gemm
 
 
@@ -135,9 +133,9 @@ _TUNE_PATH = os.environ.get("DPC_GEMM_TABLE_PATH") or os.path.join(
     os.path.dirname(os.path.abspath(__file__)), "gemm_tuned.json")
 _TUNE = os.environ.get("DPC_GEMM_TUNE", "0") == "1"
 _USE_TABLE = os.environ.get("DPC_GEMM_TABLE", "1") == "1"
-# 0 = the dispatcher policy; 16 / 19 / 20 = the persistent 4-wave 256x256 kernel (gemm7.hip)
-_CANDIDATES = (0, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 16, 19, 20)
-_TUNE_MAX_OUT_BYTES = 1 << 30
+# 0 = the dispatcher policy; 16 / 17 / 19 / 20 = the 4-wave 256x256 kernel (gemm7.hip)
+_CANDIDATES = (0, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 16, 17, 19, 20)
+_TUNE_MAX_OUT_BYTES = 16 << 30  # (the GPT-2 small LM-head logits are 6.6 GB)
 
 
 def _load_table(path: str = _TUNE_PATH) -> dict:

@@ -17,51 +17,36 @@ MI355X-first design:
   bandwidth instead of paying per-call latency 25x per step;
 * the 1/W average is folded into the AdamW kernel (``grad_scale``), so no extra pass;
 * optional bf16 reduction (``reduce_dtype``) halves the bytes on the links;
-* ``native=True`` issues the bucket all-reduces through the C++ RCCL communicator
-  (``parallel/native_comm.py``) on a dedicated high-priority HIP stream ordered with
-  events, instead of torch's process group.
+* the all-reduces go through the engine's ``Transport`` (``parallel/transport.py``): by
+  default the native C++ RCCL communicator on its own high-priority HIP stream, ordered with
+  events (capturable into the step's HIP graph); torch's process group for ``--comm torch``
+  and the gloo CPU tests.
 """
 from __future__ import annotations
 
 import torch
 import torch.distributed as dist
 
-from . import comm
 from .store import LocalStore
-
-
-class _EventWork:
-    """Completion of a collective enqueued on a side stream: ``wait`` orders the caller's
-    current stream after it (no host synchronisation)."""
-
-    def __init__(self, event: torch.cuda.Event):
-        self.event = event
-
-    def wait(self):
-        torch.cuda.current_stream().wait_event(self.event)
+from .transport import Transport, make_transport
 
 
 class DDPStore(LocalStore):
     def __init__(self, model, device, group=None, bucket_mb: float = 128.0,
                  reduce_dtype: torch.dtype = torch.float32, overlap: bool = True,
                  compute_dtype=None, units=None, broadcast_src: int | None = None,
-                 native: bool = False):
+                 transport: Transport | None = None, comm_kind: str | None = None):
         super().__init__(model, device, compute_dtype=compute_dtype, units=units)
         self.group = group
-        self.world = comm.world_size(group)
+        self.tp = transport if transport is not None else make_transport(group, self.master.device, comm_kind)
+        self.world = self.tp.size
         self.reduce_dtype = reduce_dtype
         self.overlap = overlap
-        self.native = None
-        if native and self.world > 1 and self.master.is_cuda:
-            from .native_comm import NativeComm
-
-            self.native = NativeComm(group, device=self.master.device)
-            self._comm_stream = torch.cuda.Stream(device=self.master.device, priority=-1)
-        if self.world > 1:
-            src = broadcast_src if broadcast_src is not None else (
-                dist.get_global_rank(group, 0) if group is not None else 0)
+        if self.tp.active:
+            # the reference DDP constructor's rank-0 parameter broadcast (distributed.py:864)
+            src = broadcast_src if broadcast_src is not None else 0
             with torch.no_grad():
-                comm.broadcast(self.master, src=src, group=group)
+                self.tp.broadcast(self.master, src=src)
             self.refresh_shadow()
         # buckets of whole units in backward order
         cap = int(bucket_mb * 2**20 / 4)
@@ -92,32 +77,19 @@ class DDPStore(LocalStore):
         return lo, hi
 
     def _launch(self, bi):
-        if self.world == 1 or bi in self._works:
+        if not self.tp.active or bi in self._works:
             return
         lo, hi = self._range(bi)
         g = self.grads[lo:hi]
-        if self.native is not None:
-            t = g.to(self.reduce_dtype) if self.reduce_dtype != torch.float32 else g
-            ready = torch.cuda.Event()
-            ready.record()
-            cs = self._comm_stream
-            cs.wait_event(ready)
-            if t is not g:
-                t.record_stream(cs)
-                self._tmp[bi] = t
-            self.native.all_reduce(t, stream=cs)
-            done = torch.cuda.Event()
-            done.record(cs)
-            self._works[bi] = _EventWork(done)
-        elif self.reduce_dtype != torch.float32:
+        if self.reduce_dtype != torch.float32:
             t = g.to(self.reduce_dtype)
             self._tmp[bi] = t
-            self._works[bi] = comm.all_reduce(t, group=self.group, async_op=True)
+            self._works[bi] = self.tp.all_reduce(t, async_op=True)
         else:
-            self._works[bi] = comm.all_reduce(g, group=self.group, async_op=True)
+            self._works[bi] = self.tp.all_reduce(g, async_op=True)
 
     def post_backward(self, u):
-        if self.world == 1:
+        if not self.tp.active:
             return
         bi = self.bucket_of[u]
         self._ready[bi] += 1
@@ -131,13 +103,13 @@ class DDPStore(LocalStore):
 
     def launch_all(self):
         """Enqueue every bucket not launched yet (overlap off, or buckets left partial)."""
-        if self.world > 1:
+        if self.tp.active:
             for bi in range(len(self.buckets)):
                 self._launch(bi)
 
     def wait_bucket(self, bi):
         """Order the current stream after bucket ``bi``'s all-reduce (no host sync)."""
-        if self.world > 1:
+        if self.tp.active:
             self._works[bi].wait()
             if bi in self._tmp:
                 lo, hi = self._range(bi)
@@ -150,7 +122,7 @@ class DDPStore(LocalStore):
 
     def finish_grads(self):
         """Wait for every bucket (launching any not yet launched, e.g. overlap off)."""
-        if self.world > 1:
+        if self.tp.active:
             for bi in range(len(self.buckets)):
                 self._launch(bi)
             for bi in range(len(self.buckets)):

@@ -16,7 +16,13 @@ MI355X-first design:
   stream while the current unit computes; buffers are released after use
   (``reshard_after_forward``) so activation-time memory holds only the prefetch window;
 * backward reduce-scatters each unit's f32 gradient straight into the shard gradient
-  as soon as the unit's backward has written it (overlapped with the next unit);
+  as soon as the unit's backward has written it (overlapped with the next unit), and the
+  full-unit gradient is dropped the moment its reduce-scatter is enqueued (the transport
+  ``record_stream``s it, so the allocator recycles it once the collective has read it):
+  gradient memory is the shards plus the units in flight, not the whole model;
+* with one rank the unit buffers ARE the shards (no gathers, no copies) and the weight
+  gradients accumulate straight into the shard gradient;
+* collectives ride the engine's ``Transport`` (native RCCL on a side stream by default);
 * ``cpu_offload``: master shard and Adam moments live in pinned host memory, the
   optimizer runs on the host, the bf16 shard is copied back asynchronously.
 """
@@ -28,6 +34,7 @@ import torch.distributed as dist
 from ..ops.elementwise import cast_f32_bf16
 from . import comm
 from .store import ALIGN, FlatLayout, ParamStore, default_compute_dtype
+from .transport import Transport, make_transport
 
 
 def _placeholder(shape, device):
@@ -39,11 +46,13 @@ def _placeholder(shape, device):
 class FSDPStore(ParamStore):
     def __init__(self, model, device, group=None, compute_dtype=None, prefetch: int = 1,
                  reshard_after_forward: bool = True, cpu_offload: bool = False,
-                 reduce_dtype: torch.dtype = torch.float32):
+                 reduce_dtype: torch.dtype = torch.float32, transport: Transport | None = None,
+                 comm_kind: str | None = None):
         self.device = torch.device(device)
         self.group = group
-        self.W = comm.world_size(group)
-        self.rank = comm.rank(group)
+        self.tp = transport if transport is not None else make_transport(group, self.device, comm_kind)
+        self.W = self.tp.size
+        self.rank = self.tp.rank
         self.compute_dtype = compute_dtype or default_compute_dtype(self.device)
         self.prefetch = max(0, prefetch)
         self.reshard = reshard_after_forward
@@ -104,8 +113,10 @@ class FSDPStore(ParamStore):
         self._full = {}       # unit -> (buffer, work or None)
         self._vec32 = {}      # unit -> {param id: f32 copy of 1-D params}
         self._gfull = {}      # unit -> f32 full-unit gradient buffer
-        self._rs = {}         # unit -> (work, tmp)
+        self._rs = {}         # unit -> (handle, tmp or None): reduce-scatters in flight
+        self._fresh = set(self.units)  # units whose shard gradient holds no contribution yet
         self._in_backward = False
+        self.peak_live_units = 0  # most full-unit buffers (weights + gradients) alive at once
 
     # ------------------------------------------------------------------ shards
     def shard(self, flat, u):
@@ -123,14 +134,18 @@ class FSDPStore(ParamStore):
     def _gather(self, u):
         if u in self._full or not (0 <= u < self.nunits):
             return
-        buf = torch.empty(self.unit_len[u], dtype=self.compute_dtype, device=self.device)
         sh = self.shard(self.shadow, u)
         if self.W == 1:
-            buf.copy_(sh)
-            self._full[u] = (buf, None)
+            self._full[u] = (sh, None)  # one rank: the shard is the whole unit
         else:
-            w = comm.all_gather_into(buf, sh, group=self.group, async_op=True)
-            self._full[u] = (buf, w)
+            buf = torch.empty(self.unit_len[u], dtype=self.compute_dtype, device=self.device)
+            self._full[u] = (buf, self.tp.all_gather(buf, sh, async_op=True))
+        self._track()
+
+    def _track(self):
+        if self.W > 1:
+            live = len(self._full) + len(self._gfull)
+            self.peak_live_units = max(self.peak_live_units, live)
 
     def _ensure(self, u):
         self._gather(u)
@@ -184,32 +199,40 @@ class FSDPStore(ParamStore):
             for k in range(1, self.prefetch + 1):
                 if u - k >= 1:  # the embeddings unit needs no weights in backward
                     self._gather(u - k)
-        self._gfull[u] = torch.zeros(self.unit_len[u], dtype=torch.float32, device=self.device)
+        if self.W == 1:
+            # the weight gradients accumulate straight into the shard (zeroed per step)
+            self._gfull[u] = self.shard(self.grads, u)
+        else:
+            self._gfull[u] = torch.zeros(self.unit_len[u], dtype=torch.float32, device=self.device)
+        self._track()
 
     def post_backward(self, u):
         self._release(u)
         g = self._gfull.pop(u)
-        out = self.shard(self.grads, u)
         if self.W == 1:
-            out.add_(g)
             return
+        out = self.shard(self.grads, u)
         if self.reduce_dtype != torch.float32:
-            gt = g.to(self.reduce_dtype)
+            g = g.to(self.reduce_dtype)
             tmp = torch.empty(self.shard_len[u], dtype=self.reduce_dtype, device=self.device)
-            w = comm.reduce_scatter_into(tmp, gt, group=self.group, async_op=True)
-            self._rs[u] = (w, tmp, gt)
+            self._rs[u] = (self.tp.reduce_scatter(tmp, g, async_op=True), tmp)
+        elif u in self._fresh:
+            # first contribution since zero_grad: reduce-scatter straight into the shard
+            self._rs[u] = (self.tp.reduce_scatter(out, g, async_op=True), None)
         else:
             tmp = torch.empty(self.shard_len[u], dtype=torch.float32, device=self.device)
-            w = comm.reduce_scatter_into(tmp, g, group=self.group, async_op=True)
-            self._rs[u] = (w, tmp, g)
+            self._rs[u] = (self.tp.reduce_scatter(tmp, g, async_op=True), tmp)
+        self._fresh.discard(u)
+        # g is dropped here: the transport keeps it alive until the collective has read it
 
     def finish_grads(self):
         rep_w = None
         if self.W > 1:
-            rep_w = comm.all_reduce(self.rep_grads, group=self.group, async_op=True)
-        for u, (w, tmp, _) in sorted(self._rs.items()):
+            rep_w = self.tp.all_reduce(self.rep_grads, async_op=True)
+        for u, (w, tmp) in sorted(self._rs.items()):
             w.wait()
-            self.shard(self.grads, u).add_(tmp.float())
+            if tmp is not None:
+                self.shard(self.grads, u).add_(tmp.float())
         self._rs.clear()
         if rep_w is not None:
             rep_w.wait()
@@ -223,6 +246,7 @@ class FSDPStore(ParamStore):
     def zero_grad(self):
         self.grads.zero_()
         self.rep_grads.zero_()
+        self._fresh = set(self.units)
 
     # ------------------------------------------------------------------ full state
     @torch.no_grad()
@@ -235,10 +259,7 @@ class FSDPStore(ParamStore):
         for u in self.units:
             sh = self.shard(flat_shards, u).to(self.device)
             full = torch.empty(self.unit_len[u], dtype=sh.dtype, device=self.device)
-            if self.W > 1:
-                comm.all_gather_into(full, sh.contiguous(), group=self.group)
-            else:
-                full.copy_(sh)
+            self.tp.all_gather(full, sh.contiguous())
             if out is not None:
                 lo = self.layout.unit_ranges[u][0]
                 for e in self.layout.unit_entries(u):

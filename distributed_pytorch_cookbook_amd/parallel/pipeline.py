@@ -11,16 +11,17 @@ the last stage, the rest spread over the middle -- is implemented correctly here
 gets fewer layers).
 
 MI355X-first design: one process per GPU (torchrun), stage-to-stage activations
-(f32 [micro_batch * S, D], the residual stream) and their gradients move with RCCL
-send/recv over the direct xGMI link between the two GPUs; paired send+recv are issued
-as one grouped operation (``batch_isend_irecv`` == ncclGroupStart/End) so the 1F1B
-steady state cannot deadlock; the key-padding mask and targets are NOT sent -- every
-stage of a replica reads the same batch from its own loader.
+(the f32 residual stream [micro_batch * S, D], optionally bf16 on the wire) and their
+gradients move with RCCL send/recv over the direct xGMI link between the two GPUs, issued
+asynchronously on the transport's comm stream; paired send+recv are one grouped operation
+(ncclGroupStart/End) so the 1F1B steady state cannot deadlock, and compute waits on a
+receive only where it consumes it; the executed order is exactly ``schedule_1f1b`` /
+``schedule_gpipe`` (``run_schedule``); the key-padding mask and targets are NOT sent --
+every stage of a replica reads the same batch from its own loader.
 """
 from __future__ import annotations
 
 import torch
-import torch.distributed as dist
 
 
 def unit_costs(model, seq_len: int) -> list[float]:
@@ -64,54 +65,119 @@ def partition(costs: list[float], stages: int) -> list[list[int]]:
 
 
 class P2P:
-    """Send/recv of fixed-shape activations between adjacent stages of one pipeline."""
+    """Send/recv of fixed-shape activations between adjacent stages of one pipeline, through
+    the pipeline's ``Transport`` (native RCCL on its comm stream by default).
 
-    def __init__(self, pp_ranks: list[int], stage: int, device):
-        self.ranks = pp_ranks
+    ``post`` enqueues ONE grouped exchange (ncclGroupStart/End) and returns immediately with
+    the receive buffers and a handle: the compute stream waits on a receive only when it
+    consumes it (``Recv.get``), and a send never blocks anything -- its buffer is kept alive
+    by the transport until the comm stream has read it.  ``wire_dtype`` (e.g. bf16) halves
+    the boundary bytes: activations / gradients are cast for the wire and back on arrival.
+    """
+
+    def __init__(self, tp, stage: int, n_stages: int, device, wire_dtype=None):
+        self.tp = tp
         self.stage = stage
-        self.n = len(pp_ranks)
+        self.n = n_stages
         self.device = device
-        self.prev = pp_ranks[stage - 1] if stage > 0 else None
-        self.next = pp_ranks[stage + 1] if stage < self.n - 1 else None
-        self._pending = []
-        # gloo's send/recv take host memory only: when a GPU run is rehearsed over gloo
-        # (DPC_DIST_BACKEND=gloo, several ranks on one device) stage the payloads through host
-        self.host_staged = (torch.device(device).type == "cuda" and dist.is_initialized()
-                            and dist.get_backend() == "gloo")
+        self.prev = stage - 1 if stage > 0 else None
+        self.next = stage + 1 if stage < n_stages - 1 else None
+        self.wire_dtype = wire_dtype
+        self._inflight = []  # handles of exchanges nobody waits on yet (send-only groups)
 
-    def _run(self, ops):
-        if not ops:
-            return
-        reqs = dist.batch_isend_irecv(ops)
-        for r in reqs:
-            r.wait()
+    def post(self, send_next=None, send_prev=None, recv_prev_shape=None, recv_next_shape=None,
+             dtype=torch.float32):
+        """One grouped exchange.  Returns (Recv from prev or None, Recv from next or None)."""
+        wdt = self.wire_dtype or dtype
+        sends, recvs = [], []
+        fp = fn = None
+        if send_next is not None:
+            sends.append((send_next.detach().to(wdt).contiguous(), self.next))
+        if send_prev is not None:
+            sends.append((send_prev.detach().to(wdt).contiguous(), self.prev))
+        if recv_prev_shape is not None:
+            fp = torch.empty(recv_prev_shape, device=self.device, dtype=wdt)
+            recvs.append((fp, self.prev))
+        if recv_next_shape is not None:
+            fn = torch.empty(recv_next_shape, device=self.device, dtype=wdt)
+            recvs.append((fn, self.next))
+        h = self.tp.sendrecv(sends, recvs, async_op=True) if (sends or recvs) else None
+        if h is not None and not recvs:
+            self._inflight.append(h)  # a send is never waited on mid-step (see drain)
+        return (Recv(fp, h, dtype) if fp is not None else None,
+                Recv(fn, h, dtype) if fn is not None else None)
+
+    def drain(self):
+        """Order the caller after every send-only exchange still in flight (end of a step:
+        device-side for RCCL; for gloo it also keeps the works alive until they complete)."""
+        for h in self._inflight:
+            h.wait()
+        self._inflight.clear()
 
     def exchange(self, send_next=None, send_prev=None, recv_prev_shape=None, recv_next_shape=None,
                  dtype=torch.float32):
-        """One grouped p2p step. Returns (from_prev, from_next)."""
-        ops = []
-        fp = fn = None
-        bdev = "cpu" if self.host_staged else self.device
+        """Blocking form of ``post`` (waits for the received tensors and the sends)."""
+        a, b = self.post(send_next, send_prev, recv_prev_shape, recv_next_shape, dtype)
+        out = (a.get() if a is not None else None), (b.get() if b is not None else None)
+        self.drain()
+        return out
 
-        def payload(t):
-            t = t.detach().contiguous()
-            return t.cpu() if self.host_staged else t
 
-        if send_next is not None:
-            ops.append(dist.P2POp(dist.isend, payload(send_next), self.next))
-        if send_prev is not None:
-            ops.append(dist.P2POp(dist.isend, payload(send_prev), self.prev))
-        if recv_prev_shape is not None:
-            fp = torch.empty(recv_prev_shape, device=bdev, dtype=dtype)
-            ops.append(dist.P2POp(dist.irecv, fp, self.prev))
-        if recv_next_shape is not None:
-            fn = torch.empty(recv_next_shape, device=bdev, dtype=dtype)
-            ops.append(dist.P2POp(dist.irecv, fn, self.next))
-        self._run(ops)
-        if self.host_staged:
-            fp = fp.to(self.device) if fp is not None else None
-            fn = fn.to(self.device) if fn is not None else None
-        return fp, fn
+class Recv:
+    """A receive buffer whose data is ready once its exchange's handle has been waited on."""
+
+    def __init__(self, buf, handle, dtype):
+        self.buf, self.handle, self.dtype = buf, handle, dtype
+
+    def get(self):
+        if self.handle is not None:
+            self.handle.wait()
+            self.handle = None
+        return self.buf if self.buf.dtype == self.dtype else self.buf.to(self.dtype)
+
+
+def run_schedule(order, first: bool, last: bool, forward, backward, p2p: "P2P", shape):
+    """Execute a stage's schedule -- a list of ('F', m) / ('B', m) from ``schedule_1f1b`` or
+    ``schedule_gpipe`` -- with asynchronous grouped p2p.
+
+    Rule: before the first op its receive is posted; after every op ONE grouped exchange is
+    posted holding that op's send (y_m to the next stage, dx_m to the previous) and the
+    receive the NEXT op will consume (x from the previous stage for an F, g from the next
+    for a B).  Every exchange is issued in schedule order on both sides of a link, so the
+    comm streams see the same group sequence the blocking PipeDream-flush loop issues --
+    deadlock-free -- while the compute stream waits only where a received tensor is used.
+    ``forward(m, x) -> y`` (None on the last stage), ``backward(m, g) -> dx`` (None on the
+    first stage)."""
+
+    def need(op):
+        kind, _ = op
+        if kind == "F":
+            return (shape, None) if not first else (None, None)
+        return (None, shape) if not last else (None, None)
+
+    pending = None  # the Recv the next op consumes
+    rp, rn = need(order[0]) if order else (None, None)
+    if rp is not None or rn is not None:
+        a, b = p2p.post(recv_prev_shape=rp, recv_next_shape=rn)
+        pending = a or b
+    for i, (kind, m) in enumerate(order):
+        if kind == "F":
+            x = pending.get() if (pending is not None and not first) else None
+            out = forward(m, x)
+            send_next, send_prev = (out if not last else None), None
+        else:
+            g = pending.get() if (pending is not None and not last) else None
+            dx = backward(m, g)
+            send_next, send_prev = None, (dx if not first else None)
+        pending = None
+        rp = rn = None
+        if i + 1 < len(order):
+            rp, rn = need(order[i + 1])
+        if send_next is not None or send_prev is not None or rp is not None or rn is not None:
+            a, b = p2p.post(send_next=send_next, send_prev=send_prev, recv_prev_shape=rp,
+                            recv_next_shape=rn)
+            pending = a or b
+    p2p.drain()
 
 
 def schedule_1f1b(n_micro: int, stage: int, n_stages: int):

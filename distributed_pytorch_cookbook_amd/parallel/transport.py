@@ -1,0 +1,281 @@
+"""One collective transport interface for every engine: native RCCL, torch c10d, or gloo.
+
+SURVEY.md §2.4 / §5.8: the hot-path collectives of the three engines -- DDP bucket
+all-reduces (reference ``/root/reference/main-ddp.py:55``), FSDP all-gathers and
+reduce-scatters (``main-fsdp.py:60-69``) and pipeline send/recv (``main-pipe.py:75-83``) --
+go through a ``Transport``:
+
+* ``NativeTransport`` -- the C++ RCCL communicator (``runtime/csrc/rccl_comm.cpp`` via
+  ``parallel/native_comm.py``).  Every collective is enqueued on the transport's own
+  high-priority HIP stream, ordered after the caller's work by an event, and its completion
+  is handed back as an event the caller's stream waits on (``Handle.wait``): no c10d work
+  objects, no watchdog, no host synchronisation -- and therefore capturable in a HIP graph.
+  Buffers touched on the comm stream are ``record_stream``-ed so the caching allocator does
+  not recycle them while a collective still reads or writes them.
+* ``TorchTransport`` -- torch.distributed over the same group: the ``nccl`` backend (RCCL
+  as well) for ``--comm torch``, ``gloo`` for the CPU tests and shared-GPU rehearsals.
+
+``make_transport`` picks native on a GPU with the nccl backend unless told otherwise, and
+falls back to torch at construction time -- before any collective -- if the native library
+or RCCL cannot be brought up.  torch.distributed stays the bootstrap (rendezvous, the
+``ncclUniqueId`` broadcast) and carries the few host-side scalar reductions.
+"""
+from __future__ import annotations
+
+import os
+
+import torch
+import torch.distributed as dist
+
+from . import comm
+
+
+class Handle:
+    """Completion of an asynchronous collective."""
+
+    def wait(self) -> None:  # pragma: no cover - interface
+        raise NotImplementedError
+
+
+class _Done(Handle):
+    def wait(self) -> None:
+        pass
+
+
+class _EventHandle(Handle):
+    """Completion recorded on a side stream: ``wait`` orders the caller's current stream
+    after it (device-side only)."""
+
+    def __init__(self, event):
+        self.event = event
+
+    def wait(self) -> None:
+        torch.cuda.current_stream().wait_event(self.event)
+
+
+class _WorkHandle(Handle):
+    def __init__(self, works, after=None):
+        self.works = works if isinstance(works, (list, tuple)) else [works]
+        self.after = after
+
+    def wait(self) -> None:
+        for w in self.works:
+            if w is not None:
+                w.wait()
+        if self.after is not None:
+            self.after()
+            self.after = None
+
+
+class Transport:
+    kind = "base"
+    rank = 0
+    size = 1
+    group = None
+
+    def global_rank(self, r: int) -> int:
+        """Global rank of group rank ``r``."""
+        if self.group is None or not dist.is_initialized():
+            return r
+        return dist.get_global_rank(self.group, r)
+
+    def all_reduce(self, t, async_op=False) -> Handle:
+        raise NotImplementedError
+
+    def reduce_scatter(self, out, inp, async_op=False) -> Handle:
+        raise NotImplementedError
+
+    def all_gather(self, out, inp, async_op=False) -> Handle:
+        raise NotImplementedError
+
+    def broadcast(self, t, src: int, async_op=False) -> Handle:
+        """``src`` is a rank of this transport's group."""
+        raise NotImplementedError
+
+    def sendrecv(self, sends=(), recvs=(), async_op=False) -> Handle:
+        """One grouped exchange: ``sends`` / ``recvs`` are (tensor, peer group rank) pairs."""
+        raise NotImplementedError
+
+    def capturable(self) -> bool:
+        """Whether the collectives may be recorded into a HIP graph."""
+        return False
+
+    @property
+    def active(self) -> bool:
+        """Whether collectives are issued at all (a native communicator of one rank still
+        issues them -- the single-GPU tests of the RCCL path)."""
+        return self.size > 1
+
+
+class TorchTransport(Transport):
+    kind = "torch"
+
+    def __init__(self, group=None):
+        self.group = group
+        self.rank = comm.rank(group)
+        self.size = comm.world_size(group)
+        # gloo's send/recv take host memory only: a GPU run rehearsed over gloo (several
+        # ranks on one device) stages point-to-point payloads through the host
+        self.host_staged = dist.is_initialized() and dist.get_backend(group) == "gloo"
+
+    def _ret(self, work, async_op):
+        if async_op:
+            return _WorkHandle(work)
+        if work is not None:
+            work.wait()
+        return _Done()
+
+    def all_reduce(self, t, async_op=False):
+        if self.size == 1:
+            return _Done()
+        return self._ret(comm.all_reduce(t, group=self.group, async_op=async_op), async_op)
+
+    def reduce_scatter(self, out, inp, async_op=False):
+        if self.size == 1:
+            out.copy_(inp)
+            return _Done()
+        return self._ret(comm.reduce_scatter_into(out, inp, group=self.group, async_op=async_op), async_op)
+
+    def all_gather(self, out, inp, async_op=False):
+        if self.size == 1:
+            out.copy_(inp)
+            return _Done()
+        return self._ret(comm.all_gather_into(out, inp, group=self.group, async_op=async_op), async_op)
+
+    def broadcast(self, t, src, async_op=False):
+        if self.size == 1:
+            return _Done()
+        return self._ret(comm.broadcast(t, src=self.global_rank(src), group=self.group, async_op=async_op),
+                         async_op)
+
+    def sendrecv(self, sends=(), recvs=(), async_op=False):
+        if not sends and not recvs:
+            return _Done()
+        ops, staged = [], []
+        for t, peer in sends:
+            t = t.detach().contiguous()
+            ops.append(dist.P2POp(dist.isend, t.cpu() if self.host_staged and t.is_cuda else t,
+                                  self.global_rank(peer), self.group))
+        for t, peer in recvs:
+            buf = t
+            if self.host_staged and t.is_cuda:
+                buf = torch.empty(t.shape, dtype=t.dtype)
+                staged.append((t, buf))
+            ops.append(dist.P2POp(dist.irecv, buf, self.global_rank(peer), self.group))
+        works = dist.batch_isend_irecv(ops)
+
+        def unstage():
+            for dst, src in staged:
+                dst.copy_(src)
+
+        h = _WorkHandle(works, after=unstage if staged else None)
+        if not async_op:
+            h.wait()
+            return _Done()
+        return h
+
+
+class NativeTransport(Transport):
+    kind = "native"
+
+    def __init__(self, group=None, device=None, native=None):
+        from .native_comm import NativeComm
+
+        self.group = group
+        self.device = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+        self.nc = native if native is not None else NativeComm(group, device=self.device)
+        self.rank, self.size = self.nc.rank, self.nc.size
+        # RCCL runs on its own high-priority stream, ordered with events
+        self.stream = torch.cuda.Stream(device=self.device, priority=-1)
+
+    def capturable(self) -> bool:
+        return True
+
+    @property
+    def active(self) -> bool:
+        return True
+
+    def _enqueue(self, fn, tensors, async_op):
+        cur = torch.cuda.current_stream(self.device)
+        s = self.stream
+        s.wait_stream(cur)
+        with torch.cuda.stream(s):
+            fn(s)
+        for t in tensors:
+            t.record_stream(s)
+        done = torch.cuda.Event()
+        done.record(s)
+        h = _EventHandle(done)
+        if not async_op:
+            h.wait()
+            return _Done()
+        return h
+
+    def all_reduce(self, t, async_op=False):
+        return self._enqueue(lambda s: self.nc.all_reduce(t, stream=s), (t,), async_op)
+
+    def reduce_scatter(self, out, inp, async_op=False):
+        return self._enqueue(lambda s: self.nc.reduce_scatter(out, inp, stream=s), (out, inp), async_op)
+
+    def all_gather(self, out, inp, async_op=False):
+        return self._enqueue(lambda s: self.nc.all_gather(out, inp, stream=s), (out, inp), async_op)
+
+    def broadcast(self, t, src, async_op=False):
+        return self._enqueue(lambda s: self.nc.broadcast(t, src=src, stream=s), (t,), async_op)
+
+    def sendrecv(self, sends=(), recvs=(), async_op=False):
+        if not sends and not recvs:
+            return _Done()
+        sends = [(t.detach().contiguous(), p) for t, p in sends]
+
+        def run(s):
+            with self.nc.grouped():
+                for t, p in sends:
+                    self.nc.send(t, p, stream=s)
+                for t, p in recvs:
+                    self.nc.recv(t, p, stream=s)
+
+        return self._enqueue(run, [t for t, _ in sends] + [t for t, _ in recvs], async_op)
+
+    def split(self, color: int, key: int, group=None) -> "NativeTransport":
+        """Sub-communicator (ncclCommSplit) of the ranks sharing ``color``; ``group`` is the
+        matching torch group (bootstrap / host-side reductions).  Collective."""
+        return NativeTransport(group, self.device, native=self.nc.split(color, key))
+
+
+def _want_native(kind: str, device) -> bool:
+    if kind == "torch":
+        return False
+    dev = torch.device(device) if device is not None else torch.device("cpu")
+    return (dev.type == "cuda" and dist.is_initialized() and dist.get_backend() == "nccl")
+
+
+def make_transport(group=None, device=None, kind: str | None = None) -> Transport:
+    """The engines' transport over ``group``: ``kind`` = auto (native on a GPU with the
+    nccl backend, torch otherwise) | native | torch.  Falls back to torch -- before any
+    collective -- if the native communicator cannot be built."""
+    kind = kind or os.environ.get("DPC_COMM", "auto")
+    if (comm.world_size(group) > 1 or kind == "native") and _want_native(kind, device):
+        try:
+            return NativeTransport(group, device)
+        except Exception as exc:  # library / RCCL missing: stay correct, say so
+            if comm.rank() == 0:
+                print(f"[comm] native RCCL transport unavailable ({exc}); using torch.distributed")
+    return TorchTransport(group)
+
+
+def make_mesh_transports(pp_group, dp_group, stage: int, replica: int, device=None, kind: str | None = None):
+    """(pp, dp) transports of a rank on the 2-D mesh (rank = stage * dp + replica).  Native:
+    ONE world communicator split twice with ncclCommSplit (color = replica -> the pipeline of
+    this replica, color = stage -> the replicas of this stage)."""
+    kind = kind or os.environ.get("DPC_COMM", "auto")
+    if comm.world_size() > 1 and _want_native(kind, device):
+        try:
+            world = NativeTransport(None, device)
+            pp = world.split(replica, stage, group=pp_group)
+            dp = world.split(stage, replica, group=dp_group)
+            return pp, dp
+        except Exception as exc:
+            if comm.rank() == 0:
+                print(f"[comm] native RCCL mesh unavailable ({exc}); using torch.distributed")
+    return TorchTransport(pp_group), TorchTransport(dp_group)

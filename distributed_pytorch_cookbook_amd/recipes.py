@@ -34,24 +34,32 @@ def build_model(args, vocab_size: int, device) -> TransformerDecoderLM:
     return model
 
 
+def pipe_mesh(recipe: str, world: int, pp_size: int = 0, dp_size: int = 0) -> tuple[int, int]:
+    """(pp, dp) of the pipeline recipes: ``main-pipe.py`` is one pipeline over every rank;
+    ``main-pipe-ddp.py`` defaults to the BASELINE.json hybrid, 2 stages x N / 2 replicas
+    (8 ranks: pp2 x dp4)."""
+    dp = dp_size or 1
+    if recipe == "pipe_ddp" and not dp_size:
+        pp0 = pp_size or 2
+        dp = world // pp0 if world % pp0 == 0 else 1
+    pp = pp_size or max(1, world // dp)
+    return pp, dp
+
+
 def build_engine(recipe: str, model, info, args):
     compute_dtype = torch.float32 if args.disable_amp else None
-    if info.device.type == "cuda":
-        from .ops.gemm import enable_vendor_tuning
-
-        enable_vendor_tuning()  # tuned hipBLASLt solutions for the plain products (read-only)
+    comm_kind = getattr(args, "comm", "auto")
+    # the cookbook's "compile": capture the whole step into a HIP graph (dropout masks are
+    # drawn per step on the host: not graph-replayable)
+    graph = not args.disable_compile and not args.disable_amp and not args.dropout
     if recipe in ("single", "ddp"):
         from .engine.data_parallel import DataParallelEngine
 
         return DataParallelEngine(
             model, info.device, lr=args.learning_rate, bucket_mb=args.bucket_mb,
             reduce_dtype=torch.bfloat16 if args.reduce_dtype == "bf16" else torch.float32,
-            overlap=not args.no_overlap, compute_dtype=compute_dtype,
-            # the cookbook's "compile": capture the whole single-GPU step into a HIP graph
-            # (dropout masks are drawn per step on the host: not graph-replayable)
-            graph=not args.disable_compile and not args.disable_amp and not args.dropout,
-            native_comm=getattr(args, "comm", "torch") == "native",
-            grad_scaler=getattr(args, "grad_scaler", False),
+            overlap=not args.no_overlap, compute_dtype=compute_dtype, graph=graph,
+            comm_kind=comm_kind, grad_scaler=getattr(args, "grad_scaler", False),
         )
     if recipe == "fsdp":
         from .engine.fsdp import FSDPEngine
@@ -59,18 +67,17 @@ def build_engine(recipe: str, model, info, args):
         return FSDPEngine(model, info.device, lr=args.learning_rate, prefetch=args.prefetch,
                           reshard_after_forward=not args.no_reshard_after_forward,
                           cpu_offload=args.cpu_offload, compute_dtype=compute_dtype,
-                          grad_scaler=getattr(args, "grad_scaler", False))
+                          grad_scaler=getattr(args, "grad_scaler", False), graph=graph, comm_kind=comm_kind)
     if recipe in ("pipe", "pipe_ddp"):
         from .engine.pipeline import PipelineEngine
 
-        dp = getattr(args, "dp_size", 0) or 1
-        if recipe == "pipe_ddp" and not getattr(args, "dp_size", 0):
-            dp = 2 if info.world_size % 2 == 0 and info.world_size > 2 else 1
-        pp = args.pp_size or max(1, info.world_size // dp)
+        pp, dp = pipe_mesh(recipe, info.world_size, args.pp_size, getattr(args, "dp_size", 0))
+        wire = {"fp32": None, "bf16": torch.bfloat16}[getattr(args, "pp_comm_dtype", "fp32")]
         return PipelineEngine(model, info.device, lr=args.learning_rate, pp=pp, dp=dp,
-                              num_microbatches=args.num_microbatches or 2 * pp,
+                              num_microbatches=args.num_microbatches or 4 * pp,
                               schedule=args.schedule, bucket_mb=args.bucket_mb,
-                              compute_dtype=compute_dtype, grad_scaler=getattr(args, "grad_scaler", False))
+                              compute_dtype=compute_dtype, grad_scaler=getattr(args, "grad_scaler", False),
+                              comm_kind=comm_kind, wire_dtype=wire, graph=graph)
     raise ValueError(recipe)
 
 

@@ -146,3 +146,20 @@ def worker_coll_mismatch(rank, world):
         assert "collective mismatch" in str(exc), exc
         return
     raise AssertionError("mismatched collective was not detected")
+
+
+def worker_fsdp_mem(rank, world, out):
+    """Peak number of full-unit buffers alive in the FSDP store over one training step."""
+    from distributed_pytorch_cookbook_amd.engine.fsdp import FSDPEngine
+    from distributed_pytorch_cookbook_amd.parallel import comm
+
+    comm.init_dist(force_cpu=True)
+    res = {}
+    for prefetch in (0, 1, 2):
+        m = make_model(layers=5)
+        eng = FSDPEngine(m, "cpu", lr=LR, prefetch=prefetch)
+        b, t = shard(*full_batch(step=0), rank, world)
+        eng.train_step(b, t)
+        res[prefetch] = eng.store.peak_live_units
+    if rank == 0:
+        torch.save(res, out)

@@ -6,7 +6,7 @@ import pytest
 import torch
 
 from dist_helpers import run_workers
-from dist_workers import (reference_state, worker_ddp, worker_fsdp, worker_pipe, worker_scaled)
+from dist_workers import (reference_state, worker_ddp, worker_fsdp, worker_fsdp_mem, worker_pipe, worker_scaled)
 
 from distributed_pytorch_cookbook_amd.parallel.pipeline import partition, schedule_1f1b
 
@@ -104,3 +104,61 @@ def test_comm_bw_bench_runs_on_gloo(tmp_path):
     rows = json.loads(out.read_text())
     assert {r["op"] for r in rows} == {"all_reduce", "all_gather", "reduce_scatter", "broadcast", "sendrecv"}
     assert all(r["busbw_GBps"] > 0 and r["world"] == 2 for r in rows)
+
+
+def test_pipe_ddp_default_mesh_is_pp2():
+    from distributed_pytorch_cookbook_amd.recipes import pipe_mesh
+
+    assert pipe_mesh("pipe_ddp", 8) == (2, 4)
+    assert pipe_mesh("pipe_ddp", 4) == (2, 2)
+    assert pipe_mesh("pipe_ddp", 1) == (1, 1)
+    assert pipe_mesh("pipe", 8) == (8, 1)
+    assert pipe_mesh("pipe_ddp", 8, dp_size=2) == (4, 2)
+
+
+def test_run_schedule_is_the_tested_schedule():
+    """The engine executes exactly schedule_1f1b / schedule_gpipe: record the op order the
+    executor calls on a 4-stage pipeline (no communication: a recording P2P)."""
+    from distributed_pytorch_cookbook_amd.parallel.pipeline import run_schedule, schedule_1f1b, schedule_gpipe
+
+    class RecP2P:
+        def __init__(self):
+            self.posts = []
+
+        def post(self, **kw):
+            self.posts.append({k: v is not None for k, v in kw.items()})
+
+            class R:
+                def get(self_):
+                    return torch.zeros(1)
+            rp, rn = kw.get("recv_prev_shape"), kw.get("recv_next_shape")
+            return (R() if rp is not None else None), (R() if rn is not None else None)
+
+        def drain(self):
+            pass
+
+    for sched in (schedule_1f1b, schedule_gpipe):
+        for st in range(4):
+            order = sched(8, st, 4)
+            seen = []
+            p2p = RecP2P()
+            run_schedule(order, st == 0, st == 3, lambda m, x: seen.append(("F", m)) or torch.zeros(1),
+                         lambda m, g: seen.append(("B", m)) or torch.zeros(1), p2p, (1,))
+            assert seen == order
+            # every send posted exactly once: 8 forward outputs (not the last stage) and 8
+            # input gradients (not the first stage)
+            n_send = sum(p.get("send_next", False) for p in p2p.posts), sum(p.get("send_prev", False) for p in p2p.posts)
+            assert n_send == ((8 if st < 3 else 0), (8 if st > 0 else 0))
+            n_recv = (sum(p.get("recv_prev_shape", False) for p in p2p.posts),
+                      sum(p.get("recv_next_shape", False) for p in p2p.posts))
+            assert n_recv == ((8 if st > 0 else 0), (8 if st < 3 else 0))
+
+
+def test_fsdp_memory_bounded(tmp_path):
+    """FSDP backward keeps at most prefetch + 2 full-unit buffers (weights + gradients) alive:
+    a unit's gradient is released as soon as its reduce-scatter is enqueued."""
+    out = tmp_path / "fsdp_mem.pt"
+    run_workers(worker_fsdp_mem, 2, str(out))
+    r = torch.load(out, weights_only=True)
+    for prefetch, peak in r.items():
+        assert peak <= prefetch + 2, (prefetch, peak)
