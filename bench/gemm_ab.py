@@ -34,6 +34,34 @@ GPT2S = [("qkv_fwd", T, 2304, 768, "nt"), ("out_fwd", T, 768, 768, "nt"),
          ("down_fwd", T, 768, 3072, "nt")]
 
 
+# fused-epilogue products of the GPT-2 layers: (name, M, N, K, layout, epilogue)
+#   up   = bias + gelu + aux_out (pre-activation), bf16 out          (FFN up forward)
+#   down = bias + gelu + aux_out + f32 residual, f32 out             (FFN down forward, quirk act)
+#   out  = bias + f32 residual, f32 out                              (attention out-proj forward)
+#   dact = act'(aux_in) + bias-gradient column sums, bf16 out        (FFN input gradient)
+FUSED = [("s_up_fwd", T, 3072, 768, "nt", "up"), ("s_down_fwd", T, 768, 3072, "nt", "down"),
+         ("s_out_fwd", T, 768, 768, "nt", "out"), ("s_dact", T, 3072, 768, "nn", "dact"),
+         ("xl_down_fwd", 32736, 1600, 6400, "nt", "down"), ("xl_up_fwd", 32736, 6400, 1600, "nt", "up"),
+         ("xl_out_fwd", 32736, 1600, 1600, "nt", "out"), ("xl_dact", 32736, 6400, 1600, "nn", "dact")]
+
+
+def epilogue(kind, M, N, dev="cuda"):
+    kw = {}
+    if kind in ("up", "down", "out"):
+        kw["bias"] = torch.randn(N, device=dev)
+    if kind in ("up", "down"):
+        kw["act"] = 2
+        kw["aux_out"] = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+    if kind in ("down", "out"):
+        kw["residual"] = torch.randn(M, N, device=dev)
+        kw["out_dtype"] = torch.float32
+    if kind == "dact":
+        kw["act_bwd"] = 2
+        kw["aux_in"] = torch.randn(M, N, device=dev).bfloat16()
+        kw["colsum"] = torch.zeros(N, device=dev)
+    return kw
+
+
 def operands(M, N, K, lay, dev="cuda"):
     r = lambda *s: (torch.rand(*s, device=dev) * 2 - 1).bfloat16()  # noqa: E731
     if lay == "nt":
@@ -71,7 +99,7 @@ def check(A, B, lay, out):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--impls", type=int, nargs="+", default=[12, 13, 14])
-    ap.add_argument("--shapes", default="all", choices=["square", "gpt2s", "all"])
+    ap.add_argument("--shapes", default="all", choices=["square", "gpt2s", "all", "fused"])
     ap.add_argument("--only", nargs="*", default=None)
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--iters", type=int, default=10)
@@ -81,6 +109,35 @@ def main():
     if a.only:
         shapes = [s for s in shapes if s[0] in a.only]
     rows = []
+    if a.shapes == "fused":
+        for name, M, N, K, lay, kind in FUSED:
+            if a.only and name not in a.only:
+                continue
+            torch.manual_seed(0)
+            A, B, kw, _ = operands(M, N, K, lay)
+            ekw = epilogue(kind, M, N)
+            times = {}
+            for impl in [0] + a.impls:
+                _lib.set_gemm_impl(impl if impl else -1)
+                fn = lambda: gemm(A, B, **kw, **ekw)  # noqa: E731
+                fn()
+                torch.cuda.synchronize()
+                times[f"i{impl}"] = []
+            for _ in range(a.rounds):
+                for impl in [0] + a.impls:
+                    _lib.set_gemm_impl(impl if impl else -1)
+                    times[f"i{impl}"].append(time_ms(lambda: gemm(A, B, **kw, **ekw), a.iters))
+            _lib.set_gemm_impl(-1)
+            fl = 2.0 * M * N * K
+            row = dict(case=name, M=M, N=N, K=K, layout=lay, epilogue=kind)
+            for k, v in times.items():
+                ms = statistics.median(v)
+                row[k] = dict(ms=round(ms, 4), tflops=round(fl / ms / 1e9, 1))
+            rows.append(row)
+            print(json.dumps(row), flush=True)
+            del A, B, ekw
+            torch.cuda.empty_cache()
+        shapes = []
     for name, M, N, K, lay in shapes:
         torch.manual_seed(0)
         A, B, kw, odt = operands(M, N, K, lay)

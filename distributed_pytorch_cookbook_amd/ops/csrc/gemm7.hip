@@ -34,6 +34,7 @@
 #include "gemm.h"
 
 #include <cstdlib>
+#include <utility>
 
 namespace dpc {
 
@@ -97,31 +98,50 @@ __device__ __forceinline__ void g7_wait() {
 // ---- epilogue straight from the swapped accumulators.  Lane l, accumulator (i, j), register
 // r holds C[mw + 16 i + (l & 15)][nw + 16 j + 4 (l >> 4) + r].  Same semantics and order as
 // epi_tile (gemm.hip) / ops/gemm.py:_gemm_ref.
-// GEN = false: plain products only (alpha, bf16 or f32 C, no accumulate) -- the hot path,
-// with the register budget of the main loop untouched; GEN = true: every fused operation.
-template <bool GEN>
+// MODE 0: plain products only (alpha, bf16 or f32 C, no accumulate) -- the hot path, with the
+// register budget of the main loop untouched.  MODE 1: forward epilogues (bias, activation,
+// the pre-activation aux_out, f32 residual or accumulated C).  MODE 3: input-gradient
+// epilogues (act'(aux_in) and bias-gradient column sums).  Splitting the fused work in two
+// keeps each epilogue's live set (operand prefetch + bias or column sums) small enough that
+// nothing of the main loop spills: a spill reload in the loop is a vector-memory op, which
+// breaks the counted DMA waits.
+// sfor<N>: compile-time loop -- the fused row body is beyond clang's full-unroll threshold and
+// a rolled loop indexes acc[i] dynamically, which moves all 256 accumulators to scratch.
+template <int... Is, class F>
+__device__ __forceinline__ void sfor_seq(std::integer_sequence<int, Is...>, F&& f) {
+  (f(std::integral_constant<int, Is>{}), ...);
+}
+template <int N, class F>
+__device__ __forceinline__ void sfor(F&& f) {
+  sfor_seq(std::make_integer_sequence<int, N>{}, f);
+}
+
+#define G7_AI __attribute__((always_inline))
+
+template <int MODE>
 __device__ __forceinline__ void g7_epilogue(const GemmArgs& p, floatx4 (&acc)[8][8], int mw, int nw, int lane) {
   float alpha = p.alpha;
   if (p.alpha_ptr) alpha *= *p.alpha_ptr;
   const int g = lane >> 4, rl = lane & 15;
-  if (!GEN && p.out_f32) {
+  // bf16 outputs leave in 16-B stores: after v_permlane16_swap of fragments (j, j+1) lane
+  // group g holds columns 16 j + {0, 16, 8, 24}[g] .. +7 (host: N % 8 == 0, ldc % 8 == 0,
+  // C 16-B aligned)
+  const int coff = 16 * (g & 1) + 8 * (g >> 1);
+  if constexpr (MODE == 0) {
+    if (p.out_f32) {
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const int m = mw + 16 * i + rl;
+      for (int i = 0; i < 8; ++i) {
+        const int m = mw + 16 * i + rl;
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const int n = nw + 16 * j + 4 * g;
-        if (m < p.M && n < p.N)
-          *reinterpret_cast<float4*>(static_cast<float*>(p.C) + (long long)m * p.ldc + n) =
-              make_float4(acc[i][j][0] * alpha, acc[i][j][1] * alpha, acc[i][j][2] * alpha, acc[i][j][3] * alpha);
+        for (int j = 0; j < 8; ++j) {
+          const int n = nw + 16 * j + 4 * g;
+          if (m < p.M && n < p.N)
+            *reinterpret_cast<float4*>(static_cast<float*>(p.C) + (long long)m * p.ldc + n) =
+                make_float4(acc[i][j][0] * alpha, acc[i][j][1] * alpha, acc[i][j][2] * alpha, acc[i][j][3] * alpha);
+        }
       }
+      return;
     }
-    return;
-  }
-  if (!GEN) {
-    // bf16 C, 16-B stores: after v_permlane16_swap of fragments (j, j+1) lane group g holds
-    // columns 16 j + {0, 16, 8, 24}[g] .. +7 (host: N % 8 == 0, ldc % 8 == 0, C 16-B aligned)
-    const int coff = 16 * (g & 1) + 8 * (g >> 1);
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
       const int m = mw + 16 * i + rl;
@@ -141,95 +161,137 @@ __device__ __forceinline__ void g7_epilogue(const GemmArgs& p, floatx4 (&acc)[8]
     }
     return;
   }
-  if (!GEN) return;
-  float4 bias4[8];
-#pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    const int n = nw + 16 * j + 4 * g;
-    bias4[j] = (p.bias && n < p.N) ? *reinterpret_cast<const float4*>(p.bias + n) : make_float4(0.f, 0.f, 0.f, 0.f);
-  }
-  float cs[8][4];
-#pragma unroll
-  for (int j = 0; j < 8; ++j)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) cs[j][r] = 0.f;
+  constexpr bool FWD = MODE == 1;
+  // per-element operand reads (FWD: the f32 residual / accumulated C; else act''s bf16
+  // operand), prefetched one row block ahead: as soon as fragment (i, j) is consumed, the
+  // slot is refilled with (i + 1, j) -- one slot per fragment, no double buffer
   const bf16_t* aux_in = static_cast<const bf16_t*>(p.aux_in);
   bf16_t* aux_out = static_cast<bf16_t*>(p.aux_out);
-  const float* fsrc = p.residual ? p.residual : (p.out_f32 && p.accumulate ? static_cast<const float*>(p.C) : nullptr);
+  const float* fsrc = FWD ? (p.residual ? p.residual : (p.out_f32 && p.accumulate ? static_cast<const float*>(p.C) : nullptr))
+                          : nullptr;
   const long long ldf = p.residual ? p.ldr : p.ldc;
+  const bool has_ld = FWD ? fsrc != nullptr : p.act_bwd != 0;
+  auto load_one = [&](int m, int n) G7_AI {
+    uint4 r = make_uint4(0u, 0u, 0u, 0u);
+    if (has_ld && m < p.M && n < p.N) {
+      if constexpr (FWD) {
+        r = *reinterpret_cast<const uint4*>(fsrc + (long long)m * ldf + n);
+      } else {
+        const uint2 z = *reinterpret_cast<const uint2*>(aux_in + (long long)m * p.ld_aux_in + n);
+        r.x = z.x;
+        r.y = z.y;
+      }
+    }
+    return r;
+  };
+  uint4 ld[8];
+  float4 bias4[8];
+  float cs[8][4];
+  sfor<8>([&](auto J) G7_AI {
+    constexpr int j = decltype(J)::value;
+    ld[j] = load_one(mw + rl, nw + 16 * j + 4 * g);
+    if constexpr (FWD) {
+      const int n = nw + 16 * j + 4 * g;
+      bias4[j] = (p.bias && n < p.N) ? *reinterpret_cast<const float4*>(p.bias + n) : make_float4(0.f, 0.f, 0.f, 0.f);
+    } else {
 #pragma unroll
-  for (int i = 0; i < 8; ++i) {
+      for (int r = 0; r < 4; ++r) cs[j][r] = 0.f;
+    }
+  });
+  sfor<8>([&](auto I) G7_AI {
+    constexpr int i = decltype(I)::value;
     const int m = mw + 16 * i + rl;
     const bool mok = m < p.M;
-    // this row's operand reads, all in flight before the first use
-    uint2 z[8];
-    float4 f[8];
+    sfor<4>([&](auto J) G7_AI {
+      constexpr int j = 2 * decltype(J)::value;
+      unsigned pa[2][2], pc[2][2];
+      sfor<2>([&](auto H) G7_AI {
+        constexpr int h = decltype(H)::value;
+        constexpr int jj = j + h;
+        const int n = nw + 16 * jj + 4 * g;
+        const bool ok = mok && n < p.N;
+        const uint4 cur = ld[jj];
+        if (i + 1 < 8) ld[jj] = load_one(m + 16, n);
+        float w[4];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const int n = nw + 16 * j + 4 * g;
-      const bool ok = mok && n < p.N;
-      z[j] = make_uint2(0u, 0u);
-      f[j] = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (ok && p.act_bwd) z[j] = *reinterpret_cast<const uint2*>(aux_in + (long long)m * p.ld_aux_in + n);
-      if (ok && fsrc) f[j] = *reinterpret_cast<const float4*>(fsrc + (long long)m * ldf + n);
-    }
+        for (int r = 0; r < 4; ++r) w[r] = acc[i][jj][r] * alpha;
+        if constexpr (FWD) {
+          w[0] += bias4[jj].x; w[1] += bias4[jj].y; w[2] += bias4[jj].z; w[3] += bias4[jj].w;
+          pa[h][0] = pack2bf(w[0], w[1]);  // the pre-activation (aux_out)
+          pa[h][1] = pack2bf(w[2], w[3]);
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const int n = nw + 16 * j + 4 * g;
-      if (!mok || n >= p.N) continue;
-      float v[4] = {acc[i][j][0] * alpha + bias4[j].x, acc[i][j][1] * alpha + bias4[j].y,
-                    acc[i][j][2] * alpha + bias4[j].z, acc[i][j][3] * alpha + bias4[j].w};
-      if (p.act_bwd) {
-        v[0] *= act_grad(__uint_as_float(z[j].x << 16), p.act_bwd);
-        v[1] *= act_grad(__uint_as_float(z[j].x & 0xffff0000u), p.act_bwd);
-        v[2] *= act_grad(__uint_as_float(z[j].y << 16), p.act_bwd);
-        v[3] *= act_grad(__uint_as_float(z[j].y & 0xffff0000u), p.act_bwd);
-      }
+          for (int r = 0; r < 4; ++r) w[r] = act_fwd(w[r], p.act);
+          if (fsrc) {
+            w[0] += __uint_as_float(cur.x); w[1] += __uint_as_float(cur.y);
+            w[2] += __uint_as_float(cur.z); w[3] += __uint_as_float(cur.w);
+          }
+        } else {
+          if (p.act_bwd) {
+            w[0] *= act_grad(__uint_as_float(cur.x << 16), p.act_bwd);
+            w[1] *= act_grad(__uint_as_float(cur.x & 0xffff0000u), p.act_bwd);
+            w[2] *= act_grad(__uint_as_float(cur.y << 16), p.act_bwd);
+            w[3] *= act_grad(__uint_as_float(cur.y & 0xffff0000u), p.act_bwd);
+          }
+          if (ok) {
 #pragma unroll
-      for (int r = 0; r < 4; ++r) cs[j][r] += v[r];
-      if (aux_out)
-        *reinterpret_cast<uint2*>(aux_out + (long long)m * p.ld_aux_out + n) =
-            make_uint2(pack2bf(v[0], v[1]), pack2bf(v[2], v[3]));
-#pragma unroll
-      for (int r = 0; r < 4; ++r) v[r] = act_fwd(v[r], p.act);
-      if (fsrc) {
-        v[0] += f[j].x; v[1] += f[j].y; v[2] += f[j].z; v[3] += f[j].w;
-      }
-      const long long ci = (long long)m * p.ldc + n;
-      if (p.out_f32) {
-        float4* C = reinterpret_cast<float4*>(static_cast<float*>(p.C) + ci);
-        if (p.accumulate && p.residual) {  // (no caller does both; C read late)
-          const float4 o = *C;
-          v[0] += o.x; v[1] += o.y; v[2] += o.z; v[3] += o.w;
+            for (int r = 0; r < 4; ++r) cs[jj][r] += w[r];
+          }
         }
-        *C = make_float4(v[0], v[1], v[2], v[3]);
-      } else {
-        *reinterpret_cast<uint2*>(static_cast<bf16_t*>(p.C) + ci) = make_uint2(pack2bf(v[0], v[1]), pack2bf(v[2], v[3]));
+        if (p.out_f32) {
+          if (ok) {
+            float4* C = reinterpret_cast<float4*>(static_cast<float*>(p.C) + (long long)m * p.ldc + n);
+            if (FWD && p.accumulate && p.residual) {  // (no caller does both; C read late)
+              const float4 o = *C;
+              w[0] += o.x; w[1] += o.y; w[2] += o.z; w[3] += o.w;
+            }
+            *C = make_float4(w[0], w[1], w[2], w[3]);
+          }
+        } else {
+          pc[h][0] = pack2bf(w[0], w[1]);
+          pc[h][1] = pack2bf(w[2], w[3]);
+        }
+      });
+      const int n8 = nw + 16 * j + coff;
+      const bool ok8 = mok && n8 < p.N;
+      if (FWD && aux_out) {
+        const auto s0 = __builtin_amdgcn_permlane16_swap(pa[0][0], pa[1][0], false, false);
+        const auto s1 = __builtin_amdgcn_permlane16_swap(pa[0][1], pa[1][1], false, false);
+        if (ok8)
+          *reinterpret_cast<uint4*>(aux_out + (long long)m * p.ld_aux_out + n8) = make_uint4(s0[0], s1[0], s0[1], s1[1]);
       }
-    }
-  }
-  if (p.colsum) {
-    // sum over the 16 rows of a lane group, then lane t of group g adds columns 2t, 2t+1 of the
-    // group's 32 (j = e >> 2, r = e & 3 -> column 16 j + 4 g + r)
-#pragma unroll
-    for (int j = 0; j < 8; ++j)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        float v = cs[j][r];
-        v += __shfl_xor(v, 1, 64);
-        v += __shfl_xor(v, 2, 64);
-        v += __shfl_xor(v, 4, 64);
-        v += __shfl_xor(v, 8, 64);
-        cs[j][r] = v;
+      if (!p.out_f32) {
+        const auto s0 = __builtin_amdgcn_permlane16_swap(pc[0][0], pc[1][0], false, false);
+        const auto s1 = __builtin_amdgcn_permlane16_swap(pc[0][1], pc[1][1], false, false);
+        if (ok8)
+          *reinterpret_cast<uint4*>(static_cast<bf16_t*>(p.C) + (long long)m * p.ldc + n8) =
+              make_uint4(s0[0], s1[0], s0[1], s1[1]);
       }
+    });
+  });
+  if constexpr (!FWD) {
+    if (p.colsum) {
+      // sum over the 16 rows of a lane group, then lane t of group g adds columns 2t, 2t+1 of
+      // the group's 32 (j = e >> 2, r = e & 3 -> column 16 j + 4 g + r)
 #pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      const int e = 2 * rl + h;
-      float v = 0.f;
+      for (int j = 0; j < 8; ++j)
 #pragma unroll
-      for (int k = 0; k < 32; ++k) v = (e == k) ? cs[k >> 2][k & 3] : v;
-      const int n = nw + 16 * (e >> 2) + 4 * g + (e & 3);
-      if (n < p.N) atomicAdd(p.colsum + n, v);
+        for (int r = 0; r < 4; ++r) {
+          float v = cs[j][r];
+          v += __shfl_xor(v, 1, 64);
+          v += __shfl_xor(v, 2, 64);
+          v += __shfl_xor(v, 4, 64);
+          v += __shfl_xor(v, 8, 64);
+          cs[j][r] = v;
+        }
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int e = 2 * rl + h;
+        float v = 0.f;
+#pragma unroll
+        for (int k = 0; k < 32; ++k) v = (e == k) ? cs[k >> 2][k & 3] : v;
+        const int n = nw + 16 * (e >> 2) + 4 * g + (e & 3);
+        if (n < p.N) atomicAdd(p.colsum + n, v);
+      }
     }
   }
 }
@@ -256,7 +318,8 @@ __device__ __forceinline__ void g7_epilogue_atomic(const GemmArgs& p, floatx4 (&
     }
 }
 
-// EPI: 0 = plain products (bf16 / f32 C), 1 = every fused epilogue, 2 = split-K f32 atomics.
+// EPI: 0 = plain products (bf16 / f32 C), 1 = forward fused epilogues, 2 = split-K f32 atomics,
+// 3 = input-gradient fused epilogues (act', column sums).
 template <int EPI, int SCHED, bool AK, bool BK>
 __global__ __launch_bounds__(256, 1) void gemm7_kernel(GemmArgs p, unsigned long long a_bytes,
                                                        unsigned long long b_bytes, G7Plan pl) {
@@ -416,12 +479,12 @@ __global__ __launch_bounds__(256, 1) void gemm7_kernel(GemmArgs p, unsigned long
     } else if (EPI == 2) {
       g7_epilogue_atomic(p, acc, m0 + ar, n0 + bc, lane);
     } else {
-      g7_epilogue<EPI == 1>(p, acc, m0 + ar, n0 + bc, lane);
+      g7_epilogue<EPI>(p, acc, m0 + ar, n0 + bc, lane);
     }
     // the stores were issued after this tile's last wait: the next DIST-2 waits (slices whose
     // DMA is older than the stores) may leave them in flight -- full tiles only (an edge tile
     // skips stores, and the credit must not exceed what was issued)
-    credit = (EPI == 0 && pl.store_cnt > 0 && m0 + 256 <= p.M && n0 + 256 <= p.N) ? DIST - 2 : 0;
+    credit = (EPI != 2 && pl.store_cnt > 0 && m0 + 256 <= p.M && n0 + 256 <= p.N) ? DIST - 2 : 0;
   }
 #undef G7_MFMA_ROW
 #undef G7_BODY
@@ -495,13 +558,18 @@ DPC_API int dpc_gemm7(const GemmArgs* a, int persistent, int sched, int splits, 
     }
   }
   if (s > 1 && !splittable) return -1;
+  // the input-gradient epilogue (act', column sums) carries no forward operation
+  if ((a->act_bwd || a->colsum) && (a->bias || a->act || a->aux_out || a->residual || a->accumulate)) return -1;
   pl.splits = s;
   pl.nk = 2 * ((pl.nk_all + 2 * s - 1) / (2 * s));  // even: a unit starts on register set 0
   pl.units = tiles * s;
   // persistent: one workgroup per CU streams its units through one ring; otherwise one unit
   // per workgroup
   pl.grid = (persistent && pl.units > 256) ? 256 : pl.units;
-  pl.store_cnt = (plain && !a->accumulate && s == 1) ? (a->out_f32 ? 64 : 32) : 0;
+  // vector-memory ops an epilogue issues per lane, for the store credit: only epilogues that
+  // read nothing per element and issue every store of a full tile (no column-sum atomics)
+  const bool no_loads = !a->residual && !a->act_bwd && !a->accumulate && !a->colsum;
+  pl.store_cnt = (no_loads && s == 1) ? ((a->out_f32 ? 64 : 32) + (a->aux_out ? 32 : 0)) : 0;
   static int dbg = -1;
   if (dbg < 0) dbg = getenv("DPC_G7_DEBUG") ? atoi(getenv("DPC_G7_DEBUG")) : 0;
   pl.debug = dbg;
@@ -513,8 +581,10 @@ DPC_API int dpc_gemm7(const GemmArgs* a, int persistent, int sched, int splits, 
     if (sched == 1) g7_launch<0, 1>(a, pl, stream, ab, bb);
     else if (sched == 2) g7_launch<0, 2>(a, pl, stream, ab, bb);
     else g7_launch<0, 0>(a, pl, stream, ab, bb);
-  } else {
+  } else if (!a->act_bwd && !a->colsum) {
     g7_launch<1, 2>(a, pl, stream, ab, bb);
+  } else {
+    g7_launch<3, 2>(a, pl, stream, ab, bb);
   }
   return (int)hipGetLastError();
 }
