@@ -17,8 +17,9 @@ ap.add_argument("--S", type=int, default=1023)
 ap.add_argument("--H", type=int, default=12)
 ap.add_argument("--iters", type=int, default=5)
 ap.add_argument("--bwd", action="store_true")
+ap.add_argument("--hd", type=int, default=64)
 a = ap.parse_args()
-hd = 64
+hd = a.hd
 qkv = torch.randn(a.N * a.S, 3 * a.H * hd, device="cuda").bfloat16()
 o, lse = attention_fwd(qkv, a.N, a.S, a.H, hd)
 do = torch.randn(a.N * a.S, a.H * hd, device="cuda").bfloat16()
@@ -33,4 +34,4 @@ e.record()
 torch.cuda.synchronize()
 fl = 4 * a.N * a.H * a.S * a.S * hd / 2 * (2.5 if a.bwd else 1.0)
 ms = s.elapsed_time(e) / a.iters
-print(f"{'bwd' if a.bwd else 'fwd'} N={a.N} S={a.S} H={a.H}: {ms * 1e3:.1f} us  {fl / ms / 1e9:.1f} TF/s")
+print(f"{'bwd' if a.bwd else 'fwd'} N={a.N} S={a.S} H={a.H} hd={hd}: {ms * 1e3:.1f} us  {fl / ms / 1e9:.1f} TF/s")

@@ -45,6 +45,7 @@ class AttnArgs(ctypes.Structure):
         ("N", c_int), ("S", c_int), ("H", c_int),
         ("scale", c_float),
         ("causal", c_int),
+        ("hd", c_int),
     ]
 
 

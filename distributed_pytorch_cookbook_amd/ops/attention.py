@@ -6,9 +6,10 @@ f32, output heads merged back to ``[T, H*hd]``.  One deliberate difference: a qu
 whose every key is masked yields 0 here (the reference's finfo.min / -1e9 arithmetic
 yields an ill-defined average); such rows only occur for all-padding sequences.
 
-HIP path (bf16, head_dim 64): ``dpc_attn_fwd`` / ``dpc_attn_bwd`` flash kernels
-(``csrc/attention.hip``) -- O(S) memory, f32 log-sum-exp saved for the backward.
-head_dim 32 (the reference default config) is zero-padded to 64 on the way in.
+HIP path (bf16, head_dim 32 or 64 natively): ``dpc_attn_fwd`` / ``dpc_attn_bwd`` flash
+kernels (``csrc/attention.hip``) -- O(S) memory, f32 log-sum-exp saved for the backward.
+head_dim 32 is the reference default config (``/root/reference/main-single.py:160``); other
+head sizes below 64 are zero-padded to the next kernel size on the way in.
 CPU / fp32 path: the same math with torch ops (test oracle).
 """
 from __future__ import annotations
@@ -19,7 +20,16 @@ import torch
 
 from . import _lib
 
-HD_KERNEL = 64
+HD_KERNELS = (32, 64)
+HD_KERNEL = 64  # the largest
+
+
+def kernel_head_dim(head_dim: int) -> int:
+    """The kernel size a head of ``head_dim`` runs at (itself for 32 / 64, else padded up)."""
+    for k in HD_KERNELS:
+        if head_dim <= k:
+            return k
+    raise NotImplementedError(f"attention kernel supports head_dim <= {HD_KERNEL}")
 
 
 def _use_hip(t: torch.Tensor) -> bool:
@@ -57,11 +67,11 @@ def attention_ref(qkv, N, S, heads, head_dim, pad_mask=None, causal=True, scale=
     return o.to(qkv.dtype), lse.reshape(N * heads, S)
 
 
-def _pad_heads(x: torch.Tensor, T: int, heads: int, head_dim: int) -> torch.Tensor:
-    """[T, H*hd] (strided view ok) -> contiguous [T, H*64] with zero padding."""
-    out = torch.zeros(T, heads, HD_KERNEL, device=x.device, dtype=x.dtype)
+def _pad_heads(x: torch.Tensor, T: int, heads: int, head_dim: int, kd: int) -> torch.Tensor:
+    """[T, H*hd] (strided view ok) -> contiguous [T, H*kd] with zero padding."""
+    out = torch.zeros(T, heads, kd, device=x.device, dtype=x.dtype)
     out[:, :, :head_dim] = x.reshape(T, heads, head_dim)
-    return out.reshape(T, heads * HD_KERNEL)
+    return out.reshape(T, heads * kd)
 
 
 def attention_fwd(qkv: torch.Tensor, N: int, S: int, heads: int, head_dim: int,
@@ -76,18 +86,17 @@ def attention_fwd(qkv: torch.Tensor, N: int, S: int, heads: int, head_dim: int,
             o = out
         return o, lse
     scale = 1.0 / math.sqrt(head_dim)
-    if head_dim != HD_KERNEL:
-        if head_dim > HD_KERNEL:
-            raise NotImplementedError(f"attention kernel supports head_dim <= {HD_KERNEL}")
+    kd = kernel_head_dim(head_dim)
+    if head_dim != kd:
         q, k, v = split_qkv(qkv, heads, head_dim)
-        qkv_p = torch.cat([_pad_heads(t, T, heads, head_dim) for t in (q, k, v)], dim=1)
-        o_p, lse = _attn_fwd_hip(qkv_p, N, S, heads, pad_mask, causal, scale, None)
-        o = o_p.reshape(T, heads, HD_KERNEL)[:, :, :head_dim].reshape(T, heads * head_dim)
+        qkv_p = torch.cat([_pad_heads(t, T, heads, head_dim, kd) for t in (q, k, v)], dim=1)
+        o_p, lse = _attn_fwd_hip(qkv_p, N, S, heads, kd, pad_mask, causal, scale, None)
+        o = o_p.reshape(T, heads, kd)[:, :, :head_dim].reshape(T, heads * head_dim)
         if out is not None:
             out.copy_(o)
             o = out
         return o.contiguous() if out is None else o, lse
-    return _attn_fwd_hip(qkv, N, S, heads, pad_mask, causal, scale, out)
+    return _attn_fwd_hip(qkv, N, S, heads, kd, pad_mask, causal, scale, out)
 
 
 def _check(t, T, cols, name):
@@ -97,9 +106,9 @@ def _check(t, T, cols, name):
         raise ValueError(f"attention: {name} must be 16-B aligned with row stride % 8 == 0")
 
 
-def _attn_fwd_hip(qkv, N, S, heads, pad_mask, causal, scale, out):
+def _attn_fwd_hip(qkv, N, S, heads, kd, pad_mask, causal, scale, out):
     T = N * S
-    hd = heads * HD_KERNEL
+    hd = heads * kd
     _check(qkv, T, 3 * hd, "qkv")
     if out is None:
         out = torch.empty(T, hd, device=qkv.device, dtype=torch.bfloat16)
@@ -109,11 +118,11 @@ def _attn_fwd_hip(qkv, N, S, heads, pad_mask, causal, scale, out):
     if pad_mask is not None:
         pad = pad_mask.to(torch.uint8).contiguous()
         assert pad.shape == (N, S)
-    q, k, v = split_qkv(qkv, heads, HD_KERNEL)
+    q, k, v = split_qkv(qkv, heads, kd)
     args = _lib.AttnArgs(
         q=q.data_ptr(), k=k.data_ptr(), v=v.data_ptr(), o=out.data_ptr(), lse=lse.data_ptr(),
         pad=_lib.ptr(pad), ld_qkv=qkv.stride(0), ld_o=out.stride(0), ld_dqkv=0,
-        N=N, S=S, H=heads, scale=float(scale), causal=int(causal),
+        N=N, S=S, H=heads, scale=float(scale), causal=int(causal), hd=kd,
     )
     _lib.call("dpc_attn_fwd", args, qkv.device)
     return out, lse
@@ -135,23 +144,24 @@ def attention_bwd(dout: torch.Tensor, qkv: torch.Tensor, o: torch.Tensor, lse: t
             return dqkv
         return g.to(qkv.dtype)
     scale = 1.0 / math.sqrt(head_dim)
-    if head_dim != HD_KERNEL:
+    kd = kernel_head_dim(head_dim)
+    if head_dim != kd:
         q, k, v = split_qkv(qkv, heads, head_dim)
-        qkv_p = torch.cat([_pad_heads(t, T, heads, head_dim) for t in (q, k, v)], dim=1)
-        o_p = _pad_heads(o, T, heads, head_dim)
-        do_p = _pad_heads(dout, T, heads, head_dim)
-        g_p = _attn_bwd_hip(do_p, qkv_p, o_p, lse, N, S, heads, pad_mask, causal, scale, None)
-        g = g_p.reshape(T, 3, heads, HD_KERNEL)[..., :head_dim].reshape(T, 3 * heads * head_dim)
+        qkv_p = torch.cat([_pad_heads(t, T, heads, head_dim, kd) for t in (q, k, v)], dim=1)
+        o_p = _pad_heads(o, T, heads, head_dim, kd)
+        do_p = _pad_heads(dout, T, heads, head_dim, kd)
+        g_p = _attn_bwd_hip(do_p, qkv_p, o_p, lse, N, S, heads, kd, pad_mask, causal, scale, None)
+        g = g_p.reshape(T, 3, heads, kd)[..., :head_dim].reshape(T, 3 * heads * head_dim)
         if dqkv is not None:
             dqkv.copy_(g)
             return dqkv
         return g.contiguous()
-    return _attn_bwd_hip(dout, qkv, o, lse, N, S, heads, pad_mask, causal, scale, dqkv)
+    return _attn_bwd_hip(dout, qkv, o, lse, N, S, heads, kd, pad_mask, causal, scale, dqkv)
 
 
-def _attn_bwd_hip(dout, qkv, o, lse, N, S, heads, pad_mask, causal, scale, dqkv):
+def _attn_bwd_hip(dout, qkv, o, lse, N, S, heads, kd, pad_mask, causal, scale, dqkv):
     T = N * S
-    hd = heads * HD_KERNEL
+    hd = heads * kd
     _check(qkv, T, 3 * hd, "qkv")
     _check(o, T, hd, "o")
     _check(dout, T, hd, "dout")
@@ -167,14 +177,14 @@ def _attn_bwd_hip(dout, qkv, o, lse, N, S, heads, pad_mask, causal, scale, dqkv)
     pad = None
     if pad_mask is not None:
         pad = pad_mask.to(torch.uint8).contiguous()
-    q, k, v = split_qkv(qkv, heads, HD_KERNEL)
-    dq, dk, dv = split_qkv(dqkv, heads, HD_KERNEL)
+    q, k, v = split_qkv(qkv, heads, kd)
+    dq, dk, dv = split_qkv(dqkv, heads, kd)
     args = _lib.AttnArgs(
         q=q.data_ptr(), k=k.data_ptr(), v=v.data_ptr(), o=o.data_ptr(), lse=lse.data_ptr(),
         pad=_lib.ptr(pad), dout=dout.data_ptr(), dq=dq.data_ptr(), dk=dk.data_ptr(),
         dv=dv.data_ptr(), delta=delta.data_ptr(),
         ld_qkv=qkv.stride(0), ld_o=o.stride(0), ld_dqkv=dqkv.stride(0),
-        N=N, S=S, H=heads, scale=float(scale), causal=int(causal),
+        N=N, S=S, H=heads, scale=float(scale), causal=int(causal), hd=kd,
     )
     _lib.call("dpc_attn_bwd", args, qkv.device)
     return dqkv

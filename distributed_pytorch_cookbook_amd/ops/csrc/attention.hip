@@ -1,10 +1,10 @@
-// Flash attention (forward + backward) for gfx950, head_dim 64, bf16 in / bf16 out,
-// f32 online softmax, causal + optional key-padding mask.
+// Flash attention (forward + backward) for gfx950: head_dim 32 or 64 natively (template HD),
+// bf16 in / bf16 out, f32 online softmax, causal + optional key-padding mask.
 //
-// Replaces the reference's materialised attention (models/gpt.py:75-100: q@k, host-built
-// causal mask copied H2D every layer, masked_fill, fp32 softmax, @v, head merge) with an
-// O(S) kernel that reads q/k/v straight out of the fused QKV projection ([T, 3*H*hd],
-// token-major) and writes the merged-head output [T, H*hd] -- no permute/clone copies.
+// Replaces the reference's materialised attention (/root/reference/models/gpt.py:75-100: q@k,
+// host-built causal mask copied H2D every layer, masked_fill, fp32 softmax, @v, head merge)
+// with O(S) kernels that read q/k/v straight out of the fused QKV projection ([T, 3*H*hd],
+// token-major) and write the merged-head output [T, H*hd] -- no permute/clone copies.
 //
 // MFMA layout (v_mfma_f32_32x32x16_bf16; C/D: col = lane & 31,
 // row = (r & 3) + 8 (r >> 2) + 4 (lane >> 5)):
@@ -18,15 +18,29 @@
 //            dV^T += dO^T P and dK^T += Q^T dS with dO^T / Q^T via transposing reads.
 //            dQ kernel: S^T, dP^T with the query on the lane, dQ^T += K^T dS^T.
 //            No float atomics: each output is owned by exactly one wave.
-// LDS tiles are [row][64] bf16 (128-B rows) with the 16-B chunk swizzle
-//   chunk ^ (((row >> 1) & 7) ^ (((row >> 1) & 1) << 2))
-// which is conflict free for both the ds_read_b128 row reads and the tr_b16 column reads.
+//
+// Pipeline (every kernel): the streamed 64-row tiles (K/V, or Q/dO + their per-row lse /
+// delta) arrive by LDS-DMA into a 4-slot ring, issued from inline asm two tiles ahead, so the
+// only wait is a counted vmcnt + barrier per tile at the top of the loop.  Inside a wave the
+// work of adjacent 32-row sub-blocks is software-pipelined: the score MFMAs of sub-block
+// j+1 sit in the same basic block as the softmax VALU of sub-block j (independent, so the
+// scheduler interleaves them), then the accumulate MFMAs of j -- a wave alternates MFMA and
+// VALU work on its own instead of relying on lock-stepped partner waves.
+//
+// LDS image of a tile: the [64 rows][HD] bf16 tile is stored as 128-B physical rows (HD=64:
+// one row each; HD=32: two rows each) with the 16-B chunk swizzle
+//   chunk ^ (((prow >> 1) & 7) ^ (((prow >> 1) & 1) << 2))
+// which is conflict free for the ds_read_b128 row reads and the tr_b16 column reads at both
+// head sizes.
 #include "common.h"
+
+#include <cstdio>
+#include <cstdlib>
 
 namespace dpc {
 
 struct AttnArgs {
-  const void* q; const void* k; const void* v;  // bf16, row = token (n*S + s), head h at col h*64
+  const void* q; const void* k; const void* v;  // bf16, row = token (n*S + s), head h at col h*hd
   void* o;                                      // bf16 [T][ld_o]
   float* lse;                                   // f32 [N*H][S] (natural log of scaled scores)
   const unsigned char* pad;                     // [N][S], 1 = padded key (masked), optional
@@ -37,88 +51,117 @@ struct AttnArgs {
   int N, S, H;
   float scale;
   int causal;
+  int hd;                                       // head_dim: 32 or 64
 };
 
-constexpr int HD = 64;
 constexpr int KT = 64;       // keys (or queries) per staged tile
 constexpr int QB = 128;      // rows per workgroup (4 waves x 32)
+constexpr int NSLOT = 4;     // LDS ring depth: tiles t (read), t+1 (landed), t+2, t+3 (in flight)
 constexpr float LOG2E = 1.4426950408889634f;
 
+template <int HD>
+struct AT {
+  static_assert(HD == 32 || HD == 64, "head_dim 32 or 64");
+  static constexpr int TILE = KT * HD;   // elements of one 64-row tile
+  static constexpr int NPW = HD / 32;    // 1-KiB DMA pieces per wave per tile (4 waves)
+  static constexpr int NST = HD / 16;    // k-steps of a product over head_dim (32x32x16)
+  static constexpr int NDT = HD / 32;    // 32-column blocks of an HD-wide accumulator
+};
+
 typedef short4_t __attribute__((address_space(3))) * lds4_t;
-
-__device__ __forceinline__ int aswz(int row) {
-  const int a = (row >> 1) & 7;
-  return a ^ ((a & 1) << 2);
-}
-__device__ __forceinline__ int aoff(int row, int chunk) {  // element offset in a [row][64] tile
-  return row * HD + ((chunk ^ aswz(row)) << 3);
-}
-
-// Stage a 64-row x 64-col bf16 tile (rows r0.., zero beyond `rows`) into LDS.
-__device__ __forceinline__ void tile_load(uint4 (&r)[2], const bf16_t* base, long long ld,
-                                          int row0, int rows) {
-#pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    const int c = threadIdx.x + i * 256;
-    const int row = c >> 3, ch = c & 7;
-    uint4 v = make_uint4(0, 0, 0, 0);
-    if (row0 + row < rows) v = *reinterpret_cast<const uint4*>(base + (long long)(row0 + row) * ld + ch * 8);
-    r[i] = v;
-  }
-}
-__device__ __forceinline__ void tile_store(const uint4 (&r)[2], bf16_t* lds) {
-#pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    const int c = threadIdx.x + i * 256;
-    *reinterpret_cast<uint4*>(lds + aoff(c >> 3, c & 7)) = r[i];
-  }
-}
-
-// LDS-DMA staging of a 64-row x 64-col bf16 tile (buffer_load_dwordx4 ... lds: no VGPR round
-// trip, no ds_write).  The DMA writes lane-linearly -- wave-instruction j fills rows 8j..8j+7,
-// lane l slot (l & 7) of row 8j + (l >> 3) -- so the chunk swizzle of aoff() moves to the
-// SOURCE address: the lane fetches chunk (l & 7) ^ aswz(row).  dma_voff: the lane's byte
-// offset for the wave's two instructions (4 waves x 2 x 1 KiB = the 8 KiB tile), relative to
-// the tile's first row.  num_records ends the descriptor at the sequence end (rows >= S land
-// as zeros, as the register-staged path zero-filled them).
 typedef __attribute__((address_space(3))) void* lds_void_t;
 
-__device__ __forceinline__ void dma_voff(int (&v)[2], long long ld, int wid, int lane) {
+__device__ __forceinline__ int aswz(int prow) {
+  const int a = (prow >> 1) & 7;
+  return a ^ ((a & 1) << 2);
+}
+// element offset of (row, 16-B chunk) in the LDS image of a tile
+template <int HD>
+__device__ __forceinline__ int toff(int row, int chunk) {
+  const int e = row * HD + chunk * 8;
+  const int prow = e >> 6, pch = (e >> 3) & 7;
+  return (prow << 6) + ((pch ^ aswz(prow)) << 3);
+}
+
+// ---- LDS-DMA from inline asm (buffer_load ... lds; M0 = the wave's LDS destination).
+// Issued from asm so that the compiler does not wait for it before every LDS read: the
+// kernels wait with explicit counted s_waitcnt at the ring boundary.
+__device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t rs, int voff, const void* lds) {
+  const unsigned la = (unsigned)(uintptr_t)(lds_void_t)lds;
+  unsigned keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(voff), "s"(rs), "s"(la)
+      : "memory");
+}
+__device__ __forceinline__ void dma4(__amdgpu_buffer_rsrc_t rs, int voff, const void* lds) {
+  const unsigned la = (unsigned)(uintptr_t)(lds_void_t)lds;
+  unsigned keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dword %1, %2, 0 offen lds\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(voff), "s"(rs), "s"(la)
+      : "memory");
+}
+template <int N>
+__device__ __forceinline__ void vm_wait() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+__device__ __forceinline__ void ring_barrier() {
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rows_rsrc(const void* base, long long ld_bytes, int row0, int S,
+                                                           bool valid) {
+  const long long left = valid ? (long long)(S - row0) * ld_bytes : 0;
+  const unsigned nrec = left <= 0 ? 0u : (left > 0xffffffffll ? 0xffffffffu : (unsigned)left);
+  return __builtin_amdgcn_make_buffer_rsrc((void*)((const char*)base + (long long)row0 * ld_bytes), 0, nrec,
+                                           0x00020000);
+}
+
+// The DMA writes lane-linearly -- piece g (wave wid, instruction i: g = wid * NPW + i) fills
+// physical rows 8g .. 8g+7, lane l slot (l & 7) of physical row 8g + (l >> 3) -- so the chunk
+// swizzle moves to the SOURCE address: the lane fetches the logical (row, chunk) that the
+// swizzle maps to its slot.  v: the lane's byte offsets relative to the tile's first row.
+template <int HD>
+__device__ __forceinline__ void dma_voff(int (&v)[AT<HD>::NPW], long long ld, int wid, int lane) {
 #pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    const int row = 8 * (wid * 2 + i) + (lane >> 3);
-    const int chunk = (lane & 7) ^ aswz(row);
+  for (int i = 0; i < AT<HD>::NPW; ++i) {
+    const int prow = 8 * (wid * AT<HD>::NPW + i) + (lane >> 3);
+    const int e = prow * 64 + (((lane & 7) ^ aswz(prow)) << 3);
+    const int row = e / HD, chunk = (e % HD) >> 3;
     v[i] = (int)((long long)row * ld * 2 + chunk * 16);
   }
 }
 
-__device__ __forceinline__ void tile_dma(const bf16_t* base, long long ld, int row0, int S, const int (&v)[2],
-                                         bf16_t* lds, int wid) {
-  const long long left = (long long)(S - row0) * ld * 2;
-  const unsigned nrec = left <= 0 ? 0u : (left > 0xffffffffll ? 0xffffffffu : (unsigned)left);
-  const __amdgpu_buffer_rsrc_t rs =
-      __builtin_amdgcn_make_buffer_rsrc((void*)(base + (long long)row0 * ld), 0, nrec, 0x00020000);
+// one 64-row tile (rows >= S, or the whole tile if !valid, land as zeros)
+template <int HD>
+__device__ __forceinline__ void tile_dma(const bf16_t* base, long long ld, int row0, int S, bool valid,
+                                         const int (&v)[AT<HD>::NPW], bf16_t* lds, int wid) {
+  const __amdgpu_buffer_rsrc_t rs = rows_rsrc(base, ld * 2, row0, S, valid);
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void_t)(lds + (wid * 2 + i) * 512), 16, v[i], 0, 0, 0);
+  for (int i = 0; i < AT<HD>::NPW; ++i) dma16(rs, v[i], lds + (wid * AT<HD>::NPW + i) * 512);
 }
 
 // Row fragment (A or B operand of 32x32x16): lane holds X[row0 + (lane & 31)][16 st + 8 h .. +7]
+template <int HD>
 __device__ __forceinline__ bf16x8 row_frag(const bf16_t* lds, int row0, int st, int lane) {
-  const int row = row0 + (lane & 31);
-  const int chunk = 2 * st + (lane >> 5);
-  return *reinterpret_cast<const bf16x8*>(lds + aoff(row, chunk));
+  return *reinterpret_cast<const bf16x8*>(lds + toff<HD>(row0 + (lane & 31), 2 * st + (lane >> 5)));
 }
 
 // Transposed fragment: lane gets X[rows r0 + 16 s + 8 (j >> 2) + 4 h + (j & 3)][col c0 + (lane & 31)]
 // i.e. the permuted k order of an accumulator-as-operand k-step s.
+template <int HD>
 __device__ __forceinline__ bf16x8 tr_frag(const bf16_t* lds, int r0, int s, int c0, int lane) {
   const int h = lane >> 5, g2 = (lane >> 4) & 1, i16 = lane & 15, q = i16 >> 2, p = i16 & 3;
   const int row = r0 + 16 * s + 4 * h + q;
   const int col = c0 + 16 * g2 + 4 * p;
-  const int chunk = col >> 3, within = col & 7;
-  const bf16_t* a0 = lds + row * HD + (((chunk ^ aswz(row)) << 3) | within);
-  const bf16_t* a1 = lds + (row + 8) * HD + (((chunk ^ aswz(row + 8)) << 3) | within);
+  const bf16_t* a0 = lds + toff<HD>(row, col >> 3) + (col & 7);
+  const bf16_t* a1 = lds + toff<HD>(row + 8, col >> 3) + (col & 7);
   short4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds4_t)a0);
   short4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds4_t)a1);
   typedef short short8_t __attribute__((ext_vector_type(8)));
@@ -138,7 +181,7 @@ __device__ __forceinline__ bf16x8 acc_frag(const floatx16& x, int s) {
 
 __device__ __forceinline__ int acc_row(int r, int lane) { return (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5); }
 
-// raw v_exp_f32 (2^x): inputs here are <= 0 or -inf, no denormal range reduction needed
+// raw v_exp_f32 (2^x): inputs here are <= ~8 or -inf, no denormal range reduction needed
 __device__ __forceinline__ float fast_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
 
 // v_max3_f32.  This file is built with -fno-honor-nans (nothing here produces a NaN), so
@@ -158,11 +201,15 @@ __device__ __forceinline__ bf16x8 load_row8(const bf16_t* p) {
 
 #define MFMA32(a, b, c) __builtin_amdgcn_mfma_f32_32x32x16_bf16((a), (b), (c), 0, 0, 0)
 
+__device__ __forceinline__ void zero16(floatx16& x) {
+#pragma unroll
+  for (int i = 0; i < 16; ++i) x[i] = 0.f;
+}
+
 // XCD-aware work id (1-D grid of nblk * N * H workgroups): workgroup b runs on XCD b % 8, and
 // the bijective remap gives every XCD a contiguous run of ids, so all the q- (or key-) blocks
-// of one (batch, head) -- which read the same K/V (Q/dO) rows -- share one XCD's L2 instead of
-// being spread over all eight (the 2-D grid put block i of every head on XCD i: each head's
-// K/V was fetched into eight L2s).  Returns (bh, i): i = block index within the head.
+// of one (batch, head) -- which read the same K/V (Q/dO) rows -- share one XCD's L2.
+// Returns (bh, i): i = block index within the head.
 __device__ __forceinline__ void xcd_work(int nblk, int& bh, int& i) {
   const int b = blockIdx.x, nwg = gridDim.x, xcd = b & 7, q = nwg >> 3, r = nwg & 7;
   const int t = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (b >> 3);
@@ -171,19 +218,23 @@ __device__ __forceinline__ void xcd_work(int nblk, int& bh, int& i) {
 }
 
 // ------------------------------------------------------------------ forward
-// Three workgroups (12 waves) per CU: with the K/V tiles staged by LDS-DMA the kernel fits
-// 168 VGPRs (7 spilled); a third wave per SIMD hides more of the softmax / MFMA alternation.
-// bench/attn_one.py N=64 S=1023 H=12 on one MI355X: register staging at 2 WG/CU 285.7 us,
-// DMA at 2 WG/CU 277.2 us, DMA at 3 WG/CU 264.5 us (profiles/r1_v18_attn_fwd_dma_ab.txt).
-__global__ __launch_bounds__(256, 3) void attn_fwd_kernel(AttnArgs p) {
-  __shared__ __attribute__((aligned(16))) bf16_t smem[2 * 2 * KT * HD];  // [stage][K|V]
+// Workgroup = 128 queries (4 waves x 32, query on the lane), sweeping 64-key tiles.  Per tile
+// and wave: S^T of the NEXT tile (2 x NST MFMAs) overlaps this tile's softmax, then
+// O^T += V^T P^T (4 x NDT MFMAs).
+// PIPE: 0 = plain order, 1 = next tile's S^T beside this tile's softmax, 2 = 1 + the tile's
+// LDS fragments read up front and the MFMA / VALU interleave pinned (sched_group_barrier)
+template <int HD, int PIPE, int OCC>
+__global__ __launch_bounds__(256, OCC) void attn_fwd_kernel(AttnArgs p) {
+  using A = AT<HD>;
+  __shared__ __attribute__((aligned(16))) bf16_t smem[NSLOT * 2 * A::TILE];  // [slot][K|V]
   const int S = p.S, H = p.H;
   const int nqb = (S + QB - 1) / QB;
   int bh, bi;
   xcd_work(nqb, bh, bi);
   const int qb = nqb - 1 - bi;  // heaviest causal blocks of a head first
   const int n = bh / H, h = bh % H;
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, hh = lane >> 5;
+  const int lane = threadIdx.x & 63, hh = lane >> 5;
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int q0 = qb * QB + wid * 32;
   const int q = q0 + (lane & 31);
   const long long tok0 = (long long)n * S;
@@ -191,124 +242,191 @@ __global__ __launch_bounds__(256, 3) void attn_fwd_kernel(AttnArgs p) {
   const bf16_t* K = static_cast<const bf16_t*>(p.k) + tok0 * p.ld_qkv + h * HD;
   const bf16_t* V = static_cast<const bf16_t*>(p.v) + tok0 * p.ld_qkv + h * HD;
 
-  bf16x8 qf[4];
+  bf16x8 qf[A::NST];
 #pragma unroll
-  for (int st = 0; st < 4; ++st) {
-    if (q < S) qf[st] = load_row8(Q + (tok0 + q) * p.ld_qkv + 16 * st + 8 * hh);
-    else qf[st] = bf16x8{};
-  }
+  for (int st = 0; st < A::NST; ++st)
+    qf[st] = q < S ? load_row8(Q + (tok0 + q) * p.ld_qkv + 16 * st + 8 * hh) : bf16x8{};
   const float c = p.scale * LOG2E;
   const int kend = p.causal ? min(S, qb * QB + QB) : S;
   const int ntiles = (kend + KT - 1) / KT;
+  // this wave's last tile holding a key it may attend to
+  const int last_w = p.causal ? min(ntiles - 1, max(0, min(q0 + 31, S - 1)) / KT) : ntiles - 1;
   const unsigned char* pad = p.pad ? p.pad + (long long)n * S : nullptr;
 
-  float m = -INFINITY, l = 0.f;
-  floatx16 o[2];
+  int dv[A::NPW];
+  dma_voff<HD>(dv, p.ld_qkv, wid, lane);
+  auto issue = [&](int t) {
+    bf16_t* st = smem + (t % NSLOT) * 2 * A::TILE;
+    const bool valid = t < ntiles;
+    tile_dma<HD>(K, p.ld_qkv, t * KT, S, valid, dv, st, wid);
+    tile_dma<HD>(V, p.ld_qkv, t * KT, S, valid, dv, st + A::TILE, wid);
+  };
+  // S^T = K Q^T of the tile in LDS at lk (keys on the accumulator rows, query on the lane)
+  auto qk = [&](floatx16 (&s)[2], const bf16_t* lk) {
 #pragma unroll
-  for (int i = 0; i < 16; ++i) { o[0][i] = 0.f; o[1][i] = 0.f; }
-
-  // K/V tiles stream into the LDS double buffer by DMA: tile t+1 is issued at the top of
-  // iteration t into the stage iteration t-1 read (released by its closing barrier), and
-  // lands under this iteration's MFMAs; no staging registers (16 VGPRs) as the
-  // register-staged copy needed.
-  int dv[2];
-  dma_voff(dv, p.ld_qkv, wid, lane);
-  tile_dma(K, p.ld_qkv, 0, S, dv, smem, wid);
-  tile_dma(V, p.ld_qkv, 0, S, dv, smem + KT * HD, wid);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-
-  for (int t = 0; t < ntiles; ++t) {
-    const int cur = t & 1;
-    const bool more = t + 1 < ntiles;
-    if (more) {
-      bf16_t* nx = smem + (cur ^ 1) * 2 * KT * HD;
-      tile_dma(K, p.ld_qkv, (t + 1) * KT, S, dv, nx, wid);
-      tile_dma(V, p.ld_qkv, (t + 1) * KT, S, dv, nx + KT * HD, wid);
+    for (int kb = 0; kb < 2; ++kb) {
+      zero16(s[kb]);
+#pragma unroll
+      for (int st = 0; st < A::NST; ++st) s[kb] = MFMA32(row_frag<HD>(lk, kb * 32, st, lane), qf[st], s[kb]);
     }
-    const bf16_t* lk = smem + cur * 2 * KT * HD;
-    const bf16_t* lv = lk + KT * HD;
+  };
+
+  float m = -INFINITY, l = 0.f;
+  floatx16 o[A::NDT];
+#pragma unroll
+  for (int d = 0; d < A::NDT; ++d) zero16(o[d]);
+
+  issue(0);
+  issue(1);
+  issue(2);
+  vm_wait<4 * A::NPW>();  // tile 0 landed (tiles 1, 2 may fly)
+  ring_barrier();
+  // one tile: scores of tile t in sc; the next tile's land in sn (ping-pong, no copies)
+  auto step = [&](int t, floatx16 (&sc)[2], floatx16 (&sn)[2]) {
+    vm_wait<2 * A::NPW>();  // this wave's pieces of tile t+1 landed (t+2 may fly)
+    ring_barrier();         // ... every wave's; and every wave is done with tile t-1's slot
+    issue(t + 3);
+    const bf16_t* lkn = smem + ((t + 1) % NSLOT) * 2 * A::TILE;
+    const bf16_t* lv = smem + (t % NSLOT) * 2 * A::TILE + A::TILE;
+    if (t > last_w) return;  // wave-uniform
+    if constexpr (PIPE == 0) qk(sc, lv - A::TILE);
+    // PIPE 2: the next tile's K row fragments and this tile's V^T fragments, read before the
+    // softmax so their LDS latency hides under it
+    bf16x8 kfr[2][A::NST], vfr[2][2][A::NDT];
+    if constexpr (PIPE == 2) {
+#pragma unroll
+      for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+        for (int st = 0; st < A::NST; ++st) kfr[kb][st] = row_frag<HD>(lkn, kb * 32, st, lane);
+#pragma unroll
+      for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+        for (int ss = 0; ss < 2; ++ss)
+#pragma unroll
+          for (int d = 0; d < A::NDT; ++d) vfr[kb][ss][d] = tr_frag<HD>(lv, kb * 32, ss, d * 32, lane);
+    }
     const int kt0 = t * KT;
-    const bool active = !(p.causal && kt0 > q0 + 31);  // wave-uniform
-    if (active) {
-      floatx16 s[2];
-#pragma unroll
-      for (int kb = 0; kb < 2; ++kb) {
-#pragma unroll
-        for (int i = 0; i < 16; ++i) s[kb][i] = 0.f;
-#pragma unroll
-        for (int st = 0; st < 4; ++st) s[kb] = MFMA32(row_frag(lk, kb * 32, st, lane), qf[st], s[kb]);
-      }
-      // Scores stay raw (unscaled) until the exponent: p = 2^(s*c - m) is one FMA + v_exp.
-      // Interior tiles (the vast majority) skip the mask arithmetic entirely (uniform branch).
-      const bool need_mask = (p.causal && kt0 + KT - 1 > q0) || (kt0 + KT > S) || pad;  // wave-uniform
-      if (need_mask) {
-        // key > lim is causal / past-the-end, pm is the tile's padding bitmask
-        const unsigned long long pm = pad_bits(pad, kt0, S, lane);
-        const int lim = (p.causal ? min(q, S - 1) : S - 1) - kt0;
-#pragma unroll
-        for (int kb = 0; kb < 2; ++kb)
-#pragma unroll
-          for (int r = 0; r < 16; ++r) {
-            const int kl = kb * 32 + acc_row(r, lane);
-            if (kl > lim || ((pm >> kl) & 1ull)) s[kb][r] = -INFINITY;
-          }
-      }
-      float mx = max3f(s[0][0], s[0][1], s[0][2]);
-#pragma unroll
-      for (int r = 3; r < 15; r += 2) mx = max3f(mx, s[0][r], s[0][r + 1]);
-      mx = max3f(mx, s[0][15], s[1][0]);
-#pragma unroll
-      for (int r = 1; r < 15; r += 2) mx = max3f(mx, s[1][r], s[1][r + 1]);
-      mx = fmaxf(mx, s[1][15]);
-      mx = fmaxf(mx, __shfl_xor(mx, 32, 64)) * c;  // scaled log2 units (c > 0)
-      // lazy rescale: the running max only moves when the tile max exceeds it by > 2^8, so
-      // p <= 256 (exact enough in f32 / bf16) and the O rescale is skipped on most tiles
-      if (__ballot(mx > m + 8.f)) {
-        const float mn = fmaxf(m, mx);
-        const float alpha = (mn == -INFINITY) ? 1.f : fast_exp2(m - mn);
-        m = mn;
-        l *= alpha;
-#pragma unroll
-        for (int i = 0; i < 16; ++i) { o[0][i] *= alpha; o[1][i] *= alpha; }
-      }
-      const float nmu = (m == -INFINITY) ? 0.f : -m;
-      float ls = 0.f;
+    // Scores stay raw (unscaled) until the exponent: p = 2^(s*c - m) is one FMA + v_exp.
+    const bool need_mask = (p.causal && kt0 + KT - 1 > q0) || (kt0 + KT > S) || pad;  // wave-uniform
+    if (need_mask) {
+      // key > lim is causal / past-the-end, pm is the tile's padding bitmask
+      const unsigned long long pm = pad_bits(pad, kt0, S, lane);
+      const int lim = (p.causal ? min(q, S - 1) : S - 1) - kt0;
 #pragma unroll
       for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-          const float e = fast_exp2(fmaf(s[kb][r], c, nmu));
-          s[kb][r] = e;
-          ls += e;
-        }
-      ls += __shfl_xor(ls, 32, 64);
-      l += ls;
-#pragma unroll
-      for (int kb = 0; kb < 2; ++kb)
-#pragma unroll
-        for (int ss = 0; ss < 2; ++ss) {
-          const bf16x8 pb = acc_frag(s[kb], ss);
-#pragma unroll
-          for (int dt = 0; dt < 2; ++dt) o[dt] = MFMA32(tr_frag(lv, kb * 32, ss, dt * 32, lane), pb, o[dt]);
+          const int kl = kb * 32 + acc_row(r, lane);
+          if (kl > lim || ((pm >> kl) & 1ull)) sc[kb][r] = -INFINITY;
         }
     }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's DMA of tile t+1 landed
-    __syncthreads();  // ... every wave's, and stage cur is free for tile t+2
+    float mx = max3f(sc[0][0], sc[0][1], sc[0][2]);
+#pragma unroll
+    for (int r = 3; r < 15; r += 2) mx = max3f(mx, sc[0][r], sc[0][r + 1]);
+    mx = max3f(mx, sc[0][15], sc[1][0]);
+#pragma unroll
+    for (int r = 1; r < 15; r += 2) mx = max3f(mx, sc[1][r], sc[1][r + 1]);
+    mx = fmaxf(mx, sc[1][15]);
+    mx = fmaxf(mx, __shfl_xor(mx, 32, 64)) * c;  // scaled log2 units (c > 0)
+    // lazy rescale: the running max only moves when the tile max exceeds it by > 2^8, so
+    // p <= 256 (exact enough in f32 / bf16) and the O rescale is skipped on most tiles
+    if (__ballot(mx > m + 8.f)) {
+      const float mn = fmaxf(m, mx);
+      const float alpha = (mn == -INFINITY) ? 1.f : fast_exp2(m - mn);
+      m = mn;
+      l *= alpha;
+#pragma unroll
+      for (int d = 0; d < A::NDT; ++d)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) o[d][i] *= alpha;
+    }
+    const float nmu = (m == -INFINITY) ? 0.f : -m;
+    // ---- one basic block: next tile's S^T MFMAs || this tile's exponentials
+    if constexpr (PIPE == 2) {
+      float ls = 0.f;
+#pragma unroll
+      for (int kb = 0; kb < 2; ++kb) {
+        zero16(sn[kb]);
+#pragma unroll
+        for (int st = 0; st < A::NST; ++st) sn[kb] = MFMA32(kfr[kb][st], qf[st], sn[kb]);
+      }
+      bf16x8 pb[2][2];
+#pragma unroll
+      for (int kb = 0; kb < 2; ++kb) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const float e = fast_exp2(fmaf(sc[kb][r], c, nmu));
+          sc[kb][r] = e;
+          ls += e;
+        }
+        pb[kb][0] = acc_frag(sc[kb], 0);
+        pb[kb][1] = acc_frag(sc[kb], 1);
+#pragma unroll
+        for (int ss = 0; ss < 2; ++ss)
+#pragma unroll
+          for (int d = 0; d < A::NDT; ++d) o[d] = MFMA32(vfr[kb][ss][d], pb[kb][ss], o[d]);
+      }
+      l += ls;
+      // interleave: the 2 NST score MFMAs carry the first half's ~56 VALU, the first half's
+      // 2 NDT PV MFMAs the second half's, then the last PV MFMAs
+      constexpr int NQ = 2 * A::NST, NP = 2 * A::NDT;
+#pragma unroll
+      for (int i = 0; i < NQ; ++i) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x002, 56 / NQ, 0);
+      }
+#pragma unroll
+      for (int i = 0; i < NP; ++i) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x002, 56 / NP, 0);
+      }
+      __builtin_amdgcn_sched_group_barrier(0x008, NP, 0);
+      return;
+    }
+    if constexpr (PIPE == 1) qk(sn, lkn);
+    float ls = 0.f;
+    bf16x8 pb[2][2];
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const float e = fast_exp2(fmaf(sc[kb][r], c, nmu));
+        sc[kb][r] = e;
+        ls += e;
+      }
+      pb[kb][0] = acc_frag(sc[kb], 0);
+      pb[kb][1] = acc_frag(sc[kb], 1);
+    }
+    l += ls;
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+      for (int ss = 0; ss < 2; ++ss)
+#pragma unroll
+        for (int d = 0; d < A::NDT; ++d)
+          o[d] = MFMA32(tr_frag<HD>(lv, kb * 32, ss, d * 32, lane), pb[kb][ss], o[d]);
+  };
+  floatx16 s0[2], s1[2];
+  if constexpr (PIPE != 0) qk(s0, smem);
+  for (int t = 0; t < ntiles; t += 2) {
+    step(t, s0, s1);
+    if (t + 1 < ntiles) step(t + 1, s1, s0);
   }
+  vm_wait<0>();  // the pieces issued past the last tile (empty descriptors) drained
 
+  l += __shfl_xor(l, 32, 64);  // the two lane halves summed different key rows
   if (q < S) {
     const float inv = l > 0.f ? 1.f / l : 0.f;
     bf16_t* O = static_cast<bf16_t*>(p.o) + (tok0 + q) * p.ld_o + h * HD;
 #pragma unroll
-    for (int dt = 0; dt < 2; ++dt)
+    for (int d = 0; d < A::NDT; ++d)
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
-        const int d = dt * 32 + 8 * g + 4 * hh;
+        const int col = d * 32 + 8 * g + 4 * hh;
         uint2 w;
-        w.x = pack2bf(o[dt][4 * g + 0] * inv, o[dt][4 * g + 1] * inv);
-        w.y = pack2bf(o[dt][4 * g + 2] * inv, o[dt][4 * g + 3] * inv);
-        *reinterpret_cast<uint2*>(O + d) = w;
+        w.x = pack2bf(o[d][4 * g + 0] * inv, o[d][4 * g + 1] * inv);
+        w.y = pack2bf(o[d][4 * g + 2] * inv, o[d][4 * g + 3] * inv);
+        *reinterpret_cast<uint2*>(O + col) = w;
       }
     if (hh == 0) {
       const float lse = (l > 0.f) ? (m + log2f(l)) / LOG2E : INFINITY;
@@ -318,15 +436,19 @@ __global__ __launch_bounds__(256, 3) void attn_fwd_kernel(AttnArgs p) {
 }
 
 // ------------------------------------------------------------------ backward
-// delta[n,h,s] = sum_d dO * O   (one 8-lane group per (token, head))
+// delta[n,h,s] = sum_d dO * O   (one HD/8-lane group per (token, head))
+template <int HD>
 __global__ __launch_bounds__(256) void attn_bwd_pre_kernel(AttnArgs p) {
+  constexpr int G = HD / 8;
   const long long T = (long long)p.N * p.S;
-  const long long row = ((long long)blockIdx.x * 256 + threadIdx.x) >> 3;  // (token, head)
-  const int sub = threadIdx.x & 7;
+  const long long row = ((long long)blockIdx.x * 256 + threadIdx.x) / G;  // (token, head)
+  const int sub = threadIdx.x % G;
   float acc = 0.f;
-  long long t = 0; int h = 0;
+  long long t = 0;
+  int h = 0;
   if (row < T * p.H) {
-    t = row / p.H; h = (int)(row % p.H);
+    t = row / p.H;
+    h = (int)(row % p.H);
     const bf16_t* o = static_cast<const bf16_t*>(p.o) + t * p.ld_o + h * HD + sub * 8;
     const bf16_t* d = static_cast<const bf16_t*>(p.dout) + t * p.ld_o + h * HD + sub * 8;
     float fo[8], fd[8];
@@ -335,25 +457,29 @@ __global__ __launch_bounds__(256) void attn_bwd_pre_kernel(AttnArgs p) {
 #pragma unroll
     for (int i = 0; i < 8; ++i) acc += fo[i] * fd[i];
   }
-  acc += __shfl_xor(acc, 1, 64);
-  acc += __shfl_xor(acc, 2, 64);
-  acc += __shfl_xor(acc, 4, 64);
+#pragma unroll
+  for (int o = 1; o < G; o <<= 1) acc += __shfl_xor(acc, o, 64);
   if (row < T * p.H && sub == 0) {
     const long long n = t / p.S, s = t % p.S;
     p.delta[(n * p.H + h) * p.S + s] = acc;
   }
 }
 
-// dK, dV: workgroup = 128 keys (4 waves x 32), sweep all queries >= first key.
-__global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_kernel(AttnArgs p) {
-  __shared__ __attribute__((aligned(16))) bf16_t smem[2 * 2 * KT * HD];  // [stage][Q|dO]
-  __shared__ __attribute__((aligned(16))) float srow[2][2][KT];                                    // [stage][lse2|delta]
+// dK, dV: workgroup = 128 keys (4 waves x 32, key on the lane), sweeping the 64-query tiles
+// at or after the first key.  Per 32-query sub-block j: S, dP of sub-block j+1 (2 x NST
+// MFMAs) overlap the P / dS arithmetic of j, then dV^T, dK^T += ... (4 x NDT MFMAs).
+template <int HD, bool PIPE, int OCC>
+__global__ __launch_bounds__(256, OCC) void attn_bwd_dkdv_kernel(AttnArgs p) {
+  using A = AT<HD>;
+  __shared__ __attribute__((aligned(16))) bf16_t smem[NSLOT * 2 * A::TILE];  // [slot][Q|dO]
+  __shared__ __attribute__((aligned(16))) float srow[NSLOT][2][KT];          // [slot][lse|delta]
   const int S = p.S, H = p.H;
   const int nkb = (S + QB - 1) / QB;
   int bh, kb;
   xcd_work(nkb, bh, kb);  // kb = 0 (the most queries under the causal mask) first
   const int n = bh / H, h = bh % H;
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, hh = lane >> 5;
+  const int lane = threadIdx.x & 63, hh = lane >> 5;
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int k0 = kb * QB + wid * 32;
   const int key = k0 + (lane & 31);
   const long long tok0 = (long long)n * S;
@@ -365,143 +491,153 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_kernel(AttnArgs p) {
   const float* delta = p.delta + (long long)bh * S;
   const bool key_ok = key < S && !(p.pad && p.pad[(long long)n * S + min(key, S - 1)]);
 
-  bf16x8 kf[4], vf[4];
+  bf16x8 kf[A::NST], vf[A::NST];
 #pragma unroll
-  for (int st = 0; st < 4; ++st) {
-    if (key < S) {
-      kf[st] = load_row8(Kp + (tok0 + key) * p.ld_qkv + 16 * st + 8 * hh);
-      vf[st] = load_row8(Vp + (tok0 + key) * p.ld_qkv + 16 * st + 8 * hh);
-    } else {
-      kf[st] = bf16x8{};
-      vf[st] = bf16x8{};
-    }
+  for (int st = 0; st < A::NST; ++st) {
+    kf[st] = key < S ? load_row8(Kp + (tok0 + key) * p.ld_qkv + 16 * st + 8 * hh) : bf16x8{};
+    vf[st] = key < S ? load_row8(Vp + (tok0 + key) * p.ld_qkv + 16 * st + 8 * hh) : bf16x8{};
   }
   const float c = p.scale * LOG2E;
-  floatx16 dvt[2], dkt[2];
+  floatx16 dvt[A::NDT], dkt[A::NDT];
 #pragma unroll
-  for (int i = 0; i < 16; ++i) { dvt[0][i] = dvt[1][i] = dkt[0][i] = dkt[1][i] = 0.f; }
+  for (int d = 0; d < A::NDT; ++d) {
+    zero16(dvt[d]);
+    zero16(dkt[d]);
+  }
 
   const int qt_begin = p.causal ? (kb * QB) / KT : 0;
   const int nqt = (S + KT - 1) / KT;
+  const int count = nqt - qt_begin;
 
-  // Q / dO tiles by LDS-DMA (as the forward's K / V); the per-query (lse, delta) pairs still
-  // go through two registers of the first 64 threads
-  int vq[2], vd[2];
-  dma_voff(vq, p.ld_qkv, wid, lane);
-  dma_voff(vd, p.ld_o, wid, lane);
-  float rl = 0.f, rdl = 0.f;
-  auto load_rows = [&](int qt, int stg) {
-    tile_dma(Q, p.ld_qkv, qt * KT, S, vq, smem + stg * 2 * KT * HD, wid);
-    tile_dma(dO, p.ld_o, qt * KT, S, vd, smem + stg * 2 * KT * HD + KT * HD, wid);
-    if (threadIdx.x < KT) {
-      const int qq = qt * KT + threadIdx.x;
-      rl = qq < S ? lse[qq] * LOG2E : INFINITY;
-      rdl = qq < S ? delta[qq] : 0.f;
+  // Q / dO tiles and their (lse, delta) rows by LDS-DMA (the rows: wave 0, one dword per lane)
+  int vq[A::NPW], vd[A::NPW];
+  dma_voff<HD>(vq, p.ld_qkv, wid, lane);
+  dma_voff<HD>(vd, p.ld_o, wid, lane);
+  auto issue = [&](int i) {
+    const int slot = i % NSLOT, qt = qt_begin + i;
+    const bool valid = i < count;
+    bf16_t* st = smem + slot * 2 * A::TILE;
+    tile_dma<HD>(Q, p.ld_qkv, qt * KT, S, valid, vq, st, wid);
+    tile_dma<HD>(dO, p.ld_o, qt * KT, S, valid, vd, st + A::TILE, wid);
+    if (wid == 0) {
+      dma4(rows_rsrc(lse, 4, qt * KT, S, valid), lane * 4, &srow[slot][0][0]);
+      dma4(rows_rsrc(delta, 4, qt * KT, S, valid), lane * 4, &srow[slot][1][0]);
     }
   };
-  auto store_rows = [&](int stg) {
-    if (threadIdx.x < KT) { srow[stg][0][threadIdx.x] = rl; srow[stg][1][threadIdx.x] = rdl; }
+  // S = Q K^T, dP = dO V^T of the 32-query sub-block at row r0 of the slot (key on the lane)
+  auto sdp = [&](floatx16& sa, floatx16& dp, const bf16_t* lq, int r0) {
+    zero16(sa);
+    zero16(dp);
+#pragma unroll
+    for (int st = 0; st < A::NST; ++st) {
+      sa = MFMA32(row_frag<HD>(lq, r0, st, lane), kf[st], sa);
+      dp = MFMA32(row_frag<HD>(lq + A::TILE, r0, st, lane), vf[st], dp);
+    }
   };
-  if (qt_begin < nqt) { load_rows(qt_begin, 0); store_rows(0); }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
 
-  for (int qt = qt_begin; qt < nqt; ++qt) {
-    const int cur = (qt - qt_begin) & 1;
-    const bool more = qt + 1 < nqt;
-    if (more) load_rows(qt + 1, cur ^ 1);
-    const bf16_t* lq = smem + cur * 2 * KT * HD;
-    const bf16_t* ld = lq + KT * HD;
-    const int qt0 = qt * KT;
-    const bool active = !(p.causal && qt0 + KT - 1 < k0);  // wave-uniform
-    if (active) {
+  if (count > 0) {
+    issue(0);
+    issue(1);
+    issue(2);
+    if (wid == 0) vm_wait<4 * A::NPW + 4>();  // tile 0 landed (tiles 1, 2 may fly)
+    else vm_wait<4 * A::NPW>();
+    ring_barrier();
+  }
+  // sub-block (tile i, half hf): its S / dP in (sa, dp); the next sub-block's land in (san, dpn)
+  auto half = [&](int i, int hf, floatx16& sa, floatx16& dp, floatx16& san, floatx16& dpn) {
+    const int slot = i % NSLOT;
+    const bf16_t* lq = smem + slot * 2 * A::TILE;
+    const bf16_t* ldo = lq + A::TILE;
+    // the next sub-block: second half of this tile, or first half of the next tile
+    const bf16_t* nq = hf == 0 ? lq : smem + ((i + 1) % NSLOT) * 2 * A::TILE;
+    const int nr0 = hf == 0 ? 32 : 0;
+    const int qt0 = (qt_begin + i) * KT;
+    const int qs0 = qt0 + 32 * hf;
+    const bool active = !(p.causal && qs0 + 31 < k0);  // wave-uniform: some query >= some key
+    if (!active) {
+      if constexpr (PIPE) sdp(san, dpn, nq, nr0);
+      return;
+    }
+    const bool diag = p.causal && qs0 < k0 + 31;  // wave-uniform: some key > some query
+    // ---- one basic block: next S, dP MFMAs || this sub-block's P, dS
+    if constexpr (PIPE) sdp(san, dpn, nq, nr0);
+    else sdp(sa, dp, lq, 32 * hf);
 #pragma unroll
-      for (int qs = 0; qs < 2; ++qs) {
-        floatx16 sa, dp;
+    for (int g = 0; g < 4; ++g) {
+      const int qi0 = 32 * hf + 8 * g + 4 * hh;  // rows 8g+4h..+3: consecutive queries
+      const float4 l4 = *reinterpret_cast<const float4*>(&srow[slot][0][qi0]);
+      const float4 d4 = *reinterpret_cast<const float4*>(&srow[slot][1][qi0]);
+      const float lv[4] = {l4.x * LOG2E, l4.y * LOG2E, l4.z * LOG2E, l4.w * LOG2E};
+      const float dl[4] = {d4.x, d4.y, d4.z, d4.w};
 #pragma unroll
-        for (int i = 0; i < 16; ++i) { sa[i] = 0.f; dp[i] = 0.f; }
-#pragma unroll
-        for (int st = 0; st < 4; ++st) {
-          sa = MFMA32(row_frag(lq, qs * 32, st, lane), kf[st], sa);
-          dp = MFMA32(row_frag(ld, qs * 32, st, lane), vf[st], dp);
-        }
-        // sa[r]: query qt0 + qs*32 + acc_row(r), key = lane's key.  Rows 8g+4h..+3 are
-        // consecutive queries, so their (lse, delta) come in as one 16-B LDS read each.
-        const bool diag = p.causal && qt0 + qs * 32 < k0 + 32;  // wave-uniform: mask needed
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-          const int qi0 = qs * 32 + 8 * g + 4 * hh;
-          const float4 l4 = *reinterpret_cast<const float4*>(&srow[cur][0][qi0]);
-          const float4 d4 = *reinterpret_cast<const float4*>(&srow[cur][1][qi0]);
-          const float lv[4] = {l4.x, l4.y, l4.z, l4.w}, dv[4] = {d4.x, d4.y, d4.z, d4.w};
-          // a padded key's P only reaches this lane's own dK / dV column: zeroed at the store
-          if (diag) {
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-              const int r = 4 * g + e;
-              float pv = fast_exp2(fmaf(sa[r], c, -lv[e]));
-              pv = (key > qt0 + qi0 + e) ? 0.f : pv;
-              sa[r] = pv;
-              dp[r] = pv * (dp[r] - dv[e]);
-            }
-          } else {
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-              const int r = 4 * g + e;
-              const float pv = fast_exp2(fmaf(sa[r], c, -lv[e]));
-              sa[r] = pv;
-              dp[r] = pv * (dp[r] - dv[e]);
-            }
-          }
-        }
-#pragma unroll
-        for (int ss = 0; ss < 2; ++ss) {
-          const bf16x8 pb = acc_frag(sa, ss);
-          const bf16x8 db = acc_frag(dp, ss);
-#pragma unroll
-          for (int dt = 0; dt < 2; ++dt) {
-            dvt[dt] = MFMA32(tr_frag(ld, qs * 32, ss, dt * 32, lane), pb, dvt[dt]);
-            dkt[dt] = MFMA32(tr_frag(lq, qs * 32, ss, dt * 32, lane), db, dkt[dt]);
-          }
-        }
+      for (int e = 0; e < 4; ++e) {
+        const int r = 4 * g + e;
+        float pv = fast_exp2(fmaf(sa[r], c, -lv[e]));
+        // a padded key's P only reaches this lane's own dK / dV column: zeroed at the store
+        if (diag) pv = (key > qt0 + qi0 + e) ? 0.f : pv;
+        sa[r] = pv;
+        dp[r] = pv * (dp[r] - dl[e]);
       }
     }
-    if (more) store_rows(cur ^ 1);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's DMA of tile qt+1 landed
-    __syncthreads();
+#pragma unroll
+    for (int ss = 0; ss < 2; ++ss) {
+      const bf16x8 pb = acc_frag(sa, ss);
+      const bf16x8 db = acc_frag(dp, ss);
+#pragma unroll
+      for (int d = 0; d < A::NDT; ++d) {
+        dvt[d] = MFMA32(tr_frag<HD>(ldo, 32 * hf, ss, d * 32, lane), pb, dvt[d]);
+        dkt[d] = MFMA32(tr_frag<HD>(lq, 32 * hf, ss, d * 32, lane), db, dkt[d]);
+      }
+    }
+  };
+  floatx16 sa0, dp0, sa1, dp1;
+  if constexpr (PIPE) sdp(sa0, dp0, smem, 0);
+  for (int i = 0; i < count; ++i) {
+    if (wid == 0) vm_wait<2 * A::NPW + 2>();  // tile i+1 landed (i+2 may fly)
+    else vm_wait<2 * A::NPW>();
+    ring_barrier();
+    issue(i + 3);
+    half(i, 0, sa0, dp0, sa1, dp1);
+    half(i, 1, sa1, dp1, sa0, dp0);
   }
+  vm_wait<0>();
 
   if (key < S) {
     bf16_t* dK = static_cast<bf16_t*>(p.dk) + (tok0 + key) * p.ld_dqkv + h * HD;
     bf16_t* dV = static_cast<bf16_t*>(p.dv) + (tok0 + key) * p.ld_dqkv + h * HD;
 #pragma unroll
-    for (int dt = 0; dt < 2; ++dt)
+    for (int d = 0; d < A::NDT; ++d)
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
-        const int d = dt * 32 + 8 * g + 4 * hh;
+        const int col = d * 32 + 8 * g + 4 * hh;
         uint2 w = make_uint2(0u, 0u), u = make_uint2(0u, 0u);  // padded key: dK = dV = 0
         if (key_ok) {
-          w.x = pack2bf(dkt[dt][4 * g + 0] * p.scale, dkt[dt][4 * g + 1] * p.scale);
-          w.y = pack2bf(dkt[dt][4 * g + 2] * p.scale, dkt[dt][4 * g + 3] * p.scale);
-          u.x = pack2bf(dvt[dt][4 * g + 0], dvt[dt][4 * g + 1]);
-          u.y = pack2bf(dvt[dt][4 * g + 2], dvt[dt][4 * g + 3]);
+          w.x = pack2bf(dkt[d][4 * g + 0] * p.scale, dkt[d][4 * g + 1] * p.scale);
+          w.y = pack2bf(dkt[d][4 * g + 2] * p.scale, dkt[d][4 * g + 3] * p.scale);
+          u.x = pack2bf(dvt[d][4 * g + 0], dvt[d][4 * g + 1]);
+          u.y = pack2bf(dvt[d][4 * g + 2], dvt[d][4 * g + 3]);
         }
-        *reinterpret_cast<uint2*>(dK + d) = w;
-        *reinterpret_cast<uint2*>(dV + d) = u;
+        *reinterpret_cast<uint2*>(dK + col) = w;
+        *reinterpret_cast<uint2*>(dV + col) = u;
       }
   }
 }
 
-// dQ: workgroup = 128 queries (4 waves x 32), sweep keys <= last query.
-__global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(AttnArgs p) {
-  __shared__ __attribute__((aligned(16))) bf16_t smem[2 * 2 * KT * HD];  // [stage][K|V]
+// dQ: workgroup = 128 queries (4 waves x 32, query on the lane), sweeping the key tiles up to
+// the last query.  Per 32-key sub-block j: S^T, dP^T of j+1 overlap dS^T of j, then
+// dQ^T += K^T dS^T (2 x NDT MFMAs).
+template <int HD, bool PIPE, int OCC>
+__global__ __launch_bounds__(256, OCC) void attn_bwd_dq_kernel(AttnArgs p) {
+  using A = AT<HD>;
+  __shared__ __attribute__((aligned(16))) bf16_t smem[NSLOT * 2 * A::TILE];  // [slot][K|V]
   const int S = p.S, H = p.H;
   const int nqb = (S + QB - 1) / QB;
   int bh, bi;
   xcd_work(nqb, bh, bi);
   const int qb = nqb - 1 - bi;
   const int n = bh / H, h = bh % H;
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, hh = lane >> 5;
+  const int lane = threadIdx.x & 63, hh = lane >> 5;
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int q0 = qb * QB + wid * 32;
   const int q = q0 + (lane & 31);
   const long long tok0 = (long long)n * S;
@@ -511,118 +647,172 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(AttnArgs p) {
   const bf16_t* dO = static_cast<const bf16_t*>(p.dout) + h * HD;
   const unsigned char* pad = p.pad ? p.pad + (long long)n * S : nullptr;
 
-  bf16x8 qf[4], df[4];
+  bf16x8 qf[A::NST], df[A::NST];
 #pragma unroll
-  for (int st = 0; st < 4; ++st) {
-    if (q < S) {
-      qf[st] = load_row8(Q + (tok0 + q) * p.ld_qkv + 16 * st + 8 * hh);
-      df[st] = load_row8(dO + (tok0 + q) * p.ld_o + 16 * st + 8 * hh);
-    } else {
-      qf[st] = bf16x8{};
-      df[st] = bf16x8{};
-    }
+  for (int st = 0; st < A::NST; ++st) {
+    qf[st] = q < S ? load_row8(Q + (tok0 + q) * p.ld_qkv + 16 * st + 8 * hh) : bf16x8{};
+    df[st] = q < S ? load_row8(dO + (tok0 + q) * p.ld_o + 16 * st + 8 * hh) : bf16x8{};
   }
   const float c = p.scale * LOG2E;
   const float lse2 = q < S ? p.lse[(long long)bh * S + q] * LOG2E : INFINITY;
   const float dl = q < S ? p.delta[(long long)bh * S + q] : 0.f;
-  floatx16 dqt[2];
+  floatx16 dqt[A::NDT];
 #pragma unroll
-  for (int i = 0; i < 16; ++i) { dqt[0][i] = 0.f; dqt[1][i] = 0.f; }
+  for (int d = 0; d < A::NDT; ++d) zero16(dqt[d]);
 
   const int kend = p.causal ? min(S, qb * QB + QB) : S;
   const int ntiles = (kend + KT - 1) / KT;
-  // K/V tiles stream into the LDS double buffer by DMA: tile t+1 is issued at the top of
-  // iteration t into the stage iteration t-1 read (released by its closing barrier), and
-  // lands under this iteration's MFMAs; no staging registers (16 VGPRs) as the
-  // register-staged copy needed.
-  int dv[2];
-  dma_voff(dv, p.ld_qkv, wid, lane);
-  tile_dma(K, p.ld_qkv, 0, S, dv, smem, wid);
-  tile_dma(V, p.ld_qkv, 0, S, dv, smem + KT * HD, wid);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
 
-  for (int t = 0; t < ntiles; ++t) {
-    const int cur = t & 1;
-    const bool more = t + 1 < ntiles;
-    if (more) {
-      bf16_t* nx = smem + (cur ^ 1) * 2 * KT * HD;
-      tile_dma(K, p.ld_qkv, (t + 1) * KT, S, dv, nx, wid);
-      tile_dma(V, p.ld_qkv, (t + 1) * KT, S, dv, nx + KT * HD, wid);
+  int dv[A::NPW];
+  dma_voff<HD>(dv, p.ld_qkv, wid, lane);
+  auto issue = [&](int t) {
+    bf16_t* st = smem + (t % NSLOT) * 2 * A::TILE;
+    const bool valid = t < ntiles;
+    tile_dma<HD>(K, p.ld_qkv, t * KT, S, valid, dv, st, wid);
+    tile_dma<HD>(V, p.ld_qkv, t * KT, S, valid, dv, st + A::TILE, wid);
+  };
+  // S^T = K Q^T, dP^T = V dO^T of the 32-key sub-block at row r0 of the slot
+  auto sdp = [&](floatx16& sa, floatx16& dp, const bf16_t* lk, int r0) {
+    zero16(sa);
+    zero16(dp);
+#pragma unroll
+    for (int st = 0; st < A::NST; ++st) {
+      sa = MFMA32(row_frag<HD>(lk, r0, st, lane), qf[st], sa);
+      dp = MFMA32(row_frag<HD>(lk + A::TILE, r0, st, lane), df[st], dp);
     }
-    const bf16_t* lk = smem + cur * 2 * KT * HD;
-    const bf16_t* lv = lk + KT * HD;
+  };
+
+  issue(0);
+  issue(1);
+  issue(2);
+  vm_wait<4 * A::NPW>();  // tile 0 landed (tiles 1, 2 may fly)
+  ring_barrier();
+  auto half = [&](int t, int hf, floatx16& sa, floatx16& dp, floatx16& san, floatx16& dpn) {
+    const bf16_t* lk = smem + (t % NSLOT) * 2 * A::TILE;
+    const bf16_t* nk = hf == 0 ? lk : smem + ((t + 1) % NSLOT) * 2 * A::TILE;
+    const int nr0 = hf == 0 ? 32 : 0;
     const int kt0 = t * KT;
-    const bool active = !(p.causal && kt0 > q0 + 31);
-    if (active) {
-      const bool need_mask = (p.causal && kt0 + KT - 1 > q0) || (kt0 + KT > S) || pad;  // uniform
-      const unsigned long long pm = need_mask ? pad_bits(pad, kt0, S, lane) : 0ull;
-      const int lim = need_mask ? (p.causal ? min(q, S - 1) : S - 1) - kt0 : KT;
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks) {
-        floatx16 sa, dp;
-#pragma unroll
-        for (int i = 0; i < 16; ++i) { sa[i] = 0.f; dp[i] = 0.f; }
-#pragma unroll
-        for (int st = 0; st < 4; ++st) {
-          sa = MFMA32(row_frag(lk, ks * 32, st, lane), qf[st], sa);
-          dp = MFMA32(row_frag(lv, ks * 32, st, lane), df[st], dp);
-        }
-        if (need_mask) {
-#pragma unroll
-          for (int r = 0; r < 16; ++r) {
-            const int kl = ks * 32 + acc_row(r, lane);
-            float pv = fast_exp2(fmaf(sa[r], c, -lse2));
-            pv = (kl > lim || ((pm >> kl) & 1ull)) ? 0.f : pv;
-            dp[r] = pv * (dp[r] - dl);
-          }
-        } else {
-#pragma unroll
-          for (int r = 0; r < 16; ++r) dp[r] = fast_exp2(fmaf(sa[r], c, -lse2)) * (dp[r] - dl);
-        }
-#pragma unroll
-        for (int ss = 0; ss < 2; ++ss) {
-          const bf16x8 db = acc_frag(dp, ss);
-#pragma unroll
-          for (int dt = 0; dt < 2; ++dt) dqt[dt] = MFMA32(tr_frag(lk, ks * 32, ss, dt * 32, lane), db, dqt[dt]);
-        }
-      }
+    const int ks0 = kt0 + 32 * hf;
+    const bool active = !(p.causal && ks0 > q0 + 31);  // wave-uniform: some key <= some query
+    if (!active) {
+      if constexpr (PIPE) sdp(san, dpn, nk, nr0);
+      return;
     }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's DMA of tile t+1 landed
-    __syncthreads();  // ... every wave's, and stage cur is free for tile t+2
+    const bool need_mask = (p.causal && ks0 + 31 > q0) || (ks0 + 32 > S) || pad;  // wave-uniform
+    // ---- one basic block: next S^T, dP^T MFMAs || this sub-block's dS^T
+    if constexpr (PIPE) sdp(san, dpn, nk, nr0);
+    else sdp(sa, dp, lk, 32 * hf);
+    if (need_mask) {
+      const unsigned long long pm = pad_bits(pad, kt0, S, lane);
+      const int lim = (p.causal ? min(q, S - 1) : S - 1) - kt0;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int kl = 32 * hf + acc_row(r, lane);
+        float pv = fast_exp2(fmaf(sa[r], c, -lse2));
+        pv = (kl > lim || ((pm >> kl) & 1ull)) ? 0.f : pv;
+        dp[r] = pv * (dp[r] - dl);
+      }
+    } else {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) dp[r] = fast_exp2(fmaf(sa[r], c, -lse2)) * (dp[r] - dl);
+    }
+#pragma unroll
+    for (int ss = 0; ss < 2; ++ss) {
+      const bf16x8 db = acc_frag(dp, ss);
+#pragma unroll
+      for (int d = 0; d < A::NDT; ++d)
+        dqt[d] = MFMA32(tr_frag<HD>(lk, 32 * hf, ss, d * 32, lane), db, dqt[d]);
+    }
+  };
+  floatx16 sa0, dp0, sa1, dp1;
+  if constexpr (PIPE) sdp(sa0, dp0, smem, 0);
+  for (int t = 0; t < ntiles; ++t) {
+    vm_wait<2 * A::NPW>();  // this wave's pieces of tile t+1 landed (t+2 may fly)
+    ring_barrier();         // ... every wave's; and every wave is done with tile t-1's slot
+    issue(t + 3);
+    half(t, 0, sa0, dp0, sa1, dp1);
+    half(t, 1, sa1, dp1, sa0, dp0);
   }
+  vm_wait<0>();
 
   if (q < S) {
     bf16_t* dQ = static_cast<bf16_t*>(p.dq) + (tok0 + q) * p.ld_dqkv + h * HD;
 #pragma unroll
-    for (int dt = 0; dt < 2; ++dt)
+    for (int d = 0; d < A::NDT; ++d)
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
-        const int d = dt * 32 + 8 * g + 4 * hh;
+        const int col = d * 32 + 8 * g + 4 * hh;
         uint2 w;
-        w.x = pack2bf(dqt[dt][4 * g + 0] * p.scale, dqt[dt][4 * g + 1] * p.scale);
-        w.y = pack2bf(dqt[dt][4 * g + 2] * p.scale, dqt[dt][4 * g + 3] * p.scale);
-        *reinterpret_cast<uint2*>(dQ + d) = w;
+        w.x = pack2bf(dqt[d][4 * g + 0] * p.scale, dqt[d][4 * g + 1] * p.scale);
+        w.y = pack2bf(dqt[d][4 * g + 2] * p.scale, dqt[d][4 * g + 3] * p.scale);
+        *reinterpret_cast<uint2*>(dQ + col) = w;
       }
   }
+}
+
+// kernel variant (env DPC_ATTN_VAR="<fwd>,<bwd>", measured on MI355X: bench/attn_one.py):
+// 0 = software-pipelined, 2 workgroups / CU; 1 = plain order, 2 / CU; 2 = plain, 3 / CU;
+// 3 = pipelined, 3 / CU; 4 (forward only) = pipelined + fragments up front + pinned interleave
+// Defaults per head size (GPT-2 small shape, B=64 S=1023 H=12, profiles/r2_attn/):
+//   hd 64: forward 0, backward 1;  hd 32: forward 2, backward 2.
+static int g_attn_env[2] = {-2, -2};
+static int attn_var(int hd, int bwd) {
+  if (g_attn_env[0] == -2) {
+    g_attn_env[0] = g_attn_env[1] = -1;
+    if (const char* e = getenv("DPC_ATTN_VAR")) sscanf(e, "%d,%d", &g_attn_env[0], &g_attn_env[1]);
+  }
+  if (g_attn_env[bwd] >= 0) return g_attn_env[bwd];
+  if (hd == 32) return 2;
+  return bwd ? 1 : 0;
+}
+
+#define DPC_ATTN_SWITCH(var, KERNEL, ...)                                                   \
+  switch (var) {                                                                           \
+    case 0: hipLaunchKernelGGL((KERNEL<HD, true, 2>), __VA_ARGS__); break;                  \
+    case 1: hipLaunchKernelGGL((KERNEL<HD, false, 2>), __VA_ARGS__); break;                 \
+    case 3: hipLaunchKernelGGL((KERNEL<HD, true, 3>), __VA_ARGS__); break;                  \
+    default: hipLaunchKernelGGL((KERNEL<HD, false, 3>), __VA_ARGS__); break;                \
+  }
+
+template <int HD>
+static int launch_fwd(const AttnArgs* a, hipStream_t stream) {
+  const int var = attn_var(HD, 0);
+  dim3 grid((unsigned)(((a->S + QB - 1) / QB) * a->N * a->H));  // 1-D: xcd_work() maps it
+  if (var == 4) hipLaunchKernelGGL((attn_fwd_kernel<HD, 2, 2>), grid, dim3(256), 0, stream, *a);
+  else DPC_ATTN_SWITCH(var, attn_fwd_kernel, grid, dim3(256), 0, stream, *a);
+  return (int)hipGetLastError();
+}
+
+template <int HD>
+static int launch_bwd(const AttnArgs* a, hipStream_t stream) {
+  const int var = attn_var(HD, 1);
+  const long long rows = (long long)a->N * a->S * a->H;
+  dim3 gpre((unsigned)((rows * (HD / 8) + 255) / 256));
+  hipLaunchKernelGGL(attn_bwd_pre_kernel<HD>, gpre, dim3(256), 0, stream, *a);
+  dim3 grid((unsigned)(((a->S + QB - 1) / QB) * a->N * a->H));
+  DPC_ATTN_SWITCH(var, attn_bwd_dkdv_kernel, grid, dim3(256), 0, stream, *a);
+  DPC_ATTN_SWITCH(var, attn_bwd_dq_kernel, grid, dim3(256), 0, stream, *a);
+  return (int)hipGetLastError();
 }
 
 }  // namespace dpc
 
 using namespace dpc;
 
+// Host-side checks: the kernels assume 16-B aligned rows (ld % 8 == 0) and head_dim 32 / 64.
+static bool attn_args_ok(const AttnArgs* a, bool bwd) {
+  if (a->hd != 32 && a->hd != 64) return false;
+  if (a->N <= 0 || a->S <= 0 || a->H <= 0) return false;
+  if (a->ld_qkv % 8 || a->ld_o % 8 || (bwd && a->ld_dqkv % 8)) return false;
+  return true;
+}
+
 DPC_API int dpc_attn_fwd(const AttnArgs* a, hipStream_t stream) {
-  dim3 grid((unsigned)(((a->S + QB - 1) / QB) * a->N * a->H));  // 1-D: xcd_work() maps it
-  hipLaunchKernelGGL(attn_fwd_kernel, grid, dim3(256), 0, stream, *a);
-  return (int)hipGetLastError();
+  if (!attn_args_ok(a, false)) return (int)hipErrorInvalidValue;
+  return a->hd == 32 ? launch_fwd<32>(a, stream) : launch_fwd<64>(a, stream);
 }
 
 DPC_API int dpc_attn_bwd(const AttnArgs* a, hipStream_t stream) {
-  const long long rows = (long long)a->N * a->S * a->H;
-  dim3 gpre((unsigned)((rows * 8 + 255) / 256));
-  hipLaunchKernelGGL(attn_bwd_pre_kernel, gpre, dim3(256), 0, stream, *a);
-  dim3 grid((unsigned)(((a->S + QB - 1) / QB) * a->N * a->H));
-  hipLaunchKernelGGL(attn_bwd_dkdv_kernel, grid, dim3(256), 0, stream, *a);
-  hipLaunchKernelGGL(attn_bwd_dq_kernel, grid, dim3(256), 0, stream, *a);
-  return (int)hipGetLastError();
+  if (!attn_args_ok(a, true)) return (int)hipErrorInvalidValue;
+  return a->hd == 32 ? launch_bwd<32>(a, stream) : launch_bwd<64>(a, stream);
 }

@@ -218,11 +218,19 @@ def test_gemm_epilogues(act):
     assert rel_err(acc, ref2) < 2e-3
 
 
+@pytest.mark.parametrize("hd", [64, 32])
 @pytest.mark.parametrize("S", [1023, 200, 64])
 @pytest.mark.parametrize("with_pad", [False, True])
-def test_attention_fwd_bwd(S, with_pad):
+def test_attention_fwd_bwd(S, with_pad, hd, monkeypatch):
+    """Native head sizes 32 / 64 (no pad path) against the f32 O(S^2) reference."""
+    import distributed_pytorch_cookbook_amd.ops.attention as attn_mod
+
+    def _no_pad(*a, **k):
+        raise AssertionError("native head_dim must not take the zero-pad path")
+
+    monkeypatch.setattr(attn_mod, "_pad_heads", _no_pad)
     torch.manual_seed(2)
-    N, H, hd = 2, 3, 64
+    N, H = 2, 3
     T = N * S
     qkv = (torch.randn(T, 3 * H * hd, device=dev)).bfloat16()
     pad = None
@@ -245,11 +253,12 @@ def test_attention_fwd_bwd(S, with_pad):
         assert rel_err(dqkv[:, sl], g[:, sl]) < 2e-2, name
 
 
+@pytest.mark.parametrize("hd", [64, 32])
 @pytest.mark.parametrize("S", [4096, 8191])
-def test_attention_long_context(S):
+def test_attention_long_context(S, hd):
     """O(S) flash attention at 4-8x GPT-2's context, vs the f32 O(S^2) reference."""
     torch.manual_seed(5)
-    N, H, hd = 1, 2, 64
+    N, H = 1, 2
     qkv = torch.randn(N * S, 3 * H * hd, device=dev).bfloat16()
     o, lse = attention_fwd(qkv, N, S, H, hd, None, causal=True)
     o_r, lse_r = attention_ref(qkv, N, S, H, hd, None, causal=True)
@@ -264,17 +273,21 @@ def test_attention_long_context(S):
         assert rel_err(dqkv[:, sl], g[:, sl]) < 2e-2, name
 
 
-def test_attention_head_dim_32_padded():
+@pytest.mark.parametrize("causal", [True, False])
+@pytest.mark.parametrize("hd", [16, 48, 32])
+def test_attention_head_dim_other(hd, causal):
+    """Head sizes without a kernel of their own run zero-padded to the next one (16 -> 32,
+    48 -> 64); also the non-causal form."""
     torch.manual_seed(3)
-    N, S, H, hd = 2, 100, 4, 32
+    N, S, H = 2, 100, 4
     qkv = torch.randn(N * S, 3 * H * hd, device=dev).bfloat16()
-    o, lse = attention_fwd(qkv, N, S, H, hd)
-    o_r, _ = attention_ref(qkv, N, S, H, hd)
+    o, lse = attention_fwd(qkv, N, S, H, hd, causal=causal)
+    o_r, _ = attention_ref(qkv, N, S, H, hd, causal=causal)
     assert rel_err(o, o_r) < 1e-2
     do = torch.randn_like(o)
-    d = attention_bwd(do, qkv, o, lse, N, S, H, hd)
+    d = attention_bwd(do, qkv, o, lse, N, S, H, hd, causal=causal)
     x = qkv.float().requires_grad_(True)
-    (g,) = torch.autograd.grad(attention_ref(x, N, S, H, hd)[0], x, do.float())
+    (g,) = torch.autograd.grad(attention_ref(x, N, S, H, hd, causal=causal)[0], x, do.float())
     assert rel_err(d, g) < 2e-2
 
 
