@@ -34,6 +34,7 @@ class GemmArgs(ctypes.Structure):
         ("a_r", c_int), ("a_c", c_int), ("b_r", c_int), ("b_c", c_int),
         ("ksplit", c_int),  # dispatcher-owned (pass 0)
         ("impl", c_int),    # 0 = dispatcher policy, else a measured per-shape choice
+        ("aux_f32", c_int),  # dpc_gemm_f32: f32 aux_in / aux_out (else bf16)
     ]
 
 
@@ -140,8 +141,11 @@ class DecodeAttnArgs(ctypes.Structure):
 _FUNCS = {
     "dpc_decode_attn": DecodeAttnArgs,
     "dpc_gemm": GemmArgs,
+    "dpc_gemm_f32": GemmArgs,
     "dpc_attn_fwd": AttnArgs,
     "dpc_attn_bwd": AttnArgs,
+    "dpc_attn_fwd_f32": AttnArgs,
+    "dpc_attn_bwd_f32": AttnArgs,
     "dpc_layernorm_fwd": LNArgs,
     "dpc_layernorm_bwd": LNArgs,
     "dpc_embedding_fwd": EmbArgs,

@@ -8,6 +8,8 @@ yields an ill-defined average); such rows only occur for all-padding sequences.
 
 HIP path (bf16, head_dim 32 or 64 natively): ``dpc_attn_fwd`` / ``dpc_attn_bwd`` flash
 kernels (``csrc/attention.hip``) -- O(S) memory, f32 log-sum-exp saved for the backward.
+f32 operands (``--disable_amp``) run ``dpc_attn_fwd_f32`` / ``dpc_attn_bwd_f32``
+(``csrc/attention_f32.hip``, f32 matrix cores), also O(S).
 head_dim 32 is the reference default config (``/root/reference/main-single.py:160``); other
 head sizes below 64 are zero-padded to the next kernel size on the way in.
 CPU / fp32 path: the same math with torch ops (test oracle).
@@ -33,7 +35,12 @@ def kernel_head_dim(head_dim: int) -> int:
 
 
 def _use_hip(t: torch.Tensor) -> bool:
-    return t.is_cuda and t.dtype == torch.bfloat16
+    """bf16 -> csrc/attention.hip; f32 (--disable_amp) -> csrc/attention_f32.hip."""
+    return t.is_cuda and t.dtype in (torch.bfloat16, torch.float32)
+
+
+def _suffix(t: torch.Tensor) -> str:
+    return "_f32" if t.dtype == torch.float32 else ""
 
 
 def split_qkv(qkv: torch.Tensor, heads: int, head_dim: int):
@@ -99,20 +106,21 @@ def attention_fwd(qkv: torch.Tensor, N: int, S: int, heads: int, head_dim: int,
     return _attn_fwd_hip(qkv, N, S, heads, kd, pad_mask, causal, scale, out)
 
 
-def _check(t, T, cols, name):
-    if t.shape[0] != T or t.stride(1) != 1 or t.dtype != torch.bfloat16:
+def _check(t, T, cols, name, dtype=torch.bfloat16):
+    if t.shape[0] != T or t.stride(1) != 1 or t.dtype != dtype:
         raise ValueError(f"attention: bad {name} {tuple(t.shape)} {t.stride()} {t.dtype}")
-    if t.data_ptr() % 16 or t.stride(0) % 8 or t.shape[1] < cols:
-        raise ValueError(f"attention: {name} must be 16-B aligned with row stride % 8 == 0")
+    if t.data_ptr() % 16 or t.stride(0) % (16 // t.element_size()) or t.shape[1] < cols:
+        raise ValueError(f"attention: {name} must be 16-B aligned with 16-B aligned rows")
 
 
 def _attn_fwd_hip(qkv, N, S, heads, kd, pad_mask, causal, scale, out):
     T = N * S
     hd = heads * kd
-    _check(qkv, T, 3 * hd, "qkv")
+    dt = qkv.dtype
+    _check(qkv, T, 3 * hd, "qkv", dt)
     if out is None:
-        out = torch.empty(T, hd, device=qkv.device, dtype=torch.bfloat16)
-    _check(out, T, hd, "out")
+        out = torch.empty(T, hd, device=qkv.device, dtype=dt)
+    _check(out, T, hd, "out", dt)
     lse = torch.empty(N * heads, S, device=qkv.device, dtype=torch.float32)
     pad = None
     if pad_mask is not None:
@@ -124,7 +132,7 @@ def _attn_fwd_hip(qkv, N, S, heads, kd, pad_mask, causal, scale, out):
         pad=_lib.ptr(pad), ld_qkv=qkv.stride(0), ld_o=out.stride(0), ld_dqkv=0,
         N=N, S=S, H=heads, scale=float(scale), causal=int(causal), hd=kd,
     )
-    _lib.call("dpc_attn_fwd", args, qkv.device)
+    _lib.call("dpc_attn_fwd" + _suffix(qkv), args, qkv.device)
     return out, lse
 
 
@@ -162,17 +170,19 @@ def attention_bwd(dout: torch.Tensor, qkv: torch.Tensor, o: torch.Tensor, lse: t
 def _attn_bwd_hip(dout, qkv, o, lse, N, S, heads, kd, pad_mask, causal, scale, dqkv):
     T = N * S
     hd = heads * kd
-    _check(qkv, T, 3 * hd, "qkv")
-    _check(o, T, hd, "o")
-    _check(dout, T, hd, "dout")
+    dt = qkv.dtype
+    dout = dout.to(dt)
+    _check(qkv, T, 3 * hd, "qkv", dt)
+    _check(o, T, hd, "o", dt)
+    _check(dout, T, hd, "dout", dt)
     if o.stride(0) != dout.stride(0):
         dout = dout.contiguous()
         o = o.contiguous()
         if o.stride(0) != dout.stride(0):
             raise ValueError("attention_bwd: o and dout need equal row strides")
     if dqkv is None:
-        dqkv = torch.empty(T, 3 * hd, device=qkv.device, dtype=torch.bfloat16)
-    _check(dqkv, T, 3 * hd, "dqkv")
+        dqkv = torch.empty(T, 3 * hd, device=qkv.device, dtype=dt)
+    _check(dqkv, T, 3 * hd, "dqkv", dt)
     delta = torch.empty(N * heads, S, device=qkv.device, dtype=torch.float32)
     pad = None
     if pad_mask is not None:
@@ -186,7 +196,7 @@ def _attn_bwd_hip(dout, qkv, o, lse, N, S, heads, kd, pad_mask, causal, scale, d
         ld_qkv=qkv.stride(0), ld_o=o.stride(0), ld_dqkv=dqkv.stride(0),
         N=N, S=S, H=heads, scale=float(scale), causal=int(causal), hd=kd,
     )
-    _lib.call("dpc_attn_bwd", args, qkv.device)
+    _lib.call("dpc_attn_bwd" + _suffix(qkv), args, qkv.device)
     return dqkv
 
 
@@ -208,7 +218,7 @@ def decode_attention(qkv, kc, vc, length, heads, head_dim, scale=None):
     scale = 1.0 / math.sqrt(head_dim) if scale is None else scale
     N, E = qkv.shape[0], heads * head_dim
     Smax = kc.shape[1]
-    if not _use_hip(qkv):
+    if not (qkv.is_cuda and qkv.dtype == torch.bfloat16):
         pos = int(length)
         q, k, v = split_qkv(qkv, heads, head_dim)
         kc[:, pos] = k

@@ -28,7 +28,7 @@ BUILD_DIR = HERE / "_build"
 LIB_PATH = HERE / "libdpc_kernels.so"
 ARCH = os.environ.get("DPC_OFFLOAD_ARCH", "gfx950")
 
-SOURCES = ["gemm.hip", "gemm7.hip", "attention.hip", "layernorm.hip", "misc.hip", "decode.hip"]
+SOURCES = ["gemm.hip", "gemm7.hip", "gemm_f32.hip", "attention.hip", "attention_f32.hip", "layernorm.hip", "misc.hip", "decode.hip"]
 HEADERS = ["common.h", "gemm.h"]
 
 # code-object v5 keeps the library loadable by torch's bundled ROCm 7.0 runtime as
@@ -53,7 +53,7 @@ def hipcc() -> str:
 
 # per-file extras: attention never produces NaNs (masked scores are -inf), so maxnum needs
 # no canonicalisation of MFMA results and folds into v_max3_f32
-FILE_FLAGS = {"attention.hip": ["-fno-honor-nans"]}
+FILE_FLAGS = {"attention.hip": ["-fno-honor-nans"], "attention_f32.hip": ["-fno-honor-nans"]}
 
 
 def _newest(paths) -> float:

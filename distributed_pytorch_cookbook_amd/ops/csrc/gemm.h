@@ -33,6 +33,8 @@ struct GemmArgs {
   // measured per-shape table of ops/gemm.py (autotuned on MI355X); a forced global impl
   // (dpc_gemm_set_impl, sweeps / tests) takes precedence
   int impl;
+  // gemm_f32.hip only: aux_in / aux_out are f32 (else bf16)
+  int aux_f32;
 };
 
 constexpr int BM = 128, BN = 128, BKT = 64, NT = 256;

@@ -304,8 +304,42 @@ def gemm(
             args.impl = impl or 0
         _lib.call("dpc_gemm", args, a.device)
         return out
+    if a.is_cuda and a.dtype == torch.float32 and b.dtype == torch.float32 and out.dtype == torch.float32:
+        return _gemm_f32(a, b, a_kmaj, b_kmaj, out, M, N, K, bias, act, act_bwd, aux_in, aux_out,
+                         residual, alpha, alpha_t, accumulate, colsum)
     return _gemm_ref(a, b, a_kmaj, b_kmaj, out, bias, act, act_bwd, aux_in, aux_out, residual,
                      alpha, alpha_t, accumulate, colsum)
+
+
+def _gemm_f32(a, b, a_kmaj, b_kmaj, out, M, N, K, bias, act, act_bwd, aux_in, aux_out, residual,
+              alpha, alpha_t, accumulate, colsum):
+    """f32 operands (the --disable_amp path): ``dpc_gemm_f32`` on the f32 matrix cores
+    (csrc/gemm_f32.hip), same fused epilogue as the bf16 kernels."""
+    for t, nm in ((a, "A"), (b, "B"), (out, "out")):
+        if t.stride(-1) != 1:
+            raise ValueError(f"gemm f32: {nm} inner dimension must be contiguous")
+    aux = [t for t in (aux_in, aux_out) if t is not None]
+    aux_f32 = bool(aux) and aux[0].dtype == torch.float32
+    for t, nm in ((residual, "residual"), (bias, "bias"), (colsum, "colsum")):
+        if t is not None and (t.dtype != torch.float32 or t.stride(-1) != 1):
+            raise ValueError(f"gemm f32: {nm} must be contiguous-last f32")
+    for t in aux:
+        if t.dtype != (torch.float32 if aux_f32 else torch.bfloat16) or t.stride(-1) != 1:
+            raise ValueError("gemm f32: aux_in / aux_out must share one dtype (f32 or bf16)")
+    args = _lib.GemmArgs(
+        A=a.data_ptr(), B=b.data_ptr(), C=out.data_ptr(),
+        bias=_lib.ptr(bias), residual=_lib.ptr(residual), aux_in=_lib.ptr(aux_in),
+        aux_out=_lib.ptr(aux_out), alpha_ptr=_lib.ptr(alpha_t), colsum=_lib.ptr(colsum),
+        lda=a.stride(0), ldb=b.stride(0), ldc=out.stride(0),
+        ldr=residual.stride(0) if residual is not None else 0,
+        ld_aux_in=aux_in.stride(0) if aux_in is not None else 0,
+        ld_aux_out=aux_out.stride(0) if aux_out is not None else 0,
+        M=M, N=N, K=K, alpha=float(alpha), act=act, act_bwd=act_bwd, out_f32=1,
+        accumulate=int(accumulate), a_kmaj=int(a_kmaj), b_kmaj=int(b_kmaj),
+        a_r=a.shape[0], a_c=a.shape[1], b_r=b.shape[0], b_c=b.shape[1], aux_f32=int(aux_f32),
+    )
+    _lib.call("dpc_gemm_f32", args, a.device)
+    return out
 
 
 def _pad_to(x: torch.Tensor, rows: int, cols: int) -> torch.Tensor:

@@ -13,8 +13,10 @@ from . import _lib
 from .dropout import keep_mask
 
 
-def _use_hip(x: torch.Tensor, y_dtype: torch.dtype) -> bool:
-    return x.is_cuda and y_dtype == torch.bfloat16
+def _use_hip(x: torch.Tensor, y_dtype: torch.dtype, add=None) -> bool:
+    """bf16 y (the AMP path) or f32 y (--disable_amp); the fused residual add takes a bf16 y."""
+    return (x.is_cuda and y_dtype in (torch.bfloat16, torch.float32)
+            and (add is None or add[0].dtype == torch.bfloat16))
 
 
 def layernorm_fwd(x: torch.Tensor, gamma: torch.Tensor, beta: torch.Tensor, eps: float = 1e-5,
@@ -30,7 +32,7 @@ def layernorm_fwd(x: torch.Tensor, gamma: torch.Tensor, beta: torch.Tensor, eps:
     T, D = x.shape
     if add is not None and x_out is None:
         raise ValueError("layernorm_fwd: add= needs x_out")
-    if not _use_hip(x, out_dtype):
+    if not _use_hip(x, out_dtype, add):
         if add is not None:
             y_add, b_add, drop = add
             a = y_add.float() + (b_add.float() if b_add is not None else 0.0)

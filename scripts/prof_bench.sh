@@ -14,3 +14,5 @@ python3 scripts/step_gaps.py $db --steps 8 > gpurun_out/prof_${tag}_steps.md
 python3 scripts/kstats.py $db "bench $tag" > gpurun_out/prof_${tag}_kstats.md
 tail -3 gpurun_out/prof_$tag.log
 head -12 gpurun_out/prof_${tag}_steps.md
+# the trace databases are large (gpurun copies back at most 64 MiB): keep the summaries
+[ -n "$KEEP_DB" ] || rm -rf gpurun_out/prof_$tag
