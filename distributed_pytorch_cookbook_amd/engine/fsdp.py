@@ -8,12 +8,17 @@ unit by unit to rank 0 only instead of materialising the full model on every GPU
 """
 from __future__ import annotations
 
+import os
+
 import torch
 
 from ..ops.optim import FlatAdamW
 from ..parallel import comm
 from ..parallel.fsdp import FSDPStore
 from .base import Engine, GraphedStep
+
+# A/B switch (bench/offload.py): the synchronous offload step (D2H, host AdamW, H2D in turn)
+_OFFLOAD_SYNC = os.environ.get("DPC_OFFLOAD_SYNC", "0") == "1"
 
 
 class FSDPEngine(Engine):
@@ -42,7 +47,7 @@ class FSDPEngine(Engine):
 
             self.scaler = GradScaler(self.device)
         # HIP-graph "compile" of the whole sharded step (gathers, reduce-scatters, AdamW);
-        # not with --cpu_offload, whose host optimizer synchronises mid-step
+        # not with --cpu_offload, whose optimizer runs on the host
         self.graph = (graph and self.device.type == "cuda" and not st.cpu_offload
                       and (st.W == 1 or st.tp.capturable()))
         self._stepper = GraphedStep(self, [self.opt, self.opt_rep])
@@ -58,7 +63,13 @@ class FSDPEngine(Engine):
         out = self.model(**batch, targets=targets)
         self._scaled(out.loss).backward()
         st.finish_grads()
+        if st.cpu_offload and self.scaler is None and not _OFFLOAD_SYNC:
+            # pipelined host AdamW: overlaps the next step's forward (FSDPStore.host_step)
+            st.host_step(self.opt, grad_scale=1.0 / self.dp_world)
+            self.opt_rep.step(grad_scale=1.0 / self.dp_world)
+            return out.loss.detach()
         if st.cpu_offload:
+            st.grads_host.copy_(st.grads, non_blocking=True)
             torch.cuda.current_stream().synchronize()  # grads_host D2H landed
         if self.scaler is not None:
             # shards differ per rank: the skip decision is reduced over the group
@@ -86,6 +97,7 @@ class FSDPEngine(Engine):
         return self.store.gather_full(self.store.master, dst_rank=0)
 
     def load_model_state(self, sd):
+        self.store.wait_host()
         self.store.load_full(sd, self.store.master)
         self.store.refresh_shadow()
 
@@ -97,6 +109,7 @@ class FSDPEngine(Engine):
                               "format": "canonical"}, **self._scaler_state()}
 
     def load_train_state(self, st):
+        self.store.wait_host()
         o = st["optimizer"]
         self.opt.step_count = int(o["step"])
         self.opt_rep.step_count = int(o["step"])

@@ -69,6 +69,8 @@ class FSDPStore(ParamStore):
             self.shard_off.append(self.shard_off[-1] + n)
         total = sum(self.shard_len)
         host = self.cpu_offload
+        self._host_tasks = {}  # --cpu_offload: unit -> Future of the event after its shadow upload
+        self._d2h_done = None  # event after the step's gradient copies (zero_grad waits on it)
         mdev = torch.device("cpu") if host else self.device
         self.master = torch.zeros(total, dtype=torch.float32, device=mdev,
                                   pin_memory=host)
@@ -117,13 +119,69 @@ class FSDPStore(ParamStore):
         self._fresh = set(self.units)  # units whose shard gradient holds no contribution yet
         self._in_backward = False
         self.peak_live_units = 0  # most full-unit buffers (weights + gradients) alive at once
+        # --cpu_offload: per-unit pipelined host AdamW (host_step)
+        if host:
+            from concurrent.futures import ThreadPoolExecutor
+
+            self._copy = torch.cuda.Stream(device=self.device)
+            self._pool = ThreadPoolExecutor(max_workers=1, thread_name_prefix="dpc-host-adamw")
+            self._hshadow = (torch.empty(total, dtype=torch.bfloat16, pin_memory=True)
+                             if self.compute_dtype == torch.bfloat16 else None)
 
     # ------------------------------------------------------------------ shards
     def shard(self, flat, u):
         o = self.shard_off[u]
         return flat[o:o + self.shard_len[u]]
 
+    # ------------------------------------------------------------------ host optimizer (offload)
+    def host_step(self, opt, grad_scale: float = 1.0) -> None:
+        """``--cpu_offload`` AdamW, pipelined per unit: unit u's gradient shard goes D2H on a
+        copy stream, a worker thread runs the fused native host AdamW on it
+        (``runtime.adamw_host``, OpenMP, GIL released) and queues the H2D upload of its new
+        compute copy; the next forward's gather of unit u waits for that unit only, so the
+        host update of the later units overlaps the forward of the earlier ones (reference:
+        ``CPUOffload(offload_params=True)``, ``/root/reference/main-fsdp.py:60-69``)."""
+        opt.step_count += 1
+        step = opt.step_count
+        ev = torch.cuda.Event()
+        ev.record(torch.cuda.current_stream(self.device))
+        self._copy.wait_event(ev)
+        for u in self.units:
+            sl = slice(self.shard_off[u], self.shard_off[u] + self.shard_len[u])
+            with torch.cuda.stream(self._copy):
+                self.grads_host[sl].copy_(self.grads[sl], non_blocking=True)
+                d2h = torch.cuda.Event()
+                d2h.record(self._copy)
+            self._host_tasks[u] = self._pool.submit(self._host_unit, sl, d2h, opt, step, grad_scale)
+        self._d2h_done = torch.cuda.Event()
+        self._d2h_done.record(self._copy)
+
+    def _host_unit(self, sl, d2h, opt, step, grad_scale):
+        from .. import runtime
+
+        d2h.synchronize()
+        b1, b2 = opt.betas
+        hs = self._hshadow[sl] if self._hshadow is not None else None
+        runtime.adamw_host(self.master[sl], self.grads_host[sl], opt.exp_avg[sl], opt.exp_avg_sq[sl],
+                           opt.lr, b1, b2, opt.eps, opt.weight_decay, step, grad_scale, hs)
+        with torch.cuda.device(self.device), torch.cuda.stream(self._copy):
+            self.shadow[sl].copy_(hs if hs is not None else self.master[sl], non_blocking=True)
+            up = torch.cuda.Event()
+            up.record(self._copy)
+        return up
+
+    def _wait_host(self, u) -> None:
+        f = self._host_tasks.pop(u, None)
+        if f is not None:
+            torch.cuda.current_stream(self.device).wait_event(f.result())
+
+    def wait_host(self) -> None:
+        """Every pending host update applied (before reading master / moments / shadow)."""
+        for u in list(self._host_tasks):
+            self._wait_host(u)
+
     def refresh_shadow(self):
+        self.wait_host()
         src = self.master.to(self.device, non_blocking=True) if self.cpu_offload else self.master
         if self.compute_dtype == torch.float32:
             self.shadow.copy_(src)
@@ -134,6 +192,7 @@ class FSDPStore(ParamStore):
     def _gather(self, u):
         if u in self._full or not (0 <= u < self.nunits):
             return
+        self._wait_host(u)  # --cpu_offload: this unit's updated weights uploaded
         sh = self.shard(self.shadow, u)
         if self.W == 1:
             self._full[u] = (sh, None)  # one rank: the shard is the whole unit
@@ -240,10 +299,11 @@ class FSDPStore(ParamStore):
         # anything still gathered from the forward (e.g. the head) is released now
         for u in list(self._full):
             self._release(u)
-        if self.cpu_offload:
-            self.grads_host.copy_(self.grads, non_blocking=True)
 
     def zero_grad(self):
+        if self._d2h_done is not None:  # the host optimizer's gradient copies read grads first
+            torch.cuda.current_stream(self.device).wait_event(self._d2h_done)
+            self._d2h_done = None
         self.grads.zero_()
         self.rep_grads.zero_()
         self._fresh = set(self.units)
@@ -254,6 +314,7 @@ class FSDPStore(ParamStore):
         """Canonical {name: tensor} of a sharded flat f32 buffer (params or optimizer
         moments), materialised on ``dst_rank`` (others return None).  Collective.
         ``rep_flat``: the replicated buffer holding the 1-D entries (default: rep_master)."""
+        self.wait_host()
         rep_flat = self.rep_master if rep_flat is None else rep_flat
         out = {} if self.rank == dst_rank else None
         for u in self.units:
