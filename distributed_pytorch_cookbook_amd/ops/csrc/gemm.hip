@@ -1087,7 +1087,7 @@ static int policy_impl(const GemmArgs* a) {
   return g_policy[c];
 }
 
-extern "C" int dpc_gemm7(const GemmArgs* a, int persistent, int sched, int splits, hipStream_t stream);
+extern "C" int dpc_gemm7(const GemmArgs* a, int persistent, int sched, int splits, hipStream_t stream, int wn);
 extern "C" int dpc_gemm7_ok(const GemmArgs* a);
 
 DPC_API int dpc_gemm(const GemmArgs* a, hipStream_t stream) {
@@ -1147,8 +1147,10 @@ DPC_API int dpc_gemm(const GemmArgs* a, hipStream_t stream) {
   if (impl >= 15 && impl <= 22) {  // v7 (gemm7.hip): 4-wave 256x256, split-K f32 products
     GemmArgs c = *a;
     c.ksplit = 0;
-    const int sched = impl == 19 ? 1 : (impl == 20 || impl == 17 ? 2 : 0);
-    const int rc = dpc_gemm7(&c, impl != 17, sched, g_force_splits > 0 ? g_force_splits : 0, stream);
+    const int sched = impl == 19 ? 1 : (impl == 20 || impl == 17 || impl == 21 ? 2 : 0);
+    // 21: v8 -- 256x128 tiles, two persistent workgroups per CU (epilogue beside MFMAs)
+    const int rc = dpc_gemm7(&c, impl != 17, sched, g_force_splits > 0 ? g_force_splits : 0, stream,
+                             impl == 21 ? 64 : 128);
     if (rc >= 0) return rc;
     impl = v2_ok ? 2 : 1;  // requirements not met: the 128x128 kernels
   }

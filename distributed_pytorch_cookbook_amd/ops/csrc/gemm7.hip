@@ -45,6 +45,7 @@ constexpr int G7_NL = G7_TA / 512 / 4; // 1-KiB DMA pieces per wave per operand 
 
 struct G7Plan {
   int tiles_m, tiles_n;
+  int tile_n;  // tile width: 256 (v7) or 128 (v8)
   int units;   // tiles x splits (split-major: unit = split * tiles + tile)
   int grid;    // workgroups launched
   int nk;      // k-slices per unit (even)
@@ -68,7 +69,7 @@ __device__ __forceinline__ void g7_tile(const G7Plan& pl, int u, int& m0, int& n
   const int gsz = min(pl.tiles_m - first_m, GROUP_M);
   const int w = u - gid * group;
   m0 = (first_m + w % gsz) * 256;
-  n0 = (w / gsz) * 256;
+  n0 = (w / gsz) * pl.tile_n;
 }
 
 // One 1-KiB LDS-DMA piece (buffer_load_dwordx4 ... lds: 64 lanes x 16 B, lane-linear at M0).
@@ -118,8 +119,8 @@ __device__ __forceinline__ void sfor(F&& f) {
 
 #define G7_AI __attribute__((always_inline))
 
-template <int MODE>
-__device__ __forceinline__ void g7_epilogue(const GemmArgs& p, floatx4 (&acc)[8][8], int mw, int nw, int lane) {
+template <int MODE, int NJ>
+__device__ __forceinline__ void g7_epilogue(const GemmArgs& p, floatx4 (&acc)[8][NJ], int mw, int nw, int lane) {
   float alpha = p.alpha;
   if (p.alpha_ptr) alpha *= *p.alpha_ptr;
   const int g = lane >> 4, rl = lane & 15;
@@ -133,7 +134,7 @@ __device__ __forceinline__ void g7_epilogue(const GemmArgs& p, floatx4 (&acc)[8]
       for (int i = 0; i < 8; ++i) {
         const int m = mw + 16 * i + rl;
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
+        for (int j = 0; j < NJ; ++j) {
           const int n = nw + 16 * j + 4 * g;
           if (m < p.M && n < p.N)
             *reinterpret_cast<float4*>(static_cast<float*>(p.C) + (long long)m * p.ldc + n) =
@@ -146,7 +147,7 @@ __device__ __forceinline__ void g7_epilogue(const GemmArgs& p, floatx4 (&acc)[8]
     for (int i = 0; i < 8; ++i) {
       const int m = mw + 16 * i + rl;
 #pragma unroll
-      for (int j = 0; j < 8; j += 2) {
+      for (int j = 0; j < NJ; j += 2) {
         unsigned x0 = pack2bf(acc[i][j][0] * alpha, acc[i][j][1] * alpha);
         unsigned x1 = pack2bf(acc[i][j][2] * alpha, acc[i][j][3] * alpha);
         unsigned y0 = pack2bf(acc[i][j + 1][0] * alpha, acc[i][j + 1][1] * alpha);
@@ -184,10 +185,10 @@ __device__ __forceinline__ void g7_epilogue(const GemmArgs& p, floatx4 (&acc)[8]
     }
     return r;
   };
-  uint4 ld[8];
-  float4 bias4[8];
-  float cs[8][4];
-  sfor<8>([&](auto J) G7_AI {
+  uint4 ld[NJ];
+  float4 bias4[NJ];
+  float cs[NJ][4];
+  sfor<NJ>([&](auto J) G7_AI {
     constexpr int j = decltype(J)::value;
     ld[j] = load_one(mw + rl, nw + 16 * j + 4 * g);
     if constexpr (FWD) {
@@ -202,7 +203,7 @@ __device__ __forceinline__ void g7_epilogue(const GemmArgs& p, floatx4 (&acc)[8]
     constexpr int i = decltype(I)::value;
     const int m = mw + 16 * i + rl;
     const bool mok = m < p.M;
-    sfor<4>([&](auto J) G7_AI {
+    sfor<NJ / 2>([&](auto J) G7_AI {
       constexpr int j = 2 * decltype(J)::value;
       unsigned pa[2][2], pc[2][2];
       sfor<2>([&](auto H) G7_AI {
@@ -273,7 +274,7 @@ __device__ __forceinline__ void g7_epilogue(const GemmArgs& p, floatx4 (&acc)[8]
       // sum over the 16 rows of a lane group, then lane t of group g adds columns 2t, 2t+1 of
       // the group's 32 (j = e >> 2, r = e & 3 -> column 16 j + 4 g + r)
 #pragma unroll
-      for (int j = 0; j < 8; ++j)
+      for (int j = 0; j < NJ; ++j)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           float v = cs[j][r];
@@ -288,9 +289,9 @@ __device__ __forceinline__ void g7_epilogue(const GemmArgs& p, floatx4 (&acc)[8]
         const int e = 2 * rl + h;
         float v = 0.f;
 #pragma unroll
-        for (int k = 0; k < 32; ++k) v = (e == k) ? cs[k >> 2][k & 3] : v;
+        for (int k = 0; k < 4 * NJ; ++k) v = (e == k) ? cs[k >> 2][k & 3] : v;
         const int n = nw + 16 * (e >> 2) + 4 * g + (e & 3);
-        if (n < p.N) atomicAdd(p.colsum + n, v);
+        if (e < 4 * NJ && n < p.N) atomicAdd(p.colsum + n, v);
       }
     }
   }
@@ -320,25 +321,36 @@ __device__ __forceinline__ void g7_epilogue_atomic(const GemmArgs& p, floatx4 (&
 
 // EPI: 0 = plain products (bf16 / f32 C), 1 = forward fused epilogues, 2 = split-K f32 atomics,
 // 3 = input-gradient fused epilogues (act', column sums).
-template <int EPI, int SCHED, bool AK, bool BK>
-__global__ __launch_bounds__(256, 1) void gemm7_kernel(GemmArgs p, unsigned long long a_bytes,
-                                                       unsigned long long b_bytes, G7Plan pl) {
-  constexpr int NS = 5, DIST = NS - 1;
-  static_assert(NS * G7_SLOT * 2 <= 160 * 1024, "LDS");
-  __shared__ __attribute__((aligned(16))) bf16_t smem[NS * G7_SLOT];
+// WN: output columns per wave.  128 = v7 (a 256 x 256 tile, one workgroup per CU); 64 = v8 (a
+// 256 x 128 tile, 128 accumulator registers, TWO workgroups per CU, each with a 3-slot ring:
+// the two drift out of phase, so one's epilogue -- the bias / GELU / residual / act' VALU work
+// and the store burst, which a lone wave per SIMD serialises against its MFMAs -- runs beside
+// the other's main loop).
+template <int EPI, int SCHED, bool AK, bool BK, int WN = 128>
+__global__ __launch_bounds__(256, WN == 128 ? 1 : 2) void gemm7_kernel(GemmArgs p, unsigned long long a_bytes,
+                                                                       unsigned long long b_bytes, G7Plan pl) {
+  constexpr int NJ = WN / 16;                 // 16-column accumulator blocks per wave
+  constexpr int BW = 2 * WN;                  // tile width (B rows / columns per slice)
+  constexpr int TB = BW * G7_KB;              // B elements per slice
+  constexpr int SLOT = G7_TA + TB;
+  constexpr int NLB = TB / 512 / 4;           // B pieces per wave per slice
+  constexpr int NP = G7_NL + NLB;             // pieces per wave per slice
+  constexpr int NS = WN == 128 ? 5 : 3, DIST = NS - 1;
+  static_assert(NS * SLOT * 2 * (WN == 128 ? 1 : 2) <= 160 * 1024, "LDS");
+  __shared__ __attribute__((aligned(16))) bf16_t smem[NS * SLOT];
 
   const int lane = threadIdx.x & 63;
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int wr = wid >> 1, wc = wid & 1;
-  const int ar = wr * 128, bc = wc * 128;
+  const int ar = wr * 128, bc = wc * WN;
 
   const int local = g7_local(blockIdx.x, pl.grid);
   const int nmine = local < pl.units ? (pl.units - local + pl.grid - 1) / pl.grid : 0;
   if (nmine == 0) return;
 
-  int va[G7_NL], vb[G7_NL];
+  int va[G7_NL], vb[NLB];
   dma_offsets3<32, AK, G7_NL>(va, p.lda, wid, lane);
-  dma_offsets3<32, BK, G7_NL>(vb, p.ldb, wid, lane);
+  dma_offsets3<32, BK, NLB>(vb, p.ldb, wid, lane);
   const unsigned long long a_step = AK ? 64ull : 32ull * p.lda * 2;
   const unsigned long long b_step = BK ? 64ull : 32ull * p.ldb * 2;
 
@@ -368,11 +380,11 @@ __global__ __launch_bounds__(256, 1) void gemm7_kernel(GemmArgs p, unsigned long
     const unsigned nb = valid ? ((lb >> 32) ? 0xffffffffu : (unsigned)lb) : 0u;
     rsa = __builtin_amdgcn_make_buffer_rsrc((void*)((const char*)p.A + is_aoff), 0, na, 0x00020000);
     rsb = __builtin_amdgcn_make_buffer_rsrc((void*)((const char*)p.B + is_boff), 0, nb, 0x00020000);
-    is_lds = smem + is_slot * G7_SLOT;
+    is_lds = smem + is_slot * SLOT;
   };
-  auto piece = [&](int i) {  // the pieces of one slice: A then B, NL each
+  auto piece = [&](int i) {  // the pieces of one slice: A (G7_NL) then B (NLB)
     if (i < G7_NL) g7_piece(rsa, va[i], is_lds + (wid * G7_NL + i) * 512);
-    else g7_piece(rsb, vb[i - G7_NL], is_lds + G7_TA + (wid * G7_NL + i - G7_NL) * 512);
+    else g7_piece(rsb, vb[i - G7_NL], is_lds + G7_TA + (wid * NLB + i - G7_NL) * 512);
   };
   auto advance = [&]() {
     is_slot = is_slot + 1 == NS ? 0 : is_slot + 1;
@@ -390,24 +402,24 @@ __global__ __launch_bounds__(256, 1) void gemm7_kernel(GemmArgs p, unsigned long
   for (int s = 0; s < DIST; ++s) {
     prep();
 #pragma unroll
-    for (int i = 0; i < 2 * G7_NL; ++i) piece(i);
+    for (int i = 0; i < NP; ++i) piece(i);
     advance();
   }
   prep();
 
-  floatx4 acc[8][8];  // written first by each tile's FIRST body
+  floatx4 acc[8][NJ];  // written first by each tile's FIRST body
 
   // slice 0 landed (DIST-1 slices younger) -> frags(0)
-  g7_wait<(DIST - 1) * 2 * G7_NL>();
+  g7_wait<(DIST - 1) * NP>();
   __builtin_amdgcn_s_barrier();
   asm volatile("" ::: "memory");
-  bf16x8 a0[8], b0[8], a1[8], b1[8];
+  bf16x8 a0[8], b0[NJ], a1[8], b1[NJ];
 #pragma unroll
   for (int i = 0; i < 8; ++i) a0[i] = frag3<32, AK>(smem, ar + 16 * i, 0, lane);
 #pragma unroll
-  for (int j = 0; j < 8; ++j) b0[j] = frag3<32, BK>(smem + G7_TA, bc + 16 * j, 0, lane);
+  for (int j = 0; j < NJ; ++j) b0[j] = frag3<32, BK>(smem + G7_TA, bc + 16 * j, 0, lane);
   // slice 1 landed -> its slot may be read in body(0)
-  g7_wait<(DIST - 2) * 2 * G7_NL>();
+  g7_wait<(DIST - 2) * NP>();
   __builtin_amdgcn_s_barrier();
   asm volatile("" ::: "memory");
 
@@ -418,7 +430,7 @@ __global__ __launch_bounds__(256, 1) void gemm7_kernel(GemmArgs p, unsigned long
   // then slice q+2 landed (younger: slices q+3 .. q+DIST, plus a recent epilogue's stores) +
   // barrier.  nk is even (padded with all-zero slices), so every unit starts on register set 0.
 #define G7_MFMA_ROW(i_, ac, bcur, FIRST)                                                            \
-  _Pragma("unroll") for (int j = 0; j < 8; ++j) acc[i_][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(  \
+  _Pragma("unroll") for (int j = 0; j < NJ; ++j) acc[i_][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(  \
       EPI == 2 ? ac[i_] : bcur[j], EPI == 2 ? bcur[j] : ac[i_],                                    \
       (FIRST) ? floatx4{0.f, 0.f, 0.f, 0.f} : acc[i_][j], 0, 0, 0)
   // DMA piece placement inside a body (SCHED): 0 = piece g at the head of group g, 1 = four
@@ -427,10 +439,10 @@ __global__ __launch_bounds__(256, 1) void gemm7_kernel(GemmArgs p, unsigned long
   // of the body or one at the tail of each group lost)
   auto piece_sched = [&](int g, bool tail) {
     if (pl.debug & 2) return;
-    if (SCHED == 0 && !tail) piece(g);
+    if (SCHED == 0 && !tail && g < NP) piece(g);
 
-    if (SCHED == 2 && !tail && !(g & 1)) { piece(g); piece(g + 1); }
-    if (SCHED == 1 && !tail && !(g & 3)) { piece(g); piece(g + 1); piece(g + 2); piece(g + 3); }
+    if (SCHED == 2 && !tail && !(g & 1) && g < NP) { piece(g); piece(g + 1); }
+    if (SCHED == 1 && !tail && !(g & 3) && g < NP) { piece(g); piece(g + 1); piece(g + 2); piece(g + 3); }
 
   };
   // one slice: MFMAs on (ac, bcur) -- FIRST: a tile's first slice, accumulating onto zero (an
@@ -440,12 +452,16 @@ __global__ __launch_bounds__(256, 1) void gemm7_kernel(GemmArgs p, unsigned long
   // starts on register set 0.
 #define G7_BODY(ac, bcur, an, bn, FIRST)                                                            \
   do {                                                                                              \
-    const bf16_t* la_ = smem + rd_slot * G7_SLOT;                                                   \
+    const bf16_t* la_ = smem + rd_slot * SLOT;                                                      \
     _Pragma("unroll") for (int i = 0; i < 8; ++i) {                                                 \
       piece_sched(i, false);                                                                        \
-      an[i] = frag3<32, AK>(la_, ar + 16 * i, 0, lane);                                             \
-      bn[i] = frag3<32, BK>(la_ + G7_TA, bc + 16 * i, 0, lane);                                     \
+      if (!A1) an[i] = frag3<32, AK>(la_, ar + 16 * i, 0, lane);                                    \
+      if (i < NJ) bn[i] = frag3<32, BK>(la_ + G7_TA, bc + 16 * i, 0, lane);                         \
       G7_MFMA_ROW(i, ac, bcur, FIRST);                                                              \
+      if (A1) { /* after its MFMAs issued: the fragment's registers are reused */                   \
+        __builtin_amdgcn_sched_barrier(0);                                                          \
+        an[i] = frag3<32, AK>(la_, ar + 16 * i, 0, lane);                                           \
+      }                                                                                             \
       piece_sched(i, true);                                                                         \
       if (i == 7) { /* next body's descriptors, in the shadow of this group's MFMAs */           \
         advance();                                                                                  \
@@ -456,35 +472,48 @@ __global__ __launch_bounds__(256, 1) void gemm7_kernel(GemmArgs p, unsigned long
     rd_slot = rd_slot + 1 == NS ? 0 : rd_slot + 1;                                                  \
     if (credit > 0) {                                                                               \
       --credit;                                                                                     \
-      if (pl.store_cnt >= 48) g7_wait<(DIST - 2) * 2 * G7_NL + 47>();                               \
-      else g7_wait<(DIST - 2) * 2 * G7_NL + 31>();                                                  \
+      if (pl.store_cnt >= 48) g7_wait<(DIST - 2) * NP + 47>();                                      \
+      else g7_wait<(DIST - 2) * NP + 31>();                                                         \
     } else {                                                                                        \
-      g7_wait<(DIST - 2) * 2 * G7_NL>();                                                            \
+      g7_wait<(DIST - 2) * NP>();                                                                   \
     }                                                                                               \
     __builtin_amdgcn_s_barrier();                                                                   \
     asm volatile("" ::: "memory");                                                                  \
   } while (0)
 
+  // A1 (v8): ONE A-fragment set, row i re-read for the next slice right after its MFMAs are
+  // issued (the 128 accumulators + a double B set + one A set fit 256 registers: two waves per
+  // SIMD); v7 double-buffers both
+  constexpr bool A1 = WN == 64;
   for (int u = 0; u < nmine; ++u) {
-    G7_BODY(a0, b0, a1, b1, true);
-    G7_BODY(a1, b1, a0, b0, false);
-    for (int k = 2; k < pl.nk; k += 2) {
-      G7_BODY(a0, b0, a1, b1, false);
+    if constexpr (A1) {
+      G7_BODY(a0, b0, a0, b1, true);
+      G7_BODY(a0, b1, a0, b0, false);
+      for (int k = 2; k < pl.nk; k += 2) {
+        G7_BODY(a0, b0, a0, b1, false);
+        G7_BODY(a0, b1, a0, b0, false);
+      }
+    } else {
+      G7_BODY(a0, b0, a1, b1, true);
       G7_BODY(a1, b1, a0, b0, false);
+      for (int k = 2; k < pl.nk; k += 2) {
+        G7_BODY(a0, b0, a1, b1, false);
+        G7_BODY(a1, b1, a0, b0, false);
+      }
     }
     const int uu = local + u * pl.grid;
     int m0, n0;
     g7_tile(pl, uu % ntiles, m0, n0);
     if (pl.debug & 1) {
-    } else if (EPI == 2) {
-      g7_epilogue_atomic(p, acc, m0 + ar, n0 + bc, lane);
+    } else if constexpr (EPI == 2) {
+      if constexpr (NJ == 8) g7_epilogue_atomic(p, acc, m0 + ar, n0 + bc, lane);
     } else {
-      g7_epilogue<EPI>(p, acc, m0 + ar, n0 + bc, lane);
+      g7_epilogue<EPI, NJ>(p, acc, m0 + ar, n0 + bc, lane);
     }
     // the stores were issued after this tile's last wait: the next DIST-2 waits (slices whose
     // DMA is older than the stores) may leave them in flight -- full tiles only (an edge tile
     // skips stores, and the credit must not exceed what was issued)
-    credit = (EPI != 2 && pl.store_cnt > 0 && m0 + 256 <= p.M && n0 + 256 <= p.N) ? DIST - 2 : 0;
+    credit = (EPI != 2 && pl.store_cnt > 0 && m0 + 256 <= p.M && n0 + BW <= p.N) ? DIST - 2 : 0;
   }
 #undef G7_MFMA_ROW
 #undef G7_BODY
@@ -500,14 +529,14 @@ static inline long long g7_operand_bytes(long long rows, long long cols, long lo
   return ((rows - 1) * ld + ((cols + 7) / 8) * 8) * 2;
 }
 
-template <int EPI, int SCHED>
+template <int EPI, int SCHED, int WN = 128>
 static void g7_launch(const GemmArgs* a, const G7Plan& pl, hipStream_t stream, unsigned long long ab,
                       unsigned long long bb) {
   dim3 grid(pl.grid), block(256);
-  if (a->a_kmaj && a->b_kmaj) hipLaunchKernelGGL((gemm7_kernel<EPI, SCHED, true, true>), grid, block, 0, stream, *a, ab, bb, pl);
-  else if (a->a_kmaj) hipLaunchKernelGGL((gemm7_kernel<EPI, SCHED, true, false>), grid, block, 0, stream, *a, ab, bb, pl);
-  else if (!a->b_kmaj) hipLaunchKernelGGL((gemm7_kernel<EPI, SCHED, false, false>), grid, block, 0, stream, *a, ab, bb, pl);
-  else hipLaunchKernelGGL((gemm7_kernel<EPI, SCHED, false, true>), grid, block, 0, stream, *a, ab, bb, pl);
+  if (a->a_kmaj && a->b_kmaj) hipLaunchKernelGGL((gemm7_kernel<EPI, SCHED, true, true, WN>), grid, block, 0, stream, *a, ab, bb, pl);
+  else if (a->a_kmaj) hipLaunchKernelGGL((gemm7_kernel<EPI, SCHED, true, false, WN>), grid, block, 0, stream, *a, ab, bb, pl);
+  else if (!a->b_kmaj) hipLaunchKernelGGL((gemm7_kernel<EPI, SCHED, false, false, WN>), grid, block, 0, stream, *a, ab, bb, pl);
+  else hipLaunchKernelGGL((gemm7_kernel<EPI, SCHED, false, true, WN>), grid, block, 0, stream, *a, ab, bb, pl);
 }
 
 // Returns -1 if the product does not meet v7's requirements (caller falls back), else the
@@ -532,20 +561,24 @@ DPC_API int dpc_gemm7_ok(const GemmArgs* a) {
 
 // splits: 1 = none, > 1 forced, 0 = automatic (plain f32 products only: the tiles are too few to
 // fill the chip, e.g. weight gradients -- K = tokens, M x N = a weight).
-DPC_API int dpc_gemm7(const GemmArgs* a, int persistent, int sched, int splits, hipStream_t stream) {
+// wn: 128 = v7 (256 x 256 tiles, one workgroup per CU), 64 = v8 (256 x 128 tiles, two per CU;
+// no split-K)
+DPC_API int dpc_gemm7(const GemmArgs* a, int persistent, int sched, int splits, hipStream_t stream, int wn) {
   if (a->M <= 0 || a->N <= 0) return 0;
   if (!dpc_gemm7_ok(a)) return -1;
   const long long ab = g7_operand_bytes(a->a_r, a->a_c, a->lda);
   const long long bb = g7_operand_bytes(a->b_r, a->b_c, a->ldb);
+  const bool v8 = wn == 64;
   G7Plan pl;
+  pl.tile_n = v8 ? 128 : 256;
   pl.tiles_m = (a->M + 255) / 256;
-  pl.tiles_n = (a->N + 255) / 256;
+  pl.tiles_n = (a->N + pl.tile_n - 1) / pl.tile_n;
   const int tiles = pl.tiles_m * pl.tiles_n;
   pl.nk_all = (a->K + G7_KB - 1) / G7_KB;
   const bool plain = !a->bias && !a->act_bwd && !a->aux_out && !a->act && !a->residual && !a->colsum;
   const bool splittable = plain && a->out_f32;
   int s = splits > 0 ? splits : 1;
-  if (splits <= 0 && splittable && tiles < 192) {
+  if (splits <= 0 && splittable && tiles < 192 && !v8) {
     // fill the chip: time ~ rounds * slices per unit + an atomic epilogue per unit-round
     // (256 KiB of f32 adds per CU, ~40 slices' worth at the chip's memory-side atomic rate)
     double best = 1e30;
@@ -557,7 +590,7 @@ DPC_API int dpc_gemm7(const GemmArgs* a, int persistent, int sched, int splits, 
       if (cost < best - 1e-9) { best = cost; s = c; }
     }
   }
-  if (s > 1 && !splittable) return -1;
+  if (s > 1 && (!splittable || v8)) return -1;
   // the input-gradient epilogue (act', column sums) carries no forward operation
   if ((a->act_bwd || a->colsum) && (a->bias || a->act || a->aux_out || a->residual || a->accumulate)) return -1;
   pl.splits = s;
@@ -565,11 +598,12 @@ DPC_API int dpc_gemm7(const GemmArgs* a, int persistent, int sched, int splits, 
   pl.units = tiles * s;
   // persistent: one workgroup per CU streams its units through one ring; otherwise one unit
   // per workgroup
-  pl.grid = (persistent && pl.units > 256) ? 256 : pl.units;
+  const int slots = v8 ? 512 : 256;  // workgroups resident at once
+  pl.grid = (persistent && pl.units > slots) ? slots : pl.units;
   // vector-memory ops an epilogue issues per lane, for the store credit: only epilogues that
   // read nothing per element and issue every store of a full tile (no column-sum atomics)
   const bool no_loads = !a->residual && !a->act_bwd && !a->accumulate && !a->colsum;
-  pl.store_cnt = (no_loads && s == 1) ? ((a->out_f32 ? 64 : 32) + (a->aux_out ? 32 : 0)) : 0;
+  pl.store_cnt = (no_loads && s == 1 && !v8) ? ((a->out_f32 ? 64 : 32) + (a->aux_out ? 32 : 0)) : 0;
   static int dbg = -1;
   if (dbg < 0) dbg = getenv("DPC_G7_DEBUG") ? atoi(getenv("DPC_G7_DEBUG")) : 0;
   pl.debug = dbg;
@@ -577,6 +611,10 @@ DPC_API int dpc_gemm7(const GemmArgs* a, int persistent, int sched, int splits, 
   if (s > 1) {
     if (!a->accumulate) hipMemset2DAsync(a->C, (size_t)a->ldc * 4, 0, (size_t)a->N * 4, (size_t)a->M, stream);
     g7_launch<2, 2>(a, pl, stream, ab, bb);
+  } else if (v8) {
+    if (plain && !a->accumulate) g7_launch<0, 2, 64>(a, pl, stream, ab, bb);
+    else if (!a->act_bwd && !a->colsum) g7_launch<1, 2, 64>(a, pl, stream, ab, bb);
+    else g7_launch<3, 2, 64>(a, pl, stream, ab, bb);
   } else if (plain && !a->accumulate) {
     if (sched == 1) g7_launch<0, 1>(a, pl, stream, ab, bb);
     else if (sched == 2) g7_launch<0, 2>(a, pl, stream, ab, bb);

@@ -109,7 +109,7 @@ def _store(x, kmaj):
     return buf[:, :r]
 
 
-@pytest.mark.parametrize("impl", [13, 16, 17, 19, 20])
+@pytest.mark.parametrize("impl", [13, 16, 17, 19, 20, 21])
 @pytest.mark.parametrize("a_kmaj,b_kmaj", [(True, True), (True, False), (False, False), (False, True)])
 @pytest.mark.parametrize("M,N,K", [(300, 264, 128), (1023, 768, 768), (4096, 4352, 256), (513, 2304, 1536),
                                    (300, 264, 96), (257, 520, 1000)])
