@@ -63,7 +63,10 @@ class PipelineEngine(Engine):
         self.last = self.stage == pp - 1
         self.is_logger = comm.rank() == 0
         # 4 x stages micro-batches: the 1F1B bubble is (pp - 1) / (M + pp - 1) -- 18 % at pp 8
-        self.n_micro = max(1, num_microbatches or 4 * pp)
+        # 4 x stages micro-batches (a (pp-1)/(5pp-1) bubble); one stage has no bubble to
+        # hide, so it runs the whole batch at once (the reference: chunks = num_stages,
+        # /root/reference/main-pipe.py:83)
+        self.n_micro = max(1, num_microbatches or (4 * pp if pp > 1 else 1))
         self.schedule = schedule
         S = seq_len or model.max_position_embeddings
         groups = partition(unit_costs(model, S), pp)

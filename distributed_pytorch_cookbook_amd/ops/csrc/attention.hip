@@ -110,6 +110,17 @@ template <int N>
 __device__ __forceinline__ void vm_wait() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
+// Make the compiler wait for the kernel's own register loads (the per-row operands held for
+// the whole sweep) HERE, before any LDS-DMA is in flight: left to itself it places that
+// s_waitcnt at the first use -- inside the tile loop -- and, not counting the asm DMA, as
+// vmcnt(0), which drains the ring's prefetch on every iteration.
+template <int N>
+__device__ __forceinline__ void pin_loaded(const bf16x8 (&x)[N]) {
+#pragma unroll
+  for (int i = 0; i < N; ++i) asm volatile("" ::"v"(x[i]));
+}
+__device__ __forceinline__ void pin_loaded(float x) { asm volatile("" ::"v"(x)); }
+
 __device__ __forceinline__ void ring_barrier() {
   __builtin_amdgcn_s_barrier();
   asm volatile("" ::: "memory");
@@ -246,6 +257,7 @@ __global__ __launch_bounds__(256, OCC) void attn_fwd_kernel(AttnArgs p) {
 #pragma unroll
   for (int st = 0; st < A::NST; ++st)
     qf[st] = q < S ? load_row8(Q + (tok0 + q) * p.ld_qkv + 16 * st + 8 * hh) : bf16x8{};
+  pin_loaded(qf);
   const float c = p.scale * LOG2E;
   const int kend = p.causal ? min(S, qb * QB + QB) : S;
   const int ntiles = (kend + KT - 1) / KT;
@@ -497,6 +509,8 @@ __global__ __launch_bounds__(256, OCC) void attn_bwd_dkdv_kernel(AttnArgs p) {
     kf[st] = key < S ? load_row8(Kp + (tok0 + key) * p.ld_qkv + 16 * st + 8 * hh) : bf16x8{};
     vf[st] = key < S ? load_row8(Vp + (tok0 + key) * p.ld_qkv + 16 * st + 8 * hh) : bf16x8{};
   }
+  pin_loaded(kf);
+  pin_loaded(vf);
   const float c = p.scale * LOG2E;
   floatx16 dvt[A::NDT], dkt[A::NDT];
 #pragma unroll
@@ -656,6 +670,10 @@ __global__ __launch_bounds__(256, OCC) void attn_bwd_dq_kernel(AttnArgs p) {
   const float c = p.scale * LOG2E;
   const float lse2 = q < S ? p.lse[(long long)bh * S + q] * LOG2E : INFINITY;
   const float dl = q < S ? p.delta[(long long)bh * S + q] : 0.f;
+  pin_loaded(qf);
+  pin_loaded(df);
+  pin_loaded(lse2);
+  pin_loaded(dl);
   floatx16 dqt[A::NDT];
 #pragma unroll
   for (int d = 0; d < A::NDT; ++d) zero16(dqt[d]);

@@ -74,7 +74,7 @@ def build_engine(recipe: str, model, info, args):
         pp, dp = pipe_mesh(recipe, info.world_size, args.pp_size, getattr(args, "dp_size", 0))
         wire = {"fp32": None, "bf16": torch.bfloat16}[getattr(args, "pp_comm_dtype", "fp32")]
         return PipelineEngine(model, info.device, lr=args.learning_rate, pp=pp, dp=dp,
-                              num_microbatches=args.num_microbatches or 4 * pp,
+                              num_microbatches=args.num_microbatches or (4 * pp if pp > 1 else 1),
                               schedule=args.schedule, bucket_mb=args.bucket_mb,
                               compute_dtype=compute_dtype, grad_scaler=getattr(args, "grad_scaler", False),
                               comm_kind=comm_kind, wire_dtype=wire, graph=graph)
