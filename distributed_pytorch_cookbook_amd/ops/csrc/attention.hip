@@ -234,7 +234,7 @@ __device__ __forceinline__ void xcd_work(int nblk, int& bh, int& i) {
 // O^T += V^T P^T (4 x NDT MFMAs).
 // PIPE: 0 = plain order, 1 = next tile's S^T beside this tile's softmax, 2 = 1 + the tile's
 // LDS fragments read up front and the MFMA / VALU interleave pinned (sched_group_barrier)
-template <int HD, int PIPE, int OCC>
+template <int HD, int PIPE, int OCC, int ABL = 0>
 __global__ __launch_bounds__(256, OCC) void attn_fwd_kernel(AttnArgs p) {
   using A = AT<HD>;
   __shared__ __attribute__((aligned(16))) bf16_t smem[NSLOT * 2 * A::TILE];  // [slot][K|V]
@@ -295,9 +295,9 @@ __global__ __launch_bounds__(256, OCC) void attn_fwd_kernel(AttnArgs p) {
   ring_barrier();
   // one tile: scores of tile t in sc; the next tile's land in sn (ping-pong, no copies)
   auto step = [&](int t, floatx16 (&sc)[2], floatx16 (&sn)[2]) {
-    vm_wait<2 * A::NPW>();  // this wave's pieces of tile t+1 landed (t+2 may fly)
-    ring_barrier();         // ... every wave's; and every wave is done with tile t-1's slot
-    issue(t + 3);
+    if constexpr (!(ABL & 2)) vm_wait<2 * A::NPW>();  // this wave's pieces of tile t+1 landed (t+2 may fly)
+    if constexpr (!(ABL & 4)) ring_barrier();         // ... every wave's; and every wave is done with tile t-1's slot
+    if constexpr (!(ABL & 2)) issue(t + 3);
     const bf16_t* lkn = smem + ((t + 1) % NSLOT) * 2 * A::TILE;
     const bf16_t* lv = smem + (t % NSLOT) * 2 * A::TILE + A::TILE;
     if (t > last_w) return;  // wave-uniform
@@ -319,7 +319,24 @@ __global__ __launch_bounds__(256, OCC) void attn_fwd_kernel(AttnArgs p) {
     }
     const int kt0 = t * KT;
     // Scores stay raw (unscaled) until the exponent: p = 2^(s*c - m) is one FMA + v_exp.
-    const bool need_mask = (p.causal && kt0 + KT - 1 > q0) || (kt0 + KT > S) || pad;  // wave-uniform
+    const bool need_mask = !(ABL & 32) && ((p.causal && kt0 + KT - 1 > q0) || (kt0 + KT > S) || pad);  // wave-uniform
+    if constexpr (ABL & 1) {
+      if constexpr (PIPE == 1) qk(sn, lkn);
+      bf16x8 pb[2][2];
+#pragma unroll
+      for (int kb = 0; kb < 2; ++kb) {
+        pb[kb][0] = acc_frag(sc[kb], 0);
+        pb[kb][1] = acc_frag(sc[kb], 1);
+      }
+#pragma unroll
+      for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+        for (int ss = 0; ss < 2; ++ss)
+#pragma unroll
+          for (int d = 0; d < A::NDT; ++d)
+            o[d] = MFMA32(tr_frag<HD>(lv, kb * 32, ss, d * 32, lane), pb[kb][ss], o[d]);
+      return;
+    }
     if (need_mask) {
       // key > lim is causal / past-the-end, pm is the tile's padding bitmask
       const unsigned long long pm = pad_bits(pad, kt0, S, lane);
@@ -420,7 +437,7 @@ __global__ __launch_bounds__(256, OCC) void attn_fwd_kernel(AttnArgs p) {
   };
   floatx16 s0[2], s1[2];
   if constexpr (PIPE != 0) qk(s0, smem);
-  for (int t = 0; t < ntiles; t += 2) {
+  for (int t = 0; t < ((ABL & 64) ? 0 : ntiles); t += 2) {
     step(t, s0, s1);
     if (t + 1 < ntiles) step(t + 1, s1, s0);
   }
@@ -445,6 +462,211 @@ __global__ __launch_bounds__(256, OCC) void attn_fwd_kernel(AttnArgs p) {
       p.lse[(long long)bh * S + q] = lse;
     }
   }
+}
+
+// ------------------------------------------------------------------ forward v2 (pair stream)
+// Measured on the one-launch-per-128-query-block kernel above (bench/attn_one.py, GPT-2 small
+// shape, scripts/attn_abl.sh): with its tile loop removed it still took 76 of its 267 us --
+// every workgroup pays a Q load + ring fill + drain + store tail at S = 1024, where a block
+// averages 8.5 key tiles -- and the causal triangle leaves blocks of 2 .. 16 tiles.
+// Here a workgroup runs TWO 128-query blocks of one (batch, head): the heaviest and the
+// lightest left (qa = nqb-1-pr, qb = pr), so every workgroup does the same work (2 nqb + 2
+// tiles), the second block's K/V tiles are L2 hits, and the grid is halved.  Both blocks form
+// ONE LDS-DMA stream -- Q(qa), KV(0) .. KV(na-1), Q(qb), KV(0) .. KV(nb-1) -- each element one
+// ring slot (a Q element is the block's 128 query rows as two 64-row images, read into
+// registers by the waves at the block start), so the ring never drains at the seam and no
+// global load sits in front of the first MFMA.
+// Softmax: the row sum comes from the PV MFMAs (a constant all-ones A operand: every row of
+// that accumulator is sum_k P -- 4 more MFMAs per tile instead of 32 v_add), the half-wave max
+// combine is a v_permlane32_swap (no LDS round trip), masks are 32-bit compares of
+// compile-time key offsets.
+template <int HD, int OCC, bool LMFMA>
+__global__ __launch_bounds__(256, OCC) void attn_fwd2_kernel(AttnArgs p) {
+  using A = AT<HD>;
+  __shared__ __attribute__((aligned(16))) bf16_t smem[NSLOT * 2 * A::TILE];  // [slot][K|V] or [slot][Q lo|Q hi]
+  const int S = p.S, H = p.H;
+  const int nqb = (S + QB - 1) / QB;
+  const int npr = (nqb + 1) / 2;
+  int bh, pr;
+  xcd_work(npr, bh, pr);
+  const int n = bh / H, h = bh % H;
+  const int lane = threadIdx.x & 63, hh = lane >> 5;
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const long long tok0 = (long long)n * S;
+  const bf16_t* Qb = static_cast<const bf16_t*>(p.q) + tok0 * p.ld_qkv + h * HD;
+  const bf16_t* K = static_cast<const bf16_t*>(p.k) + tok0 * p.ld_qkv + h * HD;
+  const bf16_t* V = static_cast<const bf16_t*>(p.v) + tok0 * p.ld_qkv + h * HD;
+  const unsigned char* pad = p.pad ? p.pad + (long long)n * S : nullptr;
+  const int blk0 = nqb - 1 - pr, blk1 = pr;
+  auto ntiles_of = [&](int qb) {
+    const int kend = p.causal ? min(S, qb * QB + QB) : S;
+    return (kend + KT - 1) / KT;
+  };
+  const int len0 = 1 + ntiles_of(blk0);
+  const int len = len0 + (blk1 != blk0 ? 1 + ntiles_of(blk1) : 0);
+
+  int dv[A::NPW];
+  dma_voff<HD>(dv, p.ld_qkv, wid, lane);
+  auto issue = [&](int e) {
+    bf16_t* st = smem + (e % NSLOT) * 2 * A::TILE;
+    const bool second = e >= len0;
+    const int i = e - (second ? len0 : 0);
+    const bool valid = e < len;
+    if (i == 0 || !valid) {  // Q rows of the block (or an empty element past the end)
+      const int r0 = (second ? blk1 : blk0) * QB;
+      tile_dma<HD>(Qb, p.ld_qkv, r0, S, valid, dv, st, wid);
+      tile_dma<HD>(Qb, p.ld_qkv, r0 + KT, S, valid, dv, st + A::TILE, wid);
+    } else {
+      tile_dma<HD>(K, p.ld_qkv, (i - 1) * KT, S, true, dv, st, wid);
+      tile_dma<HD>(V, p.ld_qkv, (i - 1) * KT, S, true, dv, st + A::TILE, wid);
+    }
+  };
+
+  const float c = p.scale * LOG2E;
+  bf16x8 qf[A::NST];
+  float m = -INFINITY, l = 0.f;
+  constexpr int NO = A::NDT + (LMFMA ? 1 : 0);  // O^T blocks (+ the row-sum block)
+  floatx16 o[NO];
+  int q0 = 0, q = 0, last_w = 0, blk = blk0;
+  bf16x8 ones;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) ones[i] = (__bf16)1.0f;
+
+  auto qk = [&](floatx16 (&s)[2], const bf16_t* lk) {
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb) {
+      zero16(s[kb]);
+#pragma unroll
+      for (int st = 0; st < A::NST; ++st) s[kb] = MFMA32(row_frag<HD>(lk, kb * 32, st, lane), qf[st], s[kb]);
+    }
+  };
+  auto finish = [&]() {  // the block's O and lse
+    if constexpr (LMFMA) l = o[A::NDT][0];
+    else l += __shfl_xor(l, 32, 64);  // the two lane halves summed different key rows
+    if (q < S) {
+      const float inv = l > 0.f ? __builtin_amdgcn_rcpf(l) : 0.f;
+      // (the row offset is formed here, in 32 bits: a pointer held from the kernel start is
+      // spilled, and its reload's vmcnt(0) would drain the ring at the block seam)
+      bf16_t* O = static_cast<bf16_t*>(p.o) + tok0 * p.ld_o + h * HD + q * (int)p.ld_o;
+#pragma unroll
+      for (int d = 0; d < A::NDT; ++d)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const int col = d * 32 + 8 * g + 4 * hh;
+          uint2 w;
+          w.x = pack2bf(o[d][4 * g + 0] * inv, o[d][4 * g + 1] * inv);
+          w.y = pack2bf(o[d][4 * g + 2] * inv, o[d][4 * g + 3] * inv);
+          *reinterpret_cast<uint2*>(O + col) = w;
+        }
+      if (hh == 0) p.lse[(long long)bh * S + q] = (l > 0.f) ? (m + log2f(l)) / LOG2E : INFINITY;
+    }
+  };
+
+  issue(0);
+  issue(1);
+  issue(2);
+  // element e: (block start) read Q, S^T of KV(0) into sn;  (KV tile t) softmax of sc, S^T of
+  // KV(t+1) into sn if this wave needs it, O^T += V^T P^T.
+  auto step = [&](int e, floatx16 (&sc)[2], floatx16 (&sn)[2]) {
+    vm_wait<2 * A::NPW>();  // this wave's pieces of element e+1 landed (e+2 may fly)
+    ring_barrier();         // ... every wave's; every wave is done with element e-1's slot
+    issue(e + 3);
+    const bf16_t* ls = smem + (e % NSLOT) * 2 * A::TILE;
+    const bf16_t* lsn = smem + ((e + 1) % NSLOT) * 2 * A::TILE;
+    const bool second = e >= len0;
+    const int i = e - (second ? len0 : 0);
+    if (i == 0) {
+      if (second) finish();
+      blk = second ? blk1 : blk0;
+      q0 = blk * QB + wid * 32;
+      q = q0 + (lane & 31);
+      const int nt = ntiles_of(blk);
+      last_w = p.causal ? min(nt - 1, max(0, min(q0 + 31, S - 1)) / KT) : nt - 1;
+#pragma unroll
+      for (int st = 0; st < A::NST; ++st) qf[st] = row_frag<HD>(ls + (wid >> 1) * A::TILE, 32 * (wid & 1), st, lane);
+      m = -INFINITY;
+      l = 0.f;
+#pragma unroll
+      for (int d = 0; d < NO; ++d) zero16(o[d]);
+      qk(sn, lsn);
+      return;
+    }
+    const int t = i - 1;
+    if (t > last_w) return;  // wave-uniform
+    const bf16_t* lv = ls + A::TILE;
+    const int kt0 = t * KT;
+    const bool need_mask = (p.causal && kt0 + KT - 1 > q0) || (kt0 + KT > S) || pad;  // wave-uniform
+    if (need_mask) {
+      // key kb*32 + (r&3) + 8(r>>2) + 4 hh of the tile is masked if it is > lim (causal /
+      // past the end) or padded
+      const int limh = (p.causal ? min(q, S - 1) : S - 1) - kt0 - 4 * hh;
+      const unsigned long long pm = pad_bits(pad, kt0, S, lane) >> (4 * hh);
+#pragma unroll
+      for (int kb = 0; kb < 2; ++kb) {
+        const unsigned pk = (unsigned)(pm >> (32 * kb));
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int kc = kb * 32 + (r & 3) + 8 * (r >> 2);
+          const bool masked = (kc > limh) || ((pk >> ((r & 3) + 8 * (r >> 2))) & 1u);
+          if (masked) sc[kb][r] = -INFINITY;
+        }
+      }
+    }
+    float mx = max3f(sc[0][0], sc[0][1], sc[0][2]);
+#pragma unroll
+    for (int r = 3; r < 15; r += 2) mx = max3f(mx, sc[0][r], sc[0][r + 1]);
+    mx = max3f(mx, sc[0][15], sc[1][0]);
+#pragma unroll
+    for (int r = 1; r < 15; r += 2) mx = max3f(mx, sc[1][r], sc[1][r + 1]);
+    mx = fmaxf(mx, sc[1][15]);
+    {
+      const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(mx), __float_as_uint(mx), false, false);
+      mx = fmaxf(__uint_as_float(sw[0]), __uint_as_float(sw[1])) * c;  // scaled log2 units (c > 0)
+    }
+    // lazy rescale: the running max only moves when the tile max exceeds it by > 2^8
+    if (__ballot(mx > m + 8.f)) {
+      const float mn = fmaxf(m, mx);
+      const float alpha = (m == -INFINITY) ? 1.f : fast_exp2(m - mn);
+      m = mn;
+      if constexpr (!LMFMA) l *= alpha;
+#pragma unroll
+      for (int d = 0; d < NO; ++d)
+#pragma unroll
+        for (int k = 0; k < 16; ++k) o[d][k] *= alpha;
+    }
+    const float nmu = (m == -INFINITY) ? 0.f : -m;
+    if (t + 1 <= last_w) qk(sn, lsn);  // next tile's scores beside this tile's exponentials
+    float ls_ = 0.f;
+    bf16x8 pb[2][2];
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const float ex = fast_exp2(fmaf(sc[kb][r], c, nmu));
+        sc[kb][r] = ex;
+        if constexpr (!LMFMA) ls_ += ex;
+      }
+      pb[kb][0] = acc_frag(sc[kb], 0);
+      pb[kb][1] = acc_frag(sc[kb], 1);
+    }
+    if constexpr (!LMFMA) l += ls_;
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+      for (int ss = 0; ss < 2; ++ss) {
+#pragma unroll
+        for (int d = 0; d < A::NDT; ++d)
+          o[d] = MFMA32(tr_frag<HD>(lv, kb * 32, ss, d * 32, lane), pb[kb][ss], o[d]);
+        if constexpr (LMFMA) o[A::NDT] = MFMA32(ones, pb[kb][ss], o[A::NDT]);
+      }
+  };
+  floatx16 s0[2], s1[2];
+  for (int e = 0; e < len; e += 2) {
+    step(e, s0, s1);
+    if (e + 1 < len) step(e + 1, s1, s0);
+  }
+  finish();
+  vm_wait<0>();  // the pieces issued past the end (empty descriptors) drained
 }
 
 // ------------------------------------------------------------------ backward
@@ -792,11 +1014,31 @@ static int attn_var(int hd, int bwd) {
     default: hipLaunchKernelGGL((KERNEL<HD, false, 3>), __VA_ARGS__); break;                \
   }
 
+static int g_attn_abl = -1;
 template <int HD>
 static int launch_fwd(const AttnArgs* a, hipStream_t stream) {
   const int var = attn_var(HD, 0);
   dim3 grid((unsigned)(((a->S + QB - 1) / QB) * a->N * a->H));  // 1-D: xcd_work() maps it
-  if (var == 4) hipLaunchKernelGGL((attn_fwd_kernel<HD, 2, 2>), grid, dim3(256), 0, stream, *a);
+  if (g_attn_abl < 0) g_attn_abl = getenv("DPC_ATTN_ABL") ? atoi(getenv("DPC_ATTN_ABL")) : 0;
+  if (HD == 64 && g_attn_abl > 0) {  // ablation experiments (timing only; results are wrong)
+    switch (g_attn_abl) {
+      case 1: hipLaunchKernelGGL((attn_fwd_kernel<HD, 1, 2, 1>), grid, dim3(256), 0, stream, *a); break;
+      case 2: hipLaunchKernelGGL((attn_fwd_kernel<HD, 1, 2, 2>), grid, dim3(256), 0, stream, *a); break;
+      case 6: hipLaunchKernelGGL((attn_fwd_kernel<HD, 1, 2, 6>), grid, dim3(256), 0, stream, *a); break;
+      case 7: hipLaunchKernelGGL((attn_fwd_kernel<HD, 1, 2, 7>), grid, dim3(256), 0, stream, *a); break;
+      case 32: hipLaunchKernelGGL((attn_fwd_kernel<HD, 1, 2, 32>), grid, dim3(256), 0, stream, *a); break;
+      case 33: hipLaunchKernelGGL((attn_fwd_kernel<HD, 1, 2, 33>), grid, dim3(256), 0, stream, *a); break;
+      case 64: hipLaunchKernelGGL((attn_fwd_kernel<HD, 1, 2, 64>), grid, dim3(256), 0, stream, *a); break;
+      default: hipLaunchKernelGGL((attn_fwd_kernel<HD, 1, 2, 39>), grid, dim3(256), 0, stream, *a); break;
+    }
+    return (int)hipGetLastError();
+  }
+  if (var == 5 || var == 6) {  // pair stream (attn_fwd2_kernel)
+    const int nqb = (a->S + QB - 1) / QB;
+    dim3 g2((unsigned)(((nqb + 1) / 2) * a->N * a->H));
+    if (var == 5) hipLaunchKernelGGL((attn_fwd2_kernel<HD, 2, true>), g2, dim3(256), 0, stream, *a);
+    else hipLaunchKernelGGL((attn_fwd2_kernel<HD, 2, false>), g2, dim3(256), 0, stream, *a);
+  } else if (var == 4) hipLaunchKernelGGL((attn_fwd_kernel<HD, 2, 2>), grid, dim3(256), 0, stream, *a);
   else DPC_ATTN_SWITCH(var, attn_fwd_kernel, grid, dim3(256), 0, stream, *a);
   return (int)hipGetLastError();
 }
