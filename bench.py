@@ -62,7 +62,9 @@ def main():
     ap.add_argument("--num_microbatches", type=int, default=0)
     ap.add_argument("--schedule", default="1f1b", choices=["1f1b", "gpipe"])
     ap.add_argument("--dp_size", type=int, default=0)
-    ap.add_argument("--no_graph", action="store_true", help="eager steps (no HIP-graph capture at N=1)")
+    ap.add_argument("--no_graph", action="store_true", help="eager steps (no HIP-graph capture)")
+    ap.add_argument("--graph", action="store_true",
+                    help="HIP-graph capture also at N > 1 (default: only at N = 1)")
     ap.add_argument("--json", default=None, help="also write the result line to this file")
     a = ap.parse_args()
 
@@ -82,7 +84,11 @@ def main():
         argv += ["--schedule", a.schedule, "--num_microbatches", str(a.num_microbatches)]
     if rec == "pipe_ddp" and a.dp_size:
         argv += ["--dp_size", str(a.dp_size)]
-    if a.no_graph:
+    # N > 1 runs eager steps unless --graph: on one MI355X the graphed and the eager step take
+    # the same time at the default batch (profiles/r1_v19_eager_vs_graph: 77.2 vs 77.2 ms), and
+    # a step graph with RCCL collectives inside cannot be rehearsed on a one-GPU box (RCCL
+    # refuses two ranks per device), so the scaling runs take the path without the capture
+    if a.no_graph or (int(os.environ.get("WORLD_SIZE", "1")) > 1 and not a.graph):
         argv += ["--disable_compile"]
     args = build_parser(rec).parse_args(argv)
     apply_preset(args)

@@ -7,6 +7,7 @@ observation 2); here that difference is an ``Engine`` and the loop is shared
 from __future__ import annotations
 
 import torch
+import torch.distributed as dist
 
 
 class Engine:
@@ -110,17 +111,36 @@ class GraphedStep:
         for o in self.opts:
             o.device_step = True
         g = torch.cuda.CUDAGraph()
+        multi = dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1
         torch.cuda.synchronize()
+        if multi:
+            # nothing of the process group may still be in flight when the capture starts
+            dist.barrier()
+            torch.cuda.synchronize()
+        err = None
         try:
-            with torch.cuda.graph(g):
+            # thread_local: only this thread's calls are checked -- the process group's
+            # watchdog thread keeps querying its events while the capture runs
+            with torch.cuda.graph(g, capture_error_mode="thread_local" if multi else "global"):
                 b = {"input_ids": st["ids"], "position_ids": st["pos"], "mask": st["mask"]}
                 self.loss = body(b, st["tg"])
         except Exception as exc:  # capture not possible: stay eager
+            err = exc
+        if multi:
+            # every rank graphs or none does: a rank replaying while another runs eagerly
+            # would still issue the same collectives, but a failed capture may have left
+            # RCCL work half-recorded on one side only
+            flag = torch.tensor([0.0 if err is None else 1.0], device=self.engine.device)
+            dist.all_reduce(flag)
+            if err is None and float(flag.item()) > 0:
+                err = RuntimeError("capture failed on another rank")
+        if err is not None:
             for o in self.opts:
                 o.device_step = False
             self.enabled = False
+            self.graph = None
             if self.engine.is_logger:
-                print(f"[hip-graph] capture failed ({exc!r}); running eagerly")
+                print(f"[hip-graph] capture failed ({err!r}); running eagerly")
             torch.cuda.synchronize()
             return body(batch, targets)
         self.graph = g
