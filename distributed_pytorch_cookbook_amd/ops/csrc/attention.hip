@@ -221,6 +221,10 @@ __device__ __forceinline__ void zero16(floatx16& x) {
 // the bijective remap gives every XCD a contiguous run of ids, so all the q- (or key-) blocks
 // of one (batch, head) -- which read the same K/V (Q/dO) rows -- share one XCD's L2.
 // Returns (bh, i): i = block index within the head.
+__device__ __forceinline__ int g7_local_attn(int b, int grid) {
+  const int xcd = b & 7, q = grid >> 3, r = grid & 7;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (b >> 3);
+}
 __device__ __forceinline__ void xcd_work(int nblk, int& bh, int& i) {
   const int b = blockIdx.x, nwg = gridDim.x, xcd = b & 7, q = nwg >> 3, r = nwg & 7;
   const int t = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (b >> 3);
@@ -234,7 +238,7 @@ __device__ __forceinline__ void xcd_work(int nblk, int& bh, int& i) {
 // O^T += V^T P^T (4 x NDT MFMAs).
 // PIPE: 0 = plain order, 1 = next tile's S^T beside this tile's softmax, 2 = 1 + the tile's
 // LDS fragments read up front and the MFMA / VALU interleave pinned (sched_group_barrier)
-template <int HD, int PIPE, int OCC, int ABL = 0>
+template <int HD, int PIPE, int OCC>
 __global__ __launch_bounds__(256, OCC) void attn_fwd_kernel(AttnArgs p) {
   using A = AT<HD>;
   __shared__ __attribute__((aligned(16))) bf16_t smem[NSLOT * 2 * A::TILE];  // [slot][K|V]
@@ -279,7 +283,8 @@ __global__ __launch_bounds__(256, OCC) void attn_fwd_kernel(AttnArgs p) {
     for (int kb = 0; kb < 2; ++kb) {
       zero16(s[kb]);
 #pragma unroll
-      for (int st = 0; st < A::NST; ++st) s[kb] = MFMA32(row_frag<HD>(lk, kb * 32, st, lane), qf[st], s[kb]);
+      for (int st = 0; st < A::NST; ++st)
+        s[kb] = MFMA32(row_frag<HD>(lk, kb * 32, st, lane), qf[st], s[kb]);
     }
   };
 
@@ -295,9 +300,9 @@ __global__ __launch_bounds__(256, OCC) void attn_fwd_kernel(AttnArgs p) {
   ring_barrier();
   // one tile: scores of tile t in sc; the next tile's land in sn (ping-pong, no copies)
   auto step = [&](int t, floatx16 (&sc)[2], floatx16 (&sn)[2]) {
-    if constexpr (!(ABL & 2)) vm_wait<2 * A::NPW>();  // this wave's pieces of tile t+1 landed (t+2 may fly)
-    if constexpr (!(ABL & 4)) ring_barrier();         // ... every wave's; and every wave is done with tile t-1's slot
-    if constexpr (!(ABL & 2)) issue(t + 3);
+    vm_wait<2 * A::NPW>();  // this wave's pieces of tile t+1 landed (t+2 may fly)
+    ring_barrier();         // ... every wave's; and every wave is done with tile t-1's slot
+    issue(t + 3);
     const bf16_t* lkn = smem + ((t + 1) % NSLOT) * 2 * A::TILE;
     const bf16_t* lv = smem + (t % NSLOT) * 2 * A::TILE + A::TILE;
     if (t > last_w) return;  // wave-uniform
@@ -319,24 +324,7 @@ __global__ __launch_bounds__(256, OCC) void attn_fwd_kernel(AttnArgs p) {
     }
     const int kt0 = t * KT;
     // Scores stay raw (unscaled) until the exponent: p = 2^(s*c - m) is one FMA + v_exp.
-    const bool need_mask = !(ABL & 32) && ((p.causal && kt0 + KT - 1 > q0) || (kt0 + KT > S) || pad);  // wave-uniform
-    if constexpr (ABL & 1) {
-      if constexpr (PIPE == 1) qk(sn, lkn);
-      bf16x8 pb[2][2];
-#pragma unroll
-      for (int kb = 0; kb < 2; ++kb) {
-        pb[kb][0] = acc_frag(sc[kb], 0);
-        pb[kb][1] = acc_frag(sc[kb], 1);
-      }
-#pragma unroll
-      for (int kb = 0; kb < 2; ++kb)
-#pragma unroll
-        for (int ss = 0; ss < 2; ++ss)
-#pragma unroll
-          for (int d = 0; d < A::NDT; ++d)
-            o[d] = MFMA32(tr_frag<HD>(lv, kb * 32, ss, d * 32, lane), pb[kb][ss], o[d]);
-      return;
-    }
+    const bool need_mask = (p.causal && kt0 + KT - 1 > q0) || (kt0 + KT > S) || pad;  // wave-uniform
     if (need_mask) {
       // key > lim is causal / past-the-end, pm is the tile's padding bitmask
       const unsigned long long pm = pad_bits(pad, kt0, S, lane);
@@ -437,7 +425,7 @@ __global__ __launch_bounds__(256, OCC) void attn_fwd_kernel(AttnArgs p) {
   };
   floatx16 s0[2], s1[2];
   if constexpr (PIPE != 0) qk(s0, smem);
-  for (int t = 0; t < ((ABL & 64) ? 0 : ntiles); t += 2) {
+  for (int t = 0; t < ntiles; t += 2) {
     step(t, s0, s1);
     if (t + 1 < ntiles) step(t + 1, s1, s0);
   }
@@ -480,45 +468,73 @@ __global__ __launch_bounds__(256, OCC) void attn_fwd_kernel(AttnArgs p) {
 // that accumulator is sum_k P -- 4 more MFMAs per tile instead of 32 v_add), the half-wave max
 // combine is a v_permlane32_swap (no LDS round trip), masks are 32-bit compares of
 // compile-time key offsets.
+// Persistent form: a grid of at most two workgroups per CU walks the pair items (item i:
+// head bh = i / npr, pair pr = i % npr; workgroup b takes items local(b) + k * grid, where the
+// workgroups of one XCD hold a contiguous run of locals, so the items an XCD runs at once share
+// heads and K/V tiles in its L2) and the DMA stream runs on across items: the next item's Q
+// and first K/V tiles land while the current one finishes, and its O stores drain under the
+// next item's MFMAs.  (A grid of one workgroup per item is the non-persistent form.)
+struct PairItem {
+  int bh, blk0, blk1, len0, len;
+};
+
 template <int HD, int OCC, bool LMFMA>
-__global__ __launch_bounds__(256, OCC) void attn_fwd2_kernel(AttnArgs p) {
+__global__ __launch_bounds__(256, OCC) void attn_fwd2_kernel(AttnArgs p, int nitems) {
   using A = AT<HD>;
   __shared__ __attribute__((aligned(16))) bf16_t smem[NSLOT * 2 * A::TILE];  // [slot][K|V] or [slot][Q lo|Q hi]
   const int S = p.S, H = p.H;
   const int nqb = (S + QB - 1) / QB;
   const int npr = (nqb + 1) / 2;
-  int bh, pr;
-  xcd_work(npr, bh, pr);
-  const int n = bh / H, h = bh % H;
+  const int grid = gridDim.x;
+  const int local = g7_local_attn(blockIdx.x, grid);
   const int lane = threadIdx.x & 63, hh = lane >> 5;
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const long long tok0 = (long long)n * S;
-  const bf16_t* Qb = static_cast<const bf16_t*>(p.q) + tok0 * p.ld_qkv + h * HD;
-  const bf16_t* K = static_cast<const bf16_t*>(p.k) + tok0 * p.ld_qkv + h * HD;
-  const bf16_t* V = static_cast<const bf16_t*>(p.v) + tok0 * p.ld_qkv + h * HD;
-  const unsigned char* pad = p.pad ? p.pad + (long long)n * S : nullptr;
-  const int blk0 = nqb - 1 - pr, blk1 = pr;
   auto ntiles_of = [&](int qb) {
     const int kend = p.causal ? min(S, qb * QB + QB) : S;
     return (kend + KT - 1) / KT;
   };
-  const int len0 = 1 + ntiles_of(blk0);
-  const int len = len0 + (blk1 != blk0 ? 1 + ntiles_of(blk1) : 0);
+  auto item = [&](int k) {  // k-th item of this workgroup
+    PairItem it;
+    const int id = local + k * grid;
+    it.bh = id / npr;
+    const int pr = id - it.bh * npr;
+    it.blk0 = nqb - 1 - pr;
+    it.blk1 = pr;
+    it.len0 = 1 + ntiles_of(it.blk0);
+    it.len = it.len0 + (it.blk1 != it.blk0 ? 1 + ntiles_of(it.blk1) : 0);
+    return it;
+  };
+  const int nmine = local < nitems ? (nitems - local + grid - 1) / grid : 0;
+  if (nmine == 0) return;
+  int total = 0;
+  for (int k = 0; k < nmine; ++k) total += item(k).len;
 
   int dv[A::NPW];
   dma_voff<HD>(dv, p.ld_qkv, wid, lane);
-  auto issue = [&](int e) {
+  // ---- issue cursor: (item, offset), wave-uniform
+  int is_k = 0, is_off = 0;
+  PairItem is_it = item(0);
+  auto issue_next = [&](int e) {
     bf16_t* st = smem + (e % NSLOT) * 2 * A::TILE;
-    const bool second = e >= len0;
-    const int i = e - (second ? len0 : 0);
-    const bool valid = e < len;
+    const bool valid = is_k < nmine;
+    const int n = is_it.bh / H, h = is_it.bh - n * H;
+    const long long tok0 = (long long)n * S;
+    const bf16_t* base = static_cast<const bf16_t*>(p.q) + tok0 * p.ld_qkv + h * HD;
+    const bool second = is_off >= is_it.len0;
+    const int i = is_off - (second ? is_it.len0 : 0);
     if (i == 0 || !valid) {  // Q rows of the block (or an empty element past the end)
-      const int r0 = (second ? blk1 : blk0) * QB;
-      tile_dma<HD>(Qb, p.ld_qkv, r0, S, valid, dv, st, wid);
-      tile_dma<HD>(Qb, p.ld_qkv, r0 + KT, S, valid, dv, st + A::TILE, wid);
+      const int r0 = (second ? is_it.blk1 : is_it.blk0) * QB;
+      tile_dma<HD>(base, p.ld_qkv, r0, S, valid, dv, st, wid);
+      tile_dma<HD>(base, p.ld_qkv, r0 + KT, S, valid, dv, st + A::TILE, wid);
     } else {
+      const bf16_t* K = static_cast<const bf16_t*>(p.k) + tok0 * p.ld_qkv + h * HD;
+      const bf16_t* V = static_cast<const bf16_t*>(p.v) + tok0 * p.ld_qkv + h * HD;
       tile_dma<HD>(K, p.ld_qkv, (i - 1) * KT, S, true, dv, st, wid);
       tile_dma<HD>(V, p.ld_qkv, (i - 1) * KT, S, true, dv, st + A::TILE, wid);
+    }
+    if (valid && ++is_off == is_it.len) {
+      is_off = 0;
+      if (++is_k < nmine) is_it = item(is_k);
     }
   };
 
@@ -527,7 +543,12 @@ __global__ __launch_bounds__(256, OCC) void attn_fwd2_kernel(AttnArgs p) {
   float m = -INFINITY, l = 0.f;
   constexpr int NO = A::NDT + (LMFMA ? 1 : 0);  // O^T blocks (+ the row-sum block)
   floatx16 o[NO];
-  int q0 = 0, q = 0, last_w = 0, blk = blk0;
+  int q0 = 0, q = 0, last_w = 0;
+  // ---- consume cursor
+  int c_k = 0, c_off = 0;
+  PairItem c_it = is_it;
+  int bh = c_it.bh, h = 0, n = 0;
+  const unsigned char* pad = nullptr;
   bf16x8 ones;
 #pragma unroll
   for (int i = 0; i < 8; ++i) ones[i] = (__bf16)1.0f;
@@ -545,9 +566,9 @@ __global__ __launch_bounds__(256, OCC) void attn_fwd2_kernel(AttnArgs p) {
     else l += __shfl_xor(l, 32, 64);  // the two lane halves summed different key rows
     if (q < S) {
       const float inv = l > 0.f ? __builtin_amdgcn_rcpf(l) : 0.f;
-      // (the row offset is formed here, in 32 bits: a pointer held from the kernel start is
-      // spilled, and its reload's vmcnt(0) would drain the ring at the block seam)
-      bf16_t* O = static_cast<bf16_t*>(p.o) + tok0 * p.ld_o + h * HD + q * (int)p.ld_o;
+      // (the row offset is formed here, in 32 bits: a pointer held across the loop is
+      // spilled, and its reload's vmcnt(0) would drain the ring)
+      bf16_t* O = static_cast<bf16_t*>(p.o) + (long long)n * S * p.ld_o + h * HD + q * (int)p.ld_o;
 #pragma unroll
       for (int d = 0; d < A::NDT; ++d)
 #pragma unroll
@@ -562,25 +583,36 @@ __global__ __launch_bounds__(256, OCC) void attn_fwd2_kernel(AttnArgs p) {
     }
   };
 
-  issue(0);
-  issue(1);
-  issue(2);
+  issue_next(0);
+  issue_next(1);
+  issue_next(2);
   // element e: (block start) read Q, S^T of KV(0) into sn;  (KV tile t) softmax of sc, S^T of
   // KV(t+1) into sn if this wave needs it, O^T += V^T P^T.
   auto step = [&](int e, floatx16 (&sc)[2], floatx16 (&sn)[2]) {
     vm_wait<2 * A::NPW>();  // this wave's pieces of element e+1 landed (e+2 may fly)
     ring_barrier();         // ... every wave's; every wave is done with element e-1's slot
-    issue(e + 3);
+    issue_next(e + 3);
     const bf16_t* ls = smem + (e % NSLOT) * 2 * A::TILE;
     const bf16_t* lsn = smem + ((e + 1) % NSLOT) * 2 * A::TILE;
-    const bool second = e >= len0;
-    const int i = e - (second ? len0 : 0);
-    if (i == 0) {
-      if (second) finish();
-      blk = second ? blk1 : blk0;
-      q0 = blk * QB + wid * 32;
+    const PairItem cur = c_it;
+    const bool second = c_off >= cur.len0;
+    const int i = c_off - (second ? cur.len0 : 0);
+    const int t = i - 1;
+    if (++c_off == cur.len) {  // advance the consume cursor
+      c_off = 0;
+      if (++c_k < nmine) c_it = item(c_k);
+    }
+    if (i == 0) {  // a block starts: the previous one's O, then this one's Q and first scores
+      if (e > 0) finish();
+      if (!second) {  // ... of a new item
+        bh = cur.bh;
+        n = bh / H;
+        h = bh - n * H;
+        pad = p.pad ? p.pad + (long long)n * S : nullptr;
+      }
+      q0 = (second ? cur.blk1 : cur.blk0) * QB + wid * 32;
       q = q0 + (lane & 31);
-      const int nt = ntiles_of(blk);
+      const int nt = ntiles_of(second ? cur.blk1 : cur.blk0);
       last_w = p.causal ? min(nt - 1, max(0, min(q0 + 31, S - 1)) / KT) : nt - 1;
 #pragma unroll
       for (int st = 0; st < A::NST; ++st) qf[st] = row_frag<HD>(ls + (wid >> 1) * A::TILE, 32 * (wid & 1), st, lane);
@@ -591,7 +623,6 @@ __global__ __launch_bounds__(256, OCC) void attn_fwd2_kernel(AttnArgs p) {
       qk(sn, lsn);
       return;
     }
-    const int t = i - 1;
     if (t > last_w) return;  // wave-uniform
     const bf16_t* lv = ls + A::TILE;
     const int kt0 = t * KT;
@@ -661,9 +692,9 @@ __global__ __launch_bounds__(256, OCC) void attn_fwd2_kernel(AttnArgs p) {
       }
   };
   floatx16 s0[2], s1[2];
-  for (int e = 0; e < len; e += 2) {
+  for (int e = 0; e < total; e += 2) {
     step(e, s0, s1);
-    if (e + 1 < len) step(e + 1, s1, s0);
+    if (e + 1 < total) step(e + 1, s1, s0);
   }
   finish();
   vm_wait<0>();  // the pieces issued past the end (empty descriptors) drained
@@ -992,9 +1023,11 @@ __global__ __launch_bounds__(256, OCC) void attn_bwd_dq_kernel(AttnArgs p) {
 
 // kernel variant (env DPC_ATTN_VAR="<fwd>,<bwd>", measured on MI355X: bench/attn_one.py):
 // 0 = software-pipelined, 2 workgroups / CU; 1 = plain order, 2 / CU; 2 = plain, 3 / CU;
-// 3 = pipelined, 3 / CU; 4 (forward only) = pipelined + fragments up front + pinned interleave
+// 3 = pipelined, 3 / CU; 4 (forward only) = pipelined + fragments up front + pinned interleave;
+// forward only: 5 / 6 = pair stream (attn_fwd2_kernel) with / without the MFMA row sum,
+// 7 / 8 = the same on a persistent grid.
 // Defaults per head size (GPT-2 small shape, B=64 S=1023 H=12, profiles/r2_attn/):
-//   hd 64: forward 0, backward 1;  hd 32: forward 2, backward 2.
+//   hd 64: forward 6, backward 1;  hd 32: forward 2, backward 2.
 static int g_attn_env[2] = {-2, -2};
 static int attn_var(int hd, int bwd) {
   if (g_attn_env[0] == -2) {
@@ -1003,7 +1036,7 @@ static int attn_var(int hd, int bwd) {
   }
   if (g_attn_env[bwd] >= 0) return g_attn_env[bwd];
   if (hd == 32) return 2;
-  return bwd ? 1 : 0;
+  return bwd ? 1 : 6;
 }
 
 #define DPC_ATTN_SWITCH(var, KERNEL, ...)                                                   \
@@ -1014,30 +1047,16 @@ static int attn_var(int hd, int bwd) {
     default: hipLaunchKernelGGL((KERNEL<HD, false, 3>), __VA_ARGS__); break;                \
   }
 
-static int g_attn_abl = -1;
 template <int HD>
 static int launch_fwd(const AttnArgs* a, hipStream_t stream) {
   const int var = attn_var(HD, 0);
   dim3 grid((unsigned)(((a->S + QB - 1) / QB) * a->N * a->H));  // 1-D: xcd_work() maps it
-  if (g_attn_abl < 0) g_attn_abl = getenv("DPC_ATTN_ABL") ? atoi(getenv("DPC_ATTN_ABL")) : 0;
-  if (HD == 64 && g_attn_abl > 0) {  // ablation experiments (timing only; results are wrong)
-    switch (g_attn_abl) {
-      case 1: hipLaunchKernelGGL((attn_fwd_kernel<HD, 1, 2, 1>), grid, dim3(256), 0, stream, *a); break;
-      case 2: hipLaunchKernelGGL((attn_fwd_kernel<HD, 1, 2, 2>), grid, dim3(256), 0, stream, *a); break;
-      case 6: hipLaunchKernelGGL((attn_fwd_kernel<HD, 1, 2, 6>), grid, dim3(256), 0, stream, *a); break;
-      case 7: hipLaunchKernelGGL((attn_fwd_kernel<HD, 1, 2, 7>), grid, dim3(256), 0, stream, *a); break;
-      case 32: hipLaunchKernelGGL((attn_fwd_kernel<HD, 1, 2, 32>), grid, dim3(256), 0, stream, *a); break;
-      case 33: hipLaunchKernelGGL((attn_fwd_kernel<HD, 1, 2, 33>), grid, dim3(256), 0, stream, *a); break;
-      case 64: hipLaunchKernelGGL((attn_fwd_kernel<HD, 1, 2, 64>), grid, dim3(256), 0, stream, *a); break;
-      default: hipLaunchKernelGGL((attn_fwd_kernel<HD, 1, 2, 39>), grid, dim3(256), 0, stream, *a); break;
-    }
-    return (int)hipGetLastError();
-  }
-  if (var == 5 || var == 6) {  // pair stream (attn_fwd2_kernel)
+  if (var >= 5 && var <= 8) {  // pair stream (attn_fwd2_kernel); 7, 8: persistent grid
     const int nqb = (a->S + QB - 1) / QB;
-    dim3 g2((unsigned)(((nqb + 1) / 2) * a->N * a->H));
-    if (var == 5) hipLaunchKernelGGL((attn_fwd2_kernel<HD, 2, true>), g2, dim3(256), 0, stream, *a);
-    else hipLaunchKernelGGL((attn_fwd2_kernel<HD, 2, false>), g2, dim3(256), 0, stream, *a);
+    const int nitems = ((nqb + 1) / 2) * a->N * a->H;
+    dim3 g2((unsigned)((var >= 7 && nitems > 512) ? 512 : nitems));
+    if (var == 5 || var == 8) hipLaunchKernelGGL((attn_fwd2_kernel<HD, 2, true>), g2, dim3(256), 0, stream, *a, nitems);
+    else hipLaunchKernelGGL((attn_fwd2_kernel<HD, 2, false>), g2, dim3(256), 0, stream, *a, nitems);
   } else if (var == 4) hipLaunchKernelGGL((attn_fwd_kernel<HD, 2, 2>), grid, dim3(256), 0, stream, *a);
   else DPC_ATTN_SWITCH(var, attn_fwd_kernel, grid, dim3(256), 0, stream, *a);
   return (int)hipGetLastError();
