@@ -22,6 +22,7 @@ ap.add_argument("--K", type=int, default=768)
 ap.add_argument("--layout", default="nt", choices=["nt", "nn", "tn"])
 ap.add_argument("--impl", type=int, default=-1)
 ap.add_argument("--iters", type=int, default=50)
+ap.add_argument("--splits", type=int, default=0, help="force the split-K count (0: automatic)")
 a = ap.parse_args()
 M, N, K = a.M, a.N, a.K
 r = lambda *s: torch.randn(*s, device="cuda").bfloat16()  # noqa: E731
@@ -32,6 +33,7 @@ elif a.layout == "nn":
 else:
     A, B, kw = r(K, M), r(K, N), dict(a_kmaj=False, b_kmaj=False)
 _lib.set_gemm_impl(a.impl)
+_lib.set_gemm_splits(a.splits)
 out = torch.empty(M, N, device="cuda", dtype=torch.float32 if a.layout == "tn" else torch.bfloat16)
 for _ in range(3):
     gemm(A, B, out=out, **kw)
@@ -43,4 +45,4 @@ for _ in range(a.iters):
 e.record()
 torch.cuda.synchronize()
 ms = s.elapsed_time(e) / a.iters
-print(f"{a.layout} M={M} N={N} K={K} impl={a.impl}: {ms*1e3:.1f} us  {2*M*N*K/ms/1e9:.1f} TF/s")
+print(f"{a.layout} M={M} N={N} K={K} impl={a.impl} splits={a.splits}: {ms*1e3:.1f} us  {2*M*N*K/ms/1e9:.1f} TF/s")

@@ -68,6 +68,16 @@ def build_parser(recipe: str = "single") -> argparse.ArgumentParser:
     p.add_argument("--profile", type=str, default=None, help="write a torch.profiler trace here")
     p.add_argument("--log_jsonl", type=str, default=None, help="append step metrics as JSON lines")
     p.add_argument("--cpu", action="store_true", help="force CPU (gloo) even if a GPU is present")
+    # --- debug switches
+    p.add_argument("--serialize_kernels", action="store_true",
+                   help="serialise every HIP launch / copy and synchronise after each native kernel, "
+                        "so a faulting kernel is named at its launch (DPC_SERIALIZE=1)")
+    p.add_argument("--stream_check", action="store_true",
+                   help="assert that every asynchronous collective is waited on before the step ends and "
+                        "poll RCCL for asynchronous errors (DPC_STREAM_CHECK=1)")
+    p.add_argument("--coll_check", action="store_true",
+                   help="all-gather a (sequence, op, shape, dtype) fingerprint before each collective and "
+                        "raise on a mismatch across ranks (DPC_COLL_CHECK=1)")
     if recipe in ("pipe", "pipe_ddp"):
         p.add_argument("--pp_size", type=int, default=0, help="pipeline stages (0 = world size / dp)")
         p.add_argument("--num_microbatches", type=int, default=0, help="0 = 4 x stages (1 for a single stage)")

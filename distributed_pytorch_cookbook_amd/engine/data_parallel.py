@@ -17,6 +17,7 @@ from ..ops.optim import FlatAdamW
 from ..parallel import comm
 from ..parallel.ddp import DDPStore
 from ..parallel.store import LocalStore
+from ..parallel.transport import check_drained
 from .base import Engine, GraphedStep
 
 
@@ -84,9 +85,9 @@ class DataParallelEngine(Engine):
         return out.loss.detach()
 
     def train_step(self, batch, targets):
-        if not self.graph:
-            return self._step_body(batch, targets)
-        return self._stepper(self._step_body, batch, targets)
+        out = self._stepper(self._step_body, batch, targets) if self.graph else self._step_body(batch, targets)
+        check_drained(f"the end of a {self.name} step")  # --stream_check
+        return out
 
     @torch.no_grad()
     def eval_step(self, batch, targets):

@@ -15,6 +15,7 @@ import torch
 from ..ops.optim import FlatAdamW
 from ..parallel import comm
 from ..parallel.fsdp import FSDPStore
+from ..parallel.transport import check_drained
 from .base import Engine, GraphedStep
 
 # A/B switch (bench/offload.py): the synchronous offload step (D2H, host AdamW, H2D in turn)
@@ -53,9 +54,9 @@ class FSDPEngine(Engine):
         self._stepper = GraphedStep(self, [self.opt, self.opt_rep])
 
     def train_step(self, batch, targets):
-        if self.graph:
-            return self._stepper(self._step_body, batch, targets)
-        return self._step_body(batch, targets)
+        out = self._stepper(self._step_body, batch, targets) if self.graph else self._step_body(batch, targets)
+        check_drained(f"the end of a {self.name} step")  # --stream_check
+        return out
 
     def _step_body(self, batch, targets):
         st = self.store

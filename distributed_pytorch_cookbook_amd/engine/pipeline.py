@@ -28,6 +28,7 @@ from ..parallel.fsdp import _placeholder
 from ..parallel.pipeline import P2P, partition, run_schedule, schedule_1f1b, schedule_gpipe, unit_costs
 from ..parallel.store import LocalStore
 from ..parallel.transport import TorchTransport, make_mesh_transports
+from ..parallel.transport import check_drained
 from .base import Engine, GraphedStep
 
 
@@ -139,9 +140,9 @@ class PipelineEngine(Engine):
 
     # ------------------------------------------------------------------ training
     def train_step(self, batch, targets):
-        if self.graph:
-            return self._stepper(self._step_body, batch, targets)
-        return self._step_body(batch, targets)
+        out = self._stepper(self._step_body, batch, targets) if self.graph else self._step_body(batch, targets)
+        check_drained(f"the end of a {self.name} step")  # --stream_check
+        return out
 
     def _step_body(self, batch, targets):
         st = self.store

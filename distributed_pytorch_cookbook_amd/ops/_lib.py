@@ -11,6 +11,7 @@ if that fails the error propagates -- there is no silent fallback to torch ops.
 from __future__ import annotations
 
 import ctypes
+import os
 import threading
 from ctypes import c_float, c_int, c_longlong, c_uint, c_void_p
 
@@ -224,10 +225,31 @@ def stream_ptr(device: torch.device | None = None) -> int:
     return torch.cuda.current_stream(device).cuda_stream
 
 
+# SURVEY.md §5.2 serialize switch (``--serialize_kernels`` / DPC_SERIALIZE=1): the HIP runtime
+# serialises every launch and copy (AMD_SERIALIZE_KERNEL / AMD_SERIALIZE_COPY / HIP_LAUNCH_BLOCKING,
+# which must be in the environment before the runtime starts -- ``enable_serialize``), and
+# every native launch is followed by a stream synchronize, so a faulting kernel is reported
+# by name at its own launch instead of at a later synchronisation point.
+SERIALIZE = os.environ.get("DPC_SERIALIZE", "0") == "1"
+
+
+def enable_serialize() -> None:
+    global SERIALIZE
+    SERIALIZE = True
+    os.environ["DPC_SERIALIZE"] = "1"
+    for k, v in (("AMD_SERIALIZE_KERNEL", "3"), ("AMD_SERIALIZE_COPY", "3"), ("HIP_LAUNCH_BLOCKING", "1")):
+        os.environ.setdefault(k, v)
+
+
 def call(name: str, args: ctypes.Structure, device: torch.device | None = None) -> None:
     rc = getattr(lib(), name)(ctypes.byref(args), stream_ptr(device))
     if rc != 0:
         raise RuntimeError(f"{name} launch failed: hipError {rc}")
+    if SERIALIZE and not torch.cuda.is_current_stream_capturing():
+        try:
+            torch.cuda.current_stream(device).synchronize()
+        except RuntimeError as exc:  # the fault of THIS launch
+            raise RuntimeError(f"{name} failed on the device: {exc}") from exc
 
 
 def ptr(t: torch.Tensor | None) -> int | None:

@@ -95,6 +95,11 @@ _CHECK = os.environ.get("DPC_COLL_CHECK", "0") == "1"
 _seq = {}
 
 
+def set_coll_check(on: bool) -> None:
+    global _CHECK
+    _CHECK = bool(on)
+
+
 def _fingerprint(op: str, t: torch.Tensor | None, group) -> None:
     if not _CHECK or not dist.is_initialized():
         return

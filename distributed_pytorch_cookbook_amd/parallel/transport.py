@@ -30,8 +30,54 @@ import torch.distributed as dist
 from . import comm
 
 
+# ---------------------------------------------------------------- stream-order checks
+# with DPC_STREAM_CHECK=1 (``--stream_check``) every asynchronous collective
+# handle is registered when it is issued and struck off when a stream is ordered after it
+# (``Handle.wait``); ``check_drained`` -- called by every engine at the end of its step --
+# raises, naming the collectives, if any was never waited on (a consumer could have read its
+# buffer before the collective finished), and polls each native communicator for an RCCL
+# asynchronous error.  Buffers handed to the comm stream must be contiguous and on the
+# transport's device; each is ``record_stream``-ed so the caching allocator cannot recycle
+# it under the collective.
+_STREAM_CHECK = os.environ.get("DPC_STREAM_CHECK", "0") == "1"
+_outstanding: dict = {}
+_native_comms: list = []
+
+
+def set_stream_check(on: bool) -> None:
+    global _STREAM_CHECK
+    _STREAM_CHECK = bool(on)
+    _outstanding.clear()
+
+
+def stream_check_enabled() -> bool:
+    return _STREAM_CHECK
+
+
+def check_drained(where: str = "end of step") -> None:
+    """Raise if a collective issued with ``async_op=True`` was never waited on."""
+    if not _STREAM_CHECK:
+        return
+    for nc in _native_comms:
+        nc.check_async()
+    if _outstanding:
+        pending = sorted(_outstanding.values())
+        _outstanding.clear()
+        raise RuntimeError(f"stream-order check: {len(pending)} collective(s) never waited on before "
+                           f"{where}: {pending[:8]}")
+
+
 class Handle:
     """Completion of an asynchronous collective."""
+
+    def _track(self, desc: str) -> "Handle":
+        if _STREAM_CHECK:
+            _outstanding[id(self)] = desc
+        return self
+
+    def _untrack(self) -> None:
+        if _outstanding:
+            _outstanding.pop(id(self), None)
 
     def wait(self) -> None:  # pragma: no cover - interface
         raise NotImplementedError
@@ -50,6 +96,7 @@ class _EventHandle(Handle):
         self.event = event
 
     def wait(self) -> None:
+        self._untrack()
         torch.cuda.current_stream().wait_event(self.event)
 
 
@@ -59,12 +106,18 @@ class _WorkHandle(Handle):
         self.after = after
 
     def wait(self) -> None:
+        self._untrack()
         for w in self.works:
             if w is not None:
                 w.wait()
         if self.after is not None:
             self.after()
             self.after = None
+
+
+def _desc(op: str, tensors) -> str:
+    t = next((x for x in tensors if x is not None), None)
+    return f"{op}{tuple(t.shape) if t is not None else ()}"
 
 
 class Transport:
@@ -118,9 +171,9 @@ class TorchTransport(Transport):
         # ranks on one device) stages point-to-point payloads through the host
         self.host_staged = dist.is_initialized() and dist.get_backend(group) == "gloo"
 
-    def _ret(self, work, async_op):
+    def _ret(self, work, async_op, desc="collective"):
         if async_op:
-            return _WorkHandle(work)
+            return _WorkHandle(work)._track(desc)
         if work is not None:
             work.wait()
         return _Done()
@@ -128,25 +181,28 @@ class TorchTransport(Transport):
     def all_reduce(self, t, async_op=False):
         if self.size == 1:
             return _Done()
-        return self._ret(comm.all_reduce(t, group=self.group, async_op=async_op), async_op)
+        return self._ret(comm.all_reduce(t, group=self.group, async_op=async_op), async_op,
+                         _desc("all_reduce", (t,)))
 
     def reduce_scatter(self, out, inp, async_op=False):
         if self.size == 1:
             out.copy_(inp)
             return _Done()
-        return self._ret(comm.reduce_scatter_into(out, inp, group=self.group, async_op=async_op), async_op)
+        return self._ret(comm.reduce_scatter_into(out, inp, group=self.group, async_op=async_op), async_op,
+                         _desc("reduce_scatter", (out,)))
 
     def all_gather(self, out, inp, async_op=False):
         if self.size == 1:
             out.copy_(inp)
             return _Done()
-        return self._ret(comm.all_gather_into(out, inp, group=self.group, async_op=async_op), async_op)
+        return self._ret(comm.all_gather_into(out, inp, group=self.group, async_op=async_op), async_op,
+                         _desc("all_gather", (out,)))
 
     def broadcast(self, t, src, async_op=False):
         if self.size == 1:
             return _Done()
         return self._ret(comm.broadcast(t, src=self.global_rank(src), group=self.group, async_op=async_op),
-                         async_op)
+                         async_op, _desc("broadcast", (t,)))
 
     def sendrecv(self, sends=(), recvs=(), async_op=False):
         if not sends and not recvs:
@@ -168,7 +224,8 @@ class TorchTransport(Transport):
             for dst, src in staged:
                 dst.copy_(src)
 
-        h = _WorkHandle(works, after=unstage if staged else None)
+        h = _WorkHandle(works, after=unstage if staged else None)._track(
+            _desc("sendrecv", [t for t, _ in sends] + [t for t, _ in recvs]))
         if not async_op:
             h.wait()
             return _Done()
@@ -185,6 +242,7 @@ class NativeTransport(Transport):
         self.device = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
         self.nc = native if native is not None else NativeComm(group, device=self.device)
         self.rank, self.size = self.nc.rank, self.nc.size
+        _native_comms.append(self.nc)
         # RCCL runs on its own high-priority stream, ordered with events
         self.stream = torch.cuda.Stream(device=self.device, priority=-1)
 
@@ -195,7 +253,12 @@ class NativeTransport(Transport):
     def active(self) -> bool:
         return True
 
-    def _enqueue(self, fn, tensors, async_op):
+    def _enqueue(self, fn, tensors, async_op, op="collective"):
+        if _STREAM_CHECK:
+            for t in tensors:
+                if not t.is_contiguous() or t.device != self.device:
+                    raise RuntimeError(f"stream-order check: {op} buffer {tuple(t.shape)} on {t.device} "
+                                       f"(contiguous={t.is_contiguous()}) handed to the comm stream of {self.device}")
         cur = torch.cuda.current_stream(self.device)
         s = self.stream
         s.wait_stream(cur)
@@ -205,23 +268,25 @@ class NativeTransport(Transport):
             t.record_stream(s)
         done = torch.cuda.Event()
         done.record(s)
-        h = _EventHandle(done)
+        h = _EventHandle(done)._track(_desc(op, tensors))
         if not async_op:
             h.wait()
             return _Done()
         return h
 
     def all_reduce(self, t, async_op=False):
-        return self._enqueue(lambda s: self.nc.all_reduce(t, stream=s), (t,), async_op)
+        return self._enqueue(lambda s: self.nc.all_reduce(t, stream=s), (t,), async_op, "all_reduce")
 
     def reduce_scatter(self, out, inp, async_op=False):
-        return self._enqueue(lambda s: self.nc.reduce_scatter(out, inp, stream=s), (out, inp), async_op)
+        return self._enqueue(lambda s: self.nc.reduce_scatter(out, inp, stream=s), (out, inp), async_op,
+                             "reduce_scatter")
 
     def all_gather(self, out, inp, async_op=False):
-        return self._enqueue(lambda s: self.nc.all_gather(out, inp, stream=s), (out, inp), async_op)
+        return self._enqueue(lambda s: self.nc.all_gather(out, inp, stream=s), (out, inp), async_op,
+                             "all_gather")
 
     def broadcast(self, t, src, async_op=False):
-        return self._enqueue(lambda s: self.nc.broadcast(t, src=src, stream=s), (t,), async_op)
+        return self._enqueue(lambda s: self.nc.broadcast(t, src=src, stream=s), (t,), async_op, "broadcast")
 
     def sendrecv(self, sends=(), recvs=(), async_op=False):
         if not sends and not recvs:
@@ -235,7 +300,7 @@ class NativeTransport(Transport):
                 for t, p in recvs:
                     self.nc.recv(t, p, stream=s)
 
-        return self._enqueue(run, [t for t, _ in sends] + [t for t, _ in recvs], async_op)
+        return self._enqueue(run, [t for t, _ in sends] + [t for t, _ in recvs], async_op, "sendrecv")
 
     def split(self, color: int, key: int, group=None) -> "NativeTransport":
         """Sub-communicator (ncclCommSplit) of the ranks sharing ``color``; ``group`` is the

@@ -81,8 +81,24 @@ def build_engine(recipe: str, model, info, args):
     raise ValueError(recipe)
 
 
+def apply_debug_switches(args) -> None:
+    """SURVEY.md §5.2 switches: serialised launches, stream-order checks, collective
+    fingerprints."""
+    if getattr(args, "serialize_kernels", False):
+        from .ops import _lib
+
+        _lib.enable_serialize()
+    if getattr(args, "stream_check", False):
+        from .parallel import transport
+
+        transport.set_stream_check(True)
+    if getattr(args, "coll_check", False):
+        comm.set_coll_check(True)
+
+
 def run(recipe: str, argv=None):
     args = parse("pipe_ddp" if recipe == "pipe_ddp" else recipe, argv)
+    apply_debug_switches(args)  # before the HIP runtime starts (init_dist binds the device)
     info = comm.init_dist(force_cpu=args.cpu)
     if recipe == "single" and info.world_size > 1:
         raise SystemExit("main-single.py runs one process; use main-ddp.py under torchrun")

@@ -163,3 +163,41 @@ def worker_fsdp_mem(rank, world, out):
         res[prefetch] = eng.store.peak_live_units
     if rank == 0:
         torch.save(res, out)
+
+
+def worker_stream_check(rank, world, out, kind):
+    """--stream_check: every engine's step leaves no collective un-waited, and
+    an async collective nobody waits on is reported at the end of the step."""
+    from distributed_pytorch_cookbook_amd.parallel import comm, transport
+
+    comm.init_dist(force_cpu=True)
+    transport.set_stream_check(True)
+    m = make_model()
+    if kind == "ddp":
+        from distributed_pytorch_cookbook_amd.engine.data_parallel import DataParallelEngine
+
+        eng = DataParallelEngine(m, "cpu", lr=LR, bucket_mb=0.05)
+    elif kind == "fsdp":
+        from distributed_pytorch_cookbook_amd.engine.fsdp import FSDPEngine
+
+        eng = FSDPEngine(m, "cpu", lr=LR, prefetch=1)
+    else:
+        from distributed_pytorch_cookbook_amd.engine.pipeline import PipelineEngine
+
+        eng = PipelineEngine(m, "cpu", lr=LR, pp=world, dp=1, num_microbatches=4, schedule="1f1b",
+                             bucket_mb=0.01, seq_len=S)
+    for s in range(2):
+        b, t = full_batch(step=s) if kind == "pipe" else shard(*full_batch(step=s), rank, world)
+        eng.train_step(b, t)  # raises if the engine left a collective un-waited
+    tp = transport.TorchTransport()
+    x = torch.ones(4)
+    h = tp.all_reduce(x, async_op=True)
+    caught = False
+    try:
+        transport.check_drained("the test's end")
+    except RuntimeError as exc:
+        caught = "all_reduce(4,)" in str(exc)
+    h.wait()  # (the collective itself still completes on every rank)
+    transport.check_drained("after the wait")  # nothing outstanding now
+    if rank == 0:
+        torch.save({"caught": caught}, out)

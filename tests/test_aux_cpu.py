@@ -66,3 +66,27 @@ def test_resume_mid_epoch_matches_uninterrupted(tmp_path):
     w_res = resumed.engine.lm().state_dict()
     for k, v in w_full.items():
         assert torch.equal(v, w_res[k]), k
+
+
+def test_debug_switches_set_runtime_env(monkeypatch):
+    """--serialize_kernels sets the HIP serialisation switches (before the
+    runtime starts) and turns on per-launch synchronisation; --stream_check / --coll_check
+    arm the transport and collective checks."""
+    from distributed_pytorch_cookbook_amd import recipes
+    from distributed_pytorch_cookbook_amd.config import parse
+    from distributed_pytorch_cookbook_amd.ops import _lib
+    from distributed_pytorch_cookbook_amd.parallel import comm, transport
+
+    for k in ("AMD_SERIALIZE_KERNEL", "AMD_SERIALIZE_COPY", "HIP_LAUNCH_BLOCKING", "DPC_SERIALIZE"):
+        monkeypatch.delenv(k, raising=False)
+    monkeypatch.setattr(_lib, "SERIALIZE", False)
+    args = parse("ddp", ["--serialize_kernels", "--stream_check", "--coll_check"])
+    try:
+        recipes.apply_debug_switches(args)
+        import os
+
+        assert os.environ["AMD_SERIALIZE_KERNEL"] == "3" and os.environ["HIP_LAUNCH_BLOCKING"] == "1"
+        assert _lib.SERIALIZE and transport.stream_check_enabled() and comm._CHECK
+    finally:
+        transport.set_stream_check(False)
+        comm.set_coll_check(False)

@@ -162,3 +162,14 @@ def test_fsdp_memory_bounded(tmp_path):
     r = torch.load(out, weights_only=True)
     for prefetch, peak in r.items():
         assert peak <= prefetch + 2, (prefetch, peak)
+
+
+@pytest.mark.parametrize("kind", ["ddp", "fsdp", "pipe"])
+def test_stream_check_engines_and_unwaited_collective(tmp_path, kind):
+    """with the stream-order check on, DDP / FSDP / pipeline steps leave no
+    asynchronous collective un-waited, and one that is never waited on is reported."""
+    from dist_workers import worker_stream_check
+
+    out = tmp_path / "sc.pt"
+    run_workers(worker_stream_check, 2, str(out), kind)
+    assert torch.load(out, weights_only=True)["caught"]
