@@ -35,6 +35,11 @@ struct GemmArgs {
   int impl;
   // gemm_f32.hip only: aux_in / aux_out are f32 (else bf16)
   int aux_f32;
+  // split-K workspace (optional, f32, ws_bytes long): the v7 kernel stores each k-range's
+  // partial tile there with plain stores and a reduction pass sums them into C, instead of
+  // f32 atomics into C (gemm7.hip: dpc_gemm7)
+  void* ws;
+  long long ws_bytes;
 };
 
 constexpr int BM = 128, BN = 128, BKT = 64, NT = 256;

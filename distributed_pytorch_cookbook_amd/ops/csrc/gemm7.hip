@@ -33,6 +33,7 @@
 // Reference: every nn.Linear of /root/reference/models/gpt.py:29-30,60-64,219.
 #include "gemm.h"
 
+#include <algorithm>
 #include <cstdlib>
 #include <utility>
 
@@ -320,7 +321,8 @@ __device__ __forceinline__ void g7_epilogue_atomic(const GemmArgs& p, floatx4 (&
 }
 
 // EPI: 0 = plain products (bf16 / f32 C), 1 = forward fused epilogues, 2 = split-K f32 atomics,
-// 3 = input-gradient fused epilogues (act', column sums).
+// 3 = input-gradient fused epilogues (act', column sums), 4 = split-K partial tiles stored to
+// the workspace slab of their k-range (plain 16-B stores; g7_splitk_reduce sums the slabs).
 // WN: output columns per wave.  128 = v7 (a 256 x 256 tile, one workgroup per CU); 64 = v8 (a
 // 256 x 128 tile, 128 accumulator registers, TWO workgroups per CU, each with a 3-slot ring:
 // the two drift out of phase, so one's epilogue -- the bias / GELU / residual / act' VALU work
@@ -507,6 +509,12 @@ __global__ __launch_bounds__(256, WN == 128 ? 1 : 2) void gemm7_kernel(GemmArgs 
     if (pl.debug & 1) {
     } else if constexpr (EPI == 2) {
       if constexpr (NJ == 8) g7_epilogue_atomic(p, acc, m0 + ar, n0 + bc, lane);
+    } else if constexpr (EPI == 4) {
+      GemmArgs q = p;  // the k-range's slab: [M][N] f32 at ws + split * M * N
+      q.C = static_cast<float*>(p.ws) + (long long)(uu / ntiles) * p.M * p.N;
+      q.ldc = p.N;
+      q.out_f32 = 1;
+      g7_epilogue<0, NJ>(q, acc, m0 + ar, n0 + bc, lane);
     } else {
       g7_epilogue<EPI, NJ>(p, acc, m0 + ar, n0 + bc, lane);
     }
@@ -518,6 +526,29 @@ __global__ __launch_bounds__(256, WN == 128 ? 1 : 2) void gemm7_kernel(GemmArgs 
 #undef G7_MFMA_ROW
 #undef G7_BODY
   g7_wait<0>();  // empty-descriptor DMA of the slices past the end: drained before exit
+}
+
+// C (=, or += when accumulating) the sum of the s workspace slabs [s][M][N]; 4 columns per
+// thread (N % 8 == 0, ldc % 8 == 0: 16-B rows)
+__global__ __launch_bounds__(256) void g7_splitk_reduce(float* C, long long ldc, const float* ws, int M, int N,
+                                                       int s, int accumulate) {
+  const long long nq = (long long)M * (N >> 2);
+  const long long slab = (long long)M * N;
+  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < nq; i += (long long)gridDim.x * 256) {
+    const long long m = i / (N >> 2), n = (i - m * (N >> 2)) << 2;
+    const float* w = ws + m * N + n;
+    float4 v = *reinterpret_cast<const float4*>(w);
+    for (int k = 1; k < s; ++k) {
+      const float4 u = *reinterpret_cast<const float4*>(w + k * slab);
+      v.x += u.x; v.y += u.y; v.z += u.z; v.w += u.w;
+    }
+    float4* c = reinterpret_cast<float4*>(C + m * ldc + n);
+    if (accumulate) {
+      const float4 o = *c;
+      v.x += o.x; v.y += o.y; v.z += o.z; v.w += o.w;
+    }
+    *c = v;
+  }
 }
 
 }  // namespace dpc
@@ -578,19 +609,34 @@ DPC_API int dpc_gemm7(const GemmArgs* a, int persistent, int sched, int splits, 
   const bool plain = !a->bias && !a->act_bwd && !a->aux_out && !a->act && !a->residual && !a->colsum;
   const bool splittable = plain && a->out_f32;
   int s = splits > 0 ? splits : 1;
-  if (splits <= 0 && splittable && tiles < 192 && !v8) {
-    // fill the chip: time ~ rounds * slices per unit + an atomic epilogue per unit-round
-    // (256 KiB of f32 adds per CU, ~40 slices' worth at the chip's memory-side atomic rate)
+  auto slab_fits = [&](int c) {
+    return a->ws && (long long)c * a->M * a->N * 4 <= a->ws_bytes && a->ldc % 4 == 0 && ((uintptr_t)a->ws % 16) == 0;
+  };
+  if (splits <= 0 && splittable && !v8) {
+    // fill the chip (few tiles) or even out the last round (wave quantisation): time ~ rounds
+    // * (slices per unit + the split epilogue) [+ the slab reduction].  Units are in k-slices
+    // (~0.7 us at the measured MFMA rate).  The split epilogue: 256 KiB of f32 adds per CU at
+    // the chip's memory-side atomic rate, ~40 slices, or the same bytes as plain slab stores,
+    // ~12, plus a reduction pass over (c + 1) M x N f32 at ~5 TB/s.
     double best = 1e30;
     for (int c = 1; c <= 32; ++c) {
       const int per = 2 * ((pl.nk_all + 2 * c - 1) / (2 * c));
       if (c > 1 && per < 16) break;
       const int rounds = (tiles * c + 255) / 256;
-      const double cost = (double)rounds * (per + (c > 1 ? 40.0 : 0.0));
+      double cost = (double)rounds * per;
+      if (c > 1 && slab_fits(c)) {
+        const double red_us = (double)(c + 1 + a->accumulate) * a->M * a->N * 4 / 5e6;
+        cost += rounds * 12.0 + red_us / 0.7;
+      } else if (c > 1) {
+        cost += rounds * 40.0;
+      }
       if (cost < best - 1e-9) { best = cost; s = c; }
     }
   }
   if (s > 1 && (!splittable || v8)) return -1;
+  // slab split (workspace for every k-range's partial tile) when the caller passed one that is
+  // large enough; otherwise f32 atomics into C
+  const bool slab = s > 1 && slab_fits(s);
   // the input-gradient epilogue (act', column sums) carries no forward operation
   if ((a->act_bwd || a->colsum) && (a->bias || a->act || a->aux_out || a->residual || a->accumulate)) return -1;
   pl.splits = s;
@@ -603,12 +649,18 @@ DPC_API int dpc_gemm7(const GemmArgs* a, int persistent, int sched, int splits, 
   // vector-memory ops an epilogue issues per lane, for the store credit: only epilogues that
   // read nothing per element and issue every store of a full tile (no column-sum atomics)
   const bool no_loads = !a->residual && !a->act_bwd && !a->accumulate && !a->colsum;
-  pl.store_cnt = (no_loads && s == 1 && !v8) ? ((a->out_f32 ? 64 : 32) + (a->aux_out ? 32 : 0)) : 0;
+  pl.store_cnt = (no_loads && (s == 1 || slab) && !v8) ? ((a->out_f32 || slab ? 64 : 32) + (a->aux_out ? 32 : 0)) : 0;
   static int dbg = -1;
   if (dbg < 0) dbg = getenv("DPC_G7_DEBUG") ? atoi(getenv("DPC_G7_DEBUG")) : 0;
   pl.debug = dbg;
   if (dbg & 1) pl.store_cnt = 0;
-  if (s > 1) {
+  if (slab) {
+    g7_launch<4, 2>(a, pl, stream, ab, bb);
+    const long long nq = (long long)a->M * (a->N / 4);
+    const int blocks = (int)std::min<long long>((nq + 255) / 256, 4096);
+    hipLaunchKernelGGL(g7_splitk_reduce, dim3(blocks), dim3(256), 0, stream, static_cast<float*>(a->C), a->ldc,
+                       static_cast<const float*>(a->ws), a->M, a->N, s, a->accumulate);
+  } else if (s > 1) {
     if (!a->accumulate) hipMemset2DAsync(a->C, (size_t)a->ldc * 4, 0, (size_t)a->N * 4, (size_t)a->M, stream);
     g7_launch<2, 2>(a, pl, stream, ab, bb);
   } else if (v8) {

@@ -165,6 +165,29 @@ if _TUNE:
     atexit.register(_save_table)
 
 
+# Split-K workspace of the weight-gradient products (f32, per device and stream): the v7 kernel
+# stores every k-range's partial tile there with plain stores and one reduction pass sums the
+# slabs into the gradient, instead of f32 atomics into it -- GPT-2 small's split layer weight
+# gradients ran 276-380 us with the atomics (bench/gemm_one.py --splits, scripts/
+# wgrad_split_sweep.sh).  Allocated once, outside any graph capture, and kept alive (a captured
+# step graph holds its address).  DPC_GEMM_WS_MB=0 turns it off (atomics).
+_WS_BYTES = int(float(os.environ.get("DPC_GEMM_WS_MB", "1024")) * 2**20)
+_ws: dict = {}
+
+
+def _workspace(device):
+    if _WS_BYTES <= 0:
+        return None
+    key = (device.index, torch.cuda.current_stream(device).cuda_stream)
+    t = _ws.get(key)
+    if t is None:
+        if torch.cuda.is_current_stream_capturing():
+            return None
+        t = torch.empty(_WS_BYTES // 4, dtype=torch.float32, device=device)
+        _ws[key] = t
+    return t
+
+
 def _sig(M, N, K, a_kmaj, b_kmaj, out_f32, bias, act, act_bwd, aux_out, residual, colsum,
          accumulate) -> str:
     flags = "".join(c for c, on in (("b", bias is not None), ("x", aux_out is not None),
@@ -280,6 +303,9 @@ def gemm(
         if (plain and _BLAS_PLAIN and _lib.forced_gemm_impl < 0
                 and _blas_plain(a, b, a_kmaj, b_kmaj, out, M, N, K, alpha, alpha_t)):
             return out
+        ws = (_workspace(a.device) if (out.dtype == torch.float32 and bias is None and residual is None
+                                         and aux_in is None and aux_out is None and colsum is None
+                                         and not act and not act_bwd) else None)
         args = _lib.GemmArgs(
             A=a.data_ptr(), B=b.data_ptr(), C=out.data_ptr(),
             bias=_lib.ptr(bias), residual=_lib.ptr(residual), aux_in=_lib.ptr(aux_in),
@@ -292,6 +318,7 @@ def gemm(
             out_f32=int(out.dtype == torch.float32), accumulate=int(accumulate),
             a_kmaj=int(a_kmaj), b_kmaj=int(b_kmaj),
             a_r=a.shape[0], a_c=a.shape[1], b_r=b.shape[0], b_c=b.shape[1],
+            ws=_lib.ptr(ws), ws_bytes=0 if ws is None else ws.numel() * 4,
         )
         if (_table or _TUNE) and _lib.forced_gemm_impl < 0:
             key = _sig(M, N, K, a_kmaj, b_kmaj, out.dtype == torch.float32, bias, act, act_bwd,
