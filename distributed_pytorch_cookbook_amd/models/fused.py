@@ -32,7 +32,8 @@ from ..ops.attention import DECODE_MAX_S, attention_bwd, attention_fwd, decode_a
 from ..ops.elementwise import bias_act_bwd
 from ..ops.dropout import dropout_residual
 from ..ops.embedding import embedding_bwd, embedding_fwd
-from ..ops.gemm import ACT_GELU, ACT_RELU, act_code, linear_dgrad, linear_fwd, linear_wgrad
+from ..ops.gemm import (ACT_GELU, ACT_RELU, act_code, linear_dgrad, linear_fwd, linear_wgrad,
+                        register_side_stream)
 from ..ops.loss import cross_entropy_fused, cross_entropy_rows
 from ..ops.norm import layernorm_bwd, layernorm_fwd
 
@@ -228,6 +229,7 @@ class _SideWork:
             key = torch.cuda.current_stream(device).cuda_stream
             if key not in _side_streams:
                 _side_streams[key] = torch.cuda.Stream(device=device)
+                register_side_stream(_side_streams[key])
             self.stream = _side_streams[key]
 
     def run(self, fn, *tensors):

@@ -171,14 +171,26 @@ if _TUNE:
 # gradients ran 276-380 us with the atomics (bench/gemm_one.py --splits, scripts/
 # wgrad_split_sweep.sh).  Allocated once, outside any graph capture, and kept alive (a captured
 # step graph holds its address).  DPC_GEMM_WS_MB=0 turns it off (atomics).
+# One workspace per device serves the compute stream -- and the private stream a HIP-graph
+# capture records it from, so a captured step uses the same buffer as its eager warm-up; a
+# stream that runs GEMMs CONCURRENTLY with it (the optional weight-gradient side stream,
+# models/fused.py) registers itself and gets its own.
 _WS_BYTES = int(float(os.environ.get("DPC_GEMM_WS_MB", "1024")) * 2**20)
 _ws: dict = {}
+_side_streams: set = set()
+
+
+def register_side_stream(stream) -> None:
+    """Give ``stream`` (which runs GEMMs concurrently with the compute stream) its own split-K
+    workspace."""
+    _side_streams.add(stream.cuda_stream)
 
 
 def _workspace(device):
     if _WS_BYTES <= 0:
         return None
-    key = (device.index, torch.cuda.current_stream(device).cuda_stream)
+    sid = torch.cuda.current_stream(device).cuda_stream
+    key = (device.index, sid) if sid in _side_streams else device.index
     t = _ws.get(key)
     if t is None:
         if torch.cuda.is_current_stream_capturing():
