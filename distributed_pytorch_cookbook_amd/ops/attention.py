@@ -183,7 +183,8 @@ def _attn_bwd_hip(dout, qkv, o, lse, N, S, heads, kd, pad_mask, causal, scale, d
     if dqkv is None:
         dqkv = torch.empty(T, 3 * hd, device=qkv.device, dtype=dt)
     _check(dqkv, T, 3 * hd, "dqkv", dt)
-    delta = torch.empty(N * heads, S, device=qkv.device, dtype=torch.float32)
+    # [delta | lse in log2 units] rows (attn_bwd_pre_kernel writes both)
+    delta = torch.empty(2, N * heads, S, device=qkv.device, dtype=torch.float32)
     pad = None
     if pad_mask is not None:
         pad = pad_mask.to(torch.uint8).contiguous()

@@ -46,7 +46,7 @@ struct AttnArgs {
   const unsigned char* pad;                     // [N][S], 1 = padded key (masked), optional
   const void* dout;                             // bwd: dO bf16 [T][ld_o]
   void* dq; void* dk; void* dv;                 // bwd: bf16 outputs, row stride ld_dqkv
-  float* delta;                                 // bwd: f32 [N*H][S]
+  float* delta;                                 // bwd: f32 [2][N*H][S]: delta, then lse in log2 units
   long long ld_qkv, ld_o, ld_dqkv;
   int N, S, H;
   float scale;
@@ -701,7 +701,9 @@ __global__ __launch_bounds__(256, OCC) void attn_fwd2_kernel(AttnArgs p, int nit
 }
 
 // ------------------------------------------------------------------ backward
-// delta[n,h,s] = sum_d dO * O   (one HD/8-lane group per (token, head))
+// delta[n,h,s] = sum_d dO * O   (one HD/8-lane group per (token, head)), and the second half of
+// the buffer the row's lse in log2 units (lse * log2 e) -- the kernels then form
+// p = 2^(s c - lse2) with one FMA and no per-element multiply
 template <int HD>
 __global__ __launch_bounds__(256) void attn_bwd_pre_kernel(AttnArgs p) {
   constexpr int G = HD / 8;
@@ -726,7 +728,9 @@ __global__ __launch_bounds__(256) void attn_bwd_pre_kernel(AttnArgs p) {
   for (int o = 1; o < G; o <<= 1) acc += __shfl_xor(acc, o, 64);
   if (row < T * p.H && sub == 0) {
     const long long n = t / p.S, s = t % p.S;
-    p.delta[(n * p.H + h) * p.S + s] = acc;
+    const long long i = (n * p.H + h) * p.S + s;
+    p.delta[i] = acc;
+    p.delta[T * p.H + i] = p.lse[i] * LOG2E;  // (+inf stays +inf: a fully masked row)
   }
 }
 
@@ -752,7 +756,7 @@ __global__ __launch_bounds__(256, OCC) void attn_bwd_dkdv_kernel(AttnArgs p) {
   const bf16_t* Kp = static_cast<const bf16_t*>(p.k) + h * HD;
   const bf16_t* Vp = static_cast<const bf16_t*>(p.v) + h * HD;
   const bf16_t* dO = static_cast<const bf16_t*>(p.dout) + tok0 * p.ld_o + h * HD;
-  const float* lse = p.lse + (long long)bh * S;
+  const float* lse = p.delta + (long long)p.N * H * S + (long long)bh * S;  // log2 units
   const float* delta = p.delta + (long long)bh * S;
   const bool key_ok = key < S && !(p.pad && p.pad[(long long)n * S + min(key, S - 1)]);
 
@@ -791,10 +795,20 @@ __global__ __launch_bounds__(256, OCC) void attn_bwd_dkdv_kernel(AttnArgs p) {
       dma4(rows_rsrc(delta, 4, qt * KT, S, valid), lane * 4, &srow[slot][1][0]);
     }
   };
-  // S = Q K^T, dP = dO V^T of the 32-query sub-block at row r0 of the slot (key on the lane)
+  // S = Q K^T, dP - delta = dO V^T - delta of the 32-query sub-block at row r0 of the slot
+  // (key on the lane): the dP accumulator starts at -delta of its query rows, so dS = P (dP -
+  // delta) needs no subtraction
   auto sdp = [&](floatx16& sa, floatx16& dp, const bf16_t* lq, int r0) {
     zero16(sa);
-    zero16(dp);
+    const float* drow = &srow[((lq - smem) / (2 * A::TILE))][1][0];
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const float4 d4 = *reinterpret_cast<const float4*>(drow + r0 + 8 * g + 4 * hh);
+      dp[4 * g + 0] = -d4.x;
+      dp[4 * g + 1] = -d4.y;
+      dp[4 * g + 2] = -d4.z;
+      dp[4 * g + 3] = -d4.w;
+    }
 #pragma unroll
     for (int st = 0; st < A::NST; ++st) {
       sa = MFMA32(row_frag<HD>(lq, r0, st, lane), kf[st], sa);
@@ -833,9 +847,7 @@ __global__ __launch_bounds__(256, OCC) void attn_bwd_dkdv_kernel(AttnArgs p) {
     for (int g = 0; g < 4; ++g) {
       const int qi0 = 32 * hf + 8 * g + 4 * hh;  // rows 8g+4h..+3: consecutive queries
       const float4 l4 = *reinterpret_cast<const float4*>(&srow[slot][0][qi0]);
-      const float4 d4 = *reinterpret_cast<const float4*>(&srow[slot][1][qi0]);
-      const float lv[4] = {l4.x * LOG2E, l4.y * LOG2E, l4.z * LOG2E, l4.w * LOG2E};
-      const float dl[4] = {d4.x, d4.y, d4.z, d4.w};
+      const float lv[4] = {l4.x, l4.y, l4.z, l4.w};
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         const int r = 4 * g + e;
@@ -843,7 +855,7 @@ __global__ __launch_bounds__(256, OCC) void attn_bwd_dkdv_kernel(AttnArgs p) {
         // a padded key's P only reaches this lane's own dK / dV column: zeroed at the store
         if (diag) pv = (key > qt0 + qi0 + e) ? 0.f : pv;
         sa[r] = pv;
-        dp[r] = pv * (dp[r] - dl[e]);
+        dp[r] = pv * dp[r];
       }
     }
 #pragma unroll
@@ -921,7 +933,7 @@ __global__ __launch_bounds__(256, OCC) void attn_bwd_dq_kernel(AttnArgs p) {
     df[st] = q < S ? load_row8(dO + (tok0 + q) * p.ld_o + 16 * st + 8 * hh) : bf16x8{};
   }
   const float c = p.scale * LOG2E;
-  const float lse2 = q < S ? p.lse[(long long)bh * S + q] * LOG2E : INFINITY;
+  const float lse2 = q < S ? p.delta[(long long)p.N * H * S + (long long)bh * S + q] : INFINITY;
   const float dl = q < S ? p.delta[(long long)bh * S + q] : 0.f;
   pin_loaded(qf);
   pin_loaded(df);
@@ -942,10 +954,12 @@ __global__ __launch_bounds__(256, OCC) void attn_bwd_dq_kernel(AttnArgs p) {
     tile_dma<HD>(K, p.ld_qkv, t * KT, S, valid, dv, st, wid);
     tile_dma<HD>(V, p.ld_qkv, t * KT, S, valid, dv, st + A::TILE, wid);
   };
-  // S^T = K Q^T, dP^T = V dO^T of the 32-key sub-block at row r0 of the slot
+  // S^T = K Q^T, dP^T - delta = V dO^T - delta of the 32-key sub-block at row r0 of the slot
+  // (the dP accumulator starts at -delta of this lane's query)
   auto sdp = [&](floatx16& sa, floatx16& dp, const bf16_t* lk, int r0) {
     zero16(sa);
-    zero16(dp);
+#pragma unroll
+    for (int r = 0; r < 16; ++r) dp[r] = -dl;
 #pragma unroll
     for (int st = 0; st < A::NST; ++st) {
       sa = MFMA32(row_frag<HD>(lk, r0, st, lane), qf[st], sa);
@@ -981,11 +995,11 @@ __global__ __launch_bounds__(256, OCC) void attn_bwd_dq_kernel(AttnArgs p) {
         const int kl = 32 * hf + acc_row(r, lane);
         float pv = fast_exp2(fmaf(sa[r], c, -lse2));
         pv = (kl > lim || ((pm >> kl) & 1ull)) ? 0.f : pv;
-        dp[r] = pv * (dp[r] - dl);
+        dp[r] = pv * dp[r];
       }
     } else {
 #pragma unroll
-      for (int r = 0; r < 16; ++r) dp[r] = fast_exp2(fmaf(sa[r], c, -lse2)) * (dp[r] - dl);
+      for (int r = 0; r < 16; ++r) dp[r] = fast_exp2(fmaf(sa[r], c, -lse2)) * dp[r];
     }
 #pragma unroll
     for (int ss = 0; ss < 2; ++ss) {
