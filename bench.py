@@ -38,13 +38,12 @@ METRIC = "tokens/sec (node) GPT-2 training per recipe (DDP/FSDP/PP) at 1/2/4/8 M
 # linearly with the GPU count.
 BASELINE_TOKS_PER_GPU = {("ddp", "gpt2-small", 32, 1024): 276672.6,
                          ("ddp", "gpt2-small", 64, 1024): 300633.0}
-# Per-GPU batch (sequences) per recipe when --batch_size is not given: DDP and the pipeline
-# run the reference's own default per-rank batch (--batch_size 64, main-*.py argparse,
-# SURVEY.md §5.6); GPT-2 XL (FSDP) and GPT-2 large (PP x DP) take 32, which keeps their saved
-# activations well inside one GPU's 288 GB.  Larger batches are faster per token on one MI355X
-# (profiles/r1_v17_recipe_batch_sweep.jsonl): FSDP XL 16 -> 32 +8 %, PP x DP large +15 %,
-# pipeline medium 32 -> 64 +7 %.
-DEFAULT_BATCH = {"ddp": 64, "fsdp": 32, "pipe": 64, "pipe_ddp": 32}
+# Per-GPU batch (sequences) per recipe when --batch_size is not given: every recipe runs the
+# reference's own default per-rank batch (--batch_size 64, main-*.py argparse).
+# On one MI355X that is also the fastest measured (profiles/r2_recipes/batch_sweep_s4.txt):
+# GPT-2 XL FSDP 32 / 48 / 64 -> 78.8 / 78.2 / 80.5K tok/s at 121 / 168 / 214 GiB peak, GPT-2 large
+# PP x DP 32 -> 64 +3 %, GPT-2 medium pipeline 64 -> 96 -3 %.
+DEFAULT_BATCH = {"ddp": 64, "fsdp": 64, "pipe": 64, "pipe_ddp": 64}
 
 
 def main():
@@ -152,6 +151,10 @@ def main():
     if info.world_size > 1:
         torch.distributed.all_reduce(lt)
     loss_v = float(lt[0] / lt[1]) if lt[1] > 0 else float("nan")
+    peak = torch.tensor([torch.cuda.max_memory_allocated(info.device) / 2**30 if info.device.type == "cuda" else 0.0],
+                        dtype=torch.float64, device=info.device)
+    if info.world_size > 1:
+        torch.distributed.all_reduce(peak, op=torch.distributed.ReduceOp.MAX)
     tokens_per_step = B * (S - 1) * engine.dp_world
     value = tokens_per_step * a.steps / dt
     n = info.world_size
@@ -175,6 +178,7 @@ def main():
         "config": {"model": model_name, "global_batch": B * engine.dp_world, "seq_len": S,
                    "parallelism": par, "recipe": f"main-{a.recipe.replace('_', '-')}.py",
                    "tokens_per_step": tokens_per_step, "final_loss": round(loss_v, 4),
+                   "peak_mem_gib": round(float(peak.item()), 1),
                    "mfu_per_gpu": round(mfu(value / n, train_flops_per_token(
                        args.dim, args.heads, args.head_dim, args.num_layers, vocab, S)), 4),
                    "baseline": ("stock PyTorch reference-default recipe (manual attention + torch.compile)"

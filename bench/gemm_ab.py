@@ -32,6 +32,15 @@ GPT2S = [("qkv_fwd", T, 2304, 768, "nt"), ("out_fwd", T, 768, 768, "nt"),
          ("out_dgrad", T, 768, 768, "nn"), ("up_dgrad", T, 768, 3072, "nn"),
          ("lm_dgrad", T, 768, 50304, "nn"), ("up_fwd", T, 3072, 768, "nt"),
          ("down_fwd", T, 768, 3072, "nt")]
+# GPT-2 XL (FSDP bench: 32 x 1023 tokens, D = 1600) plain products: forward, input and weight
+# gradients
+TX = 32 * 1023
+XL = [("xl_qkv_fwd", TX, 4800, 1600, "nt"), ("xl_outp_fwd", TX, 1600, 1600, "nt"),
+      ("xl_lm_fwd", TX, 50304, 1600, "nt"), ("xl_qkv_dgrad", TX, 1600, 4800, "nn"),
+      ("xl_out_dgrad", TX, 1600, 1600, "nn"), ("xl_up_dgrad", TX, 1600, 6400, "nn"),
+      ("xl_lm_dgrad", TX, 1600, 50304, "nn"), ("xl_w_qkv", 4800, 1600, TX, "tn"),
+      ("xl_w_out", 1600, 1600, TX, "tn"), ("xl_w_up", 6400, 1600, TX, "tn"),
+      ("xl_w_down", 1600, 6400, TX, "tn"), ("xl_w_lm", 50304, 1600, TX, "tn")]
 
 
 # fused-epilogue products of the GPT-2 layers: (name, M, N, K, layout, epilogue)
@@ -99,13 +108,13 @@ def check(A, B, lay, out):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--impls", type=int, nargs="+", default=[12, 13, 14])
-    ap.add_argument("--shapes", default="all", choices=["square", "gpt2s", "all", "fused"])
+    ap.add_argument("--shapes", default="all", choices=["square", "gpt2s", "all", "fused", "xl"])
     ap.add_argument("--only", nargs="*", default=None)
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--json", default=None)
     a = ap.parse_args()
-    shapes = (SQUARE if a.shapes in ("square", "all") else []) + (GPT2S if a.shapes in ("gpt2s", "all") else [])
+    shapes = (SQUARE if a.shapes in ("square", "all") else []) + (GPT2S if a.shapes in ("gpt2s", "all") else []) + (XL if a.shapes == "xl" else [])
     if a.only:
         shapes = [s for s in shapes if s[0] in a.only]
     rows = []
@@ -142,7 +151,9 @@ def main():
         torch.manual_seed(0)
         A, B, kw, odt = operands(M, N, K, lay)
         out = torch.empty(M, N, device="cuda", dtype=odt)
-        variants = {"blas": torch_fn(A, B, lay, out)}
+        variants = {"blas": torch_fn(A, B, lay, out),
+                    # the impl the shipped table (ops/gemm_tuned.json) picks, or the policy
+                    "tab": (lambda: (_lib.set_gemm_impl(-1), gemm(A, B, out=out, **kw)))}
         for impl in a.impls:
             variants[f"i{impl}"] = (lambda impl=impl: (_lib.set_gemm_impl(impl), gemm(A, B, out=out, **kw)))
         errs = {}
