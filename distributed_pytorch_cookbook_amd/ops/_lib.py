@@ -140,8 +140,18 @@ class DecodeAttnArgs(ctypes.Structure):
     ]
 
 
+class GemvArgs(ctypes.Structure):
+    _fields_ = [
+        ("x", P), ("w", P), ("bias", P), ("residual", P), ("y", P),
+        ("ldx", LL), ("ldw", LL), ("ldr", LL), ("ldy", LL),
+        ("M", c_int), ("N", c_int), ("Nw", c_int), ("K", c_int),
+        ("act", c_int), ("y_f32", c_int),
+    ]
+
+
 _FUNCS = {
     "dpc_decode_attn": DecodeAttnArgs,
+    "dpc_gemv": GemvArgs,
     "dpc_gemm": GemmArgs,
     "dpc_gemm_f32": GemmArgs,
     "dpc_attn_fwd": AttnArgs,

@@ -108,6 +108,85 @@ __global__ __launch_bounds__(DA_NT) void decode_attn_kernel(DecodeAttnArgs p) {
   }
 }
 
+
+// ---------------------------------------------------------------- few-row Linear (decode)
+// y[m, n] = act(x[m, :] . w[n, :] + bias[n]) (+ residual[m, n]) for a handful of rows (M <= 16:
+// one new token per sequence).  The product is a stream of the weight matrix (N x K bf16) with
+// nothing for an MFMA tile to reuse, so it runs on the vector ALUs at the memory rate: a wave
+// owns GV_NC consecutive output columns, lane l reads 16-B chunks k = 8 (l + 64 i) of those
+// weight rows and of every x row (x is tiny and stays in L1 / L2), f32 accumulation, a
+// butterfly reduction over the wave, and the bias / activation / f32 residual epilogue fused
+// into the same launch (the decode step was bound by its launch count, not by the weights).
+// Columns n >= Nw (a vocabulary padded past the weight's rows) are written as 0.
+struct GemvArgs {
+  const void* x;          // [M][ldx] bf16
+  const void* w;          // [Nw][ldw] bf16, k contiguous (nn.Linear layout)
+  const float* bias;      // [Nw] f32 or null
+  const float* residual;  // [M][ldr] f32 or null
+  void* y;                // [M][ldy] bf16 or f32
+  long long ldx, ldw, ldr, ldy;
+  int M, N, Nw, K;
+  int act, y_f32;
+};
+
+constexpr int GV_NC = 4;  // output columns per wave
+
+template <int MM>
+__global__ __launch_bounds__(256) void gemv_kernel(GemvArgs p) {
+  const int lane = threadIdx.x & 63;
+  const int n0 = (blockIdx.x * 4 + (threadIdx.x >> 6)) * GV_NC;
+  if (n0 >= p.N) return;
+  const bf16_t* X = static_cast<const bf16_t*>(p.x);
+  const bf16_t* W = static_cast<const bf16_t*>(p.w);
+  float acc[MM][GV_NC];
+#pragma unroll
+  for (int m = 0; m < MM; ++m)
+#pragma unroll
+    for (int c = 0; c < GV_NC; ++c) acc[m][c] = 0.f;
+  for (int k = 8 * lane; k < p.K; k += 512) {
+    float wf[GV_NC][8];
+#pragma unroll
+    for (int c = 0; c < GV_NC; ++c) {
+      const int n = n0 + c;
+      uint4 wv = make_uint4(0u, 0u, 0u, 0u);
+      if (n < p.Nw) wv = *reinterpret_cast<const uint4*>(W + (long long)n * p.ldw + k);
+      unpack8(wv, wf[c]);
+    }
+#pragma unroll
+    for (int m = 0; m < MM; ++m) {
+      if (m < p.M) {
+        float xf[8];
+        unpack8(*reinterpret_cast<const uint4*>(X + (long long)m * p.ldx + k), xf);
+#pragma unroll
+        for (int c = 0; c < GV_NC; ++c)
+#pragma unroll
+          for (int e = 0; e < 8; ++e) acc[m][c] = fmaf(xf[e], wf[c][e], acc[m][c]);
+      }
+    }
+  }
+#pragma unroll
+  for (int m = 0; m < MM; ++m)
+#pragma unroll
+    for (int c = 0; c < GV_NC; ++c) acc[m][c] = wave_sum(acc[m][c]);
+  // lane j writes (m, c) = (j / GV_NC, j % GV_NC)
+  const int m = lane / GV_NC, c = lane % GV_NC, n = n0 + c;
+  if (m >= p.M || n >= p.N) return;
+  float v = 0.f;
+#pragma unroll
+  for (int mm = 0; mm < MM; ++mm)
+#pragma unroll
+    for (int cc = 0; cc < GV_NC; ++cc) v = (mm == m && cc == c) ? acc[mm][cc] : v;
+  if (n < p.Nw) {
+    if (p.bias) v += p.bias[n];
+    v = act_fwd(v, p.act);
+    if (p.residual) v += p.residual[(long long)m * p.ldr + n];
+  } else {
+    v = 0.f;
+  }
+  if (p.y_f32) static_cast<float*>(p.y)[(long long)m * p.ldy + n] = v;
+  else static_cast<bf16_t*>(p.y)[(long long)m * p.ldy + n] = f2bf(v);
+}
+
 }  // namespace dpc
 
 using namespace dpc;
@@ -117,5 +196,20 @@ DPC_API int dpc_decode_attn(const DecodeAttnArgs* a, hipStream_t stream) {
   if (a->hd <= 0 || a->hd % 8 || a->hd > 256 || a->Smax > DA_MAX_S || a->ldqkv % 8)
     return (int)hipErrorInvalidValue;
   hipLaunchKernelGGL(decode_attn_kernel, dim3((unsigned)(a->N * a->H)), dim3(DA_NT), 0, stream, *a);
+  return (int)hipGetLastError();
+}
+
+// Requirements: M <= 16, K % 8 == 0, x / w rows 16-B aligned (ld % 8 == 0), N <= ldy.
+DPC_API int dpc_gemv(const GemvArgs* a, hipStream_t stream) {
+  if (a->M <= 0 || a->N <= 0) return 0;
+  if (a->M > 16 || a->K <= 0 || a->K % 8 || a->ldx % 8 || a->ldw % 8 || a->Nw > a->N || a->N > a->ldy ||
+      ((uintptr_t)a->x % 16) || ((uintptr_t)a->w % 16))
+    return (int)hipErrorInvalidValue;
+  const dim3 grid((unsigned)((a->N + 4 * GV_NC - 1) / (4 * GV_NC)));
+  if (a->M <= 1) hipLaunchKernelGGL(gemv_kernel<1>, grid, dim3(256), 0, stream, *a);
+  else if (a->M <= 2) hipLaunchKernelGGL(gemv_kernel<2>, grid, dim3(256), 0, stream, *a);
+  else if (a->M <= 4) hipLaunchKernelGGL(gemv_kernel<4>, grid, dim3(256), 0, stream, *a);
+  else if (a->M <= 8) hipLaunchKernelGGL(gemv_kernel<8>, grid, dim3(256), 0, stream, *a);
+  else hipLaunchKernelGGL(gemv_kernel<16>, grid, dim3(256), 0, stream, *a);
   return (int)hipGetLastError();
 }

@@ -429,26 +429,45 @@ def linear_fwd(x, w, *, bias=None, act=None, residual=None, aux_out=None, out=No
 
 
 # decode-shaped products (a handful of rows): the MFMA tile kernels would launch N / 256
-# workgroups on a 256-CU chip; the weight stream is the whole cost, so these go to the
-# library's GEMV-shaped kernels with the (tiny) epilogue as elementwise ops
+# workgroups on a 256-CU chip and the weight stream is the whole cost, so these run the
+# few-row kernel (csrc/decode.hip: dpc_gemv -- vector-ALU dot products at the memory rate,
+# bias / activation / f32 residual fused into the same launch: one launch per Linear of the
+# decode step instead of the library GEMV plus up to three elementwise launches)
 _GEMV_ROWS = 16
+_GEMV_NATIVE = os.environ.get("DPC_GEMV", "1") == "1"  # 0: the library product (A/B only)
+
+
+def _gemv_ok(x, w, bias, residual, out, N):
+    return (x.stride(1) == 1 and w.stride(1) == 1 and x.shape[1] % 8 == 0 and x.stride(0) % 8 == 0
+            and w.stride(0) % 8 == 0 and x.data_ptr() % 16 == 0 and w.data_ptr() % 16 == 0
+            and (bias is None or (bias.dtype == torch.float32 and bias.is_contiguous()))
+            and (residual is None or (residual.dtype == torch.float32 and residual.stride(1) == 1))
+            and out.stride(1) == 1 and w.shape[0] <= N)
 
 
 def _linear_fwd_few_rows(x, w, bias, act, residual, out, out_dtype):
-    # bias in the library epilogue (f32 accumulate), then at most two elementwise launches
+    M, K = x.shape
+    Nw = w.shape[0]
+    if out is None:
+        out = torch.empty(M, Nw, device=x.device, dtype=out_dtype)
+    N = out.shape[1]
+    if _GEMV_NATIVE and _gemv_ok(x, w, bias, residual, out, N) and out.dtype in (torch.float32, torch.bfloat16):
+        args = _lib.GemvArgs(
+            x=x.data_ptr(), w=w.data_ptr(), bias=_lib.ptr(bias), residual=_lib.ptr(residual),
+            y=out.data_ptr(), ldx=x.stride(0), ldw=w.stride(0),
+            ldr=residual.stride(0) if residual is not None else 0, ldy=out.stride(0),
+            M=M, N=N, Nw=Nw, K=K, act=act, y_f32=int(out.dtype == torch.float32))
+        _lib.call("dpc_gemv", args, x.device)
+        return out
+    # operands the kernel does not take (unaligned rows, K % 8): the library product
     v = torch.mm(x, w.t()) if bias is None else torch.addmm(bias.to(x.dtype), x, w.t())
     if act:
         v = act_fwd_ref(v, act)
     if residual is not None:
-        # f32 residual stream; two same-dtype launches (the mixed-dtype add measured 39 us
-        # for one 768-wide row vs ~5 us each for these)
         v = residual + v.to(residual.dtype)
-    if out is None:
-        return v if v.dtype == out_dtype else v.to(out_dtype)
-    n = v.shape[1]
-    out[:, :n].copy_(v)
-    if out.shape[1] > n:
-        out[:, n:].zero_()
+    out[:, :Nw].copy_(v)
+    if N > Nw:
+        out[:, Nw:].zero_()
     return out
 
 

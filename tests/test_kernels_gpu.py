@@ -586,3 +586,32 @@ def test_decode_attention(hd, pos):
     v = v_ref[:, :L].float().reshape(N, L, H, hd).transpose(1, 2)
     ref = (torch.softmax(q @ k.transpose(-1, -2) / math.sqrt(hd), -1) @ v).reshape(N, E)
     assert rel_err(o, ref) < 1e-2
+
+
+@pytest.mark.parametrize("M", [1, 3, 8, 16])
+@pytest.mark.parametrize("Nw,N,K", [(2304, 2304, 768), (50257, 50304, 768), (1600, 1600, 6400), (100, 104, 64)])
+@pytest.mark.parametrize("epi", ["plain", "bias_gelu", "bias_relu_res"])
+def test_gemv_few_rows(M, Nw, N, K, epi):
+    """Decode-shaped Linear (csrc/decode.hip: dpc_gemv) against an f32 torch product of the same
+    bf16 operands: bias / activation / f32 residual epilogue fused, padded output columns
+    (N > weight rows) written as 0."""
+    from distributed_pytorch_cookbook_amd.ops.gemm import _linear_fwd_few_rows, act_fwd_ref
+    torch.manual_seed(7)
+    x = torch.randn(M, K, device=dev).bfloat16()
+    w = (torch.randn(Nw, K, device=dev) / K ** 0.5).bfloat16()
+    bias = torch.randn(Nw, device=dev) if epi != "plain" else None
+    act = {"plain": 0, "bias_gelu": 2, "bias_relu_res": 1}[epi]
+    res = torch.randn(M, N, device=dev) if epi == "bias_relu_res" else None
+    odt = torch.float32 if res is not None else torch.bfloat16
+    out = torch.full((M, N), 7.0, device=dev, dtype=odt)
+    y = _linear_fwd_few_rows(x, w, bias, act, res, out, odt)
+    ref = x.float() @ w.float().t()
+    if bias is not None:
+        ref = ref + bias
+    ref = act_fwd_ref(ref, act)
+    if res is not None:
+        ref = ref + res[:, :Nw]
+    assert y is out
+    assert rel_err(y[:, :Nw], ref) < (2e-3 if odt == torch.float32 else 1e-2)
+    if N > Nw:
+        assert torch.count_nonzero(y[:, Nw:]) == 0
