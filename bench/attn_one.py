@@ -8,7 +8,7 @@ import sys
 
 import torch
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.environ.get("DPC_ROOT") or os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from distributed_pytorch_cookbook_amd.ops.attention import attention_bwd, attention_fwd  # noqa: E402
 
 ap = argparse.ArgumentParser()
