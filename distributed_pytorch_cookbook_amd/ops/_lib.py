@@ -140,6 +140,14 @@ class DecodeAttnArgs(ctypes.Structure):
     ]
 
 
+class EmbBwdArgs(ctypes.Structure):
+    _fields_ = [
+        ("ids", P), ("pos", P), ("dout", P), ("dtok", P), ("dpos", P), ("ws", P),
+        ("ws_bytes", ctypes.c_ulonglong),
+        ("T", c_int), ("D", c_int), ("V", c_int), ("P", c_int),
+    ]
+
+
 class GemvArgs(ctypes.Structure):
     _fields_ = [
         ("x", P), ("w", P), ("bias", P), ("residual", P), ("y", P),
@@ -152,6 +160,7 @@ class GemvArgs(ctypes.Structure):
 _FUNCS = {
     "dpc_decode_attn": DecodeAttnArgs,
     "dpc_gemv": GemvArgs,
+    "dpc_embedding_bwd_sorted": EmbBwdArgs,
     "dpc_gemm": GemmArgs,
     "dpc_gemm_f32": GemmArgs,
     "dpc_attn_fwd": AttnArgs,
@@ -202,6 +211,8 @@ def lib() -> ctypes.CDLL:
             handle.dpc_gemm_set_xcd_split.restype = None
             handle.dpc_gemm_set_splits.argtypes = [c_int]
             handle.dpc_gemm_set_splits.restype = None
+            handle.dpc_embedding_bwd_ws.argtypes = [c_int, c_int]
+            handle.dpc_embedding_bwd_ws.restype = ctypes.c_ulonglong
             _lib = handle
     return _lib
 

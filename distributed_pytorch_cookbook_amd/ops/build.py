@@ -28,7 +28,8 @@ BUILD_DIR = HERE / "_build"
 LIB_PATH = HERE / "libdpc_kernels.so"
 ARCH = os.environ.get("DPC_OFFLOAD_ARCH", "gfx950")
 
-SOURCES = ["gemm.hip", "gemm7.hip", "gemm_f32.hip", "attention.hip", "attention_f32.hip", "layernorm.hip", "misc.hip", "decode.hip"]
+SOURCES = ["gemm.hip", "gemm7.hip", "gemm_f32.hip", "attention.hip", "attention_f32.hip", "layernorm.hip", "misc.hip",
+           "decode.hip", "embed_bwd.hip"]
 HEADERS = ["common.h", "gemm.h"]
 
 # code-object v5 keeps the library loadable by torch's bundled ROCm 7.0 runtime as

@@ -5,6 +5,8 @@ lookups summed; the f32 result is the residual stream).
 """
 from __future__ import annotations
 
+import os
+
 import torch
 
 from . import _lib
@@ -38,6 +40,26 @@ def embedding_fwd(ids: torch.Tensor, pos: torch.Tensor, tok: torch.Tensor, ptab:
     return out
 
 
+# Deterministic backward (csrc/embed_bwd.hip): a stable radix sort of (id, row) pairs and one
+# writer per table row, summing its rows in row order -- bitwise reproducible, no float atomics.
+# DPC_EMB_ATOMIC=1 selects the atomic scatter (misc.hip) instead (A/B only).
+_ATOMIC = os.environ.get("DPC_EMB_ATOMIC", "0") == "1"
+_ws: dict = {}
+
+
+def _workspace(device, T: int, D: int):
+    """Sort workspace for T rows, per device, grown on demand outside any graph capture (a
+    captured step keeps the buffer it was recorded with)."""
+    need = int(_lib.lib().dpc_embedding_bwd_ws(int(T), int(D)))
+    t = _ws.get(device.index)
+    if t is None or t.numel() < need:
+        if torch.cuda.is_current_stream_capturing():
+            return None
+        t = torch.empty(max(need, 256), dtype=torch.uint8, device=device)
+        _ws[device.index] = t
+    return t
+
+
 def embedding_bwd(dout: torch.Tensor, ids: torch.Tensor, pos: torch.Tensor,
                   dtok: torch.Tensor | None, dpos: torch.Tensor | None) -> None:
     """dtok[ids] += dout; dpos[pos] += dout (f32 grads)."""
@@ -61,4 +83,13 @@ def embedding_bwd(dout: torch.Tensor, ids: torch.Tensor, pos: torch.Tensor,
     )
     if dtok is not None and dtok.dtype != torch.float32 or dpos is not None and dpos.dtype != torch.float32:
         raise ValueError("embedding_bwd: f32 gradient tables required")
+    D = dout.shape[1]
+    ws = None if (_ATOMIC or D % 4 or D > 2048) else _workspace(ref.device, ids.numel(), D)
+    if ws is not None:
+        sargs = _lib.EmbBwdArgs(
+            ids=ids.data_ptr(), pos=pos.data_ptr(), dout=dout.data_ptr(), dtok=_lib.ptr(dtok),
+            dpos=_lib.ptr(dpos), ws=ws.data_ptr(), ws_bytes=ws.numel(), T=ids.numel(), D=D,
+            V=args.V, P=args.P)
+        _lib.call("dpc_embedding_bwd_sorted", sargs, ref.device)
+        return
     _lib.call("dpc_embedding_bwd", args, ref.device)

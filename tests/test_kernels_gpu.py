@@ -356,6 +356,35 @@ def test_embedding(tdt):
     assert torch.allclose(dt, rt, atol=1e-4) and torch.allclose(dp, rp, atol=1e-4)
 
 
+@pytest.mark.parametrize("D", [64, 768, 1600])
+def test_embedding_bwd_deterministic(D):
+    """The sorted embedding backward (csrc/embed_bwd.hip): equals an f64 index_add, accumulates
+    into existing gradients, skips out-of-range ids, and is bitwise identical across runs even
+    with heavily repeated ids (the atomic scatter is not)."""
+    from distributed_pytorch_cookbook_amd.ops import embedding as emb
+    torch.manual_seed(9)
+    V, P, S, N = 5000, 1024, 1023, 8
+    T = N * S
+    ids = torch.randint(0, 40, (T,), device=dev)  # ~200 repeats per id
+    ids[::97] = torch.randint(0, V, (ids[::97].numel(),), device=dev)
+    ids[5] = V + 3  # out of range: ignored
+    pos = torch.arange(S, device=dev).repeat(N)
+    dx = torch.randn(T, D, device=dev)
+    base_t, base_p = torch.randn(V, D, device=dev), torch.randn(P, D, device=dev)
+    outs = []
+    for _ in range(2):
+        dt, dp = base_t.clone(), base_p.clone()
+        emb.embedding_bwd(dx, ids, pos, dt, dp)
+        outs.append((dt, dp))
+    assert emb._ws, "the sorted path did not run"
+    ok = ids < V
+    rt = base_t.double().index_add_(0, ids[ok], dx[ok].double())
+    rp = base_p.double().index_add_(0, pos, dx.double())
+    assert torch.allclose(outs[0][0].double(), rt, atol=2e-4, rtol=1e-5)
+    assert torch.allclose(outs[0][1].double(), rp, atol=2e-4, rtol=1e-5)
+    assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
+
+
 @pytest.mark.parametrize("V,mode", [(50257, 0), (1000, 0), (9000, 0), (40000, 0), (70001, 0),
                                     (50257, 1), (50257, 2)])
 def test_cross_entropy(V, mode):
