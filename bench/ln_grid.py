@@ -31,7 +31,11 @@ def timeit(fn, iters=20, reps=3):
 
 
 def main():
-    for T, D in ((32736, 768), (16368, 1600)):
+    import sys
+    shapes = ((32736, 768), (16368, 1600))
+    if len(sys.argv) > 1:  # e.g. 16320x256,65472x768
+        shapes = tuple(tuple(int(v) for v in a.split("x")) for a in sys.argv[1].split(","))
+    for T, D in shapes:
         x = torch.randn(T, D, device="cuda")
         g, b = torch.randn(D, device="cuda"), torch.randn(D, device="cuda")
         _, mean, rstd = layernorm_fwd(x, g, b)
@@ -41,7 +45,7 @@ def main():
         gout = torch.empty(T, D, device="cuda", dtype=torch.bfloat16)
         gsum = torch.zeros(D, device="cuda")
         nbytes = T * D * (4 + 2 + 4 + 4 + 2)  # x, dy, dx r/w, gout
-        for blocks in (256, 512, 1024, 2048, 4096, 8192):
+        for blocks in (64, 128, 256, 512, 1024, 2048, 4096):
             _lib.lib().dpc_layernorm_set_bwd_blocks(blocks)
             ms = timeit(lambda: layernorm_bwd(dy, x, mean, rstd, g, dx, dg, db, gout=gout, gsum=gsum))
             print(json.dumps({"T": T, "D": D, "blocks": blocks, "us": round(ms * 1e3, 1),

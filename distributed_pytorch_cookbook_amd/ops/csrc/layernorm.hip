@@ -9,6 +9,8 @@
 // before ONE f32 atomic per column per workgroup.
 //
 // One wave per row, NV float4 per lane (D <= 256 * NV), 4 rows (waves) per workgroup.
+#include <algorithm>
+
 #include "common.h"
 
 namespace dpc {
@@ -261,7 +263,8 @@ DPC_API int dpc_layernorm_fwd(const LNArgs* a, hipStream_t stream) {
 // Workgroups of the persistent backward grid.  Each workgroup ends with 2 D column atomics
 // (dgamma / dbeta), so the best grid shrinks as D grows: bench/ln_grid.py on MI355X, 1024 at
 // D = 768 (5.2 TB/s; 512: 4.6, 2048: 4.3) and 512 at D = 1600 (4.4 TB/s; 1024: 4.1) -- i.e.
-// ~786K column-atomics per launch.  0 = that rule; > 0 forces a size (sweeps).
+// ~786K column-atomics per launch, and at most one workgroup per 32 rows.  0 = that rule; > 0
+// forces a size (sweeps).
 static int g_ln_bwd_blocks = 0;
 DPC_API void dpc_layernorm_set_bwd_blocks(int n) { g_ln_bwd_blocks = n > 0 ? n : 0; }
 
@@ -269,7 +272,9 @@ DPC_API int dpc_layernorm_bwd(const LNArgs* a, hipStream_t stream) {
   if (a->T <= 0) return 0;
   if (a->D % 4) return (int)hipErrorInvalidValue;
   const long long blocks = (a->T + 3) / 4;
-  long long cap = g_ln_bwd_blocks > 0 ? g_ln_bwd_blocks : 786432 / a->D;
+  // (also at most one workgroup per 32 rows: the reference-default shape T = 16320, D = 256 ran
+  // 36 us at 1024 workgroups, 25.6 us at 256-512 -- bench/ln_grid.py)
+  long long cap = g_ln_bwd_blocks > 0 ? g_ln_bwd_blocks : std::min<long long>(786432 / a->D, (a->T + 31) / 32);
   cap = cap < 256 ? 256 : (cap > 1024 && g_ln_bwd_blocks <= 0 ? 1024 : cap);
   dim3 grid((unsigned)(blocks < cap ? blocks : cap));
   LN_DISPATCH(ln_bwd_kernel, grid);
