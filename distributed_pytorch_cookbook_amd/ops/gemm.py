@@ -148,6 +148,37 @@ def _load_table(path: str = _TUNE_PATH) -> dict:
 
 _table: dict = _load_table() if _USE_TABLE else {}
 _tuned_new: dict = {}
+_near_cache: dict = {}
+_NEAR = os.environ.get("DPC_GEMM_NEAR", "1") == "1"  # 0: exact signatures only (A/B)
+
+
+def _near(key: str):
+    """The table's choice for the closest measured product that differs from ``key`` only in its
+    token dimension (M of a forward / input-gradient product, K of a weight gradient) by at most
+    25 % -- e.g. 8 x 8191 = 65528 rows at S = 8192 against the 65472 (64 x 1023) the table was
+    measured at; the best tile / pipeline depends on the other dimensions and the epilogue."""
+    if key in _near_cache:
+        return _near_cache[key]
+    dims, rest = key.split(":", 1)
+    M, N, K = (int(v) for v in dims.split("x"))
+    best = None
+    for k2, v in _table.items():
+        d2, r2 = k2.split(":", 1)
+        if r2 != rest:
+            continue
+        M2, N2, K2 = (int(x) for x in d2.split("x"))
+        if N2 != N:
+            continue
+        if K2 == K and M2 != M:
+            diff = abs(M2 - M) / M
+        elif M2 == M and K2 != K:
+            diff = abs(K2 - K) / K
+        else:
+            continue
+        if diff <= 0.25 and (best is None or diff < best[0]):
+            best = (diff, v)
+    _near_cache[key] = best[1] if best else None
+    return _near_cache[key]
 
 
 def _save_table() -> None:
@@ -336,6 +367,8 @@ def gemm(
             key = _sig(M, N, K, a_kmaj, b_kmaj, out.dtype == torch.float32, bias, act, act_bwd,
                        aux_out, residual, colsum, accumulate)
             impl = _table.get(key)
+            if impl is None and not _TUNE and _NEAR:
+                impl = _near(key)
             if (impl is None and _TUNE and not torch.cuda.is_current_stream_capturing()
                     and out.numel() * out.element_size() <= _TUNE_MAX_OUT_BYTES):
                 impl = _tune(args, out, aux_out, colsum, a.device)

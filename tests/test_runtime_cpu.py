@@ -125,3 +125,27 @@ def test_gemm_table_signature_and_file():
     assert table and all(v in G._CANDIDATES for v in table.values())
     assert all(k.count(":") == 4 for k in table)
     assert os.path.dirname(G._TUNE_PATH).endswith("ops")
+
+
+def test_gemm_table_nearest_token_dimension():
+    """A product missing from the measured table takes the entry that differs only in its token
+    dimension (M of a forward / dgrad, K of a weight gradient) by at most 25 %."""
+    from distributed_pytorch_cookbook_amd.ops import gemm as G
+
+    saved = (dict(G._table), dict(G._near_cache))
+    try:
+        G._table.clear()
+        G._near_cache.clear()
+        G._table.update({"65472x768x3072:kk:f:20:bxr": 6, "32736x768x3072:kk:f:20:bxr": 2,
+                         "768x3072x65472:mm:f:00:a": 16, "65472x768x3072:kk:h:00:": 19})
+        assert G._near("65528x768x3072:kk:f:20:bxr") == 6       # S = 8192: 8 x 8191 rows
+        assert G._near("40000x768x3072:kk:f:20:bxr") == 2       # closer to 32736
+        assert G._near("768x3072x65528:mm:f:00:a") == 16        # weight gradient: K = tokens
+        assert G._near("65528x768x3072:kk:h:00:") == 19         # flags must match exactly
+        assert G._near("65528x1024x3072:kk:f:20:bxr") is None   # another N
+        assert G._near("16368x768x3072:kk:f:20:bxr") is None    # beyond 25 %
+    finally:
+        G._table.clear()
+        G._table.update(saved[0])
+        G._near_cache.clear()
+        G._near_cache.update(saved[1])
