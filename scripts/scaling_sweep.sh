@@ -1,0 +1,34 @@
+#!/bin/bash
+# Multi-GPU tuning sweep for a whole 8 x MI355X node (not runnable on the one-GPU boxes of this
+# project's CI): the DDP bucket size (SURVEY.md §5.8 design rule 2: 25 -> 256 MB) and the
+# gradient-reduction dtype at N = 2, 4, 8, then each recipe's default at N = 8.  One JSON line per
+# run in gpurun_out/scaling_sweep.jsonl.
+#   bash scripts/scaling_sweep.sh [max_gpus]
+set -u
+MAXG=${1:-8}
+OUT=gpurun_out/scaling_sweep.jsonl
+mkdir -p gpurun_out
+export HSA_ENABLE_IPC_MODE_LEGACY=0
+port=29650
+run() {  # $1 = N, rest = bench args
+  local n=$1; shift
+  port=$((port + 1))
+  timeout -k 10 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node "$n" --master-addr 127.0.0.1 \
+    --master-port $port bench.py --gpus "$n" --steps 10 --warmup 3 "$@" --json gpurun_out/_last.json > /dev/null 2>&1 || return $?
+  python3 -c "import json,sys; d=json.load(open('gpurun_out/_last.json')); d['args']=sys.argv[1:]; print(json.dumps(d))" "$@" >> $OUT
+}
+for n in 2 4 8; do
+  [ "$n" -gt "$MAXG" ] && break
+  for mb in 32 64 128 256; do
+    for dt in fp32 bf16; do
+      run $n --bucket_mb $mb --reduce_dtype $dt || exit $?
+    done
+  done
+done
+for r in fsdp pipe pipe_ddp; do run "$MAXG" --recipe $r || exit $?; done
+python3 - <<'PY'
+import json
+for l in open("gpurun_out/scaling_sweep.jsonl"):
+    d = json.loads(l)
+    print(d["n_gpus"], d["config"]["recipe"], " ".join(d["args"]), round(d["value"]), "tok/s")
+PY
