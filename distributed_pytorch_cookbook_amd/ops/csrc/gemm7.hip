@@ -635,7 +635,7 @@ DPC_API int dpc_gemm7_ok(const GemmArgs* a) {
 // splits: 1 = none, > 1 forced, 0 = automatic (plain f32 products only: the tiles are too few to
 // fill the chip, e.g. weight gradients -- K = tokens, M x N = a weight).
 // wn: 128 = v7 (256 x 256 tiles, one workgroup per CU), 64 = v8 (256 x 128 tiles, two per CU;
-// no split-K)
+// split-K through workspace slabs only)
 DPC_API int dpc_gemm7(const GemmArgs* a, int persistent, int sched, int splits, hipStream_t stream, int wn) {
   if (a->M <= 0 || a->N <= 0) return 0;
   if (!dpc_gemm7_ok(a)) return -1;
@@ -654,7 +654,7 @@ DPC_API int dpc_gemm7(const GemmArgs* a, int persistent, int sched, int splits, 
   auto slab_fits = [&](int c) {
     return a->ws && (long long)c * a->M * a->N * 4 <= a->ws_bytes && a->ldc % 4 == 0 && ((uintptr_t)a->ws % 16) == 0;
   };
-  if (splits <= 0 && splittable && !v8) {
+  if (splits <= 0 && splittable) {
     // fill the chip (few tiles) or even out the last round (wave quantisation): time ~ rounds
     // * (slices per unit + the split epilogue) [+ the slab reduction].  Units are in k-slices
     // (~0.7 us at the measured MFMA rate).  The split epilogue: 256 KiB of f32 adds per CU at
@@ -664,18 +664,20 @@ DPC_API int dpc_gemm7(const GemmArgs* a, int persistent, int sched, int splits, 
     for (int c = 1; c <= 32; ++c) {
       const int per = 2 * ((pl.nk_all + 2 * c - 1) / (2 * c));
       if (c > 1 && per < 16) break;
-      const int rounds = (tiles * c + 255) / 256;
+      // (v8: two 256 x 128 units per CU at once, each half a v7 unit's MFMA work)
+      const int rounds = v8 ? (tiles * c + 511) / 512 : (tiles * c + 255) / 256;
       double cost = (double)rounds * per;
       if (c > 1 && slab_fits(c)) {
         const double red_us = (double)(c + 1 + a->accumulate) * a->M * a->N * 4 / 5e6;
         cost += rounds * 12.0 + red_us / 0.7;
       } else if (c > 1) {
+        if (v8) continue;  // v8 splits through workspace slabs only (no atomic epilogue)
         cost += rounds * 40.0;
       }
       if (cost < best - 1e-9) { best = cost; s = c; }
     }
   }
-  if (s > 1 && (!splittable || v8)) return -1;
+  if (s > 1 && (!splittable || (v8 && !slab_fits(s)))) return -1;
   // slab split (workspace for every k-range's partial tile) when the caller passed one that is
   // large enough; otherwise f32 atomics into C
   const bool slab = s > 1 && slab_fits(s);
@@ -697,7 +699,8 @@ DPC_API int dpc_gemm7(const GemmArgs* a, int persistent, int sched, int splits, 
   pl.debug = dbg;
   if (dbg & 1) pl.store_cnt = 0;
   if (slab) {
-    g7_launch<4, 2>(a, pl, stream, ab, bb);
+    if (v8) g7_launch<4, 2, 64>(a, pl, stream, ab, bb);
+    else g7_launch<4, 2>(a, pl, stream, ab, bb);
     const long long nq = (long long)a->M * (a->N / 4);
     const int blocks = (int)std::min<long long>((nq + 255) / 256, 4096);
     hipLaunchKernelGGL(g7_splitk_reduce, dim3(blocks), dim3(256), 0, stream, static_cast<float*>(a->C), a->ldc,

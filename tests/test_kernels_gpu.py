@@ -161,7 +161,7 @@ def test_gemm_v6_v7(impl, a_kmaj, b_kmaj, M, N, K):
     assert rel_err(og, og_r) < 1e-2
 
 
-@pytest.mark.parametrize("impl", [2, 4, 7, 10, 11, 12, 16])
+@pytest.mark.parametrize("impl", [2, 4, 7, 10, 11, 12, 16, 21])
 @pytest.mark.parametrize("splits", [2, 3, 8])
 @pytest.mark.parametrize("M,N,K", [(77, 1000, 4160), (600, 520, 8192), (2304, 136, 4096)])
 def test_gemm_forced_split_k(impl, splits, M, N, K):
