@@ -37,21 +37,43 @@ def _entry(rank, world, port, fn, args, errq):
             dist.destroy_process_group()
 
 
-def run_workers(fn, world: int, *args, timeout: float = 240.0):
+def _run_once(fn, world: int, args, timeout: float):
+    import time
+
     ctx = mp.get_context("spawn")
     errq = ctx.Queue()
     port = free_port()
     procs = [ctx.Process(target=_entry, args=(r, world, port, fn, args, errq)) for r in range(world)]
     for p in procs:
         p.start()
+    errs = []
+    deadline = time.monotonic() + timeout
+    # poll: a rank that fails (e.g. the rendezvous port taken) must not leave its peers waiting
+    # for it until the timeout
+    while any(p.is_alive() for p in procs) and time.monotonic() < deadline:
+        while not errq.empty():
+            errs.append(errq.get())
+        if errs:
+            break
+        time.sleep(0.05)
     for p in procs:
-        p.join(timeout)
+        p.join(0 if errs else 1.0)
     alive = [p for p in procs if p.is_alive()]
     for p in alive:
         p.kill()
-    errs = []
+        p.join(5)
     while not errq.empty():
         errs.append(errq.get())
+    return procs, alive, errs
+
+
+def run_workers(fn, world: int, *args, timeout: float = 240.0):
+    for attempt in range(3):
+        procs, alive, errs = _run_once(fn, world, args, timeout)
+        # the free port can be taken between free_port() and the rendezvous: try another one
+        if errs and attempt < 2 and any("EADDRINUSE" in tb or "address already in use" in tb for _, tb in errs):
+            continue
+        break
     if errs:
         raise AssertionError("worker failure:\n" + "\n".join(f"[rank {r}]\n{tb}" for r, tb in errs))
     if alive:
