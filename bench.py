@@ -61,6 +61,7 @@ def main():
     ap.add_argument("--num_microbatches", type=int, default=0)
     ap.add_argument("--schedule", default="1f1b", choices=["1f1b", "gpipe"])
     ap.add_argument("--dp_size", type=int, default=0)
+    ap.add_argument("--prefetch", type=int, default=None, help="FSDP: units all-gathered ahead")
     ap.add_argument("--no_graph", action="store_true", help="eager steps (no HIP-graph capture)")
     ap.add_argument("--graph", action="store_true",
                     help="HIP-graph capture also at N > 1 (default: only at N = 1)")
@@ -83,6 +84,8 @@ def main():
         argv += ["--schedule", a.schedule, "--num_microbatches", str(a.num_microbatches)]
     if rec == "pipe_ddp" and a.dp_size:
         argv += ["--dp_size", str(a.dp_size)]
+    if rec == "fsdp" and a.prefetch is not None:
+        argv += ["--prefetch", str(a.prefetch)]
     # N > 1 runs eager steps unless --graph: on one MI355X the graphed and the eager step take
     # the same time at the default batch (profiles/r1_v19_eager_vs_graph: 77.2 vs 77.2 ms), and
     # a step graph with RCCL collectives inside cannot be rehearsed on a one-GPU box (RCCL
