@@ -43,6 +43,20 @@ def main():
         print(json.dumps({"mode": mode, "us": round(ms * 1e3, 1),
                           "TBps_rw": round(2 * T * ld * 2 / ms / 1e9, 2)}), flush=True)
     _lib.lib().dpc_ce_set_mode(0)
+    # the memory roofline of the same traffic: a device copy of the logits (one read, one write)
+    dst = torch.empty_like(logits)
+    for _ in range(2):
+        dst.copy_(logits)
+        torch.cuda.synchronize()
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s.record()
+        for _ in range(10):
+            dst.copy_(logits)
+        e.record()
+        e.synchronize()
+        ms = s.elapsed_time(e) / 10
+        print(json.dumps({"mode": "copy", "us": round(ms * 1e3, 1),
+                          "TBps_rw": round(2 * T * ld * 2 / ms / 1e9, 2)}), flush=True)
 
 
 if __name__ == "__main__":
