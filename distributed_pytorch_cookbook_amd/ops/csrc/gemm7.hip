@@ -120,6 +120,10 @@ __device__ __forceinline__ void sfor(F&& f) {
 
 #define G7_AI __attribute__((always_inline))
 
+#ifndef G7_EPI_PF
+#define G7_EPI_PF 0  // 0 = the default depth per epilogue (A/B builds override)
+#endif
+
 // lane l <- lane l ^ 8 within each 16-lane row (DPP row_ror:8, a VALU op)
 __device__ __forceinline__ unsigned g7_ror8(unsigned v) {
   return (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, 0x128, 0xf, 0xf, false);
@@ -207,8 +211,8 @@ __device__ __forceinline__ void g7_epilogue(const GemmArgs& p, floatx4 (&acc)[8]
   }
   constexpr bool FWD = MODE == 1;
   // per-element operand reads (FWD: the f32 residual / accumulated C; else act''s bf16
-  // operand), prefetched one row block ahead: as soon as fragment (i, j) is consumed, the
-  // slot is refilled with (i + 1, j) -- one slot per fragment, no double buffer
+  // operand), prefetched PF row blocks ahead: as soon as fragment (i, j) is consumed, its slot
+  // is refilled with (i + PF, j)
   const bf16_t* aux_in = static_cast<const bf16_t*>(p.aux_in);
   bf16_t* aux_out = static_cast<bf16_t*>(p.aux_out);
   const float* fsrc = FWD ? (p.residual ? p.residual : (p.out_f32 && p.accumulate ? static_cast<const float*>(p.C) : nullptr))
@@ -228,12 +232,18 @@ __device__ __forceinline__ void g7_epilogue(const GemmArgs& p, floatx4 (&acc)[8]
     }
     return r;
   };
-  uint4 ld[NJ];
+  // PF row blocks of operand reads in flight: the input-gradient epilogue's act' operand is an
+  // 8-B read per lane and fragment, latency-bound at one block ahead
+  constexpr int PF = G7_EPI_PF > 0 ? G7_EPI_PF : (FWD ? 1 : 2);  // (3 - 4 spill in v8)
+  uint4 ld[PF][NJ];
   float4 bias4[NJ];
   float cs[NJ][4];
   sfor<NJ>([&](auto J) G7_AI {
     constexpr int j = decltype(J)::value;
-    ld[j] = load_one(mw + rl, nw + 16 * j + 4 * g);
+    sfor<PF>([&](auto Q) G7_AI {
+      constexpr int q = decltype(Q)::value;
+      ld[q][j] = load_one(mw + 16 * q + rl, nw + 16 * j + 4 * g);
+    });
     if constexpr (FWD) {
       const int n = nw + 16 * j + 4 * g;
       bias4[j] = (p.bias && n < p.N) ? *reinterpret_cast<const float4*>(p.bias + n) : make_float4(0.f, 0.f, 0.f, 0.f);
@@ -254,8 +264,8 @@ __device__ __forceinline__ void g7_epilogue(const GemmArgs& p, floatx4 (&acc)[8]
         constexpr int jj = j + h;
         const int n = nw + 16 * jj + 4 * g;
         const bool ok = mok && n < p.N;
-        const uint4 cur = ld[jj];
-        if (i + 1 < 8) ld[jj] = load_one(m + 16, n);
+        const uint4 cur = ld[i % PF][jj];
+        if (i + PF < 8) ld[i % PF][jj] = load_one(m + 16 * PF, n);
         float w[4];
 #pragma unroll
         for (int r = 0; r < 4; ++r) w[r] = acc[i][jj][r] * alpha;
