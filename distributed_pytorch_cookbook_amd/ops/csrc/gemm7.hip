@@ -234,7 +234,7 @@ __device__ __forceinline__ void g7_epilogue(const GemmArgs& p, floatx4 (&acc)[8]
   };
   // PF row blocks of operand reads in flight: the input-gradient epilogue's act' operand is an
   // 8-B read per lane and fragment, latency-bound at one block ahead
-  constexpr int PF = G7_EPI_PF > 0 ? G7_EPI_PF : (FWD ? 1 : 2);  // (3 - 4 spill in v8)
+  constexpr int PF = G7_EPI_PF > 0 ? G7_EPI_PF : (FWD || NJ > 4 ? 1 : 2);  // (v8; 3 - 4 spill there)
   uint4 ld[PF][NJ];
   float4 bias4[NJ];
   float cs[NJ][4];
