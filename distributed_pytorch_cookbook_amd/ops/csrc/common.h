@@ -119,6 +119,21 @@ __device__ __forceinline__ float gelu_tanh_grad(float x) {
   return s + x * s * (1.f - s) * (2.f * k0) * (1.f + 3.f * k1 * x2);
 }
 
+// gelu_tanh_grad of two values in packed-f32 math (v_pk_fma / v_pk_mul: half the vector-ALU
+// issue of the scalar form; the exp / rcp stay per element).  Same formula, log2(e) folded
+// into the exponent's coefficients.
+typedef float dpc_f2_t __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ dpc_f2_t gelu_tanh_grad2(dpc_f2_t x) {
+  const float k0 = 0.7978845608028654f, k1 = 0.044715f, L2E = 1.4426950408889634f;
+  const dpc_f2_t x2 = x * x;
+  const dpc_f2_t u = x * (x2 * (-2.f * k0 * k1 * L2E) + (-2.f * k0 * L2E));  // -2 u log2(e)
+  dpc_f2_t s;
+  s.x = __builtin_amdgcn_rcpf(1.f + __builtin_amdgcn_exp2f(u.x));
+  s.y = __builtin_amdgcn_rcpf(1.f + __builtin_amdgcn_exp2f(u.y));
+  const dpc_f2_t t = x2 * (6.f * k0 * k1) + 2.f * k0;  // 2 k0 (1 + 3 k1 x^2)
+  return (x * s) * (1.f - s) * t + s;
+}
+
 enum Act { ACT_NONE = 0, ACT_RELU = 1, ACT_GELU = 2 };
 
 __device__ __forceinline__ float act_fwd(float v, int act) {

@@ -130,7 +130,9 @@ __device__ __forceinline__ unsigned g7_ror8(unsigned v) {
 }
 __device__ __forceinline__ float g7_ror8(float v) { return __uint_as_float(g7_ror8(__float_as_uint(v))); }
 
-template <int MODE, int NJ>
+// PK: GELU' in packed-f32 math (v8 with a K-major A -- the input-gradient products; the other
+// instantiations have no register room for it)
+template <int MODE, int NJ, bool PK = false>
 __device__ __forceinline__ void g7_epilogue(const GemmArgs& p, floatx4 (&acc)[8][NJ], int mw, int nw, int lane) {
   float alpha = p.alpha;
   if (p.alpha_ptr) alpha *= *p.alpha_ptr;
@@ -280,7 +282,11 @@ __device__ __forceinline__ void g7_epilogue(const GemmArgs& p, floatx4 (&acc)[8]
             w[2] += __uint_as_float(cur.z); w[3] += __uint_as_float(cur.w);
           }
         } else {
-          if (p.act_bwd) {
+          if (PK && p.act_bwd == ACT_GELU) {
+            const dpc_f2_t g01 = gelu_tanh_grad2(dpc_f2_t{__uint_as_float(cur.x << 16), __uint_as_float(cur.x & 0xffff0000u)});
+            const dpc_f2_t g23 = gelu_tanh_grad2(dpc_f2_t{__uint_as_float(cur.y << 16), __uint_as_float(cur.y & 0xffff0000u)});
+            w[0] *= g01.x; w[1] *= g01.y; w[2] *= g23.x; w[3] *= g23.y;
+          } else if (p.act_bwd) {
             w[0] *= act_grad(__uint_as_float(cur.x << 16), p.act_bwd);
             w[1] *= act_grad(__uint_as_float(cur.x & 0xffff0000u), p.act_bwd);
             w[2] *= act_grad(__uint_as_float(cur.y << 16), p.act_bwd);
@@ -568,7 +574,7 @@ __global__ __launch_bounds__(256, WN == 128 ? 1 : 2) void gemm7_kernel(GemmArgs 
       q.out_f32 = 1;
       g7_epilogue<0, NJ>(q, acc, m0 + ar, n0 + bc, lane);
     } else {
-      g7_epilogue<EPI, NJ>(p, acc, m0 + ar, n0 + bc, lane);
+      g7_epilogue<EPI, NJ, WN == 64 && AK>(p, acc, m0 + ar, n0 + bc, lane);
     }
     // the stores were issued after this tile's last wait: the next DIST-2 waits (slices whose
     // DMA is older than the stores) may leave them in flight -- full tiles only (an edge tile
