@@ -134,6 +134,15 @@ __device__ __forceinline__ dpc_f2_t gelu_tanh_grad2(dpc_f2_t x) {
   return (x * s) * (1.f - s) * t + s;
 }
 
+__device__ __forceinline__ dpc_f2_t gelu_tanh2(dpc_f2_t x) {
+  const float k0 = 0.7978845608028654f, k1 = 0.044715f, L2E = 1.4426950408889634f;
+  const dpc_f2_t u = x * ((x * x) * (-2.f * k0 * k1 * L2E) + (-2.f * k0 * L2E));
+  dpc_f2_t s;
+  s.x = __builtin_amdgcn_rcpf(1.f + __builtin_amdgcn_exp2f(u.x));
+  s.y = __builtin_amdgcn_rcpf(1.f + __builtin_amdgcn_exp2f(u.y));
+  return x * s;
+}
+
 enum Act { ACT_NONE = 0, ACT_RELU = 1, ACT_GELU = 2 };
 
 __device__ __forceinline__ float act_fwd(float v, int act) {

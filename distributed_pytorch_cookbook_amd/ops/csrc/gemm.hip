@@ -197,8 +197,13 @@ __device__ __forceinline__ void epi_tile(const GemmArgs& p, floatx4 (&acc)[FM][4
         w.y = pack2bf(v[2], v[3]);
         *reinterpret_cast<uint2*>(aux_out + (long long)m * p.ld_aux_out + n) = w;
       }
+      if (p.act == ACT_GELU) {  // packed-f32 math (common.h:gelu_tanh2)
+        const dpc_f2_t g01 = gelu_tanh2(dpc_f2_t{v[0], v[1]}), g23 = gelu_tanh2(dpc_f2_t{v[2], v[3]});
+        v[0] = g01.x; v[1] = g01.y; v[2] = g23.x; v[3] = g23.y;
+      } else {
 #pragma unroll
-      for (int q = 0; q < 4; ++q) v[q] = act_fwd(v[q], p.act);
+        for (int q = 0; q < 4; ++q) v[q] = act_fwd(v[q], p.act);
+      }
       const long long ci = (long long)m * p.ldc + n;
       if (fsrc) {
         v[0] += __uint_as_float(cur.v[t].x); v[1] += __uint_as_float(cur.v[t].y);

@@ -130,8 +130,8 @@ __device__ __forceinline__ unsigned g7_ror8(unsigned v) {
 }
 __device__ __forceinline__ float g7_ror8(float v) { return __uint_as_float(g7_ror8(__float_as_uint(v))); }
 
-// PK: GELU' in packed-f32 math (v8 with a K-major A -- the input-gradient products; the other
-// instantiations have no register room for it)
+// PK: GELU / GELU' in packed-f32 math (v8 with a K-major A; the other instantiations have no
+// register room for it)
 template <int MODE, int NJ, bool PK = false>
 __device__ __forceinline__ void g7_epilogue(const GemmArgs& p, floatx4 (&acc)[8][NJ], int mw, int nw, int lane) {
   float alpha = p.alpha;
@@ -275,8 +275,13 @@ __device__ __forceinline__ void g7_epilogue(const GemmArgs& p, floatx4 (&acc)[8]
           w[0] += bias4[jj].x; w[1] += bias4[jj].y; w[2] += bias4[jj].z; w[3] += bias4[jj].w;
           pa[h][0] = pack2bf(w[0], w[1]);  // the pre-activation (aux_out)
           pa[h][1] = pack2bf(w[2], w[3]);
+          if (PK && p.act == ACT_GELU) {
+            const dpc_f2_t g01 = gelu_tanh2(dpc_f2_t{w[0], w[1]}), g23 = gelu_tanh2(dpc_f2_t{w[2], w[3]});
+            w[0] = g01.x; w[1] = g01.y; w[2] = g23.x; w[3] = g23.y;
+          } else {
 #pragma unroll
-          for (int r = 0; r < 4; ++r) w[r] = act_fwd(w[r], p.act);
+            for (int r = 0; r < 4; ++r) w[r] = act_fwd(w[r], p.act);
+          }
           if (fsrc) {
             w[0] += __uint_as_float(cur.x); w[1] += __uint_as_float(cur.y);
             w[2] += __uint_as_float(cur.z); w[3] += __uint_as_float(cur.w);
