@@ -20,9 +20,8 @@ import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from distributed_pytorch_cookbook_amd.ops import _lib  # noqa: E402
-from distributed_pytorch_cookbook_amd.ops.gemm import gemm, set_blas_plain  # noqa: E402
+from distributed_pytorch_cookbook_amd.ops.gemm import gemm  # noqa: E402
 
-set_blas_plain(False)
 
 SQUARE = [("sq8k_nt", 8192, 8192, 8192, "nt"), ("sq8k_nn", 8192, 8192, 8192, "nn"),
           ("sq8k_tn", 8192, 8192, 8192, "tn"), ("sq4k_nt", 4096, 4096, 4096, "nt")]

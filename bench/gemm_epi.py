@@ -19,9 +19,8 @@ import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from distributed_pytorch_cookbook_amd.ops import _lib  # noqa: E402
-from distributed_pytorch_cookbook_amd.ops.gemm import ACT_GELU, gemm, set_blas_plain  # noqa: E402
+from distributed_pytorch_cookbook_amd.ops.gemm import ACT_GELU, gemm  # noqa: E402
 
-set_blas_plain(False)
 
 
 def timeit(fn, iters=20, warmup=5):

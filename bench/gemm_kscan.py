@@ -9,9 +9,8 @@ import torch
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 from distributed_pytorch_cookbook_amd.ops import _lib  # noqa: E402
-from distributed_pytorch_cookbook_amd.ops.gemm import gemm, set_blas_plain  # noqa: E402
+from distributed_pytorch_cookbook_amd.ops.gemm import gemm  # noqa: E402
 
-set_blas_plain(False)  # time the hand-written kernels, not the vendor library
 from kernels import timeit  # noqa: E402
 
 ap = argparse.ArgumentParser()

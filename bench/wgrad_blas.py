@@ -13,9 +13,8 @@ import sys
 import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-from distributed_pytorch_cookbook_amd.ops.gemm import gemm, set_blas_plain  # noqa: E402
+from distributed_pytorch_cookbook_amd.ops.gemm import gemm  # noqa: E402
 
-set_blas_plain(False)
 
 
 def timeit(fn, iters=10, reps=3):

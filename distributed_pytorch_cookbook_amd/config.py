@@ -27,7 +27,8 @@ def build_parser(recipe: str = "single") -> argparse.ArgumentParser:
     p.add_argument("--dataset_slice", type=str, default="100%")
     p.add_argument("--num_workers", type=int, default=4)
     p.add_argument("--disable_amp", action="store_true",
-                   help="f32 compute (reference-math torch ops) instead of the bf16 kernels")
+                   help="f32 compute: the f32-input MFMA GEMM and f32 flash-attention kernels "
+                        "instead of the bf16 ones")
     p.add_argument("--disable_compile", action="store_true",
                    help="do not capture the train step into a HIP graph")
     if recipe == "fsdp":
@@ -37,6 +38,9 @@ def build_parser(recipe: str = "single") -> argparse.ArgumentParser:
     p.add_argument("--model", type=str, default=None, choices=sorted(PRESETS),
                    help="architecture preset (overrides dim/head_dim/heads/num_layers/sequence_length)")
     p.add_argument("--activation", type=str, default=None, choices=["relu", "gelu"])
+    p.add_argument("--graph", action="store_true",
+                   help="capture the step into a HIP graph also at N > 1 (RCCL collectives inside the "
+                        "graph); by default only a one-rank run is captured, N > 1 runs eager steps")
     p.add_argument("--grad_scaler", action="store_true",
                    help="dynamic loss scaling as the reference's GradScaler (fused non-finite check, "
                         "skip + back-off on device); unnecessary for bf16, off by default")

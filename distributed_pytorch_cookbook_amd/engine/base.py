@@ -62,6 +62,18 @@ class Engine:
     def step_count(self) -> int:
         return 0
 
+    def reset_step_state(self) -> None:
+        """Forget the per-step bookkeeping of the store / pipeline -- collectives 'launched',
+        gathered units, in-flight sends -- after a failed HIP-graph capture: nothing the
+        capture recorded ever ran, so the eager retry must issue everything again (a bucket
+        left marked as launched would never be all-reduced: silent rank divergence)."""
+        from ..parallel import transport
+
+        for obj in (getattr(self, "store", None), getattr(self, "p2p", None)):
+            if obj is not None and hasattr(obj, "reset_step_state"):
+                obj.reset_step_state()
+        transport.forget_outstanding()  # --stream_check: the recorded handles never ran
+
 
 class GraphedStep:
     """The whole training step of an engine -- memset of the gradients, forward, backward with
@@ -85,6 +97,26 @@ class GraphedStep:
         self.static = None
         self.loss = None
 
+    # test seams: how a graph is made and captured (the CPU tests substitute a capture that
+    # fails part-way through the step body)
+    @staticmethod
+    def _new_graph():
+        return torch.cuda.CUDAGraph()
+
+    @staticmethod
+    def _capture(g, mode):
+        return torch.cuda.graph(g, capture_error_mode=mode)
+
+    def _sync(self):
+        if self.engine.device.type == "cuda":
+            torch.cuda.synchronize()
+
+    @staticmethod
+    def _watchdog():
+        from ..parallel import native_comm
+
+        return native_comm
+
     def __call__(self, body, batch, targets):
         if not self.enabled:
             return body(batch, targets)
@@ -100,6 +132,10 @@ class GraphedStep:
             self.graph.replay()
             for o in self.opts:
                 o.step_count += 1
+            # the collectives inside a replayed graph are watched as one unit
+            wd = self._watchdog()
+            if wd.watchdog_running():
+                wd.watchdog_track(torch.cuda.current_stream().cuda_stream, "hip-graph step replay")
             return None if self.loss is None else self.loss.clone()
         if self.key != key:  # first call for this signature: eager (warm-up)
             self.key = key
@@ -108,24 +144,31 @@ class GraphedStep:
         st = {"ids": batch["input_ids"].clone(), "pos": batch["position_ids"].clone(),
               "tg": targets.clone(), "mask": None if mask is None else mask.clone()}
         self.static = st
+        counts = [(o.step_count, o.device_step) for o in self.opts]
         for o in self.opts:
             o.device_step = True
-        g = torch.cuda.CUDAGraph()
+        g = self._new_graph()
         multi = dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1
-        torch.cuda.synchronize()
+        self._sync()
         if multi:
             # nothing of the process group may still be in flight when the capture starts
             dist.barrier()
-            torch.cuda.synchronize()
+            self._sync()
+        wd = self._watchdog()
+        native_wd = wd.watchdog_running()
         err = None
         try:
-            # thread_local: only this thread's calls are checked -- the process group's
-            # watchdog thread keeps querying its events while the capture runs
-            with torch.cuda.graph(g, capture_error_mode="thread_local" if multi else "global"):
+            # thread_local: only this thread's calls are checked -- the process group's and
+            # the native watchdog threads keep querying their events while the capture runs
+            # (the native one is also paused: no HIP call from it until the capture ends)
+            wd.watchdog_pause(True)
+            with self._capture(g, "thread_local" if (multi or native_wd) else "global"):
                 b = {"input_ids": st["ids"], "position_ids": st["pos"], "mask": st["mask"]}
                 self.loss = body(b, st["tg"])
         except Exception as exc:  # capture not possible: stay eager
             err = exc
+        finally:
+            wd.watchdog_pause(False)
         if multi:
             # every rank graphs or none does: a rank replaying while another runs eagerly
             # would still issue the same collectives, but a failed capture may have left
@@ -135,13 +178,18 @@ class GraphedStep:
             if err is None and float(flag.item()) > 0:
                 err = RuntimeError("capture failed on another rank")
         if err is not None:
-            for o in self.opts:
-                o.device_step = False
+            # the capture recorded work that never ran: undo its host-side effects (optimizer
+            # step counts, collectives marked as launched, gathered units) before the step is
+            # run eagerly
+            for o, (n, ds) in zip(self.opts, counts):
+                o.step_count, o.device_step = n, ds
+            self.engine.reset_step_state()
             self.enabled = False
             self.graph = None
+            self.loss = None
             if self.engine.is_logger:
                 print(f"[hip-graph] capture failed ({err!r}); running eagerly")
-            torch.cuda.synchronize()
+            self._sync()
             return body(batch, targets)
         self.graph = g
         g.replay()

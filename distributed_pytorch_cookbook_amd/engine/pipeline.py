@@ -63,10 +63,12 @@ class PipelineEngine(Engine):
         self.first = self.stage == 0
         self.last = self.stage == pp - 1
         self.is_logger = comm.rank() == 0
-        # 4 x stages micro-batches: the 1F1B bubble is (pp - 1) / (M + pp - 1) -- 18 % at pp 8
-        # 4 x stages micro-batches (a (pp-1)/(5pp-1) bubble); one stage has no bubble to
-        # hide, so it runs the whole batch at once (the reference: chunks = num_stages,
-        # /root/reference/main-pipe.py:83)
+        # micro-batches: by default the largest divisor of the per-replica batch that is at most
+        # 4 x stages (the 1F1B bubble is (pp - 1) / (M + pp - 1): 18 % at pp 8, M 32); one stage
+        # has no bubble to hide, so it runs the whole batch at once (the reference: chunks =
+        # num_stages, /root/reference/main-pipe.py:83).  The batch size is known at the first
+        # step (_micro_count).
+        self.n_micro_req = num_microbatches
         self.n_micro = max(1, num_microbatches or (4 * pp if pp > 1 else 1))
         self.schedule = schedule
         S = seq_len or model.max_position_embeddings
@@ -106,9 +108,17 @@ class PipelineEngine(Engine):
         self._stepper = GraphedStep(self, [self.opt])
 
     # ------------------------------------------------------------------ pieces
+    def _micro_count(self, N: int) -> int:
+        if self.n_micro_req:
+            return self.n_micro_req
+        if self.pp == 1:
+            return 1
+        return max(d for d in range(1, min(N, 4 * self.pp) + 1) if N % d == 0)
+
     def _split(self, batch, targets):
         N = batch["input_ids"].shape[0]
-        M = self.n_micro
+        M = self.n_micro = self._micro_count(N)
+        self.store.accum_steps = M
         if N % M:
             raise ValueError(f"batch {N} not divisible by {M} micro-batches")
         mb = N // M

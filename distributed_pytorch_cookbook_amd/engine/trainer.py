@@ -5,7 +5,8 @@ Reference loop: ``/root/reference/main-single.py:80-151`` (and its copies in
 tqdm per epoch with ``[training] Epoch e/E | loss: x.xxx`` refreshed every
 ``PRINT_FREQ = 8`` steps, validation loss / accuracy, three greedy samples, a final
 rank-0 ``torch.save``.  Kept here, with: the PRINT_FREQ averaging off-by-one fixed,
-``DistributedSampler.set_epoch`` called, metrics reduced in ONE collective per epoch
+a per-epoch reshuffle (the reference never called ``set_epoch``) whose global batches do
+not depend on the world size (``GlobalBatchSampler``), metrics reduced in ONE collective per epoch
 instead of two per batch, generation run on every rank when the engine needs it
 (FSDP, pipeline) so no collective is left unmatched, tokens/s reported, and
 ``--resume`` / ``--max_steps`` support.
@@ -18,7 +19,7 @@ import os
 import time
 
 import torch
-from torch.utils.data import DataLoader, DistributedSampler
+from torch.utils.data import DataLoader, Sampler
 
 from ..parallel import comm
 from ..utils.batch import generate, prepare_batch
@@ -53,15 +54,47 @@ class _NoBar:
         pass
 
 
+class GlobalBatchSampler(Sampler):
+    """Data-parallel sampler whose global batches do not depend on the world size.
+
+    The reference shards with ``DistributedSampler`` (``/root/reference/main-ddp.py:83-84``),
+    which deals a shuffled order round-robin, so W ranks x B sequences see different global
+    batches than one process at W x B.  Here epoch e's order is ``randperm(n)`` of a generator
+    seeded ``seed + e`` -- exactly the order a single-process ``DataLoader(shuffle=True)``
+    with that generator produces -- and global batch i is its slice [i W B, (i + 1) W B), of
+    which rank r takes the r-th B sequences.  A DDP / FSDP / PP x DP run therefore trains on
+    the same global batches as ``main-single.py`` at batch W x B (the multi-rank recipe tests
+    compare their checkpoints), and resume positions are global batch indices.  Incomplete
+    global batches are dropped (``drop_last``)."""
+
+    def __init__(self, n: int, batch_size: int, world: int = 1, rank: int = 0, shuffle: bool = True,
+                 seed: int = 0):
+        self.n, self.B, self.W, self.r = n, batch_size, max(1, world), rank
+        self.shuffle, self.seed, self.epoch = shuffle, seed, 0
+        self.nb = n // (self.B * self.W)
+
+    def set_epoch(self, epoch: int) -> None:
+        self.epoch = epoch
+
+    def __iter__(self):
+        if self.shuffle:
+            g = torch.Generator().manual_seed(self.seed + self.epoch)
+            order = torch.randperm(self.n, generator=g)
+        else:
+            order = torch.arange(self.n)
+        gb = self.B * self.W
+        for i in range(self.nb):
+            yield from order[i * gb + self.r * self.B:i * gb + (self.r + 1) * self.B].tolist()
+
+    def __len__(self):
+        return self.nb * self.B
+
+
 def make_loader(ds, batch_size, num_workers, dp_world, dp_rank, shuffle, seed, device):
-    sampler = None
-    if dp_world > 1:
-        sampler = DistributedSampler(ds, num_replicas=dp_world, rank=dp_rank, shuffle=shuffle, seed=seed)
-        shuffle = False
-    g = torch.Generator().manual_seed(seed)
-    return DataLoader(ds, batch_size=batch_size, shuffle=shuffle, sampler=sampler,
-                      num_workers=num_workers, pin_memory=device.type == "cuda", drop_last=True,
-                      generator=g, persistent_workers=num_workers > 0), sampler
+    sampler = GlobalBatchSampler(len(ds), batch_size, dp_world, dp_rank, shuffle, seed)
+    return DataLoader(ds, batch_size=batch_size, sampler=sampler, num_workers=num_workers,
+                      pin_memory=device.type == "cuda", drop_last=True,
+                      persistent_workers=num_workers > 0), sampler
 
 
 class Trainer:
@@ -122,17 +155,25 @@ class Trainer:
             vsteps = a.eval_steps or max(1, a.val_samples // (a.batch_size * e.dp_world))
 
             class _Epoch:
-                def __init__(self, it, n):
-                    self.it, self.n = it, n
+                """Epoch e of the stream: batches [e * n, (e + 1) * n), positioned by seek, so
+                a mid-epoch resume reads exactly the batches the uninterrupted run would."""
+
+                def __init__(self, loader, n, per_epoch=True):
+                    self.loader, self.n, self.per_epoch = loader, n, per_epoch
+                    self.epoch, self.start = 0, 0
+
+                def position(self, epoch, start=0):
+                    self.epoch, self.start = epoch, start
 
                 def __iter__(self):
-                    return islice(self.it, self.n)
+                    self.loader.seek((self.epoch * self.n if self.per_epoch else 0) + self.start)
+                    return islice(self.loader, self.n - self.start)
 
                 def __len__(self):
-                    return self.n
+                    return self.n - self.start
 
             train_loader, sampler = _Epoch(tl, steps), None
-            val_loader = _Epoch(vl, vsteps)
+            val_loader = _Epoch(vl, vsteps, per_epoch=False)  # the same held-out batches each epoch
         else:
             train_loader, sampler = make_loader(train_ds, a.batch_size, a.num_workers, e.dp_world, e.dp_rank,
                                                 True, a.seed, self.device)
@@ -140,12 +181,15 @@ class Trainer:
                                         False, a.seed, self.device)
         for ei in range(self.start_epoch, a.epochs):
             if sampler is not None:
-                sampler.set_epoch(ei)
-            elif getattr(train_loader, "generator", None) is not None:
                 # the shuffle order is a function of (seed, epoch) alone, so a resumed run sees
                 # the same batches as an uninterrupted one
-                train_loader.generator.manual_seed(a.seed + ei)
-            self.train_epoch(ei, train_loader, skip=self.skip_batches if ei == self.start_epoch else 0)
+                sampler.set_epoch(ei)
+            skip = self.skip_batches if ei == self.start_epoch else 0
+            if hasattr(train_loader, "position"):  # native stream: seek past the trained batches
+                train_loader.position(ei, skip)
+                self.train_epoch(ei, train_loader, skip=skip, preskipped=True)
+            else:
+                self.train_epoch(ei, train_loader, skip=skip)
             self.validate(ei, val_loader)
             if not a.no_generate:
                 self.sample()
@@ -156,7 +200,7 @@ class Trainer:
             path = self.save(a.epochs)
         return path
 
-    def train_epoch(self, ei, loader, skip: int = 0):
+    def train_epoch(self, ei, loader, skip: int = 0, preskipped: bool = False):
         a, e = self.args, self.engine
         e.model.train()  # reference main-single.py:35 / main-ddp.py:109 (dropout on)
         pb = _tqdm(loader, self.log) if self.log else _NoBar(loader)
@@ -165,7 +209,7 @@ class Trainer:
         t0 = time.perf_counter()
         tokens = 0
         prof = StepProfiler(a.profile if ei == self.start_epoch else None, comm.rank())
-        for i, batch in enumerate(pb):
+        for i, batch in enumerate(pb, start=skip if preskipped else 0):
             if a.max_steps and i >= a.max_steps:
                 break
             if i < skip:  # trained before the checkpoint this run resumed from
@@ -246,7 +290,8 @@ class Trainer:
         tstate = self.engine.train_state()
         rngs = comm.gather_objects(rng_state())  # every rank's RNG streams (collective)
         if self.log and sd is not None:
-            path = save_model_state(sd, self.args.checkpoint_dir)
+            # periodic saves carry the step in the name: two within one second never collide
+            path = save_model_state(sd, self.args.checkpoint_dir, step=self.engine.step_count if batch else None)
             tstate = dict(tstate or {})
             tstate.update({"epoch": epoch, "batch": batch, "rng": rng_state(), "rng_per_rank": rngs})
             save_train_state(path, tstate)

@@ -61,66 +61,6 @@ def act_grad_ref(z: torch.Tensor, act: int) -> torch.Tensor:
     return torch.ones_like(z)
 
 
-# Optional vendor path for PLAIN products (no epilogue beyond a scale): hipBLASLt through
-# torch.mm.  OFF by default since round 2: the persistent 4-wave kernel (csrc/gemm7.hip) runs
-# every plain product of the training step -- QKV / out / LM-head forward, the input and weight
-# gradients -- and the GPT-2 small step is as fast without the library (profiles/r2_gemm/).
-# DPC_BLAS_PLAIN=1 restores the library path for comparisons.
-_BLAS_PLAIN = os.environ.get("DPC_BLAS_PLAIN", "0") == "1"
-_BLAS_MIN_FLOP = 2 ** 34  # below ~17 GFLOP the choice does not matter: keep dpc_gemm
-
-
-# hipBLASLt / rocBLAS solution choice for those plain products: PyTorch TunableOp tuned on
-# MI355X over the bench recipes (``scripts/tunableop.sh``), shipped as ``hipblaslt_tuned.csv``
-# and used read-only (no tuning at run time; shapes missing from it use the library default).
-# The file's validator lines pin torch / HIP / hipBLASLt / rocBLAS versions and gfx950, so on
-# any other stack TunableOp ignores it.  GPT-2 small B=64: +0.7 % tokens/s
-# (profiles/r1_v18_tunableop_ab.txt).  DPC_TUNABLEOP=0 disables.
-_TUNABLEOP_CSV = os.path.join(os.path.dirname(os.path.abspath(__file__)), "hipblaslt_tuned.csv")
-_tunableop_done = False
-
-
-def enable_vendor_tuning() -> bool:
-    """Turn on TunableOp with the shipped MI355X results (read-only).  Idempotent; a no-op
-    without a GPU, with DPC_TUNABLEOP=0, or when the environment already configures
-    TunableOp (e.g. a tuning run of scripts/tunableop.sh)."""
-    global _tunableop_done
-    if _tunableop_done:
-        return torch.cuda.tunable.is_enabled()
-    _tunableop_done = True
-    if (os.environ.get("DPC_TUNABLEOP", "1") != "1" or not torch.cuda.is_available()
-            or "PYTORCH_TUNABLEOP_ENABLED" in os.environ or not os.path.exists(_TUNABLEOP_CSV)):
-        return False
-    torch.cuda.tunable.enable(True)
-    torch.cuda.tunable.tuning_enable(False)
-    torch.cuda.tunable.record_untuned_enable(False)
-    torch.cuda.tunable.set_filename(_TUNABLEOP_CSV, insert_device_ordinal=False)
-    return bool(torch.cuda.tunable.read_file(_TUNABLEOP_CSV))
-
-
-def set_blas_plain(on: bool) -> None:
-    global _BLAS_PLAIN
-    _BLAS_PLAIN = bool(on)
-
-
-def _blas_plain(a, b, a_kmaj, b_kmaj, out, M, N, K, alpha, alpha_t) -> bool:
-    """out = alpha (* alpha_t) * A @ B^T through hipBLASLt; False if not applicable."""
-    am = a if a_kmaj else a.t()   # [M, K]
-    bm = b.t() if b_kmaj else b   # [K, N]
-    if (tuple(am.shape) != (M, K) or tuple(bm.shape) != (K, N) or not out.is_contiguous()
-            or 2.0 * M * N * K < _BLAS_MIN_FLOP):
-        return False
-    if out.dtype == torch.bfloat16:
-        torch.mm(am, bm, out=out)
-    else:
-        torch.ops.aten.mm.dtype_out(am, bm, out.dtype, out=out)
-    if alpha != 1.0:
-        out.mul_(alpha)
-    if alpha_t is not None:
-        out.mul_(alpha_t)
-    return True
-
-
 # ---------------------------------------------------------------- measured per-shape choices
 # The dispatcher's built-in policy (csrc/gemm.hip) was fitted to GPT-2 small; on other shapes
 # the best tile / pipeline depends on wave quantisation (tiles vs 256 CUs), the epilogue's
@@ -341,11 +281,6 @@ def gemm(
                 raise ValueError(f"gemm: {nm} must be contiguous-last {dt}")
         if out.dtype not in (torch.float32, torch.bfloat16):
             raise ValueError("gemm: out must be f32 or bf16")
-        plain = (bias is None and residual is None and aux_in is None and aux_out is None
-                 and colsum is None and not act and not act_bwd and not accumulate)
-        if (plain and _BLAS_PLAIN and _lib.forced_gemm_impl < 0
-                and _blas_plain(a, b, a_kmaj, b_kmaj, out, M, N, K, alpha, alpha_t)):
-            return out
         ws = (_workspace(a.device) if (out.dtype == torch.float32 and bias is None and residual is None
                                          and aux_in is None and aux_out is None and colsum is None
                                          and not act and not act_bwd) else None)

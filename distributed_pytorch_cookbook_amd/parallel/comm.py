@@ -72,8 +72,14 @@ def init_dist(force_cpu: bool = False) -> DistInfo:
 
 
 def cleanup_dist() -> None:
+    """Reference ``cleanup_mp`` (``/root/reference/main-ddp.py:34-35``): the engines' native
+    RCCL communicators are destroyed (and their watchdog stopped) before the process group."""
+    from .transport import shutdown_native
+
     if dist.is_initialized():
         dist.barrier()
+    shutdown_native()
+    if dist.is_initialized():
         dist.destroy_process_group()
 
 
@@ -98,6 +104,16 @@ _seq = {}
 def set_coll_check(on: bool) -> None:
     global _CHECK
     _CHECK = bool(on)
+
+
+def coll_check_enabled() -> bool:
+    return _CHECK
+
+
+def fingerprint(op: str, t: torch.Tensor | None, group) -> None:
+    """All-gather this rank's (sequence number, crc32(op, shape, dtype)) for ``group`` and
+    raise on any mismatch (``--coll_check``; used by both transports)."""
+    _fingerprint(op, t, group)
 
 
 def _fingerprint(op: str, t: torch.Tensor | None, group) -> None:

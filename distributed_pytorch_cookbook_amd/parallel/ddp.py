@@ -95,8 +95,8 @@ class DDPStore(LocalStore):
         self._ready[bi] += 1
         # with gradient accumulation (pipeline micro-batches) a unit's backward runs
         # accum_steps times; the bucket is final after the last one
-        if self.overlap and self._ready[bi] == self.accum_steps * len(self.buckets[bi]):
-            self._launch(bi)
+        if self.overlap and self._ready[bi] >= self.accum_steps * len(self.buckets[bi]):
+            self._launch(bi)  # (once: _launch skips a bucket already in flight)
 
     def bucket_range(self, bi):
         return self._range(bi)
@@ -119,6 +119,9 @@ class DDPStore(LocalStore):
         self._works.clear()
         self._tmp.clear()
         self._ready = [0] * len(self.buckets)
+
+    def reset_step_state(self):
+        self.reset_buckets()
 
     def finish_grads(self):
         """Wait for every bucket (launching any not yet launched, e.g. overlap off)."""

@@ -115,7 +115,7 @@ class FSDPStore(ParamStore):
         self._full = {}       # unit -> (buffer, work or None)
         self._vec32 = {}      # unit -> {param id: f32 copy of 1-D params}
         self._gfull = {}      # unit -> f32 full-unit gradient buffer
-        self._rs = {}         # unit -> (handle, tmp or None): reduce-scatters in flight
+        self._rs = {}         # unit -> [(handle, tmp or None), ...]: reduce-scatters in flight
         self._fresh = set(self.units)  # units whose shard gradient holds no contribution yet
         self._in_backward = False
         self.peak_live_units = 0  # most full-unit buffers (weights + gradients) alive at once
@@ -274,13 +274,15 @@ class FSDPStore(ParamStore):
         if self.reduce_dtype != torch.float32:
             g = g.to(self.reduce_dtype)
             tmp = torch.empty(self.shard_len[u], dtype=self.reduce_dtype, device=self.device)
-            self._rs[u] = (self.tp.reduce_scatter(tmp, g, async_op=True), tmp)
+            rs = (self.tp.reduce_scatter(tmp, g, async_op=True), tmp)
         elif u in self._fresh:
             # first contribution since zero_grad: reduce-scatter straight into the shard
-            self._rs[u] = (self.tp.reduce_scatter(out, g, async_op=True), None)
+            rs = (self.tp.reduce_scatter(out, g, async_op=True), None)
         else:
             tmp = torch.empty(self.shard_len[u], dtype=torch.float32, device=self.device)
-            self._rs[u] = (self.tp.reduce_scatter(tmp, g, async_op=True), tmp)
+            rs = (self.tp.reduce_scatter(tmp, g, async_op=True), tmp)
+        # (a list: a unit whose backward runs twice in a step has two in flight, both waited)
+        self._rs.setdefault(u, []).append(rs)
         self._fresh.discard(u)
         # g is dropped here: the transport keeps it alive until the collective has read it
 
@@ -288,10 +290,11 @@ class FSDPStore(ParamStore):
         rep_w = None
         if self.W > 1:
             rep_w = self.tp.all_reduce(self.rep_grads, async_op=True)
-        for u, (w, tmp) in sorted(self._rs.items()):
-            w.wait()
-            if tmp is not None:
-                self.shard(self.grads, u).add_(tmp.float())
+        for u, lst in sorted(self._rs.items()):
+            for w, tmp in lst:
+                w.wait()
+                if tmp is not None:
+                    self.shard(self.grads, u).add_(tmp.float())
         self._rs.clear()
         if rep_w is not None:
             rep_w.wait()
@@ -299,6 +302,16 @@ class FSDPStore(ParamStore):
         # anything still gathered from the forward (e.g. the head) is released now
         for u in list(self._full):
             self._release(u)
+
+    def reset_step_state(self):
+        """After a failed HIP-graph capture: no gathered unit, gradient buffer or
+        reduce-scatter the capture recorded exists (engine/base.py:Engine.reset_step_state)."""
+        self._full.clear()
+        self._vec32.clear()
+        self._gfull.clear()
+        self._rs.clear()
+        self._fresh = set(self.units)
+        self._in_backward = False
 
     def zero_grad(self):
         if self._d2h_done is not None:  # the host optimizer's gradient copies read grads first

@@ -10,10 +10,21 @@ torch's process group only for bootstrap.  This class is that communicator:
 * collectives are enqueued on the caller's current torch stream (or an explicit one) with
   no c10d work objects: all-reduce (DDP buckets), reduce-scatter / all-gather (FSDP
   shards), broadcast (initial weights), grouped send/recv (pipeline activations);
-* ``split`` builds sub-communicators (the PP x DP mesh) with ``ncclCommSplit``.
+* ``split`` builds sub-communicators (the PP x DP mesh) with ``ncclCommSplit``;
+* a native watchdog thread (``rccl_comm.cpp``, ``dpc_wd_*``) follows every collective the
+  transport enqueues with an event, polls those events and ``ncclCommGetAsyncError``, and on
+  a collective pending past ``DPC_COLL_TIMEOUT`` seconds (default 1800, the c10d default the
+  reference relied on) or an RCCL error calls ``ncclCommAbort`` on every communicator and
+  exits the process non-zero (``DPC_WATCHDOG_EXIT``, default 17) -- torchrun then tears the
+  job down (reference: c10d's watchdog + ``destroy_process_group``,
+  ``/root/reference/main-ddp.py:26,34-35``);
+* bring-up is agreed across the group: a rank that cannot load RCCL or draw the unique id
+  still joins the id broadcast (with an error marker) and every rank raises together, so the
+  caller's fallback to torch.distributed is taken by all ranks or none.
 
-The engines use it when ``DPC_COMM=native`` (``--comm native``); the default remains
-torch's ``nccl`` process group, which is RCCL as well.
+Every engine uses this communicator at N > 1 on a GPU by default (``parallel/transport.py``,
+``--comm auto``); ``--comm torch`` selects torch's ``nccl`` process group (RCCL as well).
+``DPC_RCCL_LIB`` / ``DPC_HIP_LIB`` force other RCCL / HIP libraries (the CPU tests' fakes).
 """
 from __future__ import annotations
 
@@ -40,7 +51,17 @@ def _lib():
         h = runtime_lib()
         P, I, S = ctypes.c_void_p, ctypes.c_int, ctypes.c_size_t
         sig = {
-            "dpc_rccl_load": ([ctypes.c_char_p], I),
+            "dpc_rccl_load": ([ctypes.c_char_p, I], I),
+            "dpc_hip_load": ([ctypes.c_char_p, I], I),
+            "dpc_rccl_abort": ([P], I),
+            "dpc_wd_start": ([ctypes.c_double, I, I, I], I),
+            "dpc_wd_running": ([], I),
+            "dpc_wd_register": ([P], None),
+            "dpc_wd_unregister": ([P], None),
+            "dpc_wd_track": ([P, ctypes.c_char_p], I),
+            "dpc_wd_pending": ([], I),
+            "dpc_wd_pause": ([I], None),
+            "dpc_wd_stop": ([], None),
             "dpc_rccl_error": ([], ctypes.c_char_p),
             "dpc_rccl_unique_id": ([ctypes.c_char_p], I),
             "dpc_rccl_init": ([ctypes.c_char_p, I, I, ctypes.POINTER(P)], I),
@@ -59,11 +80,70 @@ def _lib():
         for name, (args, res) in sig.items():
             fn = getattr(h, name)
             fn.argtypes, fn.restype = args, res
-        torch_rccl = os.path.join(os.path.dirname(torch.__file__), "lib", "librccl.so")
-        if h.dpc_rccl_load(torch_rccl.encode()) != 0:
+        tlib = os.path.join(os.path.dirname(torch.__file__), "lib")
+        forced = os.environ.get("DPC_RCCL_LIB")
+        if h.dpc_rccl_load((forced or os.path.join(tlib, "librccl.so")).encode(), 1 if forced else 0) != 0:
             raise RuntimeError(f"native RCCL unavailable: {h.dpc_rccl_error().decode()}")
         _bound = h
     return _bound
+
+
+# ---------------------------------------------------------------- watchdog (rccl_comm.cpp)
+def watchdog_start(rank: int = 0) -> bool:
+    """Start the native collective watchdog once per process (``DPC_WATCHDOG=0`` disables).
+    Returns whether it runs."""
+    if os.environ.get("DPC_WATCHDOG", "1") == "0":
+        return False
+    h = _lib()
+    if h.dpc_wd_running():
+        return True
+    forced = os.environ.get("DPC_HIP_LIB")
+    hip = forced or os.path.join(os.path.dirname(torch.__file__), "lib", "libamdhip64.so")
+    if h.dpc_hip_load(hip.encode(), 1 if forced else 0) != 0:
+        return False
+    timeout = float(os.environ.get("DPC_COLL_TIMEOUT", "1800"))
+    poll_ms = int(os.environ.get("DPC_WATCHDOG_POLL_MS", "200"))
+    code = int(os.environ.get("DPC_WATCHDOG_EXIT", "17"))
+    return h.dpc_wd_start(timeout, poll_ms, rank, code) == 0
+
+
+def watchdog_running() -> bool:
+    return _bound is not None and bool(_bound.dpc_wd_running())
+
+
+def watchdog_track(stream_ptr: int, desc: str) -> None:
+    """Watch the work just enqueued on ``stream_ptr`` (no-op while not running)."""
+    if _bound is not None and _bound.dpc_wd_running():
+        _bound.dpc_wd_track(ctypes.c_void_p(stream_ptr), desc.encode())
+
+
+def watchdog_pause(on: bool) -> None:
+    """Pause the watchdog's HIP calls (around a HIP-graph capture)."""
+    if _bound is not None:
+        _bound.dpc_wd_pause(1 if on else 0)
+
+
+def watchdog_pending() -> int:
+    return int(_bound.dpc_wd_pending()) if _bound is not None else 0
+
+
+def watchdog_stop() -> None:
+    if _bound is not None:
+        _bound.dpc_wd_stop()
+
+
+def _agree(ok: bool, group) -> bool:
+    """Whether every rank of ``group`` reports ``ok`` (one MIN all-reduce over the bootstrap
+    process group; a 1-rank group trivially agrees)."""
+    if not dist.is_initialized() or dist.get_world_size(group) == 1:
+        return ok
+    dev = torch.device("cuda", torch.cuda.current_device()) if dist.get_backend(group) == "nccl" else "cpu"
+    t = torch.tensor([1 if ok else 0], dtype=torch.int32, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MIN, group=group)
+    return bool(t.item())
+
+
+_ERR = b"DPC-ERR:"
 
 
 def _check(rc: int, what: str) -> None:
@@ -79,24 +159,52 @@ class NativeComm:
         if _handle is not None:
             self.comm, self.rank, self.size = _handle, _rank, _size
             return
-        lib = _lib()
         self.rank = dist.get_rank(group)
         self.size = dist.get_world_size(group)
-        if device is not None:
+        if device is not None and torch.device(device).type == "cuda":
             torch.cuda.set_device(device)
-        uid = ctypes.create_string_buffer(128)
+        # 1. library + unique id; rank 0 broadcasts the id or an error marker, so no peer is
+        #    left waiting in the broadcast when rank 0 cannot build one
+        err = None
+        lib = None
+        try:
+            lib = _lib()
+        except Exception as exc:  # noqa: BLE001 -- reported through the agreement below
+            err = str(exc)
+        payload = b""
         if self.rank == 0:
-            _check(lib.dpc_rccl_unique_id(uid), "ncclGetUniqueId")
-        obj = [bytes(uid.raw)]
+            uid = ctypes.create_string_buffer(128)
+            if lib is not None and lib.dpc_rccl_unique_id(uid) == 0:
+                payload = bytes(uid.raw)
+            else:
+                err = err or f"ncclGetUniqueId: {lib.dpc_rccl_error().decode() if lib else '?'}"
+                payload = _ERR + err.encode()[:100]
+        obj = [payload]
         src = dist.get_global_rank(group, 0) if group is not None else 0
         dist.broadcast_object_list(obj, src=src, group=group)
+        if obj[0].startswith(_ERR):
+            err = err or "rank 0: " + obj[0][len(_ERR):].decode(errors="replace")
+        # 2. every rank enters ncclCommInitRank (itself collective) or none does
+        if not _agree(err is None, group):
+            raise RuntimeError(f"native RCCL bring-up refused ({err or 'failed on another rank'})")
         handle = ctypes.c_void_p()
-        _check(lib.dpc_rccl_init(obj[0], self.size, self.rank, ctypes.byref(handle)), "ncclCommInitRank")
+        rc = lib.dpc_rccl_init(obj[0], self.size, self.rank, ctypes.byref(handle))
+        ok = rc == 0
+        if not _agree(ok, group):
+            if ok and handle:
+                lib.dpc_rccl_destroy(handle)
+            raise RuntimeError(f"ncclCommInitRank failed ({lib.dpc_rccl_error().decode() if not ok else 'on another rank'})")
         self.comm = handle
+        if watchdog_start(dist.get_rank()):
+            lib.dpc_wd_register(self.comm)
 
     # ---------------------------------------------------------------- helpers
     @staticmethod
     def _stream(stream) -> int:
+        if isinstance(stream, int):
+            return stream
+        if stream is None and not torch.cuda.is_available():
+            return 0  # host-side fake library (CPU tests)
         s = stream if stream is not None else torch.cuda.current_stream()
         return s.cuda_stream
 
@@ -154,12 +262,18 @@ class NativeComm:
     def split(self, color: int, key: int) -> "NativeComm":
         """Sub-communicator of the ranks sharing ``color`` (ordered by ``key``), collective."""
         out = ctypes.c_void_p()
-        _check(_lib().dpc_rccl_split(self.comm, color, key, ctypes.byref(out)), "ncclCommSplit")
+        rc = _lib().dpc_rccl_split(self.comm, color, key, ctypes.byref(out))
+        if not _agree(rc == 0, self.group):  # every rank keeps its split, or none does
+            if rc == 0 and out:
+                _lib().dpc_rccl_destroy(out)
+            raise RuntimeError(f"ncclCommSplit failed ({_lib().dpc_rccl_error().decode() if rc else 'on another rank'})")
         # size/rank of the new communicator: count colours through the bootstrap group
         colors = [None] * self.size
         dist.all_gather_object(colors, (color, key, self.rank), group=self.group)
         members = sorted((k, r) for c, k, r in colors if c == color)
         rank = [r for _, r in members].index(self.rank)
+        if watchdog_running():
+            _lib().dpc_wd_register(out)
         return NativeComm(self.group, _handle=out, _rank=rank, _size=len(members))
 
     def check_async(self) -> None:
@@ -167,5 +281,13 @@ class NativeComm:
 
     def destroy(self) -> None:
         if self.comm:
+            _lib().dpc_wd_unregister(self.comm)
             _check(_lib().dpc_rccl_destroy(self.comm), "ncclCommDestroy")
+            self.comm = None
+
+    def abort(self) -> None:
+        """ncclCommAbort: tear the communicator down without waiting for peers."""
+        if self.comm:
+            _lib().dpc_wd_unregister(self.comm)
+            _lib().dpc_rccl_abort(self.comm)
             self.comm = None

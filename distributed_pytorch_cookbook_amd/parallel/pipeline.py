@@ -107,6 +107,10 @@ class P2P:
         return (Recv(fp, h, dtype) if fp is not None else None,
                 Recv(fn, h, dtype) if fn is not None else None)
 
+    def reset_step_state(self):
+        """After a failed HIP-graph capture: the recorded sends never ran."""
+        self._inflight.clear()
+
     def drain(self):
         """Order the caller after every send-only exchange still in flight (end of a step:
         device-side for RCCL; for gloo it also keeps the works alive until they complete)."""

@@ -16,9 +16,18 @@ go through a ``Transport``:
   as well) for ``--comm torch``, ``gloo`` for the CPU tests and shared-GPU rehearsals.
 
 ``make_transport`` picks native on a GPU with the nccl backend unless told otherwise, and
-falls back to torch at construction time -- before any collective -- if the native library
-or RCCL cannot be brought up.  torch.distributed stays the bootstrap (rendezvous, the
-``ncclUniqueId`` broadcast) and carries the few host-side scalar reductions.
+falls back to torch if the native library or RCCL cannot be brought up -- on every rank
+together: ``NativeComm`` agrees each bring-up step over the bootstrap group
+(``native_comm._agree``), so no rank is left inside a native collective while another has
+moved on.  torch.distributed stays the bootstrap (rendezvous, the ``ncclUniqueId``
+broadcast) and carries the few host-side scalar reductions.
+
+Safety on the native path: ``--coll_check`` fingerprints every
+native collective over the transport's torch group before it is enqueued (as
+``TorchTransport`` does through ``comm.py``); every enqueued collective is watched by the
+native watchdog (``native_comm.watchdog_*``: deadline + RCCL async errors -> ncclCommAbort
+-> non-zero exit); ``shutdown_native`` -- called by ``comm.cleanup_dist`` -- destroys every
+communicator and stops the watchdog.
 """
 from __future__ import annotations
 
@@ -52,6 +61,10 @@ def set_stream_check(on: bool) -> None:
 
 def stream_check_enabled() -> bool:
     return _STREAM_CHECK
+
+
+def forget_outstanding() -> None:
+    _outstanding.clear()
 
 
 def check_drained(where: str = "end of step") -> None:
@@ -232,6 +245,29 @@ class TorchTransport(Transport):
         return h
 
 
+def _capturing() -> bool:
+    return torch.cuda.is_available() and torch.cuda.is_current_stream_capturing()
+
+
+def shutdown_native() -> None:
+    """Destroy every native communicator (splits first) and stop the watchdog: the native
+    half of the reference's ``destroy_process_group`` (``/root/reference/main-ddp.py:34-35``).
+    Pending collectives are drained first."""
+    if not _native_comms:
+        return
+    from . import native_comm
+
+    if torch.cuda.is_available():
+        torch.cuda.synchronize()
+    native_comm.watchdog_stop()
+    while _native_comms:
+        nc = _native_comms.pop()
+        try:
+            nc.destroy()
+        except Exception as exc:  # noqa: BLE001 -- teardown goes on for the others
+            print(f"[comm] ncclCommDestroy failed: {exc}")
+
+
 class NativeTransport(Transport):
     kind = "native"
 
@@ -243,8 +279,9 @@ class NativeTransport(Transport):
         self.nc = native if native is not None else NativeComm(group, device=self.device)
         self.rank, self.size = self.nc.rank, self.nc.size
         _native_comms.append(self.nc)
-        # RCCL runs on its own high-priority stream, ordered with events
-        self.stream = torch.cuda.Stream(device=self.device, priority=-1)
+        # RCCL runs on its own high-priority stream, ordered with events (a CPU "device" is the
+        # host-side fake library of the CPU tests: calls go straight through)
+        self.stream = torch.cuda.Stream(device=self.device, priority=-1) if self.device.type == "cuda" else None
 
     def capturable(self) -> bool:
         return True
@@ -254,13 +291,24 @@ class NativeTransport(Transport):
         return True
 
     def _enqueue(self, fn, tensors, async_op, op="collective"):
+        from . import native_comm
+
         if _STREAM_CHECK:
             for t in tensors:
                 if not t.is_contiguous() or t.device != self.device:
                     raise RuntimeError(f"stream-order check: {op} buffer {tuple(t.shape)} on {t.device} "
                                        f"(contiguous={t.is_contiguous()}) handed to the comm stream of {self.device}")
-        cur = torch.cuda.current_stream(self.device)
+        capturing = _capturing()
+        if comm.coll_check_enabled() and not capturing:
+            # --coll_check on the production path: every rank's (sequence, op, shape, dtype)
+            comm.fingerprint(op, tensors[0] if tensors else None, self.group)
+        desc = _desc(op, tensors)
         s = self.stream
+        if s is None:  # host-side fake library
+            fn(0)
+            native_comm.watchdog_track(0, desc)
+            return _Done()
+        cur = torch.cuda.current_stream(self.device)
         s.wait_stream(cur)
         with torch.cuda.stream(s):
             fn(s)
@@ -268,7 +316,9 @@ class NativeTransport(Transport):
             t.record_stream(s)
         done = torch.cuda.Event()
         done.record(s)
-        h = _EventHandle(done)._track(_desc(op, tensors))
+        if not capturing:  # (a replayed graph is watched as a whole: GraphedStep)
+            native_comm.watchdog_track(s.cuda_stream, desc)
+        h = _EventHandle(done)._track(desc)
         if not async_op:
             h.wait()
             return _Done()
@@ -335,12 +385,20 @@ def make_mesh_transports(pp_group, dp_group, stage: int, replica: int, device=No
     this replica, color = stage -> the replicas of this stage)."""
     kind = kind or os.environ.get("DPC_COMM", "auto")
     if comm.world_size() > 1 and _want_native(kind, device):
+        built = []
         try:
             world = NativeTransport(None, device)
+            built.append(world)
             pp = world.split(replica, stage, group=pp_group)
+            built.append(pp)
             dp = world.split(stage, replica, group=dp_group)
             return pp, dp
         except Exception as exc:
+            # every bring-up step is agreed (native_comm._agree): all ranks land here together
+            for t in reversed(built):
+                if t.nc in _native_comms:
+                    _native_comms.remove(t.nc)
+                t.nc.destroy()
             if comm.rank() == 0:
                 print(f"[comm] native RCCL mesh unavailable ({exc}); using torch.distributed")
     return TorchTransport(pp_group), TorchTransport(dp_group)

@@ -50,8 +50,13 @@ def build_engine(recipe: str, model, info, args):
     compute_dtype = torch.float32 if args.disable_amp else None
     comm_kind = getattr(args, "comm", "auto")
     # the cookbook's "compile": capture the whole step into a HIP graph (dropout masks are
-    # drawn per step on the host: not graph-replayable)
-    graph = not args.disable_compile and not args.disable_amp and not args.dropout
+    # drawn per step on the host: not graph-replayable).  One rank by default; at N > 1 only
+    # with --graph (RCCL inside a replayed graph has not been run on a multi-GPU node yet, and
+    # bench.py's scaling runs take the same eager path); never under --coll_check, whose
+    # fingerprints are host-synchronous collectives
+    graph = (not args.disable_compile and not args.disable_amp and not args.dropout
+             and (info.world_size == 1 or getattr(args, "graph", False))
+             and not getattr(args, "coll_check", False))
     if recipe in ("single", "ddp"):
         from .engine.data_parallel import DataParallelEngine
 
@@ -74,7 +79,7 @@ def build_engine(recipe: str, model, info, args):
         pp, dp = pipe_mesh(recipe, info.world_size, args.pp_size, getattr(args, "dp_size", 0))
         wire = {"fp32": None, "bf16": torch.bfloat16}[getattr(args, "pp_comm_dtype", "fp32")]
         return PipelineEngine(model, info.device, lr=args.learning_rate, pp=pp, dp=dp,
-                              num_microbatches=args.num_microbatches or (4 * pp if pp > 1 else 1),
+                              num_microbatches=args.num_microbatches,
                               schedule=args.schedule, bucket_mb=args.bucket_mb,
                               compute_dtype=compute_dtype, grad_scaler=getattr(args, "grad_scaler", False),
                               comm_kind=comm_kind, wire_dtype=wire, graph=graph)

@@ -37,6 +37,7 @@ def lib():
                 h.dpc_loader_next.argtypes = [c_void_p, c_void_p]
                 h.dpc_loader_next.restype = c_int64
                 h.dpc_loader_destroy.argtypes = [c_void_p]
+                h.dpc_loader_seek.argtypes = [c_void_p, c_int64]
                 h.dpc_synth_markov.argtypes = [c_void_p, c_int64, c_int, c_int, c_uint64, c_int, c_int64]
                 h.dpc_adamw_host.argtypes = [c_void_p, c_void_p, c_void_p, c_void_p, c_int64] + [c_float] * 8 + [c_void_p]
                 _lib = h
@@ -109,6 +110,10 @@ class NativeBatchLoader:
         lib().dpc_loader_next(self.h, self.buf.data_ptr())
         ids = self.buf.clone()
         return {"input_ids": ids, "attention_mask": torch.ones_like(ids)}
+
+    def seek(self, batch_index: int) -> None:
+        """Continue the stream at ``batch_index`` (nothing before it is loaded)."""
+        lib().dpc_loader_seek(self.h, int(batch_index))
 
     def close(self):
         if self.h:

@@ -13,7 +13,17 @@
 #include <dlfcn.h>
 #include <stddef.h>
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
+#include <unistd.h>
+
+#include <atomic>
+#include <chrono>
+#include <deque>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <vector>
 
 #define DPC_API extern "C" __attribute__((visibility("default")))
 
@@ -29,6 +39,7 @@ struct ncclUniqueId {
 typedef ncclResult_t (*get_unique_id_t)(ncclUniqueId*);
 typedef ncclResult_t (*comm_init_rank_t)(ncclComm_t*, int, ncclUniqueId, int);
 typedef ncclResult_t (*comm_destroy_t)(ncclComm_t);
+typedef ncclResult_t (*comm_abort_t)(ncclComm_t);
 typedef ncclResult_t (*comm_split_t)(ncclComm_t, int, int, ncclComm_t*, void*);
 typedef ncclResult_t (*comm_async_error_t)(ncclComm_t, ncclResult_t*);
 typedef const char* (*error_string_t)(ncclResult_t);
@@ -45,6 +56,7 @@ struct Rccl {
   get_unique_id_t get_unique_id = nullptr;
   comm_init_rank_t comm_init_rank = nullptr;
   comm_destroy_t comm_destroy = nullptr;
+  comm_abort_t comm_abort = nullptr;
   comm_split_t comm_split = nullptr;
   comm_async_error_t comm_async_error = nullptr;
   error_string_t error_string = nullptr;
@@ -60,6 +72,7 @@ struct Rccl {
 
 Rccl g;
 char g_err[512];
+constexpr ncclResult_t kInProgress = 7;  // ncclInProgress: a non-blocking call still running
 
 template <typename F>
 bool sym(F& f, const char* name) {
@@ -71,10 +84,11 @@ bool sym(F& f, const char* name) {
 }  // namespace
 
 // Resolve RCCL: prefer the copy already mapped into the process (torch's), else dlopen(path).
-// Returns 0 on success; dpc_rccl_error() explains a failure.
-DPC_API int dpc_rccl_load(const char* path) {
+// force != 0: dlopen(path) only (the CPU tests' fake library).  Returns 0 on success;
+// dpc_rccl_error() explains a failure.
+DPC_API int dpc_rccl_load(const char* path, int force) {
   if (g.handle) return 0;
-  void* h = dlopen("librccl.so", RTLD_NOW | RTLD_NOLOAD);
+  void* h = force ? nullptr : dlopen("librccl.so", RTLD_NOW | RTLD_NOLOAD);
   if (!h && path && *path) h = dlopen(path, RTLD_NOW | RTLD_GLOBAL);
   if (!h) {
     snprintf(g_err, sizeof(g_err), "cannot load RCCL (%s): %s", path ? path : "", dlerror());
@@ -82,7 +96,8 @@ DPC_API int dpc_rccl_load(const char* path) {
   }
   g.handle = h;
   bool ok = sym(g.get_unique_id, "ncclGetUniqueId") && sym(g.comm_init_rank, "ncclCommInitRank") &&
-            sym(g.comm_destroy, "ncclCommDestroy") && sym(g.comm_async_error, "ncclCommGetAsyncError") &&
+            sym(g.comm_destroy, "ncclCommDestroy") && sym(g.comm_abort, "ncclCommAbort") &&
+            sym(g.comm_async_error, "ncclCommGetAsyncError") &&
             sym(g.error_string, "ncclGetErrorString") && sym(g.all_reduce, "ncclAllReduce") &&
             sym(g.reduce_scatter, "ncclReduceScatter") && sym(g.all_gather, "ncclAllGather") &&
             sym(g.broadcast, "ncclBroadcast") && sym(g.send, "ncclSend") && sym(g.recv, "ncclRecv") &&
@@ -131,11 +146,13 @@ DPC_API int dpc_rccl_split(void* comm, int color, int key, void** out) {
 
 DPC_API int dpc_rccl_destroy(void* comm) { return g.handle ? check(g.comm_destroy(comm), "ncclCommDestroy") : -1; }
 
+DPC_API int dpc_rccl_abort(void* comm) { return g.handle ? check(g.comm_abort(comm), "ncclCommAbort") : -1; }
+
 DPC_API int dpc_rccl_async_error(void* comm) {
   if (!g.handle) return -1;
   ncclResult_t e = 0;
   const int r = g.comm_async_error(comm, &e);
-  return r ? r : check(e, "async");
+  return r ? r : (e == kInProgress ? 0 : check(e, "async"));
 }
 
 DPC_API int dpc_rccl_all_reduce(void* comm, const void* send, void* recv, size_t count, int dtype, int op,
@@ -168,3 +185,223 @@ DPC_API int dpc_rccl_recv(void* comm, void* buf, size_t count, int dtype, int pe
 
 DPC_API int dpc_rccl_group_start() { return g.handle ? check(g.group_start(), "ncclGroupStart") : -1; }
 DPC_API int dpc_rccl_group_end() { return g.handle ? check(g.group_end(), "ncclGroupEnd") : -1; }
+
+// ---------------------------------------------------------------- collective watchdog
+// the reference gets a c10d watchdog and destroy_process_group
+// (/root/reference/main-ddp.py:26,34-35).  The engines' collectives bypass c10d, so this
+// thread is their watchdog: every collective the transport enqueues is followed by an event
+// on the comm stream (dpc_wd_track); the thread polls those events (hipEventQuery) and every
+// registered communicator's asynchronous error (ncclCommGetAsyncError).  A collective still
+// pending after the deadline, or an RCCL error, aborts every registered communicator
+// (ncclCommAbort, which also releases kernels spinning on a dead peer) and ends the process
+// with a non-zero status, so torchrun tears the job down instead of hanging forever.  It never
+// restarts anything itself.  HIP is resolved like RCCL (the runtime torch already mapped), so
+// this library still links neither.
+namespace {
+
+typedef int hipError_t;
+typedef void* hipEvent_t;
+typedef hipError_t (*ev_create_t)(hipEvent_t*, unsigned);
+typedef hipError_t (*ev_record_t)(hipEvent_t, hipStream_t);
+typedef hipError_t (*ev_query_t)(hipEvent_t);
+typedef hipError_t (*ev_destroy_t)(hipEvent_t);
+
+struct Hip {
+  void* handle = nullptr;
+  ev_create_t create = nullptr;
+  ev_record_t record = nullptr;
+  ev_query_t query = nullptr;
+  ev_destroy_t destroy = nullptr;
+};
+Hip gh;
+constexpr hipError_t kHipNotReady = 600;
+constexpr unsigned kEventDisableTiming = 2;
+
+struct Pending {
+  hipEvent_t ev;
+  std::chrono::steady_clock::time_point t0;
+  std::string desc;
+};
+
+struct Watchdog {
+  std::mutex mu;
+  std::deque<Pending> q;
+  std::vector<hipEvent_t> pool;  // completed events, re-recorded instead of re-created
+  std::vector<ncclComm_t> comms;
+  std::thread th;
+  std::atomic<bool> running{false};
+  std::atomic<int> paused{0};
+  double timeout_s = 1800.0;
+  int poll_ms = 100;
+  int exit_code = 17;
+  int rank = 0;
+};
+// Never destroyed: the thread may outlive static destruction.  An atexit hook registered at
+// start (so it runs BEFORE the HIP runtime's own teardown, registered earlier) joins it.
+Watchdog& wd = *new Watchdog;
+
+[[noreturn]] void wd_fire(const std::string& why) {
+  fprintf(stderr, "[dpc watchdog] rank %d: %s; aborting %zu RCCL communicator(s) and exiting with status %d\n",
+          wd.rank, why.c_str(), wd.comms.size(), wd.exit_code);
+  fflush(stderr);
+  // ncclCommAbort can itself wait on a wedged device: give it a bounded time, then leave anyway
+  std::vector<ncclComm_t> comms = wd.comms;
+  std::atomic<bool> done{false};
+  std::thread ab([&comms, &done] {
+    for (ncclComm_t c : comms)
+      if (g.comm_abort) g.comm_abort(c);
+    done = true;
+  });
+  ab.detach();
+  for (int i = 0; i < 100 && !done; ++i) std::this_thread::sleep_for(std::chrono::milliseconds(100));
+  fprintf(stderr, "[dpc watchdog] rank %d: communicators %s\n", wd.rank, done ? "aborted" : "abort timed out");
+  fflush(stderr);
+  _exit(wd.exit_code);
+}
+
+void wd_loop() {
+  while (wd.running) {
+    std::this_thread::sleep_for(std::chrono::milliseconds(wd.poll_ms));
+    if (wd.paused) continue;  // a HIP-graph capture is running: no HIP calls from this thread
+    std::string why;
+    {
+      std::lock_guard<std::mutex> lk(wd.mu);
+      const auto now = std::chrono::steady_clock::now();
+      for (auto it = wd.q.begin(); it != wd.q.end();) {
+        const hipError_t r = gh.query(it->ev);
+        if (r == 0) {
+          wd.pool.push_back(it->ev);
+          it = wd.q.erase(it);
+          continue;
+        }
+        const double age = std::chrono::duration<double>(now - it->t0).count();
+        if (r != kHipNotReady) {
+          why = "HIP error " + std::to_string(r) + " waiting for " + it->desc;
+          break;
+        }
+        if (age > wd.timeout_s) {
+          char b[96];
+          snprintf(b, sizeof(b), " still pending after %.1f s (timeout %.1f s)", age, wd.timeout_s);
+          why = "collective " + it->desc + b;
+          break;
+        }
+        ++it;
+      }
+      if (why.empty() && g.comm_async_error) {
+        for (ncclComm_t c : wd.comms) {
+          ncclResult_t e = 0;
+          if (g.comm_async_error(c, &e) == 0 && e != 0 && e != kInProgress) {
+            why = std::string("RCCL asynchronous error: ") + (g.error_string ? g.error_string(e) : "?");
+            break;
+          }
+        }
+      }
+    }
+    if (!why.empty()) wd_fire(why);
+  }
+}
+
+}  // namespace
+
+// Resolve the HIP event entry points (the runtime already in the process unless force).
+DPC_API int dpc_hip_load(const char* path, int force) {
+  if (gh.handle) return 0;
+  void* h = force ? nullptr : dlopen("libamdhip64.so", RTLD_NOW | RTLD_NOLOAD);
+  if (!h && path && *path) h = dlopen(path, RTLD_NOW | RTLD_GLOBAL);
+  if (!h) {
+    snprintf(g_err, sizeof(g_err), "cannot load HIP (%s): %s", path ? path : "", dlerror());
+    return 1;
+  }
+  gh.handle = h;
+  gh.create = reinterpret_cast<ev_create_t>(dlsym(h, "hipEventCreateWithFlags"));
+  gh.record = reinterpret_cast<ev_record_t>(dlsym(h, "hipEventRecord"));
+  gh.query = reinterpret_cast<ev_query_t>(dlsym(h, "hipEventQuery"));
+  gh.destroy = reinterpret_cast<ev_destroy_t>(dlsym(h, "hipEventDestroy"));
+  if (!gh.create || !gh.record || !gh.query || !gh.destroy) {
+    snprintf(g_err, sizeof(g_err), "HIP event entry points not found");
+    gh = Hip();
+    return 2;
+  }
+  return 0;
+}
+
+static void dpc_wd_stop_at_exit() {
+  if (!wd.running) return;
+  wd.running = false;
+  if (wd.th.joinable()) wd.th.join();
+}
+
+// Start the watchdog thread (idempotent; the first call's settings hold).
+DPC_API int dpc_wd_start(double timeout_s, int poll_ms, int rank, int exit_code) {
+  if (!gh.handle) return -1;
+  std::lock_guard<std::mutex> lk(wd.mu);
+  if (wd.running) return 0;
+  wd.timeout_s = timeout_s;
+  wd.poll_ms = poll_ms > 0 ? poll_ms : 100;
+  wd.rank = rank;
+  wd.exit_code = exit_code;
+  wd.running = true;
+  wd.th = std::thread(wd_loop);
+  static bool hooked = false;
+  if (!hooked) {
+    hooked = true;
+    atexit(dpc_wd_stop_at_exit);
+  }
+  return 0;
+}
+
+DPC_API int dpc_wd_running() { return wd.running ? 1 : 0; }
+
+DPC_API void dpc_wd_register(void* comm) {
+  std::lock_guard<std::mutex> lk(wd.mu);
+  wd.comms.push_back(comm);
+}
+
+DPC_API void dpc_wd_unregister(void* comm) {
+  std::lock_guard<std::mutex> lk(wd.mu);
+  for (auto it = wd.comms.begin(); it != wd.comms.end(); ++it)
+    if (*it == comm) {
+      wd.comms.erase(it);
+      break;
+    }
+}
+
+// Record an event behind the work just enqueued on `stream` and watch it.  Not during a
+// stream capture (the caller checks): the event would become a graph node.
+DPC_API int dpc_wd_track(void* stream, const char* desc) {
+  if (!wd.running) return -1;
+  std::lock_guard<std::mutex> lk(wd.mu);
+  hipEvent_t ev = nullptr;
+  if (!wd.pool.empty()) {
+    ev = wd.pool.back();
+    wd.pool.pop_back();
+  } else if (gh.create(&ev, kEventDisableTiming) != 0) {
+    return -2;
+  }
+  if (gh.record(ev, stream) != 0) {
+    gh.destroy(ev);
+    return -3;
+  }
+  wd.q.push_back(Pending{ev, std::chrono::steady_clock::now(), desc ? desc : "collective"});
+  return 0;
+}
+
+DPC_API int dpc_wd_pending() {
+  std::lock_guard<std::mutex> lk(wd.mu);
+  return (int)wd.q.size();
+}
+
+// pause != 0 while a HIP graph is being captured (no HIP call from the watchdog thread then)
+DPC_API void dpc_wd_pause(int pause) { wd.paused = pause; }
+
+DPC_API void dpc_wd_stop() {
+  if (!wd.running) return;
+  wd.running = false;
+  if (wd.th.joinable()) wd.th.join();
+  std::lock_guard<std::mutex> lk(wd.mu);
+  for (auto& p : wd.q) gh.destroy(p.ev);
+  for (hipEvent_t e : wd.pool) gh.destroy(e);
+  wd.q.clear();
+  wd.pool.clear();
+  wd.comms.clear();
+}

@@ -84,7 +84,7 @@ struct Loader {
       fill(bi, buf.data());
       {
         std::lock_guard<std::mutex> lk(mu);
-        ready.emplace_back(bi, std::move(buf));
+        if (bi >= next_to_take) ready.emplace_back(bi, std::move(buf));  // (else: made before a seek)
       }
       cv_full.notify_all();
     }
@@ -168,6 +168,19 @@ API int64_t dpc_loader_next(void* h, int64_t* out) {
   L->cv_space.notify_all();
   std::memcpy(out, data.data(), data.size() * sizeof(int64_t));
   return (int64_t)want;
+}
+
+// Position the stream at batch `bi` (batch contents are a pure function of their index, so a
+// resumed run reads exactly the batches an uninterrupted one would, without loading the
+// skipped ones).
+API void dpc_loader_seek(void* h, int64_t bi) {
+  auto* L = static_cast<Loader*>(h);
+  {
+    std::lock_guard<std::mutex> lk(L->mu);
+    L->ready.clear();
+    L->next_to_make = L->next_to_take = (uint64_t)(bi < 0 ? 0 : bi);
+  }
+  L->cv_space.notify_all();
 }
 
 API void dpc_loader_destroy(void* h) {

@@ -35,15 +35,26 @@ def canonical_key(k: str) -> str:
     return k
 
 
-def checkpoint_path(directory: str = "checkpoints", stamp: str | None = None) -> Path:
+def checkpoint_path(directory: str = "checkpoints", stamp: str | None = None, step: int | None = None) -> Path:
+    """``checkpoint-<%Y-%m-%d_%H-%M-%S>[_step<N>].pt`` -- the reference's name, plus the
+    optimizer step for periodic saves; an existing file is never overwritten (a ``.<n>``
+    suffix is added instead)."""
     d = Path(directory)
     d.mkdir(parents=True, exist_ok=True)
     stamp = stamp or datetime.now().strftime("%Y-%m-%d_%H-%M-%S")
-    return d / f"checkpoint-{stamp}.pt"
+    if step is not None:
+        stamp = f"{stamp}_step{step}"
+    path = d / f"checkpoint-{stamp}.pt"
+    n = 1
+    while path.exists():
+        path = d / f"checkpoint-{stamp}.{n}.pt"
+        n += 1
+    return path
 
 
-def save_model_state(state: dict, directory: str = "checkpoints", stamp: str | None = None) -> Path:
-    path = checkpoint_path(directory, stamp)
+def save_model_state(state: dict, directory: str = "checkpoints", stamp: str | None = None,
+                     step: int | None = None) -> Path:
+    path = checkpoint_path(directory, stamp, step)
     cpu = {canonical_key(k): v.detach().to("cpu", copy=True).contiguous() for k, v in state.items()}
     tmp = path.with_suffix(".pt.tmp")
     torch.save(cpu, tmp)
@@ -80,7 +91,7 @@ def latest_checkpoint(directory: str = "checkpoints") -> Path | None:
     files = [f for f in glob.glob(os.path.join(directory, "checkpoint-*.pt")) if not f.endswith(".train.pt")]
     if not files:
         return None
-    return Path(max(files, key=os.path.getmtime))
+    return Path(max(files, key=lambda f: (os.stat(f).st_mtime_ns, f)))
 
 
 def rng_state() -> dict:

@@ -201,3 +201,145 @@ def worker_stream_check(rank, world, out, kind):
     transport.check_drained("after the wait")  # nothing outstanding now
     if rank == 0:
         torch.save({"caught": caught}, out)
+
+
+# ---------------------------------------------------------------- native communicator safety
+def _use_fake(fake):
+    import os
+
+    os.environ["DPC_RCCL_LIB"] = fake
+    os.environ["DPC_HIP_LIB"] = fake
+    os.environ["DPC_WATCHDOG"] = "0"
+
+
+def worker_native_fingerprint(rank, world, fake, log):
+    """--coll_check on the NATIVE transport (the production path at N > 1): a rank enqueuing a
+    differently shaped collective is caught before RCCL ever sees it."""
+    import os
+
+    _use_fake(fake)
+    os.environ["FAKE_LOG"] = f"{log}.{rank}"
+    from distributed_pytorch_cookbook_amd.parallel import comm
+    from distributed_pytorch_cookbook_amd.parallel.transport import NativeTransport
+
+    comm.init_dist(force_cpu=True)
+    comm.set_coll_check(True)
+    tp = NativeTransport(None, device="cpu")
+    assert tp.kind == "native" and (tp.rank, tp.size) == (rank, world)
+    tp.all_reduce(torch.ones(4))  # matched: reaches the (fake) RCCL
+    tp.all_gather(torch.empty(8), torch.ones(4))
+    try:
+        tp.all_reduce(torch.ones(4 + rank))  # rank 1 differs
+    except RuntimeError as exc:
+        assert "collective mismatch" in str(exc), exc
+        return
+    raise AssertionError("mismatched native collective was not detected")
+
+
+def worker_native_agreement(rank, world, fake, mode, log):
+    """Native bring-up fails on ONE rank (rank 0 cannot draw the unique id, or rank 1's
+    ncclCommInitRank fails): every rank refuses together -- nobody is left inside a native
+    collective -- and the process group still works for the torch fallback."""
+    import os
+
+    import torch.distributed as dist
+
+    _use_fake(fake)
+    os.environ["FAKE_LOG"] = f"{log}.{rank}"
+    if mode == "uid" and rank == 0:
+        os.environ["FAKE_UID_FAIL"] = "1"
+    if mode == "init" and rank == 1:
+        os.environ["FAKE_INIT_FAIL"] = "1"
+    from distributed_pytorch_cookbook_amd.parallel import comm
+    from distributed_pytorch_cookbook_amd.parallel.native_comm import NativeComm
+
+    comm.init_dist(force_cpu=True)
+    try:
+        NativeComm(None, device="cpu")
+    except RuntimeError:
+        pass
+    else:
+        raise AssertionError("expected every rank to refuse the native communicator")
+    t = torch.ones(1)
+    dist.all_reduce(t)
+    assert t.item() == world
+
+
+class _FailingCapture:
+    """Stands in for ``torch.cuda.graph`` on CPU: the step body runs (as recording would)
+    until the point where the gradient collectives have been launched, then the 'capture'
+    fails, exactly as a capture error would surface on the GPU."""
+
+    def __init__(self, eng):
+        self.eng = eng
+        self.saved = []
+
+    def _boom(self, *a, **k):
+        raise RuntimeError("simulated HIP-graph capture failure")
+
+    def __enter__(self):
+        st = self.eng.store
+        tgt = st if hasattr(st, "finish_grads") and getattr(st, "tp", None) is not None else self.eng.p2p
+        name = "finish_grads" if tgt is st else "drain"
+        self.saved.append((tgt, name))
+        setattr(tgt, name, self._boom)
+        return self
+
+    def __exit__(self, *exc):
+        for tgt, name in self.saved:
+            delattr(tgt, name)  # back to the class method
+        # on the GPU nothing a failed capture recorded ever runs; on CPU the collectives the
+        # body issued did run: let them finish before the retry, or they would race with it
+        st, p2p = self.eng.store, getattr(self.eng, "p2p", None)
+        for h in list(getattr(st, "_works", {}).values()):
+            h.wait()
+        for lst in getattr(st, "_rs", {}).values():
+            for h, _ in lst:
+                h.wait()
+        for _, w in getattr(st, "_full", {}).values():
+            if w is not None:
+                w.wait()
+        for h in getattr(p2p, "_inflight", []):
+            h.wait()
+        return False
+
+
+def worker_capture_fallback(rank, world, out, kind, inject, no_reset):
+    """Three steps of an engine whose HIP-graph capture (step 2) fails part-way: the eager
+    retry must give exactly the parameters of a never-graphed run."""
+    from distributed_pytorch_cookbook_amd.engine.base import Engine
+    from distributed_pytorch_cookbook_amd.parallel import comm
+
+    comm.init_dist(force_cpu=True)
+    if no_reset:  # negative control: the fallback without forgetting the failed step's state
+        Engine.reset_step_state = lambda self: None
+    m = make_model()
+    if kind == "ddp":
+        from distributed_pytorch_cookbook_amd.engine.data_parallel import DataParallelEngine
+
+        eng = DataParallelEngine(m, "cpu", lr=LR, bucket_mb=0.02)
+        dp, idx = world, rank
+    elif kind == "fsdp":
+        from distributed_pytorch_cookbook_amd.engine.fsdp import FSDPEngine
+
+        eng = FSDPEngine(m, "cpu", lr=LR, prefetch=1)
+        dp, idx = world, rank
+    else:
+        from distributed_pytorch_cookbook_amd.engine.pipeline import PipelineEngine
+
+        pp = 2
+        eng = PipelineEngine(m, "cpu", lr=LR, pp=pp, dp=world // pp, num_microbatches=2, bucket_mb=0.01, seq_len=S)
+        dp, idx = world // pp, eng.replica
+    if inject:
+        eng.graph = True
+        st = eng._stepper
+        st._new_graph = lambda: object()
+        st._capture = lambda g, mode: _FailingCapture(eng)
+    for s in range(3):
+        b, t = shard(*full_batch(step=s), idx, dp)
+        eng.train_step(b, t)
+    if inject:
+        assert not eng._stepper.enabled  # it fell back to eager steps
+    sd = eng.full_state_dict()
+    if rank == 0:
+        torch.save({k: v.clone() for k, v in sd.items()}, out)

@@ -542,28 +542,6 @@ def test_dropout_kernels_match_torch_twin():
     assert torch.equal(dz == 0, (ref == 0))
 
 
-@pytest.mark.parametrize("out_dtype", [torch.bfloat16, torch.float32])
-@pytest.mark.parametrize("b_kmaj", [True, False])
-def test_plain_gemm_vendor_path_matches_kernel(out_dtype, b_kmaj):
-    """Large plain products go to hipBLASLt (ops/gemm.py _blas_plain); same result as dpc_gemm."""
-    from distributed_pytorch_cookbook_amd.ops.gemm import set_blas_plain
-
-    torch.manual_seed(3)
-    M, N, K = 4096, 2304, 2048
-    a = torch.randn(M, K, device=dev).bfloat16()
-    b = torch.randn(N, K, device=dev).bfloat16() if b_kmaj else torch.randn(K, N, device=dev).bfloat16()
-    scale = torch.tensor(0.37, device=dev)
-    outs = []
-    for on in (True, False):
-        set_blas_plain(on)
-        try:
-            outs.append(gemm(a, b, b_kmaj=b_kmaj, out_dtype=out_dtype, alpha=2.0, alpha_t=scale))
-        finally:
-            set_blas_plain(True)
-    ref = 2.0 * 0.37 * (a.float() @ (b.float().t() if b_kmaj else b.float()))
-    assert rel_err(outs[0], ref) < 1e-2 and rel_err(outs[1], ref) < 1e-2
-
-
 @pytest.mark.parametrize("D,p_drop", [(768, 0.0), (1600, 0.0), (768, 0.1)])
 def test_layernorm_fwd_fused_residual_add(D, p_drop):
     """LN forward with the projection's bias + dropout + residual add fused in:

@@ -5,6 +5,7 @@ must match autograd through the reference math (``reference_forward`` +
 ``F.cross_entropy``) -- this is the oracle for the hand-derived backward.
 """
 import copy
+import os
 
 import pytest
 import torch
@@ -232,3 +233,86 @@ def test_kv_cache_decode_matches_recompute(act):
             assert torch.allclose(lg, ref, atol=1e-4, rtol=1e-4), end
     tok, cpu = ByteTokenizer(), torch.device("cpu")
     assert generate(m, "One day, ", tok, cpu, 8) == generate(m, "One day, ", tok, cpu, 8, use_cache=False)
+
+
+# ---------------------------------------------------------------- parity with the reference module
+_REF_GPT = "/root/reference/models/gpt.py"
+
+
+def _reference_module():
+    """``/root/reference/models/gpt.py`` as shipped, with its two documented one-line crash
+    fixes applied in memory (``self.dim`` read before it is set,
+    ``:177-178``; undefined ``x`` in ``forward``, ``:227``)."""
+    import types
+
+    if not os.path.exists(_REF_GPT):
+        pytest.skip("reference checkout not present")
+    pytest.importorskip("einops")
+    src = open(_REF_GPT).read()
+    for bad, good in (("nn.Embedding(vocab_size, self.dim)", "nn.Embedding(vocab_size, dim)"),
+                      ("nn.Embedding(max_position_embeddings, self.dim)", "nn.Embedding(max_position_embeddings, dim)"),
+                      ("x = self.embeddings(x, position_ids)", "x = self.embeddings(input_ids, position_ids)")):
+        assert src.count(bad) == 1, bad
+        src = src.replace(bad, good)
+    mod = types.ModuleType("reference_models_gpt")
+    exec(compile(src, _REF_GPT, "exec"), mod.__dict__)
+    return mod
+
+
+def test_parity_with_reference_module():
+    """The reference's own TransformerDecoderLM (bugs fixed) vs ours: identical state-dict
+    keys and shapes, logits with and without a key-padding mask, and every parameter gradient
+    of the cross-entropy loss (fused path, manual backward)."""
+    ref_mod = _reference_module()
+    D, hd, H, L, V, S = 64, 16, 4, 2, 97, 24
+    torch.manual_seed(0)
+    ref = ref_mod.TransformerDecoderLM(dim=D, head_dim=hd, heads=H, num_layers=L, vocab_size=V,
+                                       max_position_embeddings=S).eval()
+    ours = TransformerDecoderLM(dim=D, head_dim=hd, heads=H, num_layers=L, vocab_size=V,
+                                max_position_embeddings=S)
+    rsd = ref.state_dict()
+    assert list(rsd) == list(ours.state_dict())
+    assert all(rsd[k].shape == v.shape for k, v in ours.state_dict().items())
+    ours.load_state_dict(rsd)
+    for pad in (False, True):
+        ids, pos, mask, tg = batch(pad=pad)
+        with torch.no_grad():
+            want = ref(ids, pos, mask)
+            got = ours(ids, pos, mask)
+        rows = ~mask if mask is not None else torch.ones(ids.shape, dtype=torch.bool)
+        assert torch.allclose(got[rows], want[rows], atol=2e-5, rtol=1e-5), (got[rows] - want[rows]).abs().max()
+    # gradients
+    ids, pos, mask, tg = batch(pad=True)
+    store = LocalStore(ours, "cpu")
+    store.zero_grad()
+    ours(ids, pos, mask, targets=tg).loss.backward()
+    logits = ref(ids, pos, mask)
+    F.cross_entropy(logits.reshape(-1, V), tg.reshape(-1), ignore_index=-100).backward()
+    gp = dict(ours.named_parameters())
+    for n, p in ref.named_parameters():
+        err = (gp[n].grad - p.grad).norm() / p.grad.norm().clamp_min(1e-12)
+        assert err < 1e-4, (n, err.item())
+
+
+@pytest.mark.parametrize("prefix", ["module.", "_orig_mod.", "_orig_mod.module."])
+def test_reference_checkpoint_prefixes_round_trip(tmp_path, prefix):
+    """A state dict saved by the reference's recipes -- DDP (``module.``), torch.compile
+    (``_orig_mod.``) or both (``main-ddp.py:179-185``) -- loads into an engine through the
+    checkpoint reader, and our saved file has the canonical bare keys."""
+    from distributed_pytorch_cookbook_amd.engine.data_parallel import DataParallelEngine
+    from distributed_pytorch_cookbook_amd.utils.checkpoint import load_model_state, save_model_state
+
+    ref_mod = _reference_module()
+    torch.manual_seed(1)
+    ref = ref_mod.TransformerDecoderLM(dim=32, head_dim=16, heads=2, num_layers=2, vocab_size=97,
+                                       max_position_embeddings=24)
+    path = tmp_path / "ref.pt"
+    torch.save({prefix + k: v for k, v in ref.state_dict().items()}, path)
+    eng = DataParallelEngine(tiny(D=32, H=2, hd=16), "cpu", lr=1e-3)
+    eng.load_model_state(load_model_state(path))
+    sd = eng.full_state_dict()
+    for k, v in ref.state_dict().items():
+        assert torch.equal(sd[k], v), k
+    out = save_model_state(sd, str(tmp_path / "ck"))
+    back = torch.load(out, weights_only=True)
+    assert list(back) == list(ref.state_dict())
