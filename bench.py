@@ -65,6 +65,10 @@ def main():
     ap.add_argument("--no_graph", action="store_true", help="eager steps (no HIP-graph capture)")
     ap.add_argument("--graph", action="store_true",
                     help="HIP-graph capture also at N > 1 (default: only at N = 1)")
+    ap.add_argument("--force_dist_path", action="store_true",
+                    help="one rank on the engines' N > 1 code path over a native 1-rank RCCL communicator "
+                         "(bucketed DDP store / sharded FSDP store / replica DDP store): profiles that path "
+                         "on one GPU; the result is not the headline number")
     ap.add_argument("--json", default=None, help="also write the result line to this file")
     a = ap.parse_args()
 
@@ -96,14 +100,14 @@ def main():
     apply_preset(args)
     args.sequence_length = a.seq_len
 
-    info = comm.init_dist()
+    info = comm.init_dist(force_group=a.force_dist_path)
     if info.world_size != a.gpus and info.is_main:
         print(f"warning: --gpus {a.gpus} but WORLD_SIZE {info.world_size}", file=sys.stderr)
     from distributed_pytorch_cookbook_amd.recipes import build_engine, build_model
 
     vocab = 50257
     model = build_model(args, vocab, info.device)
-    engine = build_engine(rec, model, info, args)
+    engine = build_engine(rec, model, info, args, force_dist=a.force_dist_path)
 
     # synthetic batches: a small pool of distinct random token batches per DP replica
     S = a.seq_len
@@ -145,7 +149,7 @@ def main():
         torch.cuda.synchronize()
     dt = time.perf_counter() - t0
     dt_t = torch.tensor([dt], dtype=torch.float64, device=info.device)
-    if info.world_size > 1:
+    if info.world_size > 1 or a.force_dist_path:
         torch.distributed.all_reduce(dt_t, op=torch.distributed.ReduceOp.MAX)
     dt = float(dt_t.item())
     # the loss lives on the ranks that own the head (last pipeline stage): average those
@@ -182,6 +186,7 @@ def main():
                    "parallelism": par, "recipe": f"main-{a.recipe.replace('_', '-')}.py",
                    "tokens_per_step": tokens_per_step, "final_loss": round(loss_v, 4),
                    "peak_mem_gib": round(float(peak.item()), 1),
+                   "force_dist_path": bool(a.force_dist_path),
                    "mfu_per_gpu": round(mfu(value / n, train_flops_per_token(
                        args.dim, args.heads, args.head_dim, args.num_layers, vocab, S)), 4),
                    "baseline": ("stock PyTorch reference-default recipe (manual attention + torch.compile)"

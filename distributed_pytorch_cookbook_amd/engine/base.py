@@ -73,6 +73,7 @@ class Engine:
             if obj is not None and hasattr(obj, "reset_step_state"):
                 obj.reset_step_state()
         transport.forget_outstanding()  # --stream_check: the recorded handles never ran
+        transport.reset_cu_reserve()
 
 
 class GraphedStep:

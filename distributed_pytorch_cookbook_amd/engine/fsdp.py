@@ -29,7 +29,7 @@ class FSDPEngine(Engine):
     def __init__(self, model, device, lr: float, group=None, prefetch: int = 1,
                  reshard_after_forward: bool = True, cpu_offload: bool = False, compute_dtype=None,
                  reduce_dtype=torch.float32, grad_scaler: bool = False, graph: bool = False,
-                 comm_kind: str | None = None):
+                 comm_kind: str | None = None, force_sharded: bool = False):
         self.device = torch.device(device)
         self.model = model
         self.dp_group = group
@@ -38,7 +38,8 @@ class FSDPEngine(Engine):
         self.is_logger = comm.rank() == 0
         self.store = FSDPStore(model, device, group=group, compute_dtype=compute_dtype,
                                prefetch=prefetch, reshard_after_forward=reshard_after_forward,
-                               cpu_offload=cpu_offload, reduce_dtype=reduce_dtype, comm_kind=comm_kind)
+                               cpu_offload=cpu_offload, reduce_dtype=reduce_dtype, comm_kind=comm_kind,
+                               force_sharded=force_sharded)
         st = self.store
         grad = st.grads_host if st.cpu_offload else st.grads
         self.opt = FlatAdamW(st.master, grad, lr=lr, shadow=st.shadow)
@@ -50,7 +51,7 @@ class FSDPEngine(Engine):
         # HIP-graph "compile" of the whole sharded step (gathers, reduce-scatters, AdamW);
         # not with --cpu_offload, whose optimizer runs on the host
         self.graph = (graph and self.device.type == "cuda" and not st.cpu_offload
-                      and (st.W == 1 or st.tp.capturable()))
+                      and (not st.sharded or st.tp.capturable()))
         self._stepper = GraphedStep(self, [self.opt, self.opt_rep])
 
     def train_step(self, batch, targets):

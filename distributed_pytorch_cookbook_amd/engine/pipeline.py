@@ -39,7 +39,7 @@ class PipelineEngine(Engine):
     def __init__(self, model, device, lr: float, pp: int, dp: int = 1, num_microbatches: int = 0,
                  schedule: str = "1f1b", bucket_mb: float = 128.0, compute_dtype=None,
                  seq_len: int | None = None, grad_scaler: bool = False, comm_kind: str | None = None,
-                 wire_dtype=None, graph: bool = False):
+                 wire_dtype=None, graph: bool = False, force_dist: bool = False):
         self.device = torch.device(device)
         self.model = model
         if grad_scaler:
@@ -54,6 +54,15 @@ class PipelineEngine(Engine):
             self.pp_group, self.dp_group, self.stage, self.replica, pp_ranks = comm.make_mesh(pp, dp)
             self.pp_tp, self.dp_tp = make_mesh_transports(self.pp_group, self.dp_group, self.stage,
                                                           self.replica, self.device, comm_kind)
+        elif force_dist:
+            # one rank on the N > 1 path (bench.py --force_dist_path): the replica store is the
+            # bucketed DDP store over a native 1-rank communicator (no neighbour: no p2p)
+            from ..parallel.transport import make_transport
+
+            self.pp_group = self.dp_group = None
+            self.stage, self.replica, pp_ranks = 0, 0, [0]
+            self.pp_tp = TorchTransport(None)
+            self.dp_tp = make_transport(None, self.device, "native")
         else:
             self.pp_group = self.dp_group = None
             self.stage, self.replica, pp_ranks = 0, 0, [0]
@@ -84,7 +93,7 @@ class PipelineEngine(Engine):
                 for mod in mods:
                     for p in mod.parameters():
                         p.data = _placeholder(p.shape, self.device)
-        if dp > 1:
+        if dp > 1 or force_dist:
             self.store = DDPStore(model, device, group=self.dp_group, bucket_mb=bucket_mb,
                                   compute_dtype=compute_dtype, units=self.my_units, transport=self.dp_tp)
         else:
@@ -189,7 +198,7 @@ class PipelineEngine(Engine):
 
         order = (schedule_gpipe if self.schedule == "gpipe" else schedule_1f1b)(self.n_micro, self.stage, self.pp)
         run_schedule(order, self.first, self.last, forward, backward, self.p2p, shape)
-        if self.dp > 1:
+        if isinstance(st, DDPStore):
             st.finish_grads()
         if self.scaler is not None:
             # every stage holds different gradients: one skip decision for the whole job

@@ -211,6 +211,12 @@ def lib() -> ctypes.CDLL:
             handle.dpc_gemm_set_xcd_split.restype = None
             handle.dpc_gemm_set_splits.argtypes = [c_int]
             handle.dpc_gemm_set_splits.restype = None
+            handle.dpc_set_cu_reserve.argtypes = [c_int]
+            handle.dpc_set_cu_reserve.restype = None
+            handle.dpc_get_cu_reserve.argtypes = []
+            handle.dpc_get_cu_reserve.restype = c_int
+            handle.dpc_occupy.argtypes = [c_int, ctypes.c_longlong, c_void_p, c_void_p]
+            handle.dpc_occupy.restype = c_int
             handle.dpc_embedding_bwd_ws.argtypes = [c_int, c_int]
             handle.dpc_embedding_bwd_ws.restype = ctypes.c_ulonglong
             _lib = handle
@@ -237,6 +243,24 @@ def set_gemm_splits(n: int) -> None:
 def set_gemm_xcd_split(on: bool) -> None:
     """Split-K with one k-range per XCD instead of the default remap (experiments)."""
     lib().dpc_gemm_set_xcd_split(int(bool(on)))
+
+
+def set_cu_reserve(r: int) -> None:
+    """CUs the persistent GEMMs (v7 / v8) leave free for a kernel resident beside them -- an
+    RCCL collective in flight on the comm stream (``parallel/transport.py`` drives it)."""
+    lib().dpc_set_cu_reserve(int(r))
+
+
+def get_cu_reserve() -> int:
+    return int(lib().dpc_get_cu_reserve())
+
+
+def occupy(nwg: int, ns: int, sink: torch.Tensor, stream=None) -> None:
+    """Launch ``nwg`` workgroups spinning ``ns`` nanoseconds (measurements only)."""
+    s = (stream or torch.cuda.current_stream()).cuda_stream
+    rc = lib().dpc_occupy(int(nwg), int(ns), sink.data_ptr(), s)
+    if rc != 0:
+        raise RuntimeError(f"dpc_occupy failed: hipError {rc}")
 
 
 def is_loaded() -> bool:

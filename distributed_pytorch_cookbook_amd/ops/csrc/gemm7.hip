@@ -54,7 +54,25 @@ struct G7Plan {
   int splits;
   int store_cnt;  // vector-memory ops the epilogue issues per wave-lane (0: unknown -> no credit)
   int debug;      // experiments only (DPC_G7_DEBUG): 1 = no epilogue stores, 2 = no in-loop DMA
+  int stagger_ns; // v8: the second workgroup of each CU starts this much later (0 = none)
 };
+
+// v8 (two workgroups per CU): which of a CU's workgroups arrived second.  One counter per CU
+// (XCC id, SE / SH / CU ids of HW_ID); the parity of the arrival order separates the two
+// co-resident workgroups of a launch whatever the counter's value before it.
+__device__ unsigned g8_arrivals[8192];
+
+// `slot`: one word of the (still unused) LDS ring broadcasts lane 0's answer -- no second
+// __shared__ object beside the DMA ring
+__device__ __forceinline__ bool g8_second_on_cu(unsigned* slot) {
+  const unsigned hw = __builtin_amdgcn_s_getreg(4 | (8 << 6) | (7 << 11));   // HW_ID[15:8]
+  const unsigned xcc = __builtin_amdgcn_s_getreg(20 | (0 << 6) | (3 << 11)); // XCC_ID[3:0]
+  if (threadIdx.x == 0) *slot = atomicAdd(&g8_arrivals[((xcc & 15) << 8) | (hw & 255)], 1u) & 1u;
+  __syncthreads();
+  const bool second = *slot != 0;
+  __syncthreads();
+  return second;
+}
 
 // XCD-aware assignment: round i covers units [i*grid, (i+1)*grid); inside a round the blocks
 // that share an XCD (b % 8) get a contiguous run of unit ids (bijective for any grid), and unit
@@ -90,6 +108,20 @@ __device__ __forceinline__ void g7_piece(__amdgpu_buffer_rsrc_t rs, int voff, co
       : "=&s"(keep)
       : "v"(voff), "s"(rs), "s"(la)
       : "memory");
+}
+
+// Two adjacent 1-KiB pieces under ONE M0 write (SCHED 3): the second lands 1 KiB later in
+// LDS through the instruction offset, which MUBUF adds to the LDS address and to the memory
+// offset alike -- so its voffset is pre-biased by -1024 (g7 host check: every biased voffset
+// stays >= 0).  M0 is declared clobbered instead of saved / restored around each piece.
+__device__ __forceinline__ void g7_piece2(__amdgpu_buffer_rsrc_t rs, int v0, int v1b, const bf16_t* lds) {
+  const unsigned la = (unsigned)(uintptr_t)(lds_void_t)lds;
+  asm volatile(
+      "s_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dwordx4 %0, %2, 0 offen lds\n\t"
+      "buffer_load_dwordx4 %1, %2, 0 offen offset:1024 lds"
+      :
+      : "v"(v0), "v"(v1b), "s"(rs), "s"(la)
+      : "memory", "m0");
 }
 
 template <int N>
@@ -412,6 +444,15 @@ __global__ __launch_bounds__(256, WN == 128 ? 1 : 2) void gemm7_kernel(GemmArgs 
   const int local = g7_local(blockIdx.x, pl.grid);
   const int nmine = local < pl.units ? (pl.units - local + pl.grid - 1) / pl.grid : 0;
   if (nmine == 0) return;
+  if constexpr (WN == 64) {
+    // phase-shift the two workgroups of a CU: one's epilogue (VALU + store burst) then runs
+    // beside the other's main loop instead of at the same time
+    if (pl.stagger_ns > 0 && g8_second_on_cu(reinterpret_cast<unsigned*>(smem))) {
+      const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();  // 100 MHz
+      const unsigned long long dt = (unsigned long long)pl.stagger_ns / 10;
+      while (__builtin_amdgcn_s_memrealtime() - t0 < dt) __builtin_amdgcn_s_sleep(8);
+    }
+  }
 
   int va[G7_NL], vb[NLB];
   dma_offsets3<32, AK, G7_NL>(va, p.lda, wid, lane);
@@ -451,6 +492,10 @@ __global__ __launch_bounds__(256, WN == 128 ? 1 : 2) void gemm7_kernel(GemmArgs 
     if (i < G7_NL) g7_piece(rsa, va[i], is_lds + (wid * G7_NL + i) * 512);
     else g7_piece(rsb, vb[i - G7_NL], is_lds + G7_TA + (wid * NLB + i - G7_NL) * 512);
   };
+  auto piece2 = [&](int i) {  // pieces i, i+1 (same operand: i even, NL and NLB even)
+    if (i < G7_NL) g7_piece2(rsa, va[i], va[i + 1] - 1024, is_lds + (wid * G7_NL + i) * 512);
+    else g7_piece2(rsb, vb[i - G7_NL], vb[i + 1 - G7_NL] - 1024, is_lds + G7_TA + (wid * NLB + i - G7_NL) * 512);
+  };
   auto advance = [&]() {
     is_slot = is_slot + 1 == NS ? 0 : is_slot + 1;
     is_aoff += a_step;
@@ -467,7 +512,13 @@ __global__ __launch_bounds__(256, WN == 128 ? 1 : 2) void gemm7_kernel(GemmArgs 
   for (int s = 0; s < DIST; ++s) {
     prep();
 #pragma unroll
-    for (int i = 0; i < NP; ++i) piece(i);
+    for (int i = 0; i < NP; ++i) {
+      if constexpr (SCHED == 3) {
+        if (!(i & 1)) piece2(i);
+      } else {
+        piece(i);
+      }
+    }
     advance();
   }
   prep();
@@ -507,6 +558,7 @@ __global__ __launch_bounds__(256, WN == 128 ? 1 : 2) void gemm7_kernel(GemmArgs 
     if (SCHED == 0 && !tail && g < NP) piece(g);
 
     if (SCHED == 2 && !tail && !(g & 1) && g < NP) { piece(g); piece(g + 1); }
+    if (SCHED == 3 && !tail && !(g & 1) && g < NP) piece2(g);
     if (SCHED == 1 && !tail && !(g & 3) && g < NP) { piece(g); piece(g + 1); piece(g + 2); piece(g + 3); }
 
   };
@@ -618,6 +670,31 @@ __global__ __launch_bounds__(256) void g7_splitk_reduce(float* C, long long ldc,
 
 using namespace dpc;
 
+// ---- resident-CU budget.  v7 / v8 are persistent: their grid is sized to fill every CU
+// (one / two 160 KiB workgroups each), so a kernel already resident on a CU -- an RCCL
+// collective on the comm stream -- would hold back that CU's GEMM workgroup until the
+// collective ends, and that workgroup's whole share of the tiles would then run as a second
+// round (the product's time roughly doubled, SURVEY.md §5.8 rule 4).  While the engines have
+// a collective in flight they reserve R CUs (parallel/transport.py; DPC_CU_RESERVE): the grid
+// shrinks to CUs - R workgroups, the XCD remap (g7_local) stays bijective for any grid, and the
+// tiles redistribute over the workgroups that are resident.
+static int g7_reserve = 0;
+static int g7_cus = 0;
+
+static int g7_cu_count() {
+  if (g7_cus <= 0) {
+    int dev = 0, n = 0;
+    if (hipGetDevice(&dev) == hipSuccess && hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && n > 0)
+      g7_cus = n;
+    else
+      g7_cus = 256;
+  }
+  return g7_cus;
+}
+
+DPC_API void dpc_set_cu_reserve(int r) { g7_reserve = r < 0 ? 0 : r; }
+DPC_API int dpc_get_cu_reserve() { return g7_reserve; }
+
 static inline long long g7_operand_bytes(long long rows, long long cols, long long ld) {
   if (rows <= 0 || cols <= 0) return 0;
   return ((rows - 1) * ld + ((cols + 7) / 8) * 8) * 2;
@@ -631,6 +708,13 @@ static void g7_launch(const GemmArgs* a, const G7Plan& pl, hipStream_t stream, u
   else if (a->a_kmaj) hipLaunchKernelGGL((gemm7_kernel<EPI, SCHED, true, false, WN>), grid, block, 0, stream, *a, ab, bb, pl);
   else if (!a->b_kmaj) hipLaunchKernelGGL((gemm7_kernel<EPI, SCHED, false, false, WN>), grid, block, 0, stream, *a, ab, bb, pl);
   else hipLaunchKernelGGL((gemm7_kernel<EPI, SCHED, false, true, WN>), grid, block, 0, stream, *a, ab, bb, pl);
+}
+
+// SCHED 3 pre-biases the second voffset of each piece pair by -1 KiB: every such voffset holds
+// at least one 1-KiB piece's worth of rows before it (k-major: 16 rows, mn-major: 4 k-rows)
+static bool g7_bias_ok(const GemmArgs* a) {
+  auto ok = [](bool kmaj, long long ld) { return kmaj ? ld * 2 * 16 >= 1024 : ld * 2 * 4 >= 1024; };
+  return ok(a->a_kmaj, a->lda) && ok(a->b_kmaj, a->ldb);
 }
 
 // Returns -1 if the product does not meet v7's requirements (caller falls back), else the
@@ -675,6 +759,7 @@ DPC_API int dpc_gemm7(const GemmArgs* a, int persistent, int sched, int splits, 
   auto slab_fits = [&](int c) {
     return a->ws && (long long)c * a->M * a->N * 4 <= a->ws_bytes && a->ldc % 4 == 0 && ((uintptr_t)a->ws % 16) == 0;
   };
+  const int cus = std::max(8, g7_cu_count() - g7_reserve);  // CUs the grid may occupy
   if (splits <= 0 && splittable) {
     // fill the chip (few tiles) or even out the last round (wave quantisation): time ~ rounds
     // * (slices per unit + the split epilogue) [+ the slab reduction].  Units are in k-slices
@@ -686,7 +771,7 @@ DPC_API int dpc_gemm7(const GemmArgs* a, int persistent, int sched, int splits, 
       const int per = 2 * ((pl.nk_all + 2 * c - 1) / (2 * c));
       if (c > 1 && per < 16) break;
       // (v8: two 256 x 128 units per CU at once, each half a v7 unit's MFMA work)
-      const int rounds = v8 ? (tiles * c + 511) / 512 : (tiles * c + 255) / 256;
+      const int rounds = v8 ? (tiles * c + 2 * cus - 1) / (2 * cus) : (tiles * c + cus - 1) / cus;
       double cost = (double)rounds * per;
       if (c > 1 && slab_fits(c)) {
         const double red_us = (double)(c + 1 + a->accumulate) * a->M * a->N * 4 / 5e6;
@@ -709,15 +794,17 @@ DPC_API int dpc_gemm7(const GemmArgs* a, int persistent, int sched, int splits, 
   pl.units = tiles * s;
   // persistent: one workgroup per CU streams its units through one ring; otherwise one unit
   // per workgroup
-  const int slots = v8 ? 512 : 256;  // workgroups resident at once
+  const int slots = v8 ? 2 * cus : cus;  // workgroups resident at once
   pl.grid = (persistent && pl.units > slots) ? slots : pl.units;
   // vector-memory ops an epilogue issues per lane, for the store credit: only epilogues that
   // read nothing per element and issue every store of a full tile (no column-sum atomics)
   const bool no_loads = !a->residual && !a->act_bwd && !a->accumulate && !a->colsum;
   pl.store_cnt = (no_loads && (s == 1 || slab) && !v8) ? ((a->out_f32 || slab ? 64 : 32) + (a->aux_out ? 32 : 0)) : 0;
-  static int dbg = -1;
+  static int dbg = -1, stag = -1;
   if (dbg < 0) dbg = getenv("DPC_G7_DEBUG") ? atoi(getenv("DPC_G7_DEBUG")) : 0;
+  if (stag < 0) stag = getenv("DPC_G8_STAGGER_NS") ? atoi(getenv("DPC_G8_STAGGER_NS")) : 0;
   pl.debug = dbg;
+  pl.stagger_ns = v8 ? stag : 0;
   if (dbg & 1) pl.store_cnt = 0;
   if (slab) {
     if (v8) g7_launch<4, 2, 64>(a, pl, stream, ab, bb);
@@ -736,6 +823,7 @@ DPC_API int dpc_gemm7(const GemmArgs* a, int persistent, int sched, int splits, 
   } else if (plain && !a->accumulate) {
     if (sched == 1) g7_launch<0, 1>(a, pl, stream, ab, bb);
     else if (sched == 2) g7_launch<0, 2>(a, pl, stream, ab, bb);
+    else if (sched == 3 && g7_bias_ok(a)) g7_launch<0, 3>(a, pl, stream, ab, bb);
     else g7_launch<0, 0>(a, pl, stream, ab, bb);
   } else if (!a->act_bwd && !a->colsum) {
     g7_launch<1, 2>(a, pl, stream, ab, bb);

@@ -580,3 +580,22 @@ DPC_API int dpc_dropout_residual(const DropResArgs* a, hipStream_t stream) {
                      stream, *a);
   return (int)hipGetLastError();
 }
+
+// ---- CU occupier (measurements of the GEMM resident-CU reserve, bench/cu_reserve.py): nwg
+// small workgroups that spin for `ns` nanoseconds -- the footprint of an RCCL collective's
+// channel workgroups resident beside the compute stream.  Every wave reaches the exit.
+__global__ __launch_bounds__(256) void occupy_kernel(long long ticks, unsigned* sink) {
+  const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();  // 100 MHz
+  unsigned spins = 0;
+  while ((long long)(__builtin_amdgcn_s_memrealtime() - t0) < ticks) {
+    __builtin_amdgcn_s_sleep(4);
+    ++spins;
+  }
+  if (threadIdx.x == 0 && spins == 0xffffffffu) sink[blockIdx.x] = spins;  // (never: keeps the loop)
+}
+
+DPC_API int dpc_occupy(int nwg, long long ns, void* sink, hipStream_t stream) {
+  if (nwg <= 0) return 0;
+  hipLaunchKernelGGL(occupy_kernel, dim3((unsigned)nwg), dim3(256), 0, stream, ns / 10, static_cast<unsigned*>(sink));
+  return (int)hipGetLastError();
+}

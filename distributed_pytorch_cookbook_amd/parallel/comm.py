@@ -42,8 +42,9 @@ def env_world() -> int:
     return int(os.environ.get("WORLD_SIZE", "1"))
 
 
-def init_dist(force_cpu: bool = False) -> DistInfo:
-    """Initialise the default process group from torchrun's env (no-op for 1 process)."""
+def init_dist(force_cpu: bool = False, force_group: bool = False) -> DistInfo:
+    """Initialise the default process group from torchrun's env (no-op for 1 process, unless
+    ``force_group``: a 1-rank group on 127.0.0.1 to bootstrap a native communicator)."""
     os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
     world = env_world()
     rank = int(os.environ.get("RANK", "0"))
@@ -64,6 +65,17 @@ def init_dist(force_cpu: bool = False) -> DistInfo:
         timeout = datetime.timedelta(seconds=float(os.environ.get("DPC_COLL_TIMEOUT", "1800")))
         kw = dict(backend=backend, timeout=timeout)
         if use_gpu and backend == "nccl":
+            kw["device_id"] = device
+        dist.init_process_group(**kw)
+    elif force_group and not dist.is_initialized():
+        import socket
+
+        with socket.socket() as sk:
+            sk.bind(("127.0.0.1", 0))
+            port = sk.getsockname()[1]
+        backend = "nccl" if use_gpu else "gloo"
+        kw = dict(backend=backend, init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1)
+        if use_gpu:
             kw["device_id"] = device
         dist.init_process_group(**kw)
     elif dist.is_initialized():

@@ -47,11 +47,14 @@ class FSDPStore(ParamStore):
     def __init__(self, model, device, group=None, compute_dtype=None, prefetch: int = 1,
                  reshard_after_forward: bool = True, cpu_offload: bool = False,
                  reduce_dtype: torch.dtype = torch.float32, transport: Transport | None = None,
-                 comm_kind: str | None = None):
+                 comm_kind: str | None = None, force_sharded: bool = False):
         self.device = torch.device(device)
         self.group = group
         self.tp = transport if transport is not None else make_transport(group, self.device, comm_kind)
         self.W = self.tp.size
+        # the N > 1 code path (full-unit gathers, unit gradients, reduce-scatters) even at one
+        # rank: bench.py --force_dist_path profiles it on a single GPU
+        self.sharded = self.W > 1 or force_sharded
         self.rank = self.tp.rank
         self.compute_dtype = compute_dtype or default_compute_dtype(self.device)
         self.prefetch = max(0, prefetch)
@@ -194,7 +197,7 @@ class FSDPStore(ParamStore):
             return
         self._wait_host(u)  # --cpu_offload: this unit's updated weights uploaded
         sh = self.shard(self.shadow, u)
-        if self.W == 1:
+        if not self.sharded:
             self._full[u] = (sh, None)  # one rank: the shard is the whole unit
         else:
             buf = torch.empty(self.unit_len[u], dtype=self.compute_dtype, device=self.device)
@@ -202,7 +205,7 @@ class FSDPStore(ParamStore):
         self._track()
 
     def _track(self):
-        if self.W > 1:
+        if self.sharded:
             live = len(self._full) + len(self._gfull)
             self.peak_live_units = max(self.peak_live_units, live)
 
@@ -258,7 +261,7 @@ class FSDPStore(ParamStore):
             for k in range(1, self.prefetch + 1):
                 if u - k >= 1:  # the embeddings unit needs no weights in backward
                     self._gather(u - k)
-        if self.W == 1:
+        if not self.sharded:
             # the weight gradients accumulate straight into the shard (zeroed per step)
             self._gfull[u] = self.shard(self.grads, u)
         else:
@@ -268,7 +271,7 @@ class FSDPStore(ParamStore):
     def post_backward(self, u):
         self._release(u)
         g = self._gfull.pop(u)
-        if self.W == 1:
+        if not self.sharded:
             return
         out = self.shard(self.grads, u)
         if self.reduce_dtype != torch.float32:
@@ -288,7 +291,7 @@ class FSDPStore(ParamStore):
 
     def finish_grads(self):
         rep_w = None
-        if self.W > 1:
+        if self.sharded:
             rep_w = self.tp.all_reduce(self.rep_grads, async_op=True)
         for u, lst in sorted(self._rs.items()):
             for w, tmp in lst:

@@ -67,6 +67,52 @@ def forget_outstanding() -> None:
     _outstanding.clear()
 
 
+# ---------------------------------------------------------------- resident-CU reserve
+# SURVEY.md §5.8 rule 4 (comm overlapped with compute on side streams): the persistent GEMMs
+# (ops/csrc/gemm7.hip) size their grid to occupy every CU, so an RCCL kernel resident on a
+# CU while a GEMM launches would push that CU's GEMM workgroup -- and its whole share of the
+# tiles -- into a second round.  From the moment an asynchronous GPU collective is enqueued
+# until its handle is waited on, the GEMMs leave DPC_CU_RESERVE CUs (default 16) free for it.
+# Captured into a HIP graph like every other launch parameter.
+_CU_RESERVE = int(os.environ.get("DPC_CU_RESERVE", "16"))
+_comm_inflight = 0
+
+
+def _set_reserve(r: int) -> None:
+    from ..ops import _lib
+
+    try:
+        _lib.set_cu_reserve(r)
+    except (RuntimeError, OSError):  # no kernel library (CPU): nothing to size
+        pass
+
+
+def _reserve_begin() -> None:
+    global _comm_inflight
+    _comm_inflight += 1
+    if _comm_inflight == 1 and _CU_RESERVE > 0:
+        _set_reserve(_CU_RESERVE)
+
+
+def _reserve_end() -> None:
+    global _comm_inflight
+    _comm_inflight = max(0, _comm_inflight - 1)
+    if _comm_inflight == 0 and _CU_RESERVE > 0:
+        _set_reserve(0)
+
+
+def reset_cu_reserve() -> None:
+    """No collective in flight (after a failed capture: the recorded ones never ran)."""
+    global _comm_inflight
+    if _comm_inflight:
+        _comm_inflight = 0
+        _set_reserve(0)
+
+
+def cu_reserve_active() -> bool:
+    return _comm_inflight > 0
+
+
 def check_drained(where: str = "end of step") -> None:
     """Raise if a collective issued with ``async_op=True`` was never waited on."""
     if not _STREAM_CHECK:
@@ -103,14 +149,19 @@ class _Done(Handle):
 
 class _EventHandle(Handle):
     """Completion recorded on a side stream: ``wait`` orders the caller's current stream
-    after it (device-side only)."""
+    after it (device-side only).  While it is outstanding the persistent GEMMs keep the
+    resident-CU reserve (``_reserve_begin``)."""
 
-    def __init__(self, event):
+    def __init__(self, event, reserved=False):
         self.event = event
+        self.reserved = reserved
 
     def wait(self) -> None:
         self._untrack()
         torch.cuda.current_stream().wait_event(self.event)
+        if self.reserved:
+            self.reserved = False
+            _reserve_end()
 
 
 class _WorkHandle(Handle):
@@ -318,7 +369,9 @@ class NativeTransport(Transport):
         done.record(s)
         if not capturing:  # (a replayed graph is watched as a whole: GraphedStep)
             native_comm.watchdog_track(s.cuda_stream, desc)
-        h = _EventHandle(done)._track(desc)
+        if async_op:
+            _reserve_begin()
+        h = _EventHandle(done, reserved=async_op)._track(desc)
         if not async_op:
             h.wait()
             return _Done()

@@ -46,9 +46,12 @@ def pipe_mesh(recipe: str, world: int, pp_size: int = 0, dp_size: int = 0) -> tu
     return pp, dp
 
 
-def build_engine(recipe: str, model, info, args):
+def build_engine(recipe: str, model, info, args, force_dist: bool = False):
+    """``force_dist``: at one rank, take the engines' N > 1 code path over a native 1-rank RCCL
+    communicator (bucketed DDP store, sharded FSDP store, replica DDP store of the pipeline) --
+    bench.py --force_dist_path profiles it on one GPU."""
     compute_dtype = torch.float32 if args.disable_amp else None
-    comm_kind = getattr(args, "comm", "auto")
+    comm_kind = "native" if force_dist else getattr(args, "comm", "auto")
     # the cookbook's "compile": capture the whole step into a HIP graph (dropout masks are
     # drawn per step on the host: not graph-replayable).  One rank by default; at N > 1 only
     # with --graph (RCCL inside a replayed graph has not been run on a multi-GPU node yet, and
@@ -64,7 +67,7 @@ def build_engine(recipe: str, model, info, args):
             model, info.device, lr=args.learning_rate, bucket_mb=args.bucket_mb,
             reduce_dtype=torch.bfloat16 if args.reduce_dtype == "bf16" else torch.float32,
             overlap=not args.no_overlap, compute_dtype=compute_dtype, graph=graph,
-            comm_kind=comm_kind, grad_scaler=getattr(args, "grad_scaler", False),
+            comm_kind=comm_kind, grad_scaler=getattr(args, "grad_scaler", False), force_ddp_store=force_dist,
         )
     if recipe == "fsdp":
         from .engine.fsdp import FSDPEngine
@@ -72,7 +75,8 @@ def build_engine(recipe: str, model, info, args):
         return FSDPEngine(model, info.device, lr=args.learning_rate, prefetch=args.prefetch,
                           reshard_after_forward=not args.no_reshard_after_forward,
                           cpu_offload=args.cpu_offload, compute_dtype=compute_dtype,
-                          grad_scaler=getattr(args, "grad_scaler", False), graph=graph, comm_kind=comm_kind)
+                          grad_scaler=getattr(args, "grad_scaler", False), graph=graph, comm_kind=comm_kind,
+                          force_sharded=force_dist)
     if recipe in ("pipe", "pipe_ddp"):
         from .engine.pipeline import PipelineEngine
 
@@ -82,7 +86,7 @@ def build_engine(recipe: str, model, info, args):
                               num_microbatches=args.num_microbatches,
                               schedule=args.schedule, bucket_mb=args.bucket_mb,
                               compute_dtype=compute_dtype, grad_scaler=getattr(args, "grad_scaler", False),
-                              comm_kind=comm_kind, wire_dtype=wire, graph=graph)
+                              comm_kind=comm_kind, wire_dtype=wire, graph=graph, force_dist=force_dist)
     raise ValueError(recipe)
 
 

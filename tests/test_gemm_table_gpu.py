@@ -86,3 +86,65 @@ def test_table_signature_matches_fp32(sig):
         assert _rel(kw["aux_out"], ref_aux) < 1.5e-2, sig + " aux_out"
     if ref_cs is not None:
         assert _rel(kw["colsum"], ref_cs) < 5e-3, sig + " colsum"
+
+
+@pytest.mark.parametrize("reserve", [16, 200])
+@pytest.mark.parametrize("case", ["nt_v7", "nt_v8", "nn_v7", "tn_split", "fused_v7"])
+def test_cu_reserve_products_match_fp32(reserve, case):
+    """The persistent GEMMs with a resident-CU reserve (grid = CUs - reserve, the tiles spread
+    over fewer workgroups, the split-K count re-planned) still match an fp32 product."""
+    from distributed_pytorch_cookbook_amd.ops import _lib
+
+    g = torch.Generator(device=dev).manual_seed(reserve + len(case))
+    r = lambda *s: (torch.rand(*s, device=dev, generator=g) * 2 - 1).bfloat16()  # noqa: E731
+    M, N, K = 4096, 2304, 768
+    kw = {}
+    if case == "tn_split":
+        M, N, K = 2304, 768, 16384
+        a, b = r(K, M), r(K, N)
+        kw = dict(a_kmaj=False, b_kmaj=False, out_dtype=torch.float32)
+        ref = a.float().t() @ b.float()
+    elif case == "nn_v7":
+        a, b = r(M, K), r(K, N)
+        kw = dict(b_kmaj=False)
+        ref = a.float() @ b.float()
+    else:
+        a, b = r(M, K), r(N, K)
+        ref = a.float() @ b.float().t()
+    impl = {"nt_v7": 20, "nt_v8": 21, "nn_v7": 20, "tn_split": -1, "fused_v7": 20}[case]
+    if case == "fused_v7":
+        bias = torch.randn(N, device=dev, generator=g)
+        kw = dict(bias=bias, act=2)
+        ref = torch.nn.functional.gelu(ref + bias, approximate="tanh")
+    try:
+        _lib.set_cu_reserve(reserve)
+        _lib.set_gemm_impl(impl)
+        out = gemm(a, b, **kw)
+        torch.cuda.synchronize()
+    finally:
+        _lib.set_gemm_impl(-1)
+        _lib.set_cu_reserve(0)
+    assert _lib.get_cu_reserve() == 0
+    assert _rel(out, ref) < 1e-2, _rel(out, ref)
+
+
+@pytest.mark.parametrize("lay", ["nt", "nn", "tn", "tt"])
+def test_paired_dma_variant_matches_fp32(lay):
+    """v7 with the paired LDS-DMA issue (impl 22: one M0 write per two pieces, the second
+    placed by the instruction offset) on every operand layout, edge tiles included."""
+    from distributed_pytorch_cookbook_amd.ops import _lib
+
+    g = torch.Generator(device=dev).manual_seed(22)
+    r = lambda *s: (torch.rand(*s, device=dev, generator=g) * 2 - 1).bfloat16()  # noqa: E731
+    M, N, K = 1000, 776, 1536
+    a = r(M, K) if lay[0] == "n" else r(K, M)
+    b = r(N, K) if lay[1] == "t" else r(K, N)
+    am = a.float() if lay[0] == "n" else a.float().t()
+    bm = b.float().t() if lay[1] == "t" else b.float()
+    try:
+        _lib.set_gemm_impl(22)
+        out = gemm(a, b, a_kmaj=lay[0] == "n", b_kmaj=lay[1] == "t", out_dtype=torch.float32)
+        torch.cuda.synchronize()
+    finally:
+        _lib.set_gemm_impl(-1)
+    assert _rel(out, am @ bm) < 1e-2, _rel(out, am @ bm)

@@ -173,3 +173,20 @@ def test_stream_check_engines_and_unwaited_collective(tmp_path, kind):
     out = tmp_path / "sc.pt"
     run_workers(worker_stream_check, 2, str(out), kind)
     assert torch.load(out, weights_only=True)["caught"]
+
+
+def test_fsdp_forced_sharded_path_matches_fast_path():
+    """--force_dist_path: the N > 1 FSDP code path (full-unit gathers, unit gradients,
+    reduce-scatters, replicated-vector all-reduce) at one rank gives the fast path's result."""
+    from dist_workers import LR, full_batch, make_model
+
+    from distributed_pytorch_cookbook_amd.engine.fsdp import FSDPEngine
+
+    res = []
+    for forced in (False, True):
+        eng = FSDPEngine(make_model(), "cpu", lr=LR, force_sharded=forced)
+        assert eng.store.sharded == forced
+        for s in range(2):
+            eng.train_step(*full_batch(step=s))
+        res.append(eng.full_state_dict())
+    assert_close_sd(res[0], res[1], atol=1e-6)
