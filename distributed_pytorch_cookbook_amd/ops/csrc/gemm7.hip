@@ -54,25 +54,7 @@ struct G7Plan {
   int splits;
   int store_cnt;  // vector-memory ops the epilogue issues per wave-lane (0: unknown -> no credit)
   int debug;      // experiments only (DPC_G7_DEBUG): 1 = no epilogue stores, 2 = no in-loop DMA
-  int stagger_ns; // v8: the second workgroup of each CU starts this much later (0 = none)
 };
-
-// v8 (two workgroups per CU): which of a CU's workgroups arrived second.  One counter per CU
-// (XCC id, SE / SH / CU ids of HW_ID); the parity of the arrival order separates the two
-// co-resident workgroups of a launch whatever the counter's value before it.
-__device__ unsigned g8_arrivals[8192];
-
-// `slot`: one word of the (still unused) LDS ring broadcasts lane 0's answer -- no second
-// __shared__ object beside the DMA ring
-__device__ __forceinline__ bool g8_second_on_cu(unsigned* slot) {
-  const unsigned hw = __builtin_amdgcn_s_getreg(4 | (8 << 6) | (7 << 11));   // HW_ID[15:8]
-  const unsigned xcc = __builtin_amdgcn_s_getreg(20 | (0 << 6) | (3 << 11)); // XCC_ID[3:0]
-  if (threadIdx.x == 0) *slot = atomicAdd(&g8_arrivals[((xcc & 15) << 8) | (hw & 255)], 1u) & 1u;
-  __syncthreads();
-  const bool second = *slot != 0;
-  __syncthreads();
-  return second;
-}
 
 // XCD-aware assignment: round i covers units [i*grid, (i+1)*grid); inside a round the blocks
 // that share an XCD (b % 8) get a contiguous run of unit ids (bijective for any grid), and unit
@@ -121,6 +103,21 @@ __device__ __forceinline__ void g7_piece2(__amdgpu_buffer_rsrc_t rs, int v0, int
       "buffer_load_dwordx4 %1, %2, 0 offen offset:1024 lds"
       :
       : "v"(v0), "v"(v1b), "s"(rs), "s"(la)
+      : "memory", "m0");
+}
+
+// Four adjacent pieces under one M0 write (SCHED 4): instruction offsets 0 / 1 / 2 / 3 KiB,
+// voffsets pre-biased by the same amounts.
+__device__ __forceinline__ void g7_piece4(__amdgpu_buffer_rsrc_t rs, int v0, int v1b, int v2b, int v3b,
+                                          const bf16_t* lds) {
+  const unsigned la = (unsigned)(uintptr_t)(lds_void_t)lds;
+  asm volatile(
+      "s_mov_b32 m0, %5\n\ts_nop 0\n\tbuffer_load_dwordx4 %0, %4, 0 offen lds\n\t"
+      "buffer_load_dwordx4 %1, %4, 0 offen offset:1024 lds\n\t"
+      "buffer_load_dwordx4 %2, %4, 0 offen offset:2048 lds\n\t"
+      "buffer_load_dwordx4 %3, %4, 0 offen offset:3072 lds"
+      :
+      : "v"(v0), "v"(v1b), "v"(v2b), "v"(v3b), "s"(rs), "s"(la)
       : "memory", "m0");
 }
 
@@ -444,15 +441,6 @@ __global__ __launch_bounds__(256, WN == 128 ? 1 : 2) void gemm7_kernel(GemmArgs 
   const int local = g7_local(blockIdx.x, pl.grid);
   const int nmine = local < pl.units ? (pl.units - local + pl.grid - 1) / pl.grid : 0;
   if (nmine == 0) return;
-  if constexpr (WN == 64) {
-    // phase-shift the two workgroups of a CU: one's epilogue (VALU + store burst) then runs
-    // beside the other's main loop instead of at the same time
-    if (pl.stagger_ns > 0 && g8_second_on_cu(reinterpret_cast<unsigned*>(smem))) {
-      const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();  // 100 MHz
-      const unsigned long long dt = (unsigned long long)pl.stagger_ns / 10;
-      while (__builtin_amdgcn_s_memrealtime() - t0 < dt) __builtin_amdgcn_s_sleep(8);
-    }
-  }
 
   int va[G7_NL], vb[NLB];
   dma_offsets3<32, AK, G7_NL>(va, p.lda, wid, lane);
@@ -492,6 +480,11 @@ __global__ __launch_bounds__(256, WN == 128 ? 1 : 2) void gemm7_kernel(GemmArgs 
     if (i < G7_NL) g7_piece(rsa, va[i], is_lds + (wid * G7_NL + i) * 512);
     else g7_piece(rsb, vb[i - G7_NL], is_lds + G7_TA + (wid * NLB + i - G7_NL) * 512);
   };
+  auto piece4 = [&](int i) {  // pieces i .. i+3 of one operand (NL == NLB == 4)
+    if (i < G7_NL) g7_piece4(rsa, va[i], va[i + 1] - 1024, va[i + 2] - 2048, va[i + 3] - 3072, is_lds + (wid * G7_NL + i) * 512);
+    else g7_piece4(rsb, vb[i - G7_NL], vb[i + 1 - G7_NL] - 1024, vb[i + 2 - G7_NL] - 2048, vb[i + 3 - G7_NL] - 3072,
+                   is_lds + G7_TA + (wid * NLB + i - G7_NL) * 512);
+  };
   auto piece2 = [&](int i) {  // pieces i, i+1 (same operand: i even, NL and NLB even)
     if (i < G7_NL) g7_piece2(rsa, va[i], va[i + 1] - 1024, is_lds + (wid * G7_NL + i) * 512);
     else g7_piece2(rsb, vb[i - G7_NL], vb[i + 1 - G7_NL] - 1024, is_lds + G7_TA + (wid * NLB + i - G7_NL) * 512);
@@ -513,7 +506,9 @@ __global__ __launch_bounds__(256, WN == 128 ? 1 : 2) void gemm7_kernel(GemmArgs 
     prep();
 #pragma unroll
     for (int i = 0; i < NP; ++i) {
-      if constexpr (SCHED == 3) {
+      if constexpr (SCHED == 4 && WN == 128) {
+        if (!(i & 3)) piece4(i);
+      } else if constexpr (SCHED >= 3) {
         if (!(i & 1)) piece2(i);
       } else {
         piece(i);
@@ -559,6 +554,7 @@ __global__ __launch_bounds__(256, WN == 128 ? 1 : 2) void gemm7_kernel(GemmArgs 
 
     if (SCHED == 2 && !tail && !(g & 1) && g < NP) { piece(g); piece(g + 1); }
     if (SCHED == 3 && !tail && !(g & 1) && g < NP) piece2(g);
+    if (SCHED == 4 && !tail && !(g & 3) && g < NP) piece4(g);
     if (SCHED == 1 && !tail && !(g & 3) && g < NP) { piece(g); piece(g + 1); piece(g + 2); piece(g + 3); }
 
   };
@@ -710,11 +706,24 @@ static void g7_launch(const GemmArgs* a, const G7Plan& pl, hipStream_t stream, u
   else hipLaunchKernelGGL((gemm7_kernel<EPI, SCHED, false, true, WN>), grid, block, 0, stream, *a, ab, bb, pl);
 }
 
-// SCHED 3 pre-biases the second voffset of each piece pair by -1 KiB: every such voffset holds
-// at least one 1-KiB piece's worth of rows before it (k-major: 16 rows, mn-major: 4 k-rows)
-static bool g7_bias_ok(const GemmArgs* a) {
-  auto ok = [](bool kmaj, long long ld) { return kmaj ? ld * 2 * 16 >= 1024 : ld * 2 * 4 >= 1024; };
+// SCHED 3 / 4 pre-bias the voffset of the k-th piece of a group by -k KiB: it must hold that
+// many bytes of rows before it (k-major: 16 rows per piece, mn-major: 4 k-rows per piece)
+static bool g7_bias_ok(const GemmArgs* a, long long bytes = 1024) {
+  auto ok = [bytes](bool kmaj, long long ld) { return kmaj ? ld * 2 * 16 >= bytes : ld * 2 * 4 >= bytes; };
   return ok(a->a_kmaj, a->lda) && ok(a->b_kmaj, a->ldb);
+}
+
+// The shipped schedule: two DMA pieces at the head of every even MFMA group, issued under one
+// M0 write (SCHED 3) where the operands allow it, else one M0 write per piece (SCHED 2).
+// Same-box A/B on MI355X (profiles/r3_gemm/ab22_*): +3 to +7 % on every GPT-2 product and on
+// 8192^3 (1252 -> 1330 TF/s nt).  DPC_G7_PAIR=0 restores SCHED 2.
+template <int EPI, int WN = 128>
+static void g7_launch_s(const GemmArgs* a, const G7Plan& pl, hipStream_t stream, unsigned long long ab,
+                        unsigned long long bb) {
+  static int pair_env = -1;
+  if (pair_env < 0) pair_env = getenv("DPC_G7_PAIR") ? atoi(getenv("DPC_G7_PAIR")) : 1;
+  if (pair_env && g7_bias_ok(a)) g7_launch<EPI, 3, WN>(a, pl, stream, ab, bb);
+  else g7_launch<EPI, 2, WN>(a, pl, stream, ab, bb);
 }
 
 // Returns -1 if the product does not meet v7's requirements (caller falls back), else the
@@ -800,35 +809,38 @@ DPC_API int dpc_gemm7(const GemmArgs* a, int persistent, int sched, int splits, 
   // read nothing per element and issue every store of a full tile (no column-sum atomics)
   const bool no_loads = !a->residual && !a->act_bwd && !a->accumulate && !a->colsum;
   pl.store_cnt = (no_loads && (s == 1 || slab) && !v8) ? ((a->out_f32 || slab ? 64 : 32) + (a->aux_out ? 32 : 0)) : 0;
-  static int dbg = -1, stag = -1;
+  static int dbg = -1;
   if (dbg < 0) dbg = getenv("DPC_G7_DEBUG") ? atoi(getenv("DPC_G7_DEBUG")) : 0;
-  if (stag < 0) stag = getenv("DPC_G8_STAGGER_NS") ? atoi(getenv("DPC_G8_STAGGER_NS")) : 0;
   pl.debug = dbg;
-  pl.stagger_ns = v8 ? stag : 0;
   if (dbg & 1) pl.store_cnt = 0;
   if (slab) {
-    if (v8) g7_launch<4, 2, 64>(a, pl, stream, ab, bb);
-    else g7_launch<4, 2>(a, pl, stream, ab, bb);
+    if (v8) g7_launch_s<4, 64>(a, pl, stream, ab, bb);
+    else g7_launch_s<4>(a, pl, stream, ab, bb);
     const long long nq = (long long)a->M * (a->N / 4);
     const int blocks = (int)std::min<long long>((nq + 255) / 256, 4096);
     hipLaunchKernelGGL(g7_splitk_reduce, dim3(blocks), dim3(256), 0, stream, static_cast<float*>(a->C), a->ldc,
                        static_cast<const float*>(a->ws), a->M, a->N, s, a->accumulate);
   } else if (s > 1) {
     if (!a->accumulate) hipMemset2DAsync(a->C, (size_t)a->ldc * 4, 0, (size_t)a->N * 4, (size_t)a->M, stream);
-    g7_launch<2, 2>(a, pl, stream, ab, bb);
+    g7_launch_s<2>(a, pl, stream, ab, bb);
   } else if (v8) {
-    if (plain && !a->accumulate) g7_launch<0, 2, 64>(a, pl, stream, ab, bb);
-    else if (!a->act_bwd && !a->colsum) g7_launch<1, 2, 64>(a, pl, stream, ab, bb);
-    else g7_launch<3, 2, 64>(a, pl, stream, ab, bb);
+    if (plain && !a->accumulate) g7_launch_s<0, 64>(a, pl, stream, ab, bb);
+    else if (!a->act_bwd && !a->colsum) g7_launch_s<1, 64>(a, pl, stream, ab, bb);
+    else g7_launch_s<3, 64>(a, pl, stream, ab, bb);
   } else if (plain && !a->accumulate) {
-    if (sched == 1) g7_launch<0, 1>(a, pl, stream, ab, bb);
+    // the grouped-M0 forms replace the per-piece ones: SCHED 0 / 2 (one or two pieces per
+    // group) -> pairs (3), SCHED 1 (four pieces at groups 0 and 4) -> quads (4)
+    static int pair_env = -1;
+    if (pair_env < 0) pair_env = getenv("DPC_G7_PAIR") ? atoi(getenv("DPC_G7_PAIR")) : 1;
+    if ((sched == 4 || (sched == 1 && pair_env)) && g7_bias_ok(a, 3072)) g7_launch<0, 4>(a, pl, stream, ab, bb);
+    else if (sched == 1) g7_launch<0, 1>(a, pl, stream, ab, bb);
+    else if ((sched == 3 || pair_env) && g7_bias_ok(a)) g7_launch<0, 3>(a, pl, stream, ab, bb);
     else if (sched == 2) g7_launch<0, 2>(a, pl, stream, ab, bb);
-    else if (sched == 3 && g7_bias_ok(a)) g7_launch<0, 3>(a, pl, stream, ab, bb);
     else g7_launch<0, 0>(a, pl, stream, ab, bb);
   } else if (!a->act_bwd && !a->colsum) {
-    g7_launch<1, 2>(a, pl, stream, ab, bb);
+    g7_launch_s<1>(a, pl, stream, ab, bb);
   } else {
-    g7_launch<3, 2>(a, pl, stream, ab, bb);
+    g7_launch_s<3>(a, pl, stream, ab, bb);
   }
   return (int)hipGetLastError();
 }

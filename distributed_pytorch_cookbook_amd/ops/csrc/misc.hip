@@ -584,14 +584,19 @@ DPC_API int dpc_dropout_residual(const DropResArgs* a, hipStream_t stream) {
 // ---- CU occupier (measurements of the GEMM resident-CU reserve, bench/cu_reserve.py): nwg
 // small workgroups that spin for `ns` nanoseconds -- the footprint of an RCCL collective's
 // channel workgroups resident beside the compute stream.  Every wave reaches the exit.
+// 32 KiB of LDS per workgroup, like a collective kernel's shared staging: a CU hosting one
+// cannot also host a 160 KiB GEMM workgroup
 __global__ __launch_bounds__(256) void occupy_kernel(long long ticks, unsigned* sink) {
+  __shared__ unsigned scratch[8192];
   const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();  // 100 MHz
   unsigned spins = 0;
+  scratch[threadIdx.x * 32] = threadIdx.x;
   while ((long long)(__builtin_amdgcn_s_memrealtime() - t0) < ticks) {
     __builtin_amdgcn_s_sleep(4);
     ++spins;
   }
-  if (threadIdx.x == 0 && spins == 0xffffffffu) sink[blockIdx.x] = spins;  // (never: keeps the loop)
+  __syncthreads();
+  if (threadIdx.x == 0 && spins == 0xffffffffu) sink[blockIdx.x] = scratch[(spins & 255) * 32];  // (never)
 }
 
 DPC_API int dpc_occupy(int nwg, long long ns, void* sink, hipStream_t stream) {

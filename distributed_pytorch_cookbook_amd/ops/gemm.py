@@ -73,8 +73,9 @@ _TUNE_PATH = os.environ.get("DPC_GEMM_TABLE_PATH") or os.path.join(
     os.path.dirname(os.path.abspath(__file__)), "gemm_tuned.json")
 _TUNE = os.environ.get("DPC_GEMM_TUNE", "0") == "1"
 _USE_TABLE = os.environ.get("DPC_GEMM_TABLE", "1") == "1"
-# 0 = the dispatcher policy; 16 / 17 / 19 / 20 = the 4-wave 256x256 kernel (gemm7.hip)
-_CANDIDATES = (0, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 16, 17, 19, 20, 21)
+# 0 = the dispatcher policy; 16 / 17 / 19 / 20 / 22 / 23 = the 4-wave 256x256 kernel (gemm7.hip;
+# 16 / 20 / 22 run the paired-M0 DMA issue, 19 / 23 the quad form), 21 = v8 (two per CU)
+_CANDIDATES = (0, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 16, 17, 19, 20, 21, 22, 23)
 _TUNE_MAX_OUT_BYTES = 16 << 30  # (the GPT-2 small LM-head logits are 6.6 GB)
 
 

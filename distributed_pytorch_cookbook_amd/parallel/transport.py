@@ -71,10 +71,14 @@ def forget_outstanding() -> None:
 # SURVEY.md §5.8 rule 4 (comm overlapped with compute on side streams): the persistent GEMMs
 # (ops/csrc/gemm7.hip) size their grid to occupy every CU, so an RCCL kernel resident on a
 # CU while a GEMM launches would push that CU's GEMM workgroup -- and its whole share of the
-# tiles -- into a second round.  From the moment an asynchronous GPU collective is enqueued
-# until its handle is waited on, the GEMMs leave DPC_CU_RESERVE CUs (default 16) free for it.
-# Captured into a HIP graph like every other launch parameter.
-_CU_RESERVE = int(os.environ.get("DPC_CU_RESERVE", "16"))
+# tiles -- into a second round.  With DPC_CU_RESERVE=R, from the moment an asynchronous GPU
+# collective is enqueued until its handle is waited on, the GEMMs leave R CUs free for it
+# (captured into a HIP graph like every other launch parameter).  Default 0: on one MI355X the
+# reserve itself costs a round of wave quantisation on the GPT-2 products (QKV forward +23 %,
+# input gradient +40 % at R = 16 with nothing beside them) while a blocking collective-sized
+# occupier costs a weight gradient +69 % -- and the handles are waited on only at the end of
+# the backward, so a reserve would tax every backward GEMM (profiles/r3_gemm/cu_reserve*.log).
+_CU_RESERVE = int(os.environ.get("DPC_CU_RESERVE", "0"))
 _comm_inflight = 0
 
 

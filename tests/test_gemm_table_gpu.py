@@ -128,8 +128,9 @@ def test_cu_reserve_products_match_fp32(reserve, case):
     assert _rel(out, ref) < 1e-2, _rel(out, ref)
 
 
+@pytest.mark.parametrize("impl", [22, 23])
 @pytest.mark.parametrize("lay", ["nt", "nn", "tn", "tt"])
-def test_paired_dma_variant_matches_fp32(lay):
+def test_paired_dma_variant_matches_fp32(lay, impl):
     """v7 with the paired LDS-DMA issue (impl 22: one M0 write per two pieces, the second
     placed by the instruction offset) on every operand layout, edge tiles included."""
     from distributed_pytorch_cookbook_amd.ops import _lib
@@ -142,8 +143,9 @@ def test_paired_dma_variant_matches_fp32(lay):
     am = a.float() if lay[0] == "n" else a.float().t()
     bm = b.float().t() if lay[1] == "t" else b.float()
     try:
-        _lib.set_gemm_impl(22)
-        out = gemm(a, b, a_kmaj=lay[0] == "n", b_kmaj=lay[1] == "t", out_dtype=torch.float32)
+        _lib.set_gemm_impl(impl)
+        out = gemm(a, b, a_kmaj=lay[0] == "n", b_kmaj=lay[1] == "t",
+                   out_dtype=torch.bfloat16 if lay[0] == "n" else torch.float32)
         torch.cuda.synchronize()
     finally:
         _lib.set_gemm_impl(-1)
