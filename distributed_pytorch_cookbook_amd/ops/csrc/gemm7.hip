@@ -162,7 +162,8 @@ __device__ __forceinline__ float g7_ror8(float v) { return __uint_as_float(g7_ro
 // PK: GELU / GELU' in packed-f32 math (v8 with a K-major A; the other instantiations have no
 // register room for it)
 template <int MODE, int NJ, bool PK = false>
-__device__ __forceinline__ void g7_epilogue(const GemmArgs& p, floatx4 (&acc)[8][NJ], int mw, int nw, int lane) {
+__device__ __forceinline__ void g7_epilogue(const GemmArgs& p, floatx4 (&acc)[8][NJ], int mw, int nw, int lane,
+                                            int dbg = 0) {
   float alpha = p.alpha;
   if (p.alpha_ptr) alpha *= *p.alpha_ptr;
   const int g = lane >> 4, rl = lane & 15;
@@ -231,7 +232,10 @@ __device__ __forceinline__ void g7_epilogue(const GemmArgs& p, floatx4 (&acc)[8]
         const uint4 dA = make_uint4(lo ? c0.x : rcv.x, lo ? c0.y : rcv.y, lo ? c0.z : rcv.z, lo ? c0.w : rcv.w);
         const uint4 dB = make_uint4(lo ? rcv.x : c1.x, lo ? rcv.y : c1.y, lo ? rcv.z : c1.z, lo ? rcv.w : c1.w);
         const int m = mw + 16 * i + rr, n = nw + 16 * j + coff + 32 * hi8;
-        if (n < p.N) {
+        if ((dbg & 4) || ((dbg & 8) && (blockIdx.x & 1))) {  // (experiments: the epilogue's VALU
+          // without its stores -- on every workgroup (4) or on every other one (8))
+          asm volatile("" ::"v"(dA.x), "v"(dA.y), "v"(dA.z), "v"(dA.w), "v"(dB.x), "v"(dB.y), "v"(dB.z), "v"(dB.w));
+        } else if (n < p.N) {
           bf16_t* C = static_cast<bf16_t*>(p.C) + (long long)m * p.ldc + n;
           if (m < p.M) *reinterpret_cast<uint4*>(C) = dA;
           if (m + 8 < p.M) *reinterpret_cast<uint4*>(C + 8 * p.ldc) = dB;
@@ -626,6 +630,8 @@ __global__ __launch_bounds__(256, WN == 128 ? 1 : 2) void gemm7_kernel(GemmArgs 
       q.ldc = p.N;
       q.out_f32 = 1;
       g7_epilogue<0, NJ>(q, acc, m0 + ar, n0 + bc, lane);
+    } else if constexpr (EPI == 0) {
+      g7_epilogue<EPI, NJ, WN == 64 && AK>(p, acc, m0 + ar, n0 + bc, lane, pl.debug);
     } else {
       g7_epilogue<EPI, NJ, WN == 64 && AK>(p, acc, m0 + ar, n0 + bc, lane);
     }
@@ -812,7 +818,7 @@ DPC_API int dpc_gemm7(const GemmArgs* a, int persistent, int sched, int splits, 
   static int dbg = -1;
   if (dbg < 0) dbg = getenv("DPC_G7_DEBUG") ? atoi(getenv("DPC_G7_DEBUG")) : 0;
   pl.debug = dbg;
-  if (dbg & 1) pl.store_cnt = 0;
+  if (dbg & 13) pl.store_cnt = 0;
   if (slab) {
     if (v8) g7_launch_s<4, 64>(a, pl, stream, ab, bb);
     else g7_launch_s<4>(a, pl, stream, ab, bb);
