@@ -19,6 +19,9 @@ ap.add_argument("--model", default="gpt2-medium")
 ap.add_argument("--batch", type=int, default=8)
 ap.add_argument("--steps", type=int, default=6)
 ap.add_argument("--offload", type=int, default=1)
+ap.add_argument("--breakdown", action="store_true",
+                help="time each offload stage alone (D2H grads, host AdamW, H2D weights) and the "
+                     "host memory / link bandwidths they are bound by")
 a = ap.parse_args()
 p = PRESETS[a.model]
 S = p["sequence_length"] - 1
@@ -39,3 +42,51 @@ torch.cuda.synchronize()
 ms = (time.perf_counter() - t0) / a.steps * 1e3
 mode = "none" if not a.offload else ("sync" if os.environ.get("DPC_OFFLOAD_SYNC") == "1" else "pipelined")
 print(f"offload={mode} model={a.model} batch={a.batch}: {ms:.1f} ms/step  loss {loss.item():.4f}")
+
+
+def _ev_ms(fn, reps=3):
+    ts = []
+    for _ in range(reps):
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s.record()
+        fn()
+        e.record()
+        e.synchronize()
+        ts.append(s.elapsed_time(e))
+    return min(ts)
+
+
+def _host_ms(fn, reps=3):
+    ts = []
+    for _ in range(reps):
+        t = time.perf_counter()
+        fn()
+        ts.append((time.perf_counter() - t) * 1e3)
+    return min(ts)
+
+
+if a.breakdown and a.offload:
+    from distributed_pytorch_cookbook_amd import runtime
+
+    st = eng.store
+    st.wait_host()
+    n = st.master.numel()
+    opt = eng.opt
+    gb = lambda nbytes, ms: nbytes / ms / 1e6  # noqa: E731
+    d2h = _ev_ms(lambda: st.grads_host.copy_(st.grads, non_blocking=True))
+    h2d = _ev_ms(lambda: st.shadow.copy_(st._hshadow, non_blocking=True))
+    adam = _host_ms(lambda: runtime.adamw_host(st.master, st.grads_host, opt.exp_avg, opt.exp_avg_sq, 1e-12,
+                                               0.9, 0.95, 1e-8, 0.0, 5, 1.0, st._hshadow))
+    big = torch.empty(n, dtype=torch.float32, pin_memory=True)
+    memcpy = _host_ms(lambda: big.copy_(st.master))  # 1 read + 1 write stream
+    adam_bytes = n * (4 * 4 + 3 * 4 + 2)  # reads p,g,m,v; writes p,m,v + bf16 copy
+    print(f"breakdown params={n / 1e6:.1f}M  threads={torch.get_num_threads()} "
+          f"(OMP_NUM_THREADS={os.environ.get('OMP_NUM_THREADS')})")
+    print(f"  D2H f32 grads   {n * 4 / 1e9:6.2f} GB  {d2h:7.1f} ms  {gb(n * 4, d2h):6.1f} GB/s")
+    print(f"  H2D bf16 params {n * 2 / 1e9:6.2f} GB  {h2d:7.1f} ms  {gb(n * 2, h2d):6.1f} GB/s")
+    print(f"  host AdamW      {adam_bytes / 1e9:6.2f} GB  {adam:7.1f} ms  {gb(adam_bytes, adam):6.1f} GB/s "
+          f"(30 B/param)")
+    print(f"  host memcpy     {n * 8 / 1e9:6.2f} GB  {memcpy:7.1f} ms  {gb(n * 8, memcpy):6.1f} GB/s "
+          f"(read+write; the host AdamW's bandwidth ceiling)")
+    print(f"  serial sum {d2h + adam + h2d:.1f} ms vs measured offload overhead (pipelined - none) "
+          f"-> run with --offload 0 for the none row")

@@ -668,6 +668,470 @@ __global__ __launch_bounds__(256) void g7_splitk_reduce(float* C, long long ldc,
   }
 }
 
+// ------------------------------------------------------------------ v7d: deferred epilogues
+// The fused GELU epilogues of the FFN products are VALU-heavy (~10 issue slots per element
+// forward, ~18 for GELU' in the input gradient) and a one-wave-per-SIMD kernel runs them
+// serially at the tile end: on the K = 768 GPT-2 products that is 50-60 % of the MFMA time
+// (profiles/r3_gemm/st8_fused_0.log: up 0.50 ms, act' dgrad 0.53-0.56 against 0.28-0.32 for
+// the plain products of the same shape).  Here the tile end does only the cheap part -- the
+// accumulators (+ bias) rounded to bf16 and stored (the pre-activation into aux_out, EPI 5;
+// the raw input gradient into C, EPI 6) -- and the element-wise rest is DEFERRED into the
+// next tile's main loop: the 32 16-B chunks a lane stored come back by LDS-DMA (the lane reads
+// exactly the addresses it wrote: same-wave program order), a few per k-slice, and their
+// GELU / GELU' arithmetic sits in the MFMA groups, where a wave has ~8 free issue cycles per
+// v_mfma_f32_16x16x32_bf16.  The results are stored a chunk or two per slice, so the output
+// traffic is spread over the tile instead of leaving in one chip-wide burst.
+// Rounding is the reference's (torch autocast): the GELU input is the bf16 pre-activation and
+// the GELU' product starts from the bf16 input gradient, as aten computes them.
+//   EPI 5: C = gelu(bf16(acc + bias)) bf16, aux_out = bf16(acc + bias).
+//   EPI 6: C = bf16(dy * gelu'(aux_in)), dy = bf16(acc); colsum[n] += sum_m of the same.
+// Ring: 4 slots (DIST 3) to free LDS for the unit regions ([2 parities][4 waves][2 units] x 1
+// or 2 KiB) and, EPI 5, the tile's 256 bias values (one DMA piece by wave 0 in body 1).
+// Counting: a body issues [unit DMAs for body c+2 at group 2] [the 8 ring pieces, last at
+// group 6] [its unit stores + column-sum atomic at the end]; at the end of body c the ring
+// needs slice c+2 (body c-1's pieces), and everything a body issues before its last piece is
+// older than it -- so the wait is vmcnt(ops issued after body c-1's last piece), computed per
+// body (a runtime count -> one of the immediates, g7_wait_bs).  Tiles that are partial or last
+// in a workgroup's list take the ordinary fused epilogue and drain (vmcnt(0)).
+template <int LO, int HI>
+__device__ __forceinline__ void g7_wait_bs(int n) {
+  if constexpr (LO == HI) {
+    g7_wait<LO>();
+  } else {
+    constexpr int MID = (LO + HI + 1) / 2;
+    if (n >= MID) g7_wait_bs<MID, HI>(n);
+    else g7_wait_bs<LO, MID - 1>(n);
+  }
+}
+
+// x * sigmoid(2u) (gelu_tanh) with log2(e) folded into the exponent's coefficients
+constexpr float G7_GK0 = 0.7978845608028654f, G7_GK1 = 0.044715f, G7_L2E = 1.4426950408889634f;
+__device__ __forceinline__ float g7_gelu(float x) {
+  const float e = __builtin_amdgcn_exp2f(x * fmaf(x * x, -2.f * G7_GK0 * G7_GK1 * G7_L2E, -2.f * G7_GK0 * G7_L2E));
+  return x * __builtin_amdgcn_rcpf(1.f + e);
+}
+// d/dx = s + x s (1 - s) 2 k0 (1 + 3 k1 x^2), s = sigmoid(2u)
+__device__ __forceinline__ float g7_gelu_grad(float x) {
+  const float x2 = x * x;
+  const float s = __builtin_amdgcn_rcpf(1.f + __builtin_amdgcn_exp2f(x * fmaf(x2, -2.f * G7_GK0 * G7_GK1 * G7_L2E, -2.f * G7_GK0 * G7_L2E)));
+  const float t = x * fmaf(x2, 6.f * G7_GK0 * G7_GK1, 2.f * G7_GK0);
+  return fmaf(t, fmaf(-s, s, s), s);
+}
+
+__device__ __forceinline__ unsigned g7_comp(const uint4& v, int c) {
+  return c == 0 ? v.x : (c == 1 ? v.y : (c == 2 ? v.z : v.w));
+}
+__device__ __forceinline__ void g7_setcomp(uint4& v, int c, unsigned w) {
+  if (c == 0) v.x = w;
+  else if (c == 1) v.y = w;
+  else if (c == 2) v.z = w;
+  else v.w = w;
+}
+__device__ __forceinline__ float g7_bf(unsigned w, int hi) {
+  return hi ? __uint_as_float(w & 0xffff0000u) : __uint_as_float(w << 16);
+}
+
+// The tile end of a deferred tile: bf16(acc * alpha [+ bias]) in the row-coalesced layout of
+// the MODE 0 epilogue (chunk (i, jb, half) of a lane: row mw + 16 i + rr + 8 half, columns
+// nw + 64 jb + coff + 32 hi8 .. +7), 32 unconditional 16-B stores (full tiles only).
+// CHECK (partial tiles): rows / columns past M / N skipped, the bias read from global memory
+// (bl = the bias vector) instead of the tile's LDS copy.
+template <bool BIAS, bool CHECK = false>
+__device__ __forceinline__ void g7_split_store(bf16_t* dst, long long ld, floatx4 (&acc)[8][8], int mw, int nw,
+                                               int lane, float alpha, const float* bl, int M = 0, int N = 0) {
+  const int g = lane >> 4, rl = lane & 15;
+  const int coff = 16 * (g & 1) + 8 * (g >> 1);
+  const bool lo = rl < 8;
+  const int rr = rl & 7, hi8 = rl >> 3;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+#pragma unroll
+    for (int j = 0; j < 8; j += 4) {
+      uint4 c0, c1;
+      {
+        floatx4 a0 = acc[i][j], a1 = acc[i][j + 1], a2 = acc[i][j + 2], a3 = acc[i][j + 3];
+        asm volatile("" : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3));
+        float4 b0 = make_float4(0.f, 0.f, 0.f, 0.f), b1 = b0, b2 = b0, b3 = b0;
+        if constexpr (BIAS && !CHECK) {
+          b0 = *reinterpret_cast<const float4*>(bl + 16 * j + 4 * g);
+          b1 = *reinterpret_cast<const float4*>(bl + 16 * (j + 1) + 4 * g);
+          b2 = *reinterpret_cast<const float4*>(bl + 16 * (j + 2) + 4 * g);
+          b3 = *reinterpret_cast<const float4*>(bl + 16 * (j + 3) + 4 * g);
+        } else if constexpr (BIAS) {
+          const int n = nw + 16 * j + 4 * g;
+          if (n < N) b0 = *reinterpret_cast<const float4*>(bl + n);
+          if (n + 16 < N) b1 = *reinterpret_cast<const float4*>(bl + n + 16);
+          if (n + 32 < N) b2 = *reinterpret_cast<const float4*>(bl + n + 32);
+          if (n + 48 < N) b3 = *reinterpret_cast<const float4*>(bl + n + 48);
+        }
+        const auto s0 = __builtin_amdgcn_permlane16_swap(pack2bf(fmaf(a0[0], alpha, b0.x), fmaf(a0[1], alpha, b0.y)),
+                                                         pack2bf(fmaf(a1[0], alpha, b1.x), fmaf(a1[1], alpha, b1.y)), false, false);
+        const auto s1 = __builtin_amdgcn_permlane16_swap(pack2bf(fmaf(a0[2], alpha, b0.z), fmaf(a0[3], alpha, b0.w)),
+                                                         pack2bf(fmaf(a1[2], alpha, b1.z), fmaf(a1[3], alpha, b1.w)), false, false);
+        const auto t0 = __builtin_amdgcn_permlane16_swap(pack2bf(fmaf(a2[0], alpha, b2.x), fmaf(a2[1], alpha, b2.y)),
+                                                         pack2bf(fmaf(a3[0], alpha, b3.x), fmaf(a3[1], alpha, b3.y)), false, false);
+        const auto t1 = __builtin_amdgcn_permlane16_swap(pack2bf(fmaf(a2[2], alpha, b2.z), fmaf(a2[3], alpha, b2.w)),
+                                                         pack2bf(fmaf(a3[2], alpha, b3.z), fmaf(a3[3], alpha, b3.w)), false, false);
+        c0 = make_uint4(s0[0], s1[0], s0[1], s1[1]);
+        c1 = make_uint4(t0[0], t1[0], t0[1], t1[1]);
+      }
+      const uint4 snd = make_uint4(lo ? c1.x : c0.x, lo ? c1.y : c0.y, lo ? c1.z : c0.z, lo ? c1.w : c0.w);
+      const uint4 rcv = make_uint4(g7_ror8(snd.x), g7_ror8(snd.y), g7_ror8(snd.z), g7_ror8(snd.w));
+      const uint4 dA = make_uint4(lo ? c0.x : rcv.x, lo ? c0.y : rcv.y, lo ? c0.z : rcv.z, lo ? c0.w : rcv.w);
+      const uint4 dB = make_uint4(lo ? rcv.x : c1.x, lo ? rcv.y : c1.y, lo ? rcv.z : c1.z, lo ? rcv.w : c1.w);
+      const int m = mw + 16 * i + rr, n = nw + 16 * j + coff + 32 * hi8;
+      bf16_t* C = dst + (long long)m * ld + n;
+      if (!CHECK || (n < N && m < M)) *reinterpret_cast<uint4*>(C) = dA;
+      if (!CHECK || (n < N && m + 8 < M)) *reinterpret_cast<uint4*>(C + 8 * ld) = dB;
+    }
+  }
+}
+
+// The element-wise rest of a tile whose chunks were just stored by g7_split_store, done at
+// once (partial tiles and each workgroup's last tile; the caller drained vmcnt): every lane
+// reads back its own chunks, one at a time (a rolled loop: little register pressure beside
+// the live accumulators of nothing -- the next tile has not started).
+template <int EPI>
+__device__ __forceinline__ void g7d_finish(const GemmArgs& p, int mw, int nw, int lane) {
+  const int g = lane >> 4, rl = lane & 15, rr = rl & 7, hi8 = rl >> 3;
+  const int coff = 16 * (g & 1) + 8 * (g >> 1);
+#pragma unroll 1
+  for (int jb = 0; jb < 2; ++jb) {
+    const int n = nw + 64 * jb + coff + 32 * hi8;
+    float cs[8];
+#pragma unroll
+    for (int v = 0; v < 8; ++v) cs[v] = 0.f;
+#pragma unroll 1
+    for (int t = 0; t < 16; ++t) {
+      const int m = mw + 16 * (t >> 1) + rr + 8 * (t & 1);
+      if (m < p.M && n < p.N) {
+        bf16_t* C = static_cast<bf16_t*>(p.C) + (long long)m * p.ldc + n;
+        uint4 o;
+        if constexpr (EPI == 5) {
+          const uint4 x = *reinterpret_cast<const uint4*>(static_cast<const bf16_t*>(p.aux_out) + (long long)m * p.ld_aux_out + n);
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const unsigned w = g7_comp(x, q);
+            g7_setcomp(o, q, pack2bf(g7_gelu(g7_bf(w, 0)), g7_gelu(g7_bf(w, 1))));
+          }
+        } else {
+          const uint4 dy = *reinterpret_cast<const uint4*>(C);
+          const uint4 x = *reinterpret_cast<const uint4*>(static_cast<const bf16_t*>(p.aux_in) + (long long)m * p.ld_aux_in + n);
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const float y0 = g7_bf(g7_comp(dy, q), 0) * g7_gelu_grad(g7_bf(g7_comp(x, q), 0));
+            const float y1 = g7_bf(g7_comp(dy, q), 1) * g7_gelu_grad(g7_bf(g7_comp(x, q), 1));
+            cs[2 * q] += y0;
+            cs[2 * q + 1] += y1;
+            g7_setcomp(o, q, pack2bf(y0, y1));
+          }
+        }
+        *reinterpret_cast<uint4*>(C) = o;
+      }
+    }
+    if (EPI == 6 && p.colsum) {
+      float pick = 0.f;
+#pragma unroll
+      for (int v = 0; v < 8; ++v) {
+        float s_ = cs[v];
+        s_ += __shfl_xor(s_, 1, 64);
+        s_ += __shfl_xor(s_, 2, 64);
+        s_ += __shfl_xor(s_, 4, 64);
+        pick = rr == v ? s_ : pick;
+      }
+      if (n + rr < p.N) atomicAdd(p.colsum + n + rr, pick);
+    }
+  }
+}
+
+template <int EPI, int SCHED, bool AK, bool BK>
+__global__ __launch_bounds__(256, 1) void gemm7d_kernel(GemmArgs p, unsigned long long a_bytes,
+                                                        unsigned long long b_bytes, G7Plan pl) {
+  constexpr int NJ = 8, BW = 256, TB = BW * G7_KB, SLOT = G7_TA + TB;
+  constexpr int NLB = TB / 512 / 4, NP = G7_NL + NLB;
+  constexpr int NS = 4, DIST = NS - 1;
+  constexpr int DPU = EPI == 6 ? 2 : 1;    // 1-KiB unit DMAs per unit
+  constexpr int UOFF = NS * SLOT;           // unit regions [parity][wave][unit][DPU] x 512 bf16
+  constexpr int BOFF = UOFF + 2 * 4 * 2 * DPU * 512;
+  constexpr int LDS_E = BOFF + (EPI == 5 ? 512 : 0);
+  static_assert(LDS_E * 2 <= 160 * 1024, "LDS");
+  static_assert(EPI == 5 || EPI == 6, "v7d epilogues");
+  __shared__ __attribute__((aligned(16))) bf16_t smem[LDS_E];
+
+  const int lane = threadIdx.x & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wr = wid >> 1, wc = wid & 1;
+  const int ar = wr * 128, bc = wc * 128;
+  const int rl = lane & 15, rr = rl & 7, hi8 = rl >> 3, lg = lane >> 4;
+  const int coff = 16 * (lg & 1) + 8 * (lg >> 1);
+
+  const int local = g7_local(blockIdx.x, pl.grid);
+  const int nmine = local < pl.units ? (pl.units - local + pl.grid - 1) / pl.grid : 0;
+  if (nmine == 0) return;
+
+  int va[G7_NL], vb[NLB];
+  dma_offsets3<32, AK, G7_NL>(va, p.lda, wid, lane);
+  dma_offsets3<32, BK, NLB>(vb, p.ldb, wid, lane);
+  const unsigned long long a_step = AK ? 64ull : 32ull * p.lda * 2;
+  const unsigned long long b_step = BK ? 64ull : 32ull * p.ldb * 2;
+
+  int is_u = 0, is_k = 0, is_slot = 0;
+  unsigned long long is_aoff = 0, is_boff = 0;
+  const int ntiles = pl.tiles_m * pl.tiles_n;
+  auto set_org = [&](int ui) {
+    const int uu = local + ui * pl.grid;
+    int m0, n0;
+    g7_tile(pl, uu % ntiles, m0, n0);
+    is_aoff = AK ? (unsigned long long)m0 * p.lda * 2 : (unsigned long long)m0 * 2;
+    is_boff = BK ? (unsigned long long)n0 * p.ldb * 2 : (unsigned long long)n0 * 2;
+  };
+  set_org(0);
+  __amdgpu_buffer_rsrc_t rsa, rsb;
+  const bf16_t* is_lds = smem;
+  auto prep = [&]() {
+    const bool valid = is_u < nmine && is_k < pl.nk_all;
+    const unsigned long long la = a_bytes - is_aoff, lb = b_bytes - is_boff;
+    const unsigned na = valid ? ((la >> 32) ? 0xffffffffu : (unsigned)la) : 0u;
+    const unsigned nb = valid ? ((lb >> 32) ? 0xffffffffu : (unsigned)lb) : 0u;
+    rsa = __builtin_amdgcn_make_buffer_rsrc((void*)((const char*)p.A + is_aoff), 0, na, 0x00020000);
+    rsb = __builtin_amdgcn_make_buffer_rsrc((void*)((const char*)p.B + is_boff), 0, nb, 0x00020000);
+    is_lds = smem + is_slot * SLOT;
+  };
+  auto piece = [&](int i) {
+    if (i < G7_NL) g7_piece(rsa, va[i], is_lds + (wid * G7_NL + i) * 512);
+    else g7_piece(rsb, vb[i - G7_NL], is_lds + G7_TA + (wid * NLB + i - G7_NL) * 512);
+  };
+  auto piece2 = [&](int i) {
+    if (i < G7_NL) g7_piece2(rsa, va[i], va[i + 1] - 1024, is_lds + (wid * G7_NL + i) * 512);
+    else g7_piece2(rsb, vb[i - G7_NL], vb[i + 1 - G7_NL] - 1024, is_lds + G7_TA + (wid * NLB + i - G7_NL) * 512);
+  };
+  auto advance = [&]() {
+    is_slot = is_slot + 1 == NS ? 0 : is_slot + 1;
+    is_aoff += a_step;
+    is_boff += b_step;
+    if (++is_k == pl.nk) {
+      is_k = 0;
+      ++is_u;
+      if (is_u < nmine) set_org(is_u);
+    }
+  };
+  auto piece_sched = [&](int g) {  // two pieces at the head of every even group
+    if (!(g & 1) && g < NP) {
+      if constexpr (SCHED == 3) piece2(g);
+      else { piece(g); piece(g + 1); }
+    }
+  };
+
+#pragma unroll
+  for (int s = 0; s < DIST; ++s) {
+    prep();
+#pragma unroll
+    for (int i = 0; i < NP; i += 2) piece_sched(i);
+    advance();
+  }
+  prep();
+
+  floatx4 acc[8][NJ];
+  g7_wait<(DIST - 1) * NP>();
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+  bf16x8 a0[8], b0[NJ], a1[8], b1[NJ];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) a0[i] = frag3<32, AK>(smem, ar + 16 * i, 0, lane);
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) b0[j] = frag3<32, BK>(smem + G7_TA, bc + 16 * j, 0, lane);
+  g7_wait<(DIST - 2) * NP>();
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+  int rd_slot = 1;
+
+  // ---- deferred-unit state (scalars unless noted).  Schedule of a tile's consuming bodies
+  // 2 .. nk-1 (B of them): nA bodies take two units, then nB one each (2 nA + nB = 32), the
+  // rest none -- three sequential loops of one body form each (a per-body choice between
+  // forms makes the register allocator spill the accumulators).
+  const int Bc = pl.nk - 2;
+  const int nA = Bc >= 32 ? 0 : 32 - Bc, nB = Bc >= 32 ? 32 : 2 * Bc - 32;
+  int pend = 0, pm0 = 0, pn0 = 0;  // the previous tile left its units; its origin
+  int post = 0;                    // vm ops issued after the previous body's last ring piece
+  auto sched_at = [&](int cc, int& u0) G7_AI {  // units consumed in body cc (of a pending tile)
+    const int q = cc - 2;
+    if (q < 0) return 0;
+    if (q < nA) { u0 = 2 * q; return 2; }
+    if (q < nA + nB) { u0 = 2 * nA + (q - nA); return 1; }
+    return 0;
+  };
+  const long long ld0 = EPI == 5 ? p.ld_aux_out : p.ldc;  // unit source 0: pre-activation / dy
+  const long long ld1 = p.ld_aux_in;                      // EPI 6 unit source 1: act' operand
+  const int lb0 = (int)(((long long)(ar + rr) * ld0 + bc + coff + 32 * hi8) * 2);
+  const int lb1 = EPI == 6 ? (int)(((long long)(ar + rr) * ld1 + bc + coff + 32 * hi8) * 2) : 0;
+  __amdgpu_buffer_rsrc_t rsu0 = rsa, rsu1 = rsa;
+  uint4 ud[2], ua[2], uo[2];
+  float yev[2], cs[8];
+#pragma unroll
+  for (int v = 0; v < 8; ++v) cs[v] = 0.f;
+  float alpha = p.alpha;
+  if (p.alpha_ptr) alpha *= *p.alpha_ptr;
+  const float* bl = reinterpret_cast<const float*>(smem + BOFF);
+  auto ureg = [&](int r, int k, int q) G7_AI { return smem + UOFF + ((r * 4 + wid) * 2 * DPU + k * DPU + q) * 512; };
+  auto ugeo = [&](int u, long long ld) G7_AI {  // uniform byte offset of unit u in the tile
+    const int i = (u >> 1) & 7, half = u & 1, jb = u >> 4;
+    return (int)(((long long)(16 * i + 8 * half) * ld + 64 * jb) * 2);
+  };
+  auto udma = [&](int r, int n, int u0) G7_AI {  // units u0 .. u0+n-1 -> region r
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this region's last reads retired
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      if (k < n) {
+        g7_piece(rsu0, lb0 + ugeo(u0 + k, ld0), ureg(r, k, 0));
+        if constexpr (EPI == 6) g7_piece(rsu1, lb1 + ugeo(u0 + k, ld1), ureg(r, k, 1));
+      }
+    }
+  };
+  auto bias_dma = [&](int n0) G7_AI {
+    const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc((void*)(p.bias + n0), 0, 1024u, 0x00020000);
+    g7_piece(rb, lane * 16, smem + BOFF);
+  };
+  // value v of this body's unit k (in a compile-time group: v is a constant after unrolling)
+  auto dvalue = [&](int k, int v) G7_AI {
+    const unsigned w = g7_comp(ud[k], v >> 1);
+    float y;
+    if constexpr (EPI == 5) {
+      y = g7_gelu(g7_bf(w, v & 1));
+    } else {
+      y = g7_bf(w, v & 1) * g7_gelu_grad(g7_bf(g7_comp(ua[k], v >> 1), v & 1));
+      cs[v] += y;
+    }
+    if (!(v & 1)) yev[k] = y;
+    else g7_setcomp(uo[k], v >> 1, pack2bf(yev[k], y));
+  };
+
+#define G7_MFMA_ROW(i_, ac, bcur, FIRST)                                                            \
+  _Pragma("unroll") for (int j = 0; j < NJ; ++j) acc[i_][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16( \
+      bcur[j], ac[i_], (FIRST) ? floatx4{0.f, 0.f, 0.f, 0.f} : acc[i_][j], 0, 0, 0)
+  // one slice (body c of the tile) with NU deferred units consumed
+#define G7D_BODY(ac, bcur, an, bn, FIRST, NU)                                                       \
+  do {                                                                                              \
+    const int rg = c & 1;                                                                           \
+    int ud0 = 0, uc0 = 0;                                                                           \
+    const int nd = pend ? sched_at(c + 2, ud0) : 0; /* units DMA'd now for body c+2 */             \
+    if constexpr (NU > 0) sched_at(c, uc0);                                                         \
+    if constexpr (NU > 0) {                                                                         \
+      _Pragma("unroll") for (int k = 0; k < NU; ++k) {                                              \
+        ud[k] = *reinterpret_cast<const uint4*>(ureg(rg, k, 0) + lane * 8);                         \
+        if constexpr (EPI == 6) ua[k] = *reinterpret_cast<const uint4*>(ureg(rg, k, 1) + lane * 8); \
+      }                                                                                             \
+    }                                                                                               \
+    const bf16_t* la_ = smem + rd_slot * SLOT;                                                      \
+    _Pragma("unroll") for (int i = 0; i < 8; ++i) {                                                 \
+      piece_sched(i);                                                                               \
+      if (i == 2 && nd > 0) udma(rg, nd, ud0);                                                      \
+      if (i == 4 && c == 1 && bdma) bias_dma(n0);                                                   \
+      an[i] = frag3<32, AK>(la_, ar + 16 * i, 0, lane);                                             \
+      bn[i] = frag3<32, BK>(la_ + G7_TA, bc + 16 * i, 0, lane);                                     \
+      G7_MFMA_ROW(i, ac, bcur, FIRST);                                                              \
+      _Pragma("unroll") for (int k = 0; k < NU; ++k) dvalue(k, i);                                  \
+      if (i == 7) {                                                                                 \
+        advance();                                                                                  \
+        prep();                                                                                     \
+      }                                                                                             \
+      __builtin_amdgcn_sched_barrier(0);                                                            \
+    }                                                                                               \
+    rd_slot = rd_slot + 1 == NS ? 0 : rd_slot + 1;                                                  \
+    int tail = 0;                                                                                   \
+    if constexpr (NU > 0) {                                                                         \
+      _Pragma("unroll") for (int k = 0; k < NU; ++k) {                                              \
+        const int u_ = uc0 + k, i_ = (u_ >> 1) & 7, h_ = u_ & 1, jb_ = u_ >> 4;                     \
+        bf16_t* dst = static_cast<bf16_t*>(p.C) + (long long)(pm0 + ar + 16 * i_ + rr + 8 * h_) * p.ldc + \
+                      pn0 + bc + 64 * jb_ + coff + 32 * hi8;                                        \
+        *reinterpret_cast<uint4*>(dst) = uo[k];                                                     \
+      }                                                                                             \
+      tail = NU;                                                                                    \
+      if constexpr (EPI == 6) {                                                                     \
+        if (p.colsum && ((uc0 + NU) & 15) == 0) { /* a half (one column set) done */             \
+          float pick = 0.f;                                                                         \
+          _Pragma("unroll") for (int v = 0; v < 8; ++v) {                                           \
+            float s_ = cs[v];                                                                       \
+            s_ += __shfl_xor(s_, 1, 64);                                                            \
+            s_ += __shfl_xor(s_, 2, 64);                                                            \
+            s_ += __shfl_xor(s_, 4, 64);                                                            \
+            pick = rr == v ? s_ : pick;                                                             \
+            cs[v] = 0.f;                                                                            \
+          }                                                                                         \
+          atomicAdd(p.colsum + pn0 + bc + 64 * ((uc0 + NU - 1) >> 4) + coff + 32 * hi8 + rr, pick); \
+          tail += 1;                                                                                \
+        }                                                                                           \
+      }                                                                                             \
+    }                                                                                               \
+    g7_wait_bs<0, 63>(min(63, post + NP + nd * DPU + ((c == 1 && bdma) ? 1 : 0) + tail));           \
+    post = tail;                                                                                    \
+    __builtin_amdgcn_s_barrier();                                                                   \
+    asm volatile("" ::: "memory");                                                                  \
+    ++c;                                                                                            \
+  } while (0)
+
+  for (int u = 0; u < nmine; ++u) {
+    const int uu = local + u * pl.grid;
+    int m0, n0;
+    g7_tile(pl, uu % ntiles, m0, n0);
+    const bool defer_me = m0 + 256 <= p.M && n0 + 256 <= p.N && u + 1 < nmine;
+    const bool bdma = EPI == 5 && defer_me && p.bias && wid == 0;
+    // this tile consumes the previous tile's units in its bodies 2 .. nk-1
+    if (pend) {
+      const long long ob0 = ((long long)pm0 * ld0 + pn0) * 2;
+      const void* src0 = EPI == 5 ? p.aux_out : p.C;
+      rsu0 = __builtin_amdgcn_make_buffer_rsrc((void*)((const char*)src0 + ob0), 0, 0xffffffffu, 0x00020000);
+      if constexpr (EPI == 6) {
+        const long long ob1 = ((long long)pm0 * ld1 + pn0) * 2;
+        rsu1 = __builtin_amdgcn_make_buffer_rsrc((void*)((const char*)p.aux_in + ob1), 0, 0xffffffffu, 0x00020000);
+      }
+    }
+    int c = 0;
+    G7D_BODY(a0, b0, a1, b1, true, 0);
+    G7D_BODY(a1, b1, a0, b0, false, 0);
+    const int eA = pend ? 2 + nA : 2, eB = pend ? 2 + nA + nB : 2;
+    for (; c < eA; ) {
+      G7D_BODY(a0, b0, a1, b1, false, 2);
+      G7D_BODY(a1, b1, a0, b0, false, 2);
+    }
+    for (; c < eB; ) {
+      G7D_BODY(a0, b0, a1, b1, false, 1);
+      G7D_BODY(a1, b1, a0, b0, false, 1);
+    }
+    for (; c < pl.nk; ) {
+      G7D_BODY(a0, b0, a1, b1, false, 0);
+      G7D_BODY(a1, b1, a0, b0, false, 0);
+    }
+    if (defer_me) {
+      if constexpr (EPI == 5) {
+        if (p.bias) g7_split_store<true>(static_cast<bf16_t*>(p.aux_out), p.ld_aux_out, acc, m0 + ar, n0 + bc, lane, alpha, bl + bc);
+        else g7_split_store<false>(static_cast<bf16_t*>(p.aux_out), p.ld_aux_out, acc, m0 + ar, n0 + bc, lane, alpha, bl);
+      } else {
+        g7_split_store<false>(static_cast<bf16_t*>(p.C), p.ldc, acc, m0 + ar, n0 + bc, lane, alpha, bl);
+      }
+      post += 32;
+      pend = 1;
+      pm0 = m0;
+      pn0 = n0;
+    } else {
+      // partial or last tile: the same two halves back to back
+      if constexpr (EPI == 5) {
+        if (p.bias) g7_split_store<true, true>(static_cast<bf16_t*>(p.aux_out), p.ld_aux_out, acc, m0 + ar, n0 + bc, lane, alpha, p.bias, p.M, p.N);
+        else g7_split_store<false, true>(static_cast<bf16_t*>(p.aux_out), p.ld_aux_out, acc, m0 + ar, n0 + bc, lane, alpha, p.bias, p.M, p.N);
+      } else {
+        g7_split_store<false, true>(static_cast<bf16_t*>(p.C), p.ldc, acc, m0 + ar, n0 + bc, lane, alpha, bl, p.M, p.N);
+      }
+      g7_wait<0>();
+      g7d_finish<EPI>(p, m0 + ar, n0 + bc, lane);
+      g7_wait<0>();
+      post = 0;
+      pend = 0;
+    }
+  }
+#undef G7_MFMA_ROW
+#undef G7D_BODY
+  g7_wait<0>();
+}
+
 }  // namespace dpc
 
 using namespace dpc;
@@ -730,6 +1194,24 @@ static void g7_launch_s(const GemmArgs* a, const G7Plan& pl, hipStream_t stream,
   if (pair_env < 0) pair_env = getenv("DPC_G7_PAIR") ? atoi(getenv("DPC_G7_PAIR")) : 1;
   if (pair_env && g7_bias_ok(a)) g7_launch<EPI, 3, WN>(a, pl, stream, ab, bb);
   else g7_launch<EPI, 2, WN>(a, pl, stream, ab, bb);
+}
+
+// v7d (deferred GELU epilogues): the forward up-projection form (both operands k-major) and
+// the input-gradient form (A k-major, B n-major) with the paired-M0 DMA schedule
+template <int EPI>
+static bool g7d_launch(const GemmArgs* a, const G7Plan& pl, hipStream_t stream, unsigned long long ab,
+                       unsigned long long bb) {
+  dim3 grid(pl.grid), block(256);
+  if (!g7_bias_ok(a)) return false;
+  if (EPI == 5 && a->a_kmaj && a->b_kmaj) {
+    hipLaunchKernelGGL((gemm7d_kernel<5, 3, true, true>), grid, block, 0, stream, *a, ab, bb, pl);
+    return true;
+  }
+  if (EPI == 6 && a->a_kmaj && !a->b_kmaj) {
+    hipLaunchKernelGGL((gemm7d_kernel<6, 3, true, false>), grid, block, 0, stream, *a, ab, bb, pl);
+    return true;
+  }
+  return false;
 }
 
 // Returns -1 if the product does not meet v7's requirements (caller falls back), else the
@@ -819,6 +1301,17 @@ DPC_API int dpc_gemm7(const GemmArgs* a, int persistent, int sched, int splits, 
   if (dbg < 0) dbg = getenv("DPC_G7_DEBUG") ? atoi(getenv("DPC_G7_DEBUG")) : 0;
   pl.debug = dbg;
   if (dbg & 13) pl.store_cnt = 0;
+  // v7d: sched 5 (impl 24) takes the GELU / GELU' fused epilogues of full-depth products
+  // (nk >= 18: at least 16 slices to spread a tile's deferred chunks over)
+  if (sched == 5 && !v8 && s == 1 && pl.nk >= 18) {
+    auto a16 = [](const void* q) { return ((uintptr_t)q % 16) == 0; };
+    const bool dfwd = a->act == ACT_GELU && a->aux_out && !a->residual && !a->accumulate && !a->out_f32 &&
+                      !a->act_bwd && !a->colsum && a->ld_aux_out % 8 == 0 && a16(a->aux_out);
+    const bool dbwd = a->act_bwd == ACT_GELU && a->aux_in && !a->out_f32 && !a->accumulate && !a->bias && !a->act &&
+                      !a->aux_out && !a->residual && a->ld_aux_in % 8 == 0 && a16(a->aux_in);
+    if (dfwd && g7d_launch<5>(a, pl, stream, ab, bb)) return (int)hipGetLastError();
+    if (dbwd && g7d_launch<6>(a, pl, stream, ab, bb)) return (int)hipGetLastError();
+  }
   if (slab) {
     if (v8) g7_launch_s<4, 64>(a, pl, stream, ab, bb);
     else g7_launch_s<4>(a, pl, stream, ab, bb);

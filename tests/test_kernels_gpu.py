@@ -161,6 +161,43 @@ def test_gemm_v6_v7(impl, a_kmaj, b_kmaj, M, N, K):
     assert rel_err(og, og_r) < 1e-2
 
 
+@pytest.mark.parametrize("M,N,K", [(16000, 3072, 768), (12000, 2560, 1600), (10000, 2048, 576), (4096, 4352, 768),
+                                   (65472, 3072, 768)])
+def test_gemm_v7d_deferred_gelu_epilogues(M, N, K):
+    """impl 24 (gemm7.hip gemm7d_kernel): the FFN's GELU forward (bias + GELU + pre-activation,
+    both operands k-major) and GELU' input gradient (act'(aux_in) + column sums, B n-major)
+    with the element-wise half deferred into the next tile's main loop.  Shapes give every
+    persistent workgroup 1-3+ tiles (deferred steady state, the last-tile and ragged-M
+    fallbacks) at the three schedule regimes: nk = 18 (two chunks per slice), 24 (two, then
+    one) and 50 (one, then none)."""
+    torch.manual_seed(5)
+    a = torch.randn(M, K, device=dev).bfloat16()
+    b = torch.randn(N, K, device=dev).bfloat16()
+    bias = torch.randn(N, device=dev)
+    z = torch.randn(M, N, device=dev).bfloat16()
+    aux = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+    cs = torch.zeros(N, device=dev)
+    A, Bk, Bn = _store(a, True), _store(b, True), _store(b, False)
+    _lib.set_gemm_impl(24)
+    try:
+        og = gemm(A, Bk, a_kmaj=True, b_kmaj=True, bias=bias, act=2, aux_out=aux)
+        od = gemm(A, Bn, a_kmaj=True, b_kmaj=False, act_bwd=2, aux_in=z, colsum=cs)
+    finally:
+        _lib.set_gemm_impl(-1)
+    og_r = torch.empty(M, N, device=dev)
+    aux_r = torch.empty_like(aux)
+    _gemm_ref(a, b, True, True, og_r, bias, 2, 0, None, aux_r, None, 1.0, None, False)
+    assert rel_err(aux, aux_r) < 1e-2
+    assert rel_err(og, og_r) < 1e-2
+    od_r = torch.empty(M, N, device=dev)
+    cs_r = torch.zeros(N, device=dev)
+    _gemm_ref(a, b, True, True, od_r, None, 0, 2, z, None, None, 1.0, None, False, cs_r)
+    assert rel_err(od, od_r) < 1e-2
+    assert rel_err(cs, cs_r) < 2e-3
+    # every element written (no chunk skipped by the deferred schedule)
+    assert torch.isfinite(og.float()).all() and torch.isfinite(od.float()).all()
+
+
 @pytest.mark.parametrize("impl", [2, 4, 7, 10, 11, 12, 16, 21])
 @pytest.mark.parametrize("splits", [2, 3, 8])
 @pytest.mark.parametrize("M,N,K", [(77, 1000, 4160), (600, 520, 8192), (2304, 136, 4096)])
