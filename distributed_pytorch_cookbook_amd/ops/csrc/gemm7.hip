@@ -685,6 +685,9 @@ __global__ __launch_bounds__(256) void g7_splitk_reduce(float* C, long long ldc,
 // the GELU' product starts from the bf16 input gradient, as aten computes them.
 //   EPI 5: C = gelu(bf16(acc + bias)) bf16, aux_out = bf16(acc + bias).
 //   EPI 6: C = bf16(dy * gelu'(aux_in)), dy = bf16(acc); colsum[n] += sum_m of the same.
+//   EPI 7: C = residual + gelu(bf16(acc + bias)) f32, aux_out = bf16(acc + bias) (the FFN
+//          down projection with the reference's second activation; K >= 1088, one chunk per
+//          slice: a chunk carries 48 B of operands).
 // Ring: 4 slots (DIST 3) to free LDS for the unit regions ([2 parities][4 waves][2 units] x 1
 // or 2 KiB) and, EPI 5, the tile's 256 bias values (one DMA piece by wave 0 in body 1).
 // Counting: a body issues [unit DMAs for body c+2 at group 2] [the 8 ring pieces, last at
@@ -807,7 +810,17 @@ __device__ __forceinline__ void g7d_finish(const GemmArgs& p, int mw, int nw, in
       if (m < p.M && n < p.N) {
         bf16_t* C = static_cast<bf16_t*>(p.C) + (long long)m * p.ldc + n;
         uint4 o;
-        if constexpr (EPI == 5) {
+        if constexpr (EPI == 7) {
+          const uint4 x = *reinterpret_cast<const uint4*>(static_cast<const bf16_t*>(p.aux_out) + (long long)m * p.ld_aux_out + n);
+          const float* R = p.residual + (long long)m * p.ldr + n;
+          const float4 r0 = *reinterpret_cast<const float4*>(R), r1 = *reinterpret_cast<const float4*>(R + 4);
+          float* Cf = static_cast<float*>(p.C) + (long long)m * p.ldc + n;
+          *reinterpret_cast<float4*>(Cf) = make_float4(r0.x + g7_gelu(g7_bf(x.x, 0)), r0.y + g7_gelu(g7_bf(x.x, 1)),
+                                                       r0.z + g7_gelu(g7_bf(x.y, 0)), r0.w + g7_gelu(g7_bf(x.y, 1)));
+          *reinterpret_cast<float4*>(Cf + 4) = make_float4(r1.x + g7_gelu(g7_bf(x.z, 0)), r1.y + g7_gelu(g7_bf(x.z, 1)),
+                                                           r1.z + g7_gelu(g7_bf(x.w, 0)), r1.w + g7_gelu(g7_bf(x.w, 1)));
+          continue;
+        } else if constexpr (EPI == 5) {
           const uint4 x = *reinterpret_cast<const uint4*>(static_cast<const bf16_t*>(p.aux_out) + (long long)m * p.ld_aux_out + n);
 #pragma unroll
           for (int q = 0; q < 4; ++q) {
@@ -850,12 +863,14 @@ __global__ __launch_bounds__(256, 1) void gemm7d_kernel(GemmArgs p, unsigned lon
   constexpr int NJ = 8, BW = 256, TB = BW * G7_KB, SLOT = G7_TA + TB;
   constexpr int NLB = TB / 512 / 4, NP = G7_NL + NLB;
   constexpr int NS = 4, DIST = NS - 1;
-  constexpr int DPU = EPI == 6 ? 2 : 1;    // 1-KiB unit DMAs per unit
-  constexpr int UOFF = NS * SLOT;           // unit regions [parity][wave][unit][DPU] x 512 bf16
-  constexpr int BOFF = UOFF + 2 * 4 * 2 * DPU * 512;
-  constexpr int LDS_E = BOFF + (EPI == 5 ? 512 : 0);
+  constexpr int DPU = EPI == 5 ? 1 : (EPI == 6 ? 2 : 3);  // 1-KiB unit DMAs per unit
+  constexpr int MAXU = EPI == 7 ? 1 : 2;                   // units per body at most
+  constexpr bool FWD = EPI != 6;                           // bias + GELU of the pre-activation
+  constexpr int UOFF = NS * SLOT;  // unit regions [parity][wave][unit][DPU] x 512 bf16
+  constexpr int BOFF = UOFF + 2 * 4 * MAXU * DPU * 512;
+  constexpr int LDS_E = BOFF + (FWD ? 512 : 0);
   static_assert(LDS_E * 2 <= 160 * 1024, "LDS");
-  static_assert(EPI == 5 || EPI == 6, "v7d epilogues");
+  static_assert(EPI >= 5 && EPI <= 7, "v7d epilogues");
   __shared__ __attribute__((aligned(16))) bf16_t smem[LDS_E];
 
   const int lane = threadIdx.x & 63;
@@ -960,19 +975,21 @@ __global__ __launch_bounds__(256, 1) void gemm7d_kernel(GemmArgs p, unsigned lon
     if (q < nA + nB) { u0 = 2 * nA + (q - nA); return 1; }
     return 0;
   };
-  const long long ld0 = EPI == 5 ? p.ld_aux_out : p.ldc;  // unit source 0: pre-activation / dy
+  const long long ld0 = FWD ? p.ld_aux_out : p.ldc;  // unit source 0: pre-activation / dy
   const long long ld1 = p.ld_aux_in;                      // EPI 6 unit source 1: act' operand
   const int lb0 = (int)(((long long)(ar + rr) * ld0 + bc + coff + 32 * hi8) * 2);
   const int lb1 = EPI == 6 ? (int)(((long long)(ar + rr) * ld1 + bc + coff + 32 * hi8) * 2) : 0;
+  const int lbr = EPI == 7 ? (int)(((long long)(ar + rr) * p.ldr + bc + coff + 32 * hi8) * 4) : 0;
   __amdgpu_buffer_rsrc_t rsu0 = rsa, rsu1 = rsa;
   uint4 ud[2], ua[2], uo[2];
+  float4 ur0[2], ur1[2], of0[2], of1[2];  // EPI 7: residual in, f32 out
   float yev[2], cs[8];
 #pragma unroll
   for (int v = 0; v < 8; ++v) cs[v] = 0.f;
   float alpha = p.alpha;
   if (p.alpha_ptr) alpha *= *p.alpha_ptr;
   const float* bl = reinterpret_cast<const float*>(smem + BOFF);
-  auto ureg = [&](int r, int k, int q) G7_AI { return smem + UOFF + ((r * 4 + wid) * 2 * DPU + k * DPU + q) * 512; };
+  auto ureg = [&](int r, int k, int q) G7_AI { return smem + UOFF + ((r * 4 + wid) * MAXU * DPU + k * DPU + q) * 512; };
   auto ugeo = [&](int u, long long ld) G7_AI {  // uniform byte offset of unit u in the tile
     const int i = (u >> 1) & 7, half = u & 1, jb = u >> 4;
     return (int)(((long long)(16 * i + 8 * half) * ld + 64 * jb) * 2);
@@ -984,6 +1001,11 @@ __global__ __launch_bounds__(256, 1) void gemm7d_kernel(GemmArgs p, unsigned lon
       if (k < n) {
         g7_piece(rsu0, lb0 + ugeo(u0 + k, ld0), ureg(r, k, 0));
         if constexpr (EPI == 6) g7_piece(rsu1, lb1 + ugeo(u0 + k, ld1), ureg(r, k, 1));
+        if constexpr (EPI == 7) {  // the f32 residual: two 16-B halves of the lane's 8 columns
+          const int o = lbr + 2 * ugeo(u0 + k, p.ldr);
+          g7_piece(rsu1, o, ureg(r, k, 1));
+          g7_piece(rsu1, o + 16, ureg(r, k, 2));
+        }
       }
     }
   };
@@ -995,7 +1017,18 @@ __global__ __launch_bounds__(256, 1) void gemm7d_kernel(GemmArgs p, unsigned lon
   auto dvalue = [&](int k, int v) G7_AI {
     const unsigned w = g7_comp(ud[k], v >> 1);
     float y;
-    if constexpr (EPI == 5) {
+    if constexpr (EPI == 7) {
+      y = g7_gelu(g7_bf(w, v & 1));
+      const float4& rq = v < 4 ? ur0[k] : ur1[k];
+      float4& oq = v < 4 ? of0[k] : of1[k];
+      const int e = v & 3;
+      const float r = e == 0 ? rq.x : (e == 1 ? rq.y : (e == 2 ? rq.z : rq.w));
+      if (e == 0) oq.x = r + y;
+      else if (e == 1) oq.y = r + y;
+      else if (e == 2) oq.z = r + y;
+      else oq.w = r + y;
+      return;
+    } else if constexpr (EPI == 5) {
       y = g7_gelu(g7_bf(w, v & 1));
     } else {
       y = g7_bf(w, v & 1) * g7_gelu_grad(g7_bf(g7_comp(ua[k], v >> 1), v & 1));
@@ -1019,6 +1052,10 @@ __global__ __launch_bounds__(256, 1) void gemm7d_kernel(GemmArgs p, unsigned lon
       _Pragma("unroll") for (int k = 0; k < NU; ++k) {                                              \
         ud[k] = *reinterpret_cast<const uint4*>(ureg(rg, k, 0) + lane * 8);                         \
         if constexpr (EPI == 6) ua[k] = *reinterpret_cast<const uint4*>(ureg(rg, k, 1) + lane * 8); \
+        if constexpr (EPI == 7) {                                                                   \
+          ur0[k] = *reinterpret_cast<const float4*>(ureg(rg, k, 1) + lane * 8);                     \
+          ur1[k] = *reinterpret_cast<const float4*>(ureg(rg, k, 2) + lane * 8);                     \
+        }                                                                                           \
       }                                                                                             \
     }                                                                                               \
     const bf16_t* la_ = smem + rd_slot * SLOT;                                                      \
@@ -1041,11 +1078,16 @@ __global__ __launch_bounds__(256, 1) void gemm7d_kernel(GemmArgs p, unsigned lon
     if constexpr (NU > 0) {                                                                         \
       _Pragma("unroll") for (int k = 0; k < NU; ++k) {                                              \
         const int u_ = uc0 + k, i_ = (u_ >> 1) & 7, h_ = u_ & 1, jb_ = u_ >> 4;                     \
-        bf16_t* dst = static_cast<bf16_t*>(p.C) + (long long)(pm0 + ar + 16 * i_ + rr + 8 * h_) * p.ldc + \
-                      pn0 + bc + 64 * jb_ + coff + 32 * hi8;                                        \
-        *reinterpret_cast<uint4*>(dst) = uo[k];                                                     \
+        const long long e_ = (long long)(pm0 + ar + 16 * i_ + rr + 8 * h_) * p.ldc + pn0 + bc + 64 * jb_ + \
+                             coff + 32 * hi8;                                                       \
+        if constexpr (EPI == 7) {                                                                   \
+          *reinterpret_cast<float4*>(static_cast<float*>(p.C) + e_) = of0[k];                       \
+          *reinterpret_cast<float4*>(static_cast<float*>(p.C) + e_ + 4) = of1[k];                   \
+        } else {                                                                                    \
+          *reinterpret_cast<uint4*>(static_cast<bf16_t*>(p.C) + e_) = uo[k];                        \
+        }                                                                                           \
       }                                                                                             \
-      tail = NU;                                                                                    \
+      tail = EPI == 7 ? 2 * NU : NU;                                                                \
       if constexpr (EPI == 6) {                                                                     \
         if (p.colsum && ((uc0 + NU) & 15) == 0) { /* a half (one column set) done */             \
           float pick = 0.f;                                                                         \
@@ -1074,24 +1116,30 @@ __global__ __launch_bounds__(256, 1) void gemm7d_kernel(GemmArgs p, unsigned lon
     int m0, n0;
     g7_tile(pl, uu % ntiles, m0, n0);
     const bool defer_me = m0 + 256 <= p.M && n0 + 256 <= p.N && u + 1 < nmine;
-    const bool bdma = EPI == 5 && defer_me && p.bias && wid == 0;
+    const bool bdma = FWD && defer_me && p.bias && wid == 0;
     // this tile consumes the previous tile's units in its bodies 2 .. nk-1
     if (pend) {
       const long long ob0 = ((long long)pm0 * ld0 + pn0) * 2;
-      const void* src0 = EPI == 5 ? p.aux_out : p.C;
+      const void* src0 = FWD ? p.aux_out : p.C;
       rsu0 = __builtin_amdgcn_make_buffer_rsrc((void*)((const char*)src0 + ob0), 0, 0xffffffffu, 0x00020000);
       if constexpr (EPI == 6) {
         const long long ob1 = ((long long)pm0 * ld1 + pn0) * 2;
         rsu1 = __builtin_amdgcn_make_buffer_rsrc((void*)((const char*)p.aux_in + ob1), 0, 0xffffffffu, 0x00020000);
+      }
+      if constexpr (EPI == 7) {
+        const long long obr = ((long long)pm0 * p.ldr + pn0) * 4;
+        rsu1 = __builtin_amdgcn_make_buffer_rsrc((void*)((const char*)p.residual + obr), 0, 0xffffffffu, 0x00020000);
       }
     }
     int c = 0;
     G7D_BODY(a0, b0, a1, b1, true, 0);
     G7D_BODY(a1, b1, a0, b0, false, 0);
     const int eA = pend ? 2 + nA : 2, eB = pend ? 2 + nA + nB : 2;
-    for (; c < eA; ) {
-      G7D_BODY(a0, b0, a1, b1, false, 2);
-      G7D_BODY(a1, b1, a0, b0, false, 2);
+    if constexpr (MAXU == 2) {  // (EPI 7: nA == 0, host nk >= 34)
+      for (; c < eA; ) {
+        G7D_BODY(a0, b0, a1, b1, false, 2);
+        G7D_BODY(a1, b1, a0, b0, false, 2);
+      }
     }
     for (; c < eB; ) {
       G7D_BODY(a0, b0, a1, b1, false, 1);
@@ -1102,7 +1150,7 @@ __global__ __launch_bounds__(256, 1) void gemm7d_kernel(GemmArgs p, unsigned lon
       G7D_BODY(a1, b1, a0, b0, false, 0);
     }
     if (defer_me) {
-      if constexpr (EPI == 5) {
+      if constexpr (FWD) {
         if (p.bias) g7_split_store<true>(static_cast<bf16_t*>(p.aux_out), p.ld_aux_out, acc, m0 + ar, n0 + bc, lane, alpha, bl + bc);
         else g7_split_store<false>(static_cast<bf16_t*>(p.aux_out), p.ld_aux_out, acc, m0 + ar, n0 + bc, lane, alpha, bl);
       } else {
@@ -1114,7 +1162,7 @@ __global__ __launch_bounds__(256, 1) void gemm7d_kernel(GemmArgs p, unsigned lon
       pn0 = n0;
     } else {
       // partial or last tile: the same two halves back to back
-      if constexpr (EPI == 5) {
+      if constexpr (FWD) {
         if (p.bias) g7_split_store<true, true>(static_cast<bf16_t*>(p.aux_out), p.ld_aux_out, acc, m0 + ar, n0 + bc, lane, alpha, p.bias, p.M, p.N);
         else g7_split_store<false, true>(static_cast<bf16_t*>(p.aux_out), p.ld_aux_out, acc, m0 + ar, n0 + bc, lane, alpha, p.bias, p.M, p.N);
       } else {
@@ -1209,6 +1257,10 @@ static bool g7d_launch(const GemmArgs* a, const G7Plan& pl, hipStream_t stream, 
   }
   if (EPI == 6 && a->a_kmaj && !a->b_kmaj) {
     hipLaunchKernelGGL((gemm7d_kernel<6, 3, true, false>), grid, block, 0, stream, *a, ab, bb, pl);
+    return true;
+  }
+  if (EPI == 7 && a->a_kmaj && a->b_kmaj && pl.nk >= 34) {
+    hipLaunchKernelGGL((gemm7d_kernel<7, 3, true, true>), grid, block, 0, stream, *a, ab, bb, pl);
     return true;
   }
   return false;
@@ -1309,7 +1361,11 @@ DPC_API int dpc_gemm7(const GemmArgs* a, int persistent, int sched, int splits, 
                       !a->act_bwd && !a->colsum && a->ld_aux_out % 8 == 0 && a16(a->aux_out);
     const bool dbwd = a->act_bwd == ACT_GELU && a->aux_in && !a->out_f32 && !a->accumulate && !a->bias && !a->act &&
                       !a->aux_out && !a->residual && a->ld_aux_in % 8 == 0 && a16(a->aux_in);
+    const bool ddown = a->act == ACT_GELU && a->aux_out && a->residual && !a->accumulate && a->out_f32 &&
+                       !a->act_bwd && !a->colsum && a->ld_aux_out % 8 == 0 && a16(a->aux_out) && a->ldr % 4 == 0 &&
+                       a16(a->residual);  // (residual may alias C: a chunk is read, then written, by one lane)
     if (dfwd && g7d_launch<5>(a, pl, stream, ab, bb)) return (int)hipGetLastError();
+    if (ddown && g7d_launch<7>(a, pl, stream, ab, bb)) return (int)hipGetLastError();
     if (dbwd && g7d_launch<6>(a, pl, stream, ab, bb)) return (int)hipGetLastError();
   }
   if (slab) {

@@ -162,7 +162,7 @@ def test_gemm_v6_v7(impl, a_kmaj, b_kmaj, M, N, K):
 
 
 @pytest.mark.parametrize("M,N,K", [(16000, 3072, 768), (12000, 2560, 1600), (10000, 2048, 576), (4096, 4352, 768),
-                                   (65472, 3072, 768)])
+                                   (65472, 3072, 768), (65472, 768, 3072), (9000, 1600, 2048)])
 def test_gemm_v7d_deferred_gelu_epilogues(M, N, K):
     """impl 24 (gemm7.hip gemm7d_kernel): the FFN's GELU forward (bias + GELU + pre-activation,
     both operands k-major) and GELU' input gradient (act'(aux_in) + column sums, B n-major)
@@ -196,6 +196,20 @@ def test_gemm_v7d_deferred_gelu_epilogues(M, N, K):
     assert rel_err(cs, cs_r) < 2e-3
     # every element written (no chunk skipped by the deferred schedule)
     assert torch.isfinite(og.float()).all() and torch.isfinite(od.float()).all()
+    # the down projection (f32 residual in, f32 out; deferred at K >= 1088)
+    res = torch.randn(M, N, device=dev)
+    aux2 = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+    _lib.set_gemm_impl(24)
+    try:
+        ox = gemm(A, Bk, a_kmaj=True, b_kmaj=True, bias=bias, act=2, aux_out=aux2, residual=res,
+                  out_dtype=torch.float32)
+    finally:
+        _lib.set_gemm_impl(-1)
+    ox_r = torch.empty(M, N, device=dev)
+    aux2_r = torch.empty_like(aux2)
+    _gemm_ref(a, b, True, True, ox_r, bias, 2, 0, None, aux2_r, res, 1.0, None, False)
+    assert rel_err(aux2, aux2_r) < 1e-2
+    assert rel_err(ox, ox_r) < 5e-3
 
 
 @pytest.mark.parametrize("impl", [2, 4, 7, 10, 11, 12, 16, 21])
