@@ -1,7 +1,7 @@
 // Standalone A/B + ablation driver for the persistent GEMM kernels (gemm7_kern.h), no torch:
 //
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=fast bench/g7lab.hip -o bench/g7lab
-//   bench/g7lab M N K [nt|nn] [rounds] [reps]
+//   bench/g7lab M N K [nt|nn|tn] [rounds] [reps] [sched|abl]
 //
 // Every variant runs on the same random bf16 operands (uniform [-1, 1): DVFS reads high on
 // zeros), interleaved in rounds inside one process (median per variant).  The ABL variants
@@ -57,18 +57,19 @@ struct Variant {
   std::vector<double> ms;
 };
 
-template <int ABL, bool BK>
+template <int ABL, bool AK, bool BK, int SCHED = 3>
 static void launch(const GemmArgs& a, G7Plan pl, unsigned long long ab, unsigned long long bb) {
-  hipLaunchKernelGGL((gemm7_kernel<0, 3, true, BK, 128, ABL>), dim3(pl.grid), dim3(256), 0, 0, a, ab, bb, pl);
+  hipLaunchKernelGGL((gemm7_kernel<0, SCHED, AK, BK, 128, ABL>), dim3(pl.grid), dim3(256), 0, 0, a, ab, bb, pl);
 }
 
 int main(int argc, char** argv) {
   if (argc < 4) {
-    fprintf(stderr, "usage: %s M N K [nt|nn] [rounds] [reps]\n", argv[0]);
+    fprintf(stderr, "usage: %s M N K [nt|nn|tn] [rounds] [reps] [sched|abl]\n", argv[0]);
     return 1;
   }
   const int M = atoi(argv[1]), N = atoi(argv[2]), K = atoi(argv[3]);
-  const bool nn = argc > 4 && std::string(argv[4]) == "nn";
+  const std::string lay = argc > 4 ? argv[4] : "nt";
+  const bool nn = lay == "nn", tn = lay == "tn";
   const int rounds = argc > 5 ? atoi(argv[5]) : 5;
   const int reps = argc > 6 ? atoi(argv[6]) : 10;
   if (M % 256 || N % 256 || K % 64) {
@@ -92,15 +93,15 @@ int main(int argc, char** argv) {
   a.N = N;
   a.K = K;
   a.alpha = 1.f;
-  a.a_kmaj = 1;
-  a.b_kmaj = nn ? 0 : 1;
-  a.lda = K;
-  a.ldb = nn ? N : K;
+  a.a_kmaj = tn ? 0 : 1;
+  a.b_kmaj = (nn || tn) ? 0 : 1;
+  a.lda = tn ? M : K;
+  a.ldb = (nn || tn) ? N : K;
   a.ldc = N;
-  a.a_r = M;
-  a.a_c = K;
-  a.b_r = nn ? K : N;
-  a.b_c = nn ? N : K;
+  a.a_r = tn ? K : M;
+  a.a_c = tn ? M : K;
+  a.b_r = (nn || tn) ? K : N;
+  a.b_c = (nn || tn) ? N : K;
   const unsigned long long ab = (unsigned long long)M * K * 2, bb = (unsigned long long)N * K * 2;
 
   G7Plan pl;
@@ -114,54 +115,62 @@ int main(int argc, char** argv) {
   pl.units = pl.tiles_m * pl.tiles_n;
   pl.grid = std::min(pl.units, 256);
   pl.store_cnt = 32;
-  G7Plan nodma = pl, noepi = pl;
-  nodma.debug = 2;
+  G7Plan noepi = pl;
   noepi.debug = 1;
 
   std::vector<Variant> vs;
-  if (nn) {
-    vs.push_back({"base", [&] { launch<0, false>(a, pl, ab, bb); }, false, {}});
-    vs.push_back({"clk", [&] { launch<128, false>(a, pl, ab, bb); }, true, {}});
-    vs.push_back({"no_dma", [&] { launch<128, false>(a, nodma, ab, bb); }, true, {}});
-    vs.push_back({"no_read", [&] { launch<128 | 32, false>(a, pl, ab, bb); }, true, {}});
-  } else {
-    vs.push_back({"base", [&] { launch<0, true>(a, pl, ab, bb); }, false, {}});
-    vs.push_back({"clk", [&] { launch<128, true>(a, pl, ab, bb); }, true, {}});
-    vs.push_back({"no_epilogue", [&] { launch<128, true>(a, noepi, ab, bb); }, true, {}});
-    vs.push_back({"no_dma", [&] { launch<128, true>(a, nodma, ab, bb); }, true, {}});
-    vs.push_back({"no_barrier", [&] { launch<128 | 16, true>(a, pl, ab, bb); }, true, {}});
-    vs.push_back({"no_read", [&] { launch<128 | 32, true>(a, pl, ab, bb); }, true, {}});
-    vs.push_back({"no_wait", [&] { launch<128 | 64, true>(a, pl, ab, bb); }, true, {}});
-    vs.push_back({"no_read_no_dma", [&] { launch<128 | 32, true>(a, nodma, ab, bb); }, true, {}});
-    vs.push_back({"mfma_only", [&] { launch<128 | 32 | 16, true>(a, nodma, ab, bb); }, true, {}});
+  const std::string set = argc > 7 ? argv[7] : "sched";
+#define LAB_SET(AK_, BK_)                                                                                 \
+  if (set == "abl") {                                                                                     \
+    vs.push_back({"base", [&] { launch<0, AK_, BK_>(a, pl, ab, bb); }, false, {}});                       \
+    vs.push_back({"clk", [&] { launch<128, AK_, BK_>(a, pl, ab, bb); }, true, {}});                       \
+    vs.push_back({"no_epilogue", [&] { launch<128, AK_, BK_>(a, noepi, ab, bb); }, true, {}});            \
+    vs.push_back({"no_dma", [&] { launch<128 | 2, AK_, BK_>(a, pl, ab, bb); }, true, {}});                \
+    vs.push_back({"no_barrier", [&] { launch<128 | 16, AK_, BK_>(a, pl, ab, bb); }, true, {}});           \
+    vs.push_back({"no_read", [&] { launch<128 | 32, AK_, BK_>(a, pl, ab, bb); }, true, {}});              \
+    vs.push_back({"no_read_no_dma", [&] { launch<128 | 32 | 2, AK_, BK_>(a, pl, ab, bb); }, true, {}});   \
+    vs.push_back({"mfma_only", [&] { launch<128 | 32 | 16 | 2, AK_, BK_>(a, pl, ab, bb); }, true, {}});   \
+  } else {                                                                                                \
+    vs.push_back({"s3", [&] { launch<0, AK_, BK_>(a, pl, ab, bb); }, false, {}});                         \
+    vs.push_back({"s3_old", [&] { launch<256, AK_, BK_>(a, pl, ab, bb); }, false, {}});                   \
+    vs.push_back({"s6", [&] { launch<0, AK_, BK_, 6>(a, pl, ab, bb); }, false, {}});                      \
+    vs.push_back({"s3_clk", [&] { launch<128, AK_, BK_>(a, pl, ab, bb); }, true, {}});                    \
+    vs.push_back({"s6_clk", [&] { launch<128, AK_, BK_, 6>(a, pl, ab, bb); }, true, {}});                 \
+    vs.push_back({"s6_no_dma", [&] { launch<128 | 2, AK_, BK_, 6>(a, pl, ab, bb); }, true, {}});          \
   }
+  if (tn) { LAB_SET(false, false) }
+  else if (nn) { LAB_SET(true, false) }
+  else { LAB_SET(true, true) }
 
-  // correctness of the base variant at sampled points
-  vs[0].run();
-  CK(hipGetLastError());
-  CK(hipDeviceSynchronize());
-  {
-    std::vector<unsigned short> hA((size_t)M * K), hB((size_t)N * K), hC((size_t)M * N);
-    CK(hipMemcpy(hA.data(), A, hA.size() * 2, hipMemcpyDeviceToHost));
-    CK(hipMemcpy(hB.data(), B, hB.size() * 2, hipMemcpyDeviceToHost));
+  // correctness of every non-ablation variant at sampled points
+  std::vector<unsigned short> hA((size_t)M * K), hB((size_t)N * K), hC((size_t)M * N);
+  CK(hipMemcpy(hA.data(), A, hA.size() * 2, hipMemcpyDeviceToHost));
+  CK(hipMemcpy(hB.data(), B, hB.size() * 2, hipMemcpyDeviceToHost));
+  for (auto& v : vs) {
+    if (v.clock) continue;  // (clock variants of a checked schedule, or ablations)
+    CK(hipMemset(C, 0, (size_t)M * N * 2));
+    v.run();
+    CK(hipGetLastError());
+    CK(hipDeviceSynchronize());
     CK(hipMemcpy(hC.data(), C, hC.size() * 2, hipMemcpyDeviceToHost));
     double maxerr = 0, maxref = 0;
     unsigned s = 12345;
-    for (int t = 0; t < 512; ++t) {
+    for (int t = 0; t < 1024; ++t) {
       s = s * 1103515245u + 12345u;
       const int m = (int)((s >> 8) % (unsigned)M);
       s = s * 1103515245u + 12345u;
       const int n = (int)((s >> 8) % (unsigned)N);
       double ref = 0;
       for (int k = 0; k < K; ++k) {
-        const float bv = nn ? h_bf(hB[(size_t)k * N + n]) : h_bf(hB[(size_t)n * K + k]);
-        ref += (double)h_bf(hA[(size_t)m * K + k]) * bv;
+        const float bv = (nn || tn) ? h_bf(hB[(size_t)k * N + n]) : h_bf(hB[(size_t)n * K + k]);
+        const float av = tn ? h_bf(hA[(size_t)k * M + m]) : h_bf(hA[(size_t)m * K + k]);
+        ref += (double)av * bv;
       }
       maxerr = std::max(maxerr, std::fabs(ref - (double)h_bf(hC[(size_t)m * N + n])));
       maxref = std::max(maxref, std::fabs(ref));
     }
-    printf("{\"check\": \"base\", \"max_abs_err\": %.4g, \"max_abs_ref\": %.4g, \"rel\": %.3g}\n", maxerr, maxref,
-           maxerr / maxref);
+    printf("{\"check\": \"%s\", \"max_abs_err\": %.4g, \"max_abs_ref\": %.4g, \"rel\": %.3g, \"ok\": %s}\n",
+           v.name.c_str(), maxerr, maxref, maxerr / maxref, maxerr / maxref < 0.01 ? "true" : "false");
   }
   for (auto& v : vs) v.run();  // warm every variant
   CK(hipDeviceSynchronize());
@@ -196,7 +205,7 @@ int main(int argc, char** argv) {
     const double med = m[m.size() / 2];
     printf("{\"M\": %d, \"N\": %d, \"K\": %d, \"layout\": \"%s\", \"variant\": \"%s\", \"ms\": %.4f, \"min_ms\": %.4f, "
            "\"tflops\": %.1f, \"clock_ghz\": %.3f}\n",
-           M, N, K, nn ? "nn" : "nt", vs[i].name.c_str(), med, m[0], flop / med / 1e9, ghz[i]);
+           M, N, K, lay.c_str(), vs[i].name.c_str(), med, m[0], flop / med / 1e9, ghz[i]);
   }
   CK(hipFree(A));
   CK(hipFree(B));

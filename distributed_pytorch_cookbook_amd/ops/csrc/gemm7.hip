@@ -86,12 +86,24 @@ static bool g7_bias_ok(const GemmArgs* a, long long bytes = 1024) {
 // M0 write (SCHED 3) where the operands allow it, else one M0 write per piece (SCHED 2).
 // Same-box A/B on MI355X (profiles/r3_gemm/ab22_*): +3 to +7 % on every GPT-2 product and on
 // 8192^3 (1252 -> 1330 TF/s nt).  DPC_G7_PAIR=0 restores SCHED 2.
+// v7 products with an mn-major operand (input and weight gradients) take the split interleave
+// (SCHED 6: one M0 / DMA instruction per MFMA gap): same-box bench/g7lab A/B +4..8 % on nn and
+// tn (8192^3 nn 1331 -> 1409, tn 1335 -> 1437 TF/s; GPT-2 out / up / LM-head input gradients
+// +5.4 / +4.8 / +5.1 %), within 1 % on nt (profiles/r3_gemm/lab_sched6.log).  DPC_G7_SPLIT=0
+// keeps the pairs.
+static bool g7_split_sched(const GemmArgs* a) {
+  static int env = -1;
+  if (env < 0) env = getenv("DPC_G7_SPLIT") ? atoi(getenv("DPC_G7_SPLIT")) : 1;
+  return env && (!a->a_kmaj || !a->b_kmaj);
+}
+
 template <int EPI, int WN = 128>
 static void g7_launch_s(const GemmArgs* a, const G7Plan& pl, hipStream_t stream, unsigned long long ab,
                         unsigned long long bb) {
   static int pair_env = -1;
   if (pair_env < 0) pair_env = getenv("DPC_G7_PAIR") ? atoi(getenv("DPC_G7_PAIR")) : 1;
-  if (pair_env && g7_bias_ok(a)) g7_launch<EPI, 3, WN>(a, pl, stream, ab, bb);
+  if (WN == 128 && g7_bias_ok(a) && g7_split_sched(a)) g7_launch<EPI, 6, WN>(a, pl, stream, ab, bb);
+  else if (pair_env && g7_bias_ok(a)) g7_launch<EPI, 3, WN>(a, pl, stream, ab, bb);
   else g7_launch<EPI, 2, WN>(a, pl, stream, ab, bb);
 }
 
@@ -238,7 +250,9 @@ DPC_API int dpc_gemm7(const GemmArgs* a, int persistent, int sched, int splits, 
     // group) -> pairs (3), SCHED 1 (four pieces at groups 0 and 4) -> quads (4)
     static int pair_env = -1;
     if (pair_env < 0) pair_env = getenv("DPC_G7_PAIR") ? atoi(getenv("DPC_G7_PAIR")) : 1;
-    if ((sched == 4 || (sched == 1 && pair_env)) && g7_bias_ok(a, 3072)) g7_launch<0, 4>(a, pl, stream, ab, bb);
+    if (sched == 6 && g7_bias_ok(a)) g7_launch<0, 6>(a, pl, stream, ab, bb);
+    else if ((sched == 2 || sched == 3) && g7_bias_ok(a) && g7_split_sched(a)) g7_launch<0, 6>(a, pl, stream, ab, bb);
+    else if ((sched == 4 || (sched == 1 && pair_env)) && g7_bias_ok(a, 3072)) g7_launch<0, 4>(a, pl, stream, ab, bb);
     else if (sched == 1) g7_launch<0, 1>(a, pl, stream, ab, bb);
     else if ((sched == 3 || pair_env) && g7_bias_ok(a)) g7_launch<0, 3>(a, pl, stream, ab, bb);
     else if (sched == 2) g7_launch<0, 2>(a, pl, stream, ab, bb);

@@ -24,7 +24,7 @@ struct G7Plan {
   int nk_all;  // k-slices of the whole product (slices of a unit past it read zeros)
   int splits;
   int store_cnt;  // vector-memory ops the epilogue issues per wave-lane (0: unknown -> no credit)
-  int debug;      // experiments only (DPC_G7_DEBUG): 1 = no epilogue stores, 2 = no in-loop DMA
+  int debug;      // experiments only (DPC_G7_DEBUG): 1 = no epilogue (main-loop ablations: ABL, bench/g7lab.hip)
 };
 
 // XCD-aware assignment: round i covers units [i*grid, (i+1)*grid); inside a round the blocks
@@ -90,6 +90,20 @@ __device__ __forceinline__ void g7_piece4(__amdgpu_buffer_rsrc_t rs, int v0, int
       :
       : "v"(v0), "v"(v1b), "v"(v2b), "v"(v3b), "s"(rs), "s"(la)
       : "memory", "m0");
+}
+
+// SCHED 6: a DMA pair split into its three instructions, so that each can sit in its own MFMA
+// gap (one vector-memory / M0 instruction per 16-cycle MFMA instead of a 4-instruction burst at
+// the head of a group).  M0 is written by the first and read by the two loads; nothing the
+// compiler places between them (MFMAs, ds_read_b128 / ds_read_b64_tr_b16, SALU) uses M0 on
+// gfx950.  The loads' voffsets are pre-biased as for g7_piece2.
+__device__ __forceinline__ void g7_m0(const bf16_t* lds) {
+  const unsigned la = (unsigned)(uintptr_t)(lds_void_t)lds;
+  asm volatile("s_mov_b32 m0, %0" ::"s"(la) : "memory", "m0");
+}
+template <int OFF>
+__device__ __forceinline__ void g7_ld(__amdgpu_buffer_rsrc_t rs, int voff) {
+  asm volatile("buffer_load_dwordx4 %0, %1, 0 offen offset:%2 lds" ::"v"(voff), "s"(rs), "n"(OFF) : "memory");
 }
 
 template <int N>
@@ -541,7 +555,8 @@ __global__ __launch_bounds__(256, WN == 128 ? 1 : 2) void gemm7_kernel(GemmArgs 
   // (measured on MI355X, bench/gemm_ab.py: 1 and 2 beat 0 by 2-6 %; all eight at the head
   // of the body or one at the tail of each group lost)
   auto piece_sched = [&](int g, bool tail) {
-    if (pl.debug & 2) return;
+    if ((ABL & 256) && (pl.debug & 2)) return;  // (the old runtime switch, A/B only)
+    if (ABL & 2) return;
     if (SCHED == 0 && !tail && g < NP) piece(g);
 
     if (SCHED == 2 && !tail && !(g & 1) && g < NP) { piece(g); piece(g + 1); }
@@ -555,9 +570,57 @@ __global__ __launch_bounds__(256, WN == 128 ? 1 : 2) void gemm7_kernel(GemmArgs 
   // into (an, bn), DMA of slice q+DIST, then slice q+2 landed (younger: slices q+3 .. q+DIST,
   // plus a recent epilogue's stores) + barrier.  nk is even (padded with all-zero slices), so every unit
   // starts on register set 0.
-#define G7_BODY(ac, bcur, an, bn, FIRST)                                                            \
+  // SCHED 6 (v7 only): group i = the 8 MFMAs of row i with one other instruction in each gap:
+  // the two fragment reads after MFMAs 0 and 1, and in the even groups the DMA pair's M0 write
+  // and its two loads after MFMAs 2, 3 and 4; the next body's cursor (advance / prep) in group
+  // 7 after MFMAs 1 and 4.  Every boundary pinned by sched_barrier.
+  auto mf = [&](int i, int j, const bf16x8* ac, const bf16x8* bcur, bool first) G7_AI {
+    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bcur[j], ac[i], first ? floatx4{0.f, 0.f, 0.f, 0.f} : acc[i][j],
+                                                        0, 0, 0);
+  };
+  auto dma5 = [&](int g, int step) G7_AI {  // step 0: M0, 1 / 2: the pair's loads
+    if constexpr ((ABL & 2) != 0) return;
+    const int i = g;  // pieces i, i+1 (A: 0..3, B: 4..7)
+    if (step == 0) {
+      if (i < G7_NL) g7_m0(is_lds + (wid * G7_NL + i) * 512);
+      else g7_m0(is_lds + G7_TA + (wid * NLB + i - G7_NL) * 512);
+    } else if (step == 1) {
+      if (i < G7_NL) g7_ld<0>(rsa, va[i]);
+      else g7_ld<0>(rsb, vb[i - G7_NL]);
+    } else {
+      if (i < G7_NL) g7_ld<1024>(rsa, va[i + 1] - 1024);
+      else g7_ld<1024>(rsb, vb[i + 1 - G7_NL] - 1024);
+    }
+  };
+#define G7_SB __builtin_amdgcn_sched_barrier(0)
+#define G7_GROUP5(i, ac, bcur, an, bn, FIRST)                                                        \
+  do {                                                                                              \
+    mf(i, 0, ac, bcur, FIRST); G7_SB;                                                               \
+    if (!(ABL & 32)) an[i] = frag3<32, AK>(la_, ar + 16 * i, 0, lane);                              \
+    G7_SB; mf(i, 1, ac, bcur, FIRST); G7_SB;                                                        \
+    if (!(ABL & 32)) bn[i] = frag3<32, BK>(la_ + G7_TA, bc + 16 * i, 0, lane);                      \
+    G7_SB; mf(i, 2, ac, bcur, FIRST); G7_SB;                                                        \
+    if (!((i) & 1) && (i) < NP) dma5(i, 0);                                                         \
+    if ((i) == 7) advance();                                                                        \
+    G7_SB; mf(i, 3, ac, bcur, FIRST); G7_SB;                                                        \
+    if (!((i) & 1) && (i) < NP) dma5(i, 1);                                                         \
+    G7_SB; mf(i, 4, ac, bcur, FIRST); G7_SB;                                                        \
+    if (!((i) & 1) && (i) < NP) dma5(i, 2);                                                         \
+    G7_SB; mf(i, 5, ac, bcur, FIRST); G7_SB;                                                        \
+    if ((i) == 7) prep();                                                                           \
+    G7_SB; mf(i, 6, ac, bcur, FIRST); G7_SB;                                                        \
+    mf(i, 7, ac, bcur, FIRST); G7_SB;                                                               \
+  } while (0)
+#define G7_BODY(ac, bcur, an, bn, FIRST) G7_BODYC(ac, bcur, an, bn, FIRST, false)
+#define G7_BODYC(ac, bcur, an, bn, FIRST, CREDIT)                                                   \
   do {                                                                                              \
     const bf16_t* la_ = smem + rd_slot * SLOT;                                                      \
+    if constexpr (SCHED == 6 && !A1) {                                                              \
+      G7_GROUP5(0, ac, bcur, an, bn, FIRST); G7_GROUP5(1, ac, bcur, an, bn, FIRST);                 \
+      G7_GROUP5(2, ac, bcur, an, bn, FIRST); G7_GROUP5(3, ac, bcur, an, bn, FIRST);                 \
+      G7_GROUP5(4, ac, bcur, an, bn, FIRST); G7_GROUP5(5, ac, bcur, an, bn, FIRST);                 \
+      G7_GROUP5(6, ac, bcur, an, bn, FIRST); G7_GROUP5(7, ac, bcur, an, bn, FIRST);                 \
+    } else                                                                                          \
     _Pragma("unroll") for (int i = 0; i < 8; ++i) {                                                 \
       piece_sched(i, false);                                                                        \
       if (!A1 && !(ABL & 32)) an[i] = frag3<32, AK>(la_, ar + 16 * i, 0, lane);                     \
@@ -576,7 +639,7 @@ __global__ __launch_bounds__(256, WN == 128 ? 1 : 2) void gemm7_kernel(GemmArgs 
     }                                                                                               \
     rd_slot = rd_slot + 1 == NS ? 0 : rd_slot + 1;                                                  \
     if (ABL & 64) {                                                                                 \
-    } else if (credit > 0) {                                                                        \
+    } else if ((CREDIT || (ABL & 256)) && credit > 0) {                                             \
       --credit;                                                                                     \
       if (pl.store_cnt >= 48) g7_wait<(DIST - 2) * NP + 47>();                                      \
       else g7_wait<(DIST - 2) * NP + 31>();                                                         \
@@ -593,15 +656,15 @@ __global__ __launch_bounds__(256, WN == 128 ? 1 : 2) void gemm7_kernel(GemmArgs 
   constexpr bool A1 = WN == 64;
   for (int u = 0; u < nmine; ++u) {
     if constexpr (A1) {
-      G7_BODY(a0, b0, a0, b1, true);
-      G7_BODY(a0, b1, a0, b0, false);
+      G7_BODYC(a0, b0, a0, b1, true, true);
+      G7_BODYC(a0, b1, a0, b0, false, true);
       for (int k = 2; k < pl.nk; k += 2) {
         G7_BODY(a0, b0, a0, b1, false);
         G7_BODY(a0, b1, a0, b0, false);
       }
     } else {
-      G7_BODY(a0, b0, a1, b1, true);
-      G7_BODY(a1, b1, a0, b0, false);
+      G7_BODYC(a0, b0, a1, b1, true, true);
+      G7_BODYC(a1, b1, a0, b0, false, true);
       for (int k = 2; k < pl.nk; k += 2) {
         G7_BODY(a0, b0, a1, b1, false);
         G7_BODY(a1, b1, a0, b0, false);
@@ -631,6 +694,9 @@ __global__ __launch_bounds__(256, WN == 128 ? 1 : 2) void gemm7_kernel(GemmArgs 
   }
 #undef G7_MFMA_ROW
 #undef G7_BODY
+#undef G7_BODYC
+#undef G7_GROUP5
+#undef G7_SB
   g7_wait<0>();  // empty-descriptor DMA of the slices past the end: drained before exit
   if constexpr ((ABL & 128) != 0) {
     const unsigned long long t1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();

@@ -1,0 +1,5 @@
+#!/bin/bash
+# Full GPU test suite, the GPT-2 GEMM A/B against hipBLASLt, the 1-GPU bench.
+scripts/gpu_step.sh "400:gputests:python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread" \
+  "300:ab_gpt2s:python -u bench/gemm_ab.py --shapes gpt2s --impls 22 25 --rounds 3" \
+  "300:bench1:python -u bench.py"
