@@ -250,8 +250,9 @@ DPC_API int dpc_gemm7(const GemmArgs* a, int persistent, int sched, int splits, 
     // group) -> pairs (3), SCHED 1 (four pieces at groups 0 and 4) -> quads (4)
     static int pair_env = -1;
     if (pair_env < 0) pair_env = getenv("DPC_G7_PAIR") ? atoi(getenv("DPC_G7_PAIR")) : 1;
-    if (sched == 6 && g7_bias_ok(a)) g7_launch<0, 6>(a, pl, stream, ab, bb);
-    else if ((sched == 2 || sched == 3) && g7_bias_ok(a) && g7_split_sched(a)) g7_launch<0, 6>(a, pl, stream, ab, bb);
+    // (every DMA placement of the table's v7 choices -- 16 / 19 / 20 / 22 / 23 -- gives way to the
+    // split interleave when an operand is mn-major: it beat each of them there)
+    if ((sched == 6 || g7_split_sched(a)) && g7_bias_ok(a)) g7_launch<0, 6>(a, pl, stream, ab, bb);
     else if ((sched == 4 || (sched == 1 && pair_env)) && g7_bias_ok(a, 3072)) g7_launch<0, 4>(a, pl, stream, ab, bb);
     else if (sched == 1) g7_launch<0, 1>(a, pl, stream, ab, bb);
     else if ((sched == 3 || pair_env) && g7_bias_ok(a)) g7_launch<0, 3>(a, pl, stream, ab, bb);
