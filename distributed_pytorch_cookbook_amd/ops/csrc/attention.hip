@@ -192,6 +192,19 @@ __device__ __forceinline__ bf16x8 acc_frag(const floatx16& x, int s) {
 
 __device__ __forceinline__ int acc_row(int r, int lane) { return (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5); }
 
+// Row-per-lane epilogue stores, widened: lane (row = lane & 31, hh = lane >> 5) holds the 4
+// bf16 at columns 8 g + 4 hh .. +3 of column group g (wa: group g, wb: group g + 1, g even).
+// One v_permlane32_swap per dword (lanes 32..63 of wa <-> lanes 0..31 of wb) leaves lanes 0..31
+// with columns 8 g .. 8 g + 7 and lanes 32..63 with 8 g + 8 .. 8 g + 15 of the SAME row, so the
+// pair leaves in one 16-B store per lane instead of two 8-B ones: half the store instructions
+// of a store-issue-bound tail (cdna_hip_programming.md T21).  Lanes l and l + 32 hold the same
+// row, so a row guard (key / query < S) keeps both or neither active.
+__device__ __forceinline__ void store_pair16(bf16_t* row, int g, int hh, uint2 wa, uint2 wb) {
+  const auto s0 = __builtin_amdgcn_permlane32_swap(wa.x, wb.x, false, false);
+  const auto s1 = __builtin_amdgcn_permlane32_swap(wa.y, wb.y, false, false);
+  *reinterpret_cast<uint4*>(row + 8 * g + 8 * hh) = make_uint4(s0[0], s1[0], s0[1], s1[1]);
+}
+
 // raw v_exp_f32 (2^x): inputs here are <= ~8 or -inf, no denormal range reduction needed
 __device__ __forceinline__ float fast_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
 
@@ -438,12 +451,13 @@ __global__ __launch_bounds__(256, OCC) void attn_fwd_kernel(AttnArgs p) {
 #pragma unroll
     for (int d = 0; d < A::NDT; ++d)
 #pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const int col = d * 32 + 8 * g + 4 * hh;
-        uint2 w;
-        w.x = pack2bf(o[d][4 * g + 0] * inv, o[d][4 * g + 1] * inv);
-        w.y = pack2bf(o[d][4 * g + 2] * inv, o[d][4 * g + 3] * inv);
-        *reinterpret_cast<uint2*>(O + col) = w;
+      for (int g = 0; g < 4; g += 2) {
+        uint2 wa, wb;
+        wa.x = pack2bf(o[d][4 * g + 0] * inv, o[d][4 * g + 1] * inv);
+        wa.y = pack2bf(o[d][4 * g + 2] * inv, o[d][4 * g + 3] * inv);
+        wb.x = pack2bf(o[d][4 * g + 4] * inv, o[d][4 * g + 5] * inv);
+        wb.y = pack2bf(o[d][4 * g + 6] * inv, o[d][4 * g + 7] * inv);
+        store_pair16(O + d * 32, g, hh, wa, wb);
       }
     if (hh == 0) {
       const float lse = (l > 0.f) ? (m + log2f(l)) / LOG2E : INFINITY;
@@ -572,12 +586,13 @@ __global__ __launch_bounds__(256, OCC) void attn_fwd2_kernel(AttnArgs p, int nit
 #pragma unroll
       for (int d = 0; d < A::NDT; ++d)
 #pragma unroll
-        for (int g = 0; g < 4; ++g) {
-          const int col = d * 32 + 8 * g + 4 * hh;
-          uint2 w;
-          w.x = pack2bf(o[d][4 * g + 0] * inv, o[d][4 * g + 1] * inv);
-          w.y = pack2bf(o[d][4 * g + 2] * inv, o[d][4 * g + 3] * inv);
-          *reinterpret_cast<uint2*>(O + col) = w;
+        for (int g = 0; g < 4; g += 2) {
+          uint2 wa, wb;
+          wa.x = pack2bf(o[d][4 * g + 0] * inv, o[d][4 * g + 1] * inv);
+          wa.y = pack2bf(o[d][4 * g + 2] * inv, o[d][4 * g + 3] * inv);
+          wb.x = pack2bf(o[d][4 * g + 4] * inv, o[d][4 * g + 5] * inv);
+          wb.y = pack2bf(o[d][4 * g + 6] * inv, o[d][4 * g + 7] * inv);
+          store_pair16(O + d * 32, g, hh, wa, wb);
         }
       if (hh == 0) p.lse[(long long)bh * S + q] = (l > 0.f) ? (m + log2f(l)) / LOG2E : INFINITY;
     }
@@ -884,20 +899,28 @@ __global__ __launch_bounds__(256, OCC) void attn_bwd_dkdv_kernel(AttnArgs p) {
   if (key < S) {
     bf16_t* dK = static_cast<bf16_t*>(p.dk) + (tok0 + key) * p.ld_dqkv + h * HD;
     bf16_t* dV = static_cast<bf16_t*>(p.dv) + (tok0 + key) * p.ld_dqkv + h * HD;
+    auto wk = [&](int d, int g) {  // (padded key: dK = dV = 0)
+      uint2 w = make_uint2(0u, 0u);
+      if (key_ok) {
+        w.x = pack2bf(dkt[d][4 * g + 0] * p.scale, dkt[d][4 * g + 1] * p.scale);
+        w.y = pack2bf(dkt[d][4 * g + 2] * p.scale, dkt[d][4 * g + 3] * p.scale);
+      }
+      return w;
+    };
+    auto wv = [&](int d, int g) {
+      uint2 u = make_uint2(0u, 0u);
+      if (key_ok) {
+        u.x = pack2bf(dvt[d][4 * g + 0], dvt[d][4 * g + 1]);
+        u.y = pack2bf(dvt[d][4 * g + 2], dvt[d][4 * g + 3]);
+      }
+      return u;
+    };
 #pragma unroll
     for (int d = 0; d < A::NDT; ++d)
 #pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const int col = d * 32 + 8 * g + 4 * hh;
-        uint2 w = make_uint2(0u, 0u), u = make_uint2(0u, 0u);  // padded key: dK = dV = 0
-        if (key_ok) {
-          w.x = pack2bf(dkt[d][4 * g + 0] * p.scale, dkt[d][4 * g + 1] * p.scale);
-          w.y = pack2bf(dkt[d][4 * g + 2] * p.scale, dkt[d][4 * g + 3] * p.scale);
-          u.x = pack2bf(dvt[d][4 * g + 0], dvt[d][4 * g + 1]);
-          u.y = pack2bf(dvt[d][4 * g + 2], dvt[d][4 * g + 3]);
-        }
-        *reinterpret_cast<uint2*>(dK + col) = w;
-        *reinterpret_cast<uint2*>(dV + col) = u;
+      for (int g = 0; g < 4; g += 2) {
+        store_pair16(dK + d * 32, g, hh, wk(d, g), wk(d, g + 1));
+        store_pair16(dV + d * 32, g, hh, wv(d, g), wv(d, g + 1));
       }
   }
 }
@@ -1025,12 +1048,13 @@ __global__ __launch_bounds__(256, OCC) void attn_bwd_dq_kernel(AttnArgs p) {
 #pragma unroll
     for (int d = 0; d < A::NDT; ++d)
 #pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const int col = d * 32 + 8 * g + 4 * hh;
-        uint2 w;
-        w.x = pack2bf(dqt[d][4 * g + 0] * p.scale, dqt[d][4 * g + 1] * p.scale);
-        w.y = pack2bf(dqt[d][4 * g + 2] * p.scale, dqt[d][4 * g + 3] * p.scale);
-        *reinterpret_cast<uint2*>(dQ + col) = w;
+      for (int g = 0; g < 4; g += 2) {
+        uint2 wa, wb;
+        wa.x = pack2bf(dqt[d][4 * g + 0] * p.scale, dqt[d][4 * g + 1] * p.scale);
+        wa.y = pack2bf(dqt[d][4 * g + 2] * p.scale, dqt[d][4 * g + 3] * p.scale);
+        wb.x = pack2bf(dqt[d][4 * g + 4] * p.scale, dqt[d][4 * g + 5] * p.scale);
+        wb.y = pack2bf(dqt[d][4 * g + 6] * p.scale, dqt[d][4 * g + 7] * p.scale);
+        store_pair16(dQ + d * 32, g, hh, wa, wb);
       }
   }
 }
