@@ -752,7 +752,10 @@ __global__ __launch_bounds__(256) void attn_bwd_pre_kernel(AttnArgs p) {
 // dK, dV: workgroup = 128 keys (4 waves x 32, key on the lane), sweeping the 64-query tiles
 // at or after the first key.  Per 32-query sub-block j: S, dP of sub-block j+1 (2 x NST
 // MFMAs) overlap the P / dS arithmetic of j, then dV^T, dK^T += ... (4 x NDT MFMAs).
-template <int HD, bool PIPE, int OCC>
+// ABL (dpc_attn_bwd_lab only; the library launches ABL = 0): per-workgroup cost ablations --
+// 1 = no tile loop (the ring prologue stays), 2 = no per-row register loads, 4 = no epilogue
+// stores, 8 = no ring prologue.  Outputs are wrong by design.
+template <int HD, bool PIPE, int OCC, int ABL = 0>
 __global__ __launch_bounds__(256, OCC) void attn_bwd_dkdv_kernel(AttnArgs p) {
   using A = AT<HD>;
   __shared__ __attribute__((aligned(16))) bf16_t smem[NSLOT * 2 * A::TILE];  // [slot][Q|dO]
@@ -778,8 +781,8 @@ __global__ __launch_bounds__(256, OCC) void attn_bwd_dkdv_kernel(AttnArgs p) {
   bf16x8 kf[A::NST], vf[A::NST];
 #pragma unroll
   for (int st = 0; st < A::NST; ++st) {
-    kf[st] = key < S ? load_row8(Kp + (tok0 + key) * p.ld_qkv + 16 * st + 8 * hh) : bf16x8{};
-    vf[st] = key < S ? load_row8(Vp + (tok0 + key) * p.ld_qkv + 16 * st + 8 * hh) : bf16x8{};
+    kf[st] = (key < S && !(ABL & 2)) ? load_row8(Kp + (tok0 + key) * p.ld_qkv + 16 * st + 8 * hh) : bf16x8{};
+    vf[st] = (key < S && !(ABL & 2)) ? load_row8(Vp + (tok0 + key) * p.ld_qkv + 16 * st + 8 * hh) : bf16x8{};
   }
   pin_loaded(kf);
   pin_loaded(vf);
@@ -831,7 +834,7 @@ __global__ __launch_bounds__(256, OCC) void attn_bwd_dkdv_kernel(AttnArgs p) {
     }
   };
 
-  if (count > 0) {
+  if (count > 0 && !(ABL & 8)) {
     issue(0);
     issue(1);
     issue(2);
@@ -886,7 +889,7 @@ __global__ __launch_bounds__(256, OCC) void attn_bwd_dkdv_kernel(AttnArgs p) {
   };
   floatx16 sa0, dp0, sa1, dp1;
   if constexpr (PIPE) sdp(sa0, dp0, smem, 0);
-  for (int i = 0; i < count; ++i) {
+  for (int i = 0; i < ((ABL & 1) ? 0 : count); ++i) {
     if (wid == 0) vm_wait<2 * A::NPW + 2>();  // tile i+1 landed (i+2 may fly)
     else vm_wait<2 * A::NPW>();
     ring_barrier();
@@ -896,7 +899,7 @@ __global__ __launch_bounds__(256, OCC) void attn_bwd_dkdv_kernel(AttnArgs p) {
   }
   vm_wait<0>();
 
-  if (key < S) {
+  if (key < S && !(ABL & 4)) {
     bf16_t* dK = static_cast<bf16_t*>(p.dk) + (tok0 + key) * p.ld_dqkv + h * HD;
     bf16_t* dV = static_cast<bf16_t*>(p.dv) + (tok0 + key) * p.ld_dqkv + h * HD;
     auto wk = [&](int d, int g) {  // (padded key: dK = dV = 0)
@@ -928,7 +931,11 @@ __global__ __launch_bounds__(256, OCC) void attn_bwd_dkdv_kernel(AttnArgs p) {
 // dQ: workgroup = 128 queries (4 waves x 32, query on the lane), sweeping the key tiles up to
 // the last query.  Per 32-key sub-block j: S^T, dP^T of j+1 overlap dS^T of j, then
 // dQ^T += K^T dS^T (2 x NDT MFMAs).
-template <int HD, bool PIPE, int OCC>
+// PRE: the delta pre-pass fused in (the default): the kernel also loads its query rows of O,
+// forms delta = rowsum(dO * O) itself (each lane holds half of a row, the other half on lane
+// ^ 32) and writes delta and the log2-unit lse rows that the dK / dV kernel -- launched after
+// it -- streams.  Saves attn_bwd_pre_kernel's pass over O and dO (the dQ kernel holds dO anyway).
+template <int HD, bool PIPE, int OCC, int ABL = 0, bool PRE = false>  // (ABL: as attn_bwd_dkdv_kernel)
 __global__ __launch_bounds__(256, OCC) void attn_bwd_dq_kernel(AttnArgs p) {
   using A = AT<HD>;
   __shared__ __attribute__((aligned(16))) bf16_t smem[NSLOT * 2 * A::TILE];  // [slot][K|V]
@@ -952,12 +959,36 @@ __global__ __launch_bounds__(256, OCC) void attn_bwd_dq_kernel(AttnArgs p) {
   bf16x8 qf[A::NST], df[A::NST];
 #pragma unroll
   for (int st = 0; st < A::NST; ++st) {
-    qf[st] = q < S ? load_row8(Q + (tok0 + q) * p.ld_qkv + 16 * st + 8 * hh) : bf16x8{};
-    df[st] = q < S ? load_row8(dO + (tok0 + q) * p.ld_o + 16 * st + 8 * hh) : bf16x8{};
+    qf[st] = (q < S && !(ABL & 2)) ? load_row8(Q + (tok0 + q) * p.ld_qkv + 16 * st + 8 * hh) : bf16x8{};
+    df[st] = (q < S && !(ABL & 2)) ? load_row8(dO + (tok0 + q) * p.ld_o + 16 * st + 8 * hh) : bf16x8{};
   }
   const float c = p.scale * LOG2E;
-  const float lse2 = q < S ? p.delta[(long long)p.N * H * S + (long long)bh * S + q] : INFINITY;
-  const float dl = q < S ? p.delta[(long long)bh * S + q] : 0.f;
+  float lse2, dl;
+  if constexpr (PRE) {
+    const bf16_t* Op = static_cast<const bf16_t*>(p.o) + h * HD;
+    float acc = 0.f;
+    if (q < S) {
+#pragma unroll
+      for (int st = 0; st < A::NST; ++st) {
+        const bf16x8 of = load_row8(Op + (tok0 + q) * p.ld_o + 16 * st + 8 * hh);
+        float fo[8], fd[8];
+        unpack8(__builtin_bit_cast(uint4, of), fo);
+        unpack8(__builtin_bit_cast(uint4, df[st]), fd);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) acc = fmaf(fo[i], fd[i], acc);
+      }
+    }
+    dl = acc + __shfl_xor(acc, 32, 64);  // (the row's other half on lane ^ 32)
+    // (+inf stays +inf: a fully masked row)
+    lse2 = q < S ? p.lse[(long long)bh * S + q] * LOG2E : INFINITY;
+    if (q < S && hh == 0) {
+      p.delta[(long long)bh * S + q] = dl;
+      p.delta[(long long)p.N * H * S + (long long)bh * S + q] = lse2;
+    }
+  } else {
+    lse2 = q < S ? p.delta[(long long)p.N * H * S + (long long)bh * S + q] : INFINITY;
+    dl = q < S ? p.delta[(long long)bh * S + q] : 0.f;
+  }
   pin_loaded(qf);
   pin_loaded(df);
   pin_loaded(lse2);
@@ -990,11 +1021,13 @@ __global__ __launch_bounds__(256, OCC) void attn_bwd_dq_kernel(AttnArgs p) {
     }
   };
 
-  issue(0);
-  issue(1);
-  issue(2);
-  vm_wait<4 * A::NPW>();  // tile 0 landed (tiles 1, 2 may fly)
-  ring_barrier();
+  if (!(ABL & 8)) {
+    issue(0);
+    issue(1);
+    issue(2);
+    vm_wait<4 * A::NPW>();  // tile 0 landed (tiles 1, 2 may fly)
+    ring_barrier();
+  }
   auto half = [&](int t, int hf, floatx16& sa, floatx16& dp, floatx16& san, floatx16& dpn) {
     const bf16_t* lk = smem + (t % NSLOT) * 2 * A::TILE;
     const bf16_t* nk = hf == 0 ? lk : smem + ((t + 1) % NSLOT) * 2 * A::TILE;
@@ -1034,7 +1067,7 @@ __global__ __launch_bounds__(256, OCC) void attn_bwd_dq_kernel(AttnArgs p) {
   };
   floatx16 sa0, dp0, sa1, dp1;
   if constexpr (PIPE) sdp(sa0, dp0, smem, 0);
-  for (int t = 0; t < ntiles; ++t) {
+  for (int t = 0; t < ((ABL & 1) ? 0 : ntiles); ++t) {
     vm_wait<2 * A::NPW>();  // this wave's pieces of tile t+1 landed (t+2 may fly)
     ring_barrier();         // ... every wave's; and every wave is done with tile t-1's slot
     issue(t + 3);
@@ -1043,7 +1076,7 @@ __global__ __launch_bounds__(256, OCC) void attn_bwd_dq_kernel(AttnArgs p) {
   }
   vm_wait<0>();
 
-  if (q < S) {
+  if (q < S && !(ABL & 4)) {
     bf16_t* dQ = static_cast<bf16_t*>(p.dq) + (tok0 + q) * p.ld_dqkv + h * HD;
 #pragma unroll
     for (int d = 0; d < A::NDT; ++d)
@@ -1100,13 +1133,24 @@ static int launch_fwd(const AttnArgs* a, hipStream_t stream) {
   return (int)hipGetLastError();
 }
 
+// The shipped backward (variant 1 at hd 64, 2 at hd 32): the dQ kernel first, with the delta
+// pre-pass fused in (it writes delta / lse2 for the dK / dV kernel); DPC_ATTN_PRE=1 (or a forced
+// variant) keeps the separate pre-pass kernel and the dK / dV -> dQ order.
 template <int HD>
 static int launch_bwd(const AttnArgs* a, hipStream_t stream) {
   const int var = attn_var(HD, 1);
+  static int pre_env = -1;
+  if (pre_env < 0) pre_env = getenv("DPC_ATTN_PRE") ? atoi(getenv("DPC_ATTN_PRE")) : 0;
+  dim3 grid((unsigned)(((a->S + QB - 1) / QB) * a->N * a->H));
+  if (!pre_env && var == (HD == 32 ? 2 : 1)) {
+    if (HD == 32) hipLaunchKernelGGL((attn_bwd_dq_kernel<HD, false, 3, 0, true>), grid, dim3(256), 0, stream, *a);
+    else hipLaunchKernelGGL((attn_bwd_dq_kernel<HD, false, 2, 0, true>), grid, dim3(256), 0, stream, *a);
+    DPC_ATTN_SWITCH(var, attn_bwd_dkdv_kernel, grid, dim3(256), 0, stream, *a);
+    return (int)hipGetLastError();
+  }
   const long long rows = (long long)a->N * a->S * a->H;
   dim3 gpre((unsigned)((rows * (HD / 8) + 255) / 256));
   hipLaunchKernelGGL(attn_bwd_pre_kernel<HD>, gpre, dim3(256), 0, stream, *a);
-  dim3 grid((unsigned)(((a->S + QB - 1) / QB) * a->N * a->H));
   DPC_ATTN_SWITCH(var, attn_bwd_dkdv_kernel, grid, dim3(256), 0, stream, *a);
   DPC_ATTN_SWITCH(var, attn_bwd_dq_kernel, grid, dim3(256), 0, stream, *a);
   return (int)hipGetLastError();
@@ -1127,6 +1171,37 @@ static bool attn_args_ok(const AttnArgs* a, bool bwd) {
 DPC_API int dpc_attn_fwd(const AttnArgs* a, hipStream_t stream) {
   if (!attn_args_ok(a, false)) return (int)hipErrorInvalidValue;
   return a->hd == 32 ? launch_fwd<32>(a, stream) : launch_fwd<64>(a, stream);
+}
+
+// Lab entry (bench/attn_lab.py): one backward kernel (which: 0 = delta / lse pre-pass, 1 = dK / dV,
+// 2 = dQ) of the hd-64 shipped variant (plain order, 2 workgroups per CU) with the
+// per-workgroup cost ablation bits ABL (attn_bwd_dkdv_kernel).
+template <int ABL>
+static void attn_lab_launch(const AttnArgs* a, int which, hipStream_t stream) {
+  dim3 grid((unsigned)(((a->S + QB - 1) / QB) * a->N * a->H));
+  if (which == 1) hipLaunchKernelGGL((attn_bwd_dkdv_kernel<64, false, 2, ABL>), grid, dim3(256), 0, stream, *a);
+  else hipLaunchKernelGGL((attn_bwd_dq_kernel<64, false, 2, ABL>), grid, dim3(256), 0, stream, *a);
+}
+DPC_API int dpc_attn_bwd_lab(const AttnArgs* a, int which, int abl, hipStream_t stream) {
+  if (!attn_args_ok(a, true) || a->hd != 64) return (int)hipErrorInvalidValue;
+  if (which == 0) {
+    const long long rows = (long long)a->N * a->S * a->H;
+    hipLaunchKernelGGL(attn_bwd_pre_kernel<64>, dim3((unsigned)((rows * 8 + 255) / 256)), dim3(256), 0, stream, *a);
+    return (int)hipGetLastError();
+  }
+  switch (abl) {
+    case 0: attn_lab_launch<0>(a, which, stream); break;
+    case 1: attn_lab_launch<1>(a, which, stream); break;
+    case 2: attn_lab_launch<2>(a, which, stream); break;
+    case 4: attn_lab_launch<4>(a, which, stream); break;
+    case 6: attn_lab_launch<6>(a, which, stream); break;
+    case 3: attn_lab_launch<3>(a, which, stream); break;
+    case 5: attn_lab_launch<5>(a, which, stream); break;
+    case 7: attn_lab_launch<7>(a, which, stream); break;
+    case 15: attn_lab_launch<15>(a, which, stream); break;
+    default: return (int)hipErrorInvalidValue;
+  }
+  return (int)hipGetLastError();
 }
 
 DPC_API int dpc_attn_bwd(const AttnArgs* a, hipStream_t stream) {
