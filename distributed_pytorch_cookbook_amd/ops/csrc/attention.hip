@@ -781,11 +781,9 @@ __global__ __launch_bounds__(256, OCC) void attn_bwd_dkdv_kernel(AttnArgs p) {
   bf16x8 kf[A::NST], vf[A::NST];
 #pragma unroll
   for (int st = 0; st < A::NST; ++st) {
-    kf[st] = (key < S && !(ABL & 2)) ? load_row8(Kp + (tok0 + key) * p.ld_qkv + 16 * st + 8 * hh) : bf16x8{};
-    vf[st] = (key < S && !(ABL & 2)) ? load_row8(Vp + (tok0 + key) * p.ld_qkv + 16 * st + 8 * hh) : bf16x8{};
+    kf[st] = bf16x8{};
+    vf[st] = bf16x8{};
   }
-  pin_loaded(kf);
-  pin_loaded(vf);
   const float c = p.scale * LOG2E;
   floatx16 dvt[A::NDT], dkt[A::NDT];
 #pragma unroll
@@ -835,8 +833,35 @@ __global__ __launch_bounds__(256, OCC) void attn_bwd_dkdv_kernel(AttnArgs p) {
   };
 
   if (count > 0 && !(ABL & 8)) {
+    // The workgroup's 128 K and V rows arrive by LDS-DMA as tile images in ring slots 2 / 3
+    // (1-KiB coalesced pieces; per-lane 16-B row loads touched 32 lines per instruction), the
+    // lanes read their row fragments from there, and only then does tile 2 reuse slot 2.
+    if constexpr (!(ABL & 2)) {
+      bf16_t* sk = smem + 2 * 2 * A::TILE;
+      bf16_t* sv = smem + 3 * 2 * A::TILE;
+      const bf16_t* K0 = Kp + tok0 * p.ld_qkv;
+      const bf16_t* V0 = Vp + tok0 * p.ld_qkv;
+      tile_dma<HD>(K0, p.ld_qkv, kb * QB, S, true, vq, sk, wid);
+      tile_dma<HD>(K0, p.ld_qkv, kb * QB + KT, S, true, vq, sk + A::TILE, wid);
+      tile_dma<HD>(V0, p.ld_qkv, kb * QB, S, true, vq, sv, wid);
+      tile_dma<HD>(V0, p.ld_qkv, kb * QB + KT, S, true, vq, sv + A::TILE, wid);
+    }
     issue(0);
     issue(1);
+    if constexpr (!(ABL & 2)) {
+      if (wid == 0) vm_wait<4 * A::NPW + 4>();  // K / V landed (tiles 0, 1 may fly)
+      else vm_wait<4 * A::NPW>();
+      ring_barrier();
+      const bf16_t* sk = smem + 2 * 2 * A::TILE + (wid >> 1) * A::TILE;
+#pragma unroll
+      for (int st = 0; st < A::NST; ++st) {
+        kf[st] = row_frag<HD>(sk, 32 * (wid & 1), st, lane);
+        vf[st] = row_frag<HD>(sk + 2 * A::TILE, 32 * (wid & 1), st, lane);
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // every wave done with slots 2 / 3
+      __builtin_amdgcn_sched_barrier(0);
+      ring_barrier();
+    }
     issue(2);
     if (wid == 0) vm_wait<4 * A::NPW + 4>();  // tile 0 landed (tiles 1, 2 may fly)
     else vm_wait<4 * A::NPW>();
