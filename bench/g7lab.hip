@@ -9,7 +9,7 @@
 // variant is checked against a host double-precision product at sampled points.  Variants
 // built with ABL 128 also report the in-kernel clock (s_memtime / s_memrealtime, median over
 // workgroups).
-#include "../distributed_pytorch_cookbook_amd/ops/csrc/gemm7_kern.h"
+#include "../distributed_pytorch_cookbook_amd/ops/csrc/gemm9_kern.h"
 
 #include <hip/hip_runtime.h>
 
@@ -60,6 +60,11 @@ struct Variant {
 template <int ABL, bool AK, bool BK, int SCHED = 3>
 static void launch(const GemmArgs& a, G7Plan pl, unsigned long long ab, unsigned long long bb) {
   hipLaunchKernelGGL((gemm7_kernel<0, SCHED, AK, BK, 128, ABL>), dim3(pl.grid), dim3(256), 0, 0, a, ab, bb, pl);
+}
+template <int ABL, bool AK, bool BK>
+static void launch9(const GemmArgs& a, G7Plan pl, unsigned long long ab, unsigned long long bb) {
+  pl.nk = a.K / 64;  // (v9: 64-deep stages)
+  hipLaunchKernelGGL((gemm9_kernel<0, AK, BK, ABL>), dim3(pl.grid), dim3(256), 0, 0, a, ab, bb, pl);
 }
 
 int main(int argc, char** argv) {
@@ -137,6 +142,9 @@ int main(int argc, char** argv) {
     vs.push_back({"s3_clk", [&] { launch<128, AK_, BK_>(a, pl, ab, bb); }, true, {}});                    \
     vs.push_back({"s6_clk", [&] { launch<128, AK_, BK_, 6>(a, pl, ab, bb); }, true, {}});                 \
     vs.push_back({"s6_no_dma", [&] { launch<128 | 2, AK_, BK_, 6>(a, pl, ab, bb); }, true, {}});          \
+    vs.push_back({"v9", [&] { launch9<0, AK_, BK_>(a, pl, ab, bb); }, false, {}});                        \
+    vs.push_back({"v9_clk", [&] { launch9<128, AK_, BK_>(a, pl, ab, bb); }, true, {}});                   \
+    vs.push_back({"v9_no_dma", [&] { launch9<128 | 2, AK_, BK_>(a, pl, ab, bb); }, true, {}});            \
   }
   if (tn) { LAB_SET(false, false) }
   else if (nn) { LAB_SET(true, false) }

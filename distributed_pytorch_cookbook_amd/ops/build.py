@@ -30,7 +30,7 @@ ARCH = os.environ.get("DPC_OFFLOAD_ARCH", "gfx950")
 
 SOURCES = ["gemm.hip", "gemm7.hip", "gemm_f32.hip", "attention.hip", "attention_f32.hip", "layernorm.hip", "misc.hip",
            "decode.hip", "embed_bwd.hip"]
-HEADERS = ["common.h", "gemm.h", "gemm7_kern.h"]
+HEADERS = ["common.h", "gemm.h", "gemm7_kern.h", "gemm9_kern.h"]
 
 # code-object v5 keeps the library loadable by torch's bundled ROCm 7.0 runtime as
 # well as by the 7.2 toolchain in /opt/rocm.

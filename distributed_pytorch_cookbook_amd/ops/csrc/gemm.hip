@@ -1149,12 +1149,13 @@ DPC_API int dpc_gemm(const GemmArgs* a, hipStream_t stream) {
     if (t128 < 100) impl = 2;
     else if (impl != 20) impl = 12;
   }
-  if (impl >= 15 && impl <= 25) {  // v7 (gemm7.hip): 4-wave 256x256, split-K f32 products
+  if (impl >= 15 && impl <= 26) {  // v7 (gemm7.hip): 4-wave 256x256, split-K f32 products
     GemmArgs c = *a;
     c.ksplit = 0;
     // (25: the split DMA interleave forced for plain products, SCHED 6; 20 / 22 pick it for
-    // products with an mn-major operand)
-    const int sched = impl == 19 ? 1 : (impl == 20 || impl == 17 || impl == 21 ? 2 : (impl == 22 ? 3 : (impl == 23 ? 4 : (impl == 24 ? 5 : (impl == 25 ? 6 : 0)))));
+    // products with an mn-major operand; 26: v9, the 64-deep-stage kernel, which every other v7
+    // placement takes for plain nt products)
+    const int sched = impl == 19 ? 1 : (impl == 20 || impl == 17 || impl == 21 ? 2 : (impl == 22 ? 3 : (impl == 23 ? 4 : (impl == 24 ? 5 : (impl == 25 ? 6 : (impl == 26 ? 7 : 0))))));
     // 21: v8 -- 256x128 tiles, two persistent workgroups per CU (epilogue beside MFMAs)
     const int rc = dpc_gemm7(&c, impl != 17, sched, g_force_splits > 0 ? g_force_splits : 0, stream,
                              impl == 21 ? 64 : 128);

@@ -31,7 +31,7 @@
 //        body(q-1), i.e. retired before every wave passed barrier(q-1) -- before any wave
 //        can be in body(q).
 // Reference: every nn.Linear of /root/reference/models/gpt.py:29-30,60-64,219.
-#include "gemm7_kern.h"
+#include "gemm9_kern.h"
 
 using namespace dpc;
 
@@ -230,6 +230,22 @@ DPC_API int dpc_gemm7(const GemmArgs* a, int persistent, int sched, int splits, 
     if (dfwd && g7d_launch<5>(a, pl, stream, ab, bb)) return (int)hipGetLastError();
     if (ddown && g7d_launch<7>(a, pl, stream, ab, bb)) return (int)hipGetLastError();
     if (dbwd && g7d_launch<6>(a, pl, stream, ab, bb)) return (int)hipGetLastError();
+  }
+  // v9 (64-deep stages, whole-line DMA pieces of the k-major operands) for the plain nt
+  // products -- every GPT-2 forward projection: same-box bench/g7lab A/B +0.7..+8.7 % over v7
+  // (8192^3 1383 -> 1429, out-projection 1045 -> 1136 TF/s; profiles/r3_gemm/lab_v9.log);
+  // impl 26 forces it, DPC_G9=0 keeps v7 there.
+  {
+    static int g9_env = -1;
+    if (g9_env < 0) g9_env = getenv("DPC_G9") ? atoi(getenv("DPC_G9")) : 1;
+    const bool g9_ok = plain && !a->accumulate && s == 1 && !v8 && a->a_kmaj && a->b_kmaj && a->K % 64 == 0 &&
+                       a->lda >= 64 && a->ldb >= 64;
+    if (g9_ok && (sched == 7 || (g9_env && sched != 6 && sched != 5))) {
+      G7Plan p9 = pl;
+      p9.nk = a->K / 64;
+      hipLaunchKernelGGL((gemm9_kernel<0, true, true>), dim3(p9.grid), dim3(256), 0, stream, *a, ab, bb, p9);
+      return (int)hipGetLastError();
+    }
   }
   if (slab) {
     if (v8) g7_launch_s<4, 64>(a, pl, stream, ab, bb);

@@ -76,8 +76,9 @@ _USE_TABLE = os.environ.get("DPC_GEMM_TABLE", "1") == "1"
 # 0 = the dispatcher policy; 16 / 17 / 19 / 20 / 22 / 23 = the 4-wave 256x256 kernel (gemm7.hip;
 # 16 / 20 / 22 run the paired-M0 DMA issue, 19 / 23 the quad form), 21 = v8 (two per CU),
 # 24 = v7d (the GELU / GELU' epilogues deferred into the next tile's main loop), 25 = v7 with the
-# split DMA interleave forced (20 / 22 already take it when an operand is mn-major)
-_CANDIDATES = (0, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 16, 17, 19, 20, 21, 22, 23, 24, 25)
+# split DMA interleave forced (20 / 22 already take it when an operand is mn-major), 26 = v9 (64-deep
+# stages; 16 / 20 / 22 / 23 already take it for plain nt products)
+_CANDIDATES = (0, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 16, 17, 19, 20, 21, 22, 23, 24, 25, 26)
 _TUNE_MAX_OUT_BYTES = 16 << 30  # (the GPT-2 small LM-head logits are 6.6 GB)
 
 
