@@ -42,6 +42,11 @@ XL = [("xl_qkv_fwd", TX, 4800, 1600, "nt"), ("xl_outp_fwd", TX, 1600, 1600, "nt"
       ("xl_w_down", 1600, 6400, TX, "tn"), ("xl_w_lm", 50304, 1600, TX, "tn")]
 
 
+# GPT-2 small weight gradients (tn, f32 out, split K through workspace slabs)
+WGRAD = [("w_qkv", 2304, 768, T, "tn"), ("w_out", 768, 768, T, "tn"), ("w_up", 3072, 768, T, "tn"),
+         ("w_down", 768, 3072, T, "tn"), ("w_lm", 50304, 768, T, "tn")]
+
+
 # fused-epilogue products of the GPT-2 layers: (name, M, N, K, layout, epilogue)
 #   up   = bias + gelu + aux_out (pre-activation), bf16 out          (FFN up forward)
 #   down = bias + gelu + aux_out + f32 residual, f32 out             (FFN down forward, quirk act)
@@ -107,13 +112,13 @@ def check(A, B, lay, out):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--impls", type=int, nargs="+", default=[12, 13, 14])
-    ap.add_argument("--shapes", default="all", choices=["square", "gpt2s", "all", "fused", "xl"])
+    ap.add_argument("--shapes", default="all", choices=["square", "gpt2s", "all", "fused", "xl", "wgrad"])
     ap.add_argument("--only", nargs="*", default=None)
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--json", default=None)
     a = ap.parse_args()
-    shapes = (SQUARE if a.shapes in ("square", "all") else []) + (GPT2S if a.shapes in ("gpt2s", "all") else []) + (XL if a.shapes == "xl" else [])
+    shapes = (SQUARE if a.shapes in ("square", "all") else []) + (GPT2S if a.shapes in ("gpt2s", "all") else []) + (XL if a.shapes == "xl" else []) + (WGRAD if a.shapes == "wgrad" else [])
     if a.only:
         shapes = [s for s in shapes if s[0] in a.only]
     rows = []

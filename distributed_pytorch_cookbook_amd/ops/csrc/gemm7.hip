@@ -243,7 +243,28 @@ DPC_API int dpc_gemm7(const GemmArgs* a, int persistent, int sched, int splits, 
     if (g9_ok && (sched == 7 || (g9_env && sched != 6 && sched != 5))) {
       G7Plan p9 = pl;
       p9.nk = a->K / 64;
+      p9.nk_all = p9.nk;
       hipLaunchKernelGGL((gemm9_kernel<0, true, true>), dim3(p9.grid), dim3(256), 0, stream, *a, ab, bb, p9);
+      return (int)hipGetLastError();
+    }
+    // weight gradients (both operands mn-major, split K through workspace slabs) on v9, with the
+    // split count of v7's plan and the stages per split recomputed: measured SLOWER than v7
+    // schedule 6 (GPT-2 small QKV / up weight gradients 0.205 -> 0.216 / 0.269 -> 0.285 ms, DDP
+    // step -0.9 %; profiles/r3_gemm/v9_wgrad_negative.txt) -- the mn-major pieces were whole lines
+    // already, and the two-buffer ring leaves the HBM-streamed operands less latency slack.
+    // Off unless DPC_G9_WGRAD=1 (or impl 26).
+    static int g9w_env = -1;
+    if (g9w_env < 0) g9w_env = getenv("DPC_G9_WGRAD") ? atoi(getenv("DPC_G9_WGRAD")) : 0;
+    if (slab && !v8 && !a->a_kmaj && !a->b_kmaj && a->lda >= 128 && a->ldb >= 128 &&
+        (sched == 7 || (g9w_env && sched != 5))) {
+      G7Plan p9 = pl;
+      p9.nk_all = (a->K + 63) / 64;
+      p9.nk = (p9.nk_all + s - 1) / s;
+      hipLaunchKernelGGL((gemm9_kernel<4, false, false>), dim3(p9.grid), dim3(256), 0, stream, *a, ab, bb, p9);
+      const long long nq = (long long)a->M * (a->N / 4);
+      const int blocks = (int)std::min<long long>((nq + 255) / 256, 4096);
+      hipLaunchKernelGGL(g7_splitk_reduce, dim3(blocks), dim3(256), 0, stream, static_cast<float*>(a->C), a->ldc,
+                         static_cast<const float*>(a->ws), a->M, a->N, s, a->accumulate);
       return (int)hipGetLastError();
     }
   }

@@ -36,10 +36,13 @@ constexpr int G9_TA = 256 * G9_KB;          // elements per operand per stage (3
 constexpr int G9_SLOT = 2 * G9_TA;          // A + B (64 KiB)
 constexpr int G9_NL = G9_TA / 512 / 4;      // 1-KiB pieces per wave per operand per stage (8)
 
+// EPI 0: plain products; EPI 4: split-K partial tiles into the f32 workspace slab of their
+// k-range (as v7 EPI 4: unit = split * tiles + tile, pl.nk = stages per split, pl.nk_all =
+// stages of the whole product -- whole stages past it are issued with empty descriptors).
 template <int EPI, bool AK, bool BK, int ABL = 0>
 __global__ __launch_bounds__(256, 1) void gemm9_kernel(GemmArgs p, unsigned long long a_bytes,
                                                        unsigned long long b_bytes, G7Plan pl) {
-  static_assert(EPI == 0, "v9: plain products");
+  static_assert(EPI == 0 || EPI == 4, "v9: plain products, split-K slabs");
   constexpr int NJ = 8;
   __shared__ __attribute__((aligned(16))) bf16_t smem[2 * G9_SLOT];
 
@@ -65,21 +68,23 @@ __global__ __launch_bounds__(256, 1) void gemm9_kernel(GemmArgs p, unsigned long
 
   // ---- DMA issue cursor (unit, stage, buffer, byte offsets), wave-uniform (pl.nk = stages per
   // unit here)
-  int is_u = 0, is_k = 0, is_buf = 0;
+  int is_u = 0, is_k = 0, is_buf = 0, is_kt0 = 0;
   unsigned long long is_aoff = 0, is_boff = 0;
   const int ntiles = pl.tiles_m * pl.tiles_n;
   auto set_org = [&](int ui) {
     const int uu = local + ui * pl.grid;
+    const int sp = uu / ntiles;
     int m0, n0;
-    g7_tile(pl, uu % ntiles, m0, n0);
-    is_aoff = AK ? (unsigned long long)m0 * p.lda * 2 : (unsigned long long)m0 * 2;
-    is_boff = BK ? (unsigned long long)n0 * p.ldb * 2 : (unsigned long long)n0 * 2;
+    g7_tile(pl, uu - sp * ntiles, m0, n0);
+    is_kt0 = sp * pl.nk;
+    is_aoff = (AK ? (unsigned long long)m0 * p.lda * 2 : (unsigned long long)m0 * 2) + a_step * is_kt0;
+    is_boff = (BK ? (unsigned long long)n0 * p.ldb * 2 : (unsigned long long)n0 * 2) + b_step * is_kt0;
   };
   set_org(0);
   __amdgpu_buffer_rsrc_t rsa, rsb;
   const bf16_t* is_lds = smem;
   auto prep = [&]() {
-    const bool valid = is_u < nmine;
+    const bool valid = is_u < nmine && is_kt0 + is_k < pl.nk_all;
     const unsigned long long la = a_bytes - is_aoff, lb = b_bytes - is_boff;
     const unsigned na = valid ? ((la >> 32) ? 0xffffffffu : (unsigned)la) : 0u;
     const unsigned nb = valid ? ((lb >> 32) ? 0xffffffffu : (unsigned)lb) : 0u;
@@ -203,6 +208,12 @@ __global__ __launch_bounds__(256, 1) void gemm9_kernel(GemmArgs p, unsigned long
     int m0, n0;
     g7_tile(pl, uu % ntiles, m0, n0);
     if (pl.debug & 1) {
+    } else if constexpr (EPI == 4) {
+      GemmArgs q = p;  // the k-range's slab: [M][N] f32 at ws + split * M * N
+      q.C = static_cast<float*>(p.ws) + (long long)(uu / ntiles) * p.M * p.N;
+      q.ldc = p.N;
+      q.out_f32 = 1;
+      g7_epilogue<0, NJ>(q, acc, m0 + ar, n0 + bc, lane, 0);
     } else {
       g7_epilogue<0, NJ>(p, acc, m0 + ar, n0 + bc, lane, 0);
     }
