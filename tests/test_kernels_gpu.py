@@ -109,14 +109,16 @@ def _store(x, kmaj):
     return buf[:, :r]
 
 
-@pytest.mark.parametrize("impl", [13, 16, 17, 19, 20, 21])
+@pytest.mark.parametrize("impl", [13, 16, 17, 19, 20, 21, 22, 25, 26])
 @pytest.mark.parametrize("a_kmaj,b_kmaj", [(True, True), (True, False), (False, False), (False, True)])
 @pytest.mark.parametrize("M,N,K", [(300, 264, 128), (1023, 768, 768), (4096, 4352, 256), (513, 2304, 1536),
                                    (300, 264, 96), (257, 520, 1000)])
 def test_gemm_v6_v7(impl, a_kmaj, b_kmaj, M, N, K):
     """The 256x256 kernels on the shapes they serve: ragged M, N % 8 == 0, K % 64 == 0, and
     (4096 x 4352: 272 tiles) more tiles than CUs, so a persistent v7 workgroup streams two
-    tiles through one ring -- plain bf16 / f32 outputs, accumulate and every fused epilogue."""
+    tiles through one ring -- plain bf16 / f32 outputs, accumulate and every fused epilogue.
+    22 / 25: v7 with paired / split DMA issue; 26: v9 (64-deep stages) for the plain products it
+    takes (K % 64 == 0), v7 for the rest; 16 / 19 / 20 / 22 also run v9 on plain nt products."""
     torch.manual_seed(3)
     a = torch.randn(M, K, device=dev).bfloat16()
     b = torch.randn(N, K, device=dev).bfloat16()
@@ -212,7 +214,7 @@ def test_gemm_v7d_deferred_gelu_epilogues(M, N, K):
     assert rel_err(ox, ox_r) < 5e-3
 
 
-@pytest.mark.parametrize("impl", [2, 4, 7, 10, 11, 12, 16, 21])
+@pytest.mark.parametrize("impl", [2, 4, 7, 10, 11, 12, 16, 21, 25, 26])
 @pytest.mark.parametrize("splits", [2, 3, 8])
 @pytest.mark.parametrize("M,N,K", [(77, 1000, 4160), (600, 520, 8192), (2304, 136, 4096)])
 def test_gemm_forced_split_k(impl, splits, M, N, K):
