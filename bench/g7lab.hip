@@ -109,7 +109,7 @@ int main(int argc, char** argv) {
   a.b_c = (nn || tn) ? N : K;
   const unsigned long long ab = (unsigned long long)M * K * 2, bb = (unsigned long long)N * K * 2;
 
-  G7Plan pl;
+  G7Plan pl{};
   memset(&pl, 0, sizeof(pl));
   pl.tile_n = 256;
   pl.tiles_m = M / 256;

@@ -137,6 +137,9 @@ static bool g7d_launch(const GemmArgs* a, const G7Plan& pl, hipStream_t stream, 
 // Whether v7 takes this product: k-major operands hold exactly K columns with K % 32 == 0 (a
 // slice never straddles a row end; mn-major operands end at row K, so their last slice reads
 // zeros past it), N % 8 == 0, 16-B aligned C / bias / residual, 8-B aligned aux.
+static int g7_act_lds = -1;  // -1: DPC_G7_ACTLDS (default on); 0 / 1 forced (A/B sweeps)
+DPC_API void dpc_gemm7_set_act_lds(int v) { g7_act_lds = v; }
+
 DPC_API int dpc_gemm7_ok(const GemmArgs* a) {
   const long long ab = g7_operand_bytes(a->a_r, a->a_c, a->lda);
   const long long bb = g7_operand_bytes(a->b_r, a->b_c, a->ldb);
@@ -159,7 +162,7 @@ DPC_API int dpc_gemm7(const GemmArgs* a, int persistent, int sched, int splits, 
   const long long ab = g7_operand_bytes(a->a_r, a->a_c, a->lda);
   const long long bb = g7_operand_bytes(a->b_r, a->b_c, a->ldb);
   const bool v8 = wn == 64;
-  G7Plan pl;
+  G7Plan pl{};
   pl.tile_n = v8 ? 128 : 256;
   pl.tiles_m = (a->M + 255) / 256;
   pl.tiles_n = (a->N + pl.tile_n - 1) / pl.tile_n;
@@ -216,6 +219,16 @@ DPC_API int dpc_gemm7(const GemmArgs* a, int persistent, int sched, int splits, 
   if (dbg < 0) dbg = getenv("DPC_G7_DEBUG") ? atoi(getenv("DPC_G7_DEBUG")) : 0;
   pl.debug = dbg;
   if (dbg & 13) pl.store_cnt = 0;
+  // v7 input-gradient epilogue with an act' operand: the operand staged through LDS by DMA
+  bool act_lds = false;
+  // (g7_epilogue_act_lds; DPC_G7_ACTLDS=0 or dpc_gemm7_set_act_lds(0) keeps the per-lane reads)
+  {
+    static int env = -1;
+    if (env < 0) env = getenv("DPC_G7_ACTLDS") ? atoi(getenv("DPC_G7_ACTLDS")) : 1;
+    const int on = g7_act_lds >= 0 ? g7_act_lds : env;
+    act_lds = on && !v8 && s == 1 && a->act_bwd && a->aux_in && a->ld_aux_in % 8 == 0 &&
+              ((uintptr_t)a->aux_in % 16) == 0 && a->ld_aux_in <= (1 << 20);
+  }
   // v7d: sched 5 (impl 24) takes the GELU / GELU' fused epilogues of full-depth products
   // (nk >= 18: at least 16 slices to spread a tile's deferred chunks over)
   if (sched == 5 && !v8 && s == 1 && pl.nk >= 18) {
@@ -297,6 +310,18 @@ DPC_API int dpc_gemm7(const GemmArgs* a, int persistent, int sched, int splits, 
     else g7_launch<0, 0>(a, pl, stream, ab, bb);
   } else if (!a->act_bwd && !a->colsum) {
     g7_launch_s<1>(a, pl, stream, ab, bb);
+  } else if (act_lds) {
+    // column sums through the workspace ([2 tiles_m][N] partials + g7_colsum_reduce) when the
+    // caller passed one large enough, else f32 atomics from the epilogue
+    const long long rows = 2ll * pl.tiles_m;
+    const bool cs_ws = a->colsum && a->ws && rows * a->N * 4 <= a->ws_bytes && ((uintptr_t)a->ws % 16) == 0 &&
+                       a->N % 4 == 0 && ((uintptr_t)a->colsum % 16) == 0;
+    GemmArgs q = *a;
+    if (!cs_ws) q.ws = nullptr;
+    g7_launch_s<8>(&q, pl, stream, ab, bb);
+    if (cs_ws)
+      hipLaunchKernelGGL(g7_colsum_reduce, dim3((unsigned)((a->N / 4 + 255) / 256), (unsigned)((rows + 15) / 16)),
+                         dim3(256), 0, stream, a->colsum, static_cast<const float*>(a->ws), (int)rows, a->N);
   } else {
     g7_launch_s<3>(a, pl, stream, ab, bb);
   }

@@ -144,8 +144,7 @@ __device__ __forceinline__ unsigned g7_ror8(unsigned v) {
 }
 __device__ __forceinline__ float g7_ror8(float v) { return __uint_as_float(g7_ror8(__float_as_uint(v))); }
 
-// PK: GELU / GELU' in packed-f32 math (v8 with a K-major A; the other instantiations have no
-// register room for it)
+// PK: GELU / GELU' in packed-f32 math (v8 with a K-major A, v7's forward epilogues)
 template <int MODE, int NJ, bool PK = false>
 __device__ __forceinline__ void g7_epilogue(const GemmArgs& p, floatx4 (&acc)[8][NJ], int mw, int nw, int lane,
                                             int dbg = 0) {
@@ -379,6 +378,179 @@ __device__ __forceinline__ void g7_epilogue(const GemmArgs& p, floatx4 (&acc)[8]
   }
 }
 
+// MODE 3 with an act' operand on v7 (256 x 256 tiles), the operand staged through LDS: the
+// per-lane 8-B reads of g7_epilogue (one 16-row block in flight ahead) leave the tile's act'
+// operand as eight dependent HBM round trips -- measured ~35 us per tile on the GPT-2 up-proj
+// input gradient (718 us against 299 us for the plain product).  Here the 128-KiB operand
+// tile comes in four 64-row quarters (32 KiB each: the rows 32 q .. 32 q + 31 of both wave
+// rows) by LDS-DMA into the two ring slots that are idle during an epilogue -- the last
+// slice's (its next write is the next tile's body 0) and the next tile's slice 0 (read into
+// registers by the last body) -- double-buffered, quarter q+2's DMA behind quarter q's
+// processing.  A piece holds two 512-B rows; the 16-B chunk c of local row r sits at chunk
+// position c ^ (r & 15), so the 16 rows a lane group reads at one column are 16 different
+// bank groups.  Waits are counted: a quarter's DMA is older than the previous quarter's stores
+// and the next DMA, which may stay in flight (full tiles; an edge tile, which may skip stores,
+// waits for everything but the next DMA).
+template <int NJ>
+__device__ __forceinline__ void g7_epilogue_act_lds(const GemmArgs& p, floatx4 (&acc)[8][NJ], int m0, int n0,
+                                                    int wid, int lane_in, bf16_t* buf0, bf16_t* buf1) {
+  static_assert(NJ == 8, "v7 tiles");
+  // the lane id through an opaque move: every per-lane address below is tile-invariant, and
+  // hoisted out of the persistent tile loop they would stay live across the main loop (spills)
+  int lane;
+  asm volatile("v_mov_b32 %0, %1" : "=v"(lane) : "v"(lane_in));
+  float alpha = p.alpha;
+  if (p.alpha_ptr) alpha *= *p.alpha_ptr;
+  const int g = lane >> 4, rl = lane & 15;
+  const int wr = wid >> 1, wc = wid & 1;
+  const int mw = m0 + wr * 128, nw = n0 + wc * 128;
+  const int coff = 16 * (g & 1) + 8 * (g >> 1);
+  const int ld = (int)p.ld_aux_in;
+  const long long org = (long long)m0 * ld + n0;
+  const long long rem = ((long long)(p.M - 1) * ld + p.N - org) * 2;  // bytes to the operand's end
+  const unsigned nrec = rem <= 0 ? 0u : (rem >= 0xffffffffll ? 0xffffffffu : (unsigned)rem);
+  const __amdgpu_buffer_rsrc_t rz =
+      __builtin_amdgcn_make_buffer_rsrc((void*)(static_cast<const bf16_t*>(p.aux_in) + org), 0, nrec, 0x00020000);
+  auto zdma = [&](int q, bf16_t* buf) G7_AI {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const int lr = wid * 16 + 2 * k + (lane >> 5);  // local row 0..63
+      const int tr = ((lr & 32) ? 128 : 0) + 32 * q + (lr & 31);
+      const int c = (lane & 31) ^ (lr & 15);
+      g7_piece(rz, (tr * ld + c * 8) * 2, buf + (wid * 8 + k) * 512);
+    }
+  };
+  const bool full = m0 + 256 <= p.M && n0 + 256 <= p.N;
+  float cs[NJ][4];
+#pragma unroll
+  for (int j = 0; j < NJ; ++j)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) cs[j][r] = 0.f;
+  auto proc = [&](auto Q, const bf16_t* buf) G7_AI {
+    constexpr int q = decltype(Q)::value;
+    sfor<2>([&](auto II) G7_AI {
+      constexpr int i = 2 * q + decltype(II)::value;
+      const int m = mw + 16 * i + rl;
+      const bool mok = m < p.M;
+      const bf16_t* zrow = buf + (wr * 32 + 16 * decltype(II)::value + rl) * 256;
+      sfor<NJ / 2>([&](auto J) G7_AI {
+        constexpr int j = 2 * decltype(J)::value;
+        unsigned pc[2][2];
+        sfor<2>([&](auto H) G7_AI {
+          constexpr int h = decltype(H)::value;
+          constexpr int jj = j + h;
+          const int n = nw + 16 * jj + 4 * g;
+          const bool ok = mok && n < p.N;
+          const int c = wc * 16 + 2 * jj + (g >> 1);
+          const uint2 z = *reinterpret_cast<const uint2*>(zrow + (c ^ rl) * 8 + 4 * (g & 1));
+          float w[4];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) w[r] = acc[i][jj][r] * alpha;
+          if (p.act_bwd == ACT_GELU) {  // packed-f32 GELU' (half the VALU issue of the scalar form)
+            const dpc_f2_t g01 = gelu_tanh_grad2(dpc_f2_t{__uint_as_float(z.x << 16), __uint_as_float(z.x & 0xffff0000u)});
+            const dpc_f2_t g23 = gelu_tanh_grad2(dpc_f2_t{__uint_as_float(z.y << 16), __uint_as_float(z.y & 0xffff0000u)});
+            w[0] *= g01.x; w[1] *= g01.y; w[2] *= g23.x; w[3] *= g23.y;
+          } else {
+            w[0] *= act_grad(__uint_as_float(z.x << 16), p.act_bwd);
+            w[1] *= act_grad(__uint_as_float(z.x & 0xffff0000u), p.act_bwd);
+            w[2] *= act_grad(__uint_as_float(z.y << 16), p.act_bwd);
+            w[3] *= act_grad(__uint_as_float(z.y & 0xffff0000u), p.act_bwd);
+          }
+          if (ok) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) cs[jj][r] += w[r];
+          }
+          if (p.out_f32) {
+            if (ok) *reinterpret_cast<float4*>(static_cast<float*>(p.C) + (long long)m * p.ldc + n) =
+                make_float4(w[0], w[1], w[2], w[3]);
+          } else {
+            pc[h][0] = pack2bf(w[0], w[1]);
+            pc[h][1] = pack2bf(w[2], w[3]);
+          }
+        });
+        if (!p.out_f32) {
+          const int n8 = nw + 16 * j + coff;
+          const auto s0 = __builtin_amdgcn_permlane16_swap(pc[0][0], pc[1][0], false, false);
+          const auto s1 = __builtin_amdgcn_permlane16_swap(pc[0][1], pc[1][1], false, false);
+          if (mok && n8 < p.N)
+            *reinterpret_cast<uint4*>(static_cast<bf16_t*>(p.C) + (long long)m * p.ldc + n8) =
+                make_uint4(s0[0], s1[0], s0[1], s1[1]);
+        }
+        __builtin_amdgcn_sched_barrier(0);  // one column pair at a time (else all are live: spills)
+      });
+    });
+  };
+  // wait until quarter q's pieces landed (every wave's): younger ops = the previous quarter's
+  // stores (st, full tiles only) + the next quarter's DMA (8) when one was issued
+  auto landed = [&](bool st, bool next) G7_AI {
+    if (!next) {
+      if (st && full) {
+        if (p.out_f32) g7_wait<16>();
+        else g7_wait<8>();
+      } else {
+        g7_wait<0>();
+      }
+    } else if (st && full) {
+      if (p.out_f32) g7_wait<24>();
+      else g7_wait<16>();
+    } else {
+      g7_wait<8>();
+    }
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+  };
+  auto reads_done = [&]() G7_AI {  // every wave's reads of a buffer retired -> it may be refilled
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+  };
+  reads_done();  // (the last body's fragment reads of the next tile's slice 0 -- buf1)
+  zdma(0, buf0);
+  zdma(1, buf1);
+  landed(false, true);
+  proc(std::integral_constant<int, 0>{}, buf0);
+  reads_done();
+  zdma(2, buf0);
+  landed(true, true);
+  proc(std::integral_constant<int, 1>{}, buf1);
+  reads_done();
+  zdma(3, buf1);
+  landed(true, true);
+  proc(std::integral_constant<int, 2>{}, buf0);
+  landed(true, false);
+  proc(std::integral_constant<int, 3>{}, buf1);
+  if (p.colsum) {
+#pragma unroll
+    for (int j = 0; j < NJ; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        float v = cs[j][r];
+        v += __shfl_xor(v, 1, 64);
+        v += __shfl_xor(v, 2, 64);
+        v += __shfl_xor(v, 4, 64);
+        v += __shfl_xor(v, 8, 64);
+        cs[j][r] = v;
+      }
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int e = 2 * rl + h;
+      float v = 0.f;
+#pragma unroll
+      for (int k = 0; k < 4 * NJ; ++k) v = (e == k) ? cs[k >> 2][k & 3] : v;
+      const int n = nw + 16 * (e >> 2) + 4 * g + (e & 3);
+      if (n < p.N) {
+        // the workspace form: this wave's partial column sums as row 2 (m0 / 256) + wr of a
+        // [2 tiles_m][N] f32 matrix (g7_colsum_reduce adds its rows into colsum) -- the f32
+        // atomics of every tile of a column block land on the same 256 addresses at nearly the
+        // same time and serialise
+        if (p.ws) static_cast<float*>(p.ws)[(long long)(2 * (m0 >> 8) + wr) * p.N + n] = v;
+        else atomicAdd(p.colsum + n, v);
+      }
+    }
+  }
+  reads_done();  // both buffers are ring slots again: the next tile's bodies 0 / 1 refill them
+}
+
 // split-K partial tile (non-swapped accumulators: lane l, register r of accumulator (i, j) holds
 // C[mw + 16 i + 4 (l >> 4) + r][nw + 16 j + (l & 15)]): f32 atomic adds, each wave-instruction
 // four rows x 64 contiguous bytes.  The host zeroes C first unless the product accumulates.
@@ -403,7 +575,8 @@ __device__ __forceinline__ void g7_epilogue_atomic(const GemmArgs& p, floatx4 (&
 
 // EPI: 0 = plain products (bf16 / f32 C), 1 = forward fused epilogues, 2 = split-K f32 atomics,
 // 3 = input-gradient fused epilogues (act', column sums), 4 = split-K partial tiles stored to
-// the workspace slab of their k-range (plain 16-B stores; g7_splitk_reduce sums the slabs).
+// the workspace slab of their k-range (plain 16-B stores; g7_splitk_reduce sums the slabs),
+// 8 = EPI 3 with an act' operand staged through LDS (v7 only; g7_epilogue_act_lds).
 // WN: output columns per wave.  128 = v7 (a 256 x 256 tile, one workgroup per CU); 64 = v8 (a
 // 256 x 128 tile, 128 accumulator registers, TWO workgroups per CU, each with a 3-slot ring:
 // the two drift out of phase, so one's epilogue -- the bias / GELU / residual / act' VALU work
@@ -684,8 +857,17 @@ __global__ __launch_bounds__(256, WN == 128 ? 1 : 2) void gemm7_kernel(GemmArgs 
       g7_epilogue<0, NJ>(q, acc, m0 + ar, n0 + bc, lane);
     } else if constexpr (EPI == 0) {
       g7_epilogue<EPI, NJ, WN == 64 && AK>(p, acc, m0 + ar, n0 + bc, lane, pl.debug);
+    } else if constexpr (EPI == 8) {
+      // (its own instantiation: beside g7_epilogue<3> in one kernel the register allocator
+      // spilled ~120 registers, alone it spills 2)
+      static_assert(WN == 128, "v7 only");
+      g7_epilogue_act_lds<NJ>(p, acc, m0, n0, wid, lane, smem + ((rd_slot + 3) % NS) * SLOT,
+                              smem + ((rd_slot + 4) % NS) * SLOT);
     } else {
-      g7_epilogue<EPI, NJ, WN == 64 && AK>(p, acc, m0 + ar, n0 + bc, lane);
+      // packed-f32 GELU: v8 with a k-major A, and the v7 forward epilogues (measured: the act'
+      // epilogue's GELU' in packed math took the GPT-2 up-projection input gradient from 531 to
+      // 725 TF/s -- the epilogue was VALU-bound)
+      g7_epilogue<EPI, NJ, (WN == 64 && AK) || (WN == 128 && EPI == 1)>(p, acc, m0 + ar, n0 + bc, lane);
     }
     // the stores were issued after this tile's last wait: the next DIST-2 waits (slices whose
     // DMA is older than the stores) may leave them in flight -- full tiles only (an edge tile
@@ -705,6 +887,25 @@ __global__ __launch_bounds__(256, WN == 128 ? 1 : 2) void gemm7_kernel(GemmArgs 
       g7_clk[2 * blockIdx.x + 1] = r1 - clk_r0;
     }
   }
+}
+
+// colsum[n] += sum over the R rows of ws [R][N] (g7_epilogue_act_lds's per-tile partial column
+// sums): 4 columns per thread, 16 rows per workgroup row (grid.y), one atomic per column per 16
+// rows
+__global__ __launch_bounds__(256) void g7_colsum_reduce(float* colsum, const float* ws, int R, int N) {
+  const int c4 = (blockIdx.x * 256 + threadIdx.x) * 4;
+  if (c4 >= N) return;
+  const int r0 = blockIdx.y * 16, r1 = min(R, r0 + 16);
+  float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll 16
+  for (int r = r0; r < r1; ++r) {
+    const float4 v = *reinterpret_cast<const float4*>(ws + (long long)r * N + c4);
+    s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+  }
+  atomicAdd(colsum + c4, s.x);
+  atomicAdd(colsum + c4 + 1, s.y);
+  atomicAdd(colsum + c4 + 2, s.z);
+  atomicAdd(colsum + c4 + 3, s.w);
 }
 
 // C (=, or += when accumulating) the sum of the s workspace slabs [s][M][N]; 4 columns per

@@ -285,9 +285,12 @@ def gemm(
                 raise ValueError(f"gemm: {nm} must be contiguous-last {dt}")
         if out.dtype not in (torch.float32, torch.bfloat16):
             raise ValueError("gemm: out must be f32 or bf16")
-        ws = (_workspace(a.device) if (out.dtype == torch.float32 and bias is None and residual is None
-                                         and aux_in is None and aux_out is None and colsum is None
-                                         and not act and not act_bwd) else None)
+        # the workspace: split-K slabs of plain f32 products, and the per-tile partial column
+        # sums of the input-gradient epilogue (act' + bias-gradient column sums)
+        ws = (_workspace(a.device) if ((out.dtype == torch.float32 and bias is None and residual is None
+                                          and aux_in is None and aux_out is None and colsum is None
+                                          and not act and not act_bwd)
+                                         or (colsum is not None and act_bwd)) else None)
         args = _lib.GemmArgs(
             A=a.data_ptr(), B=b.data_ptr(), C=out.data_ptr(),
             bias=_lib.ptr(bias), residual=_lib.ptr(residual), aux_in=_lib.ptr(aux_in),

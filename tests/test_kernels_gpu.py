@@ -163,6 +163,45 @@ def test_gemm_v6_v7(impl, a_kmaj, b_kmaj, M, N, K):
     assert rel_err(og, og_r) < 1e-2
 
 
+@pytest.mark.parametrize("act_lds", [0, 1])
+@pytest.mark.parametrize("use_ws", [False, True])
+@pytest.mark.parametrize("a_kmaj,b_kmaj", [(True, False), (True, True), (False, False)])
+@pytest.mark.parametrize("M,N,K", [(1023, 768, 768), (4096, 4352, 256), (300, 264, 96), (2048, 3072, 512)])
+def test_gemm_v7_act_grad_epilogue_paths(monkeypatch, act_lds, use_ws, a_kmaj, b_kmaj, M, N, K):
+    """The v7 input-gradient epilogue (act' of a bf16 operand + bias-gradient column sums) on
+    both paths: the act' operand staged through LDS in quarters (gemm7_kern.h
+    g7_epilogue_act_lds, EPI 8; column sums as per-tile partials in the workspace + a reduction,
+    or f32 atomics without one) and the per-lane operand reads (DPC_G7_ACTLDS=0) -- ragged edge
+    tiles, and more tiles than CUs (4096 x 4352: a workgroup streams two through its ring)."""
+    from distributed_pytorch_cookbook_amd.ops import gemm as G
+
+    if not use_ws:
+        monkeypatch.setattr(G, "_workspace", lambda device: None)
+    torch.manual_seed(5)
+    a = torch.randn(M, K, device=dev).bfloat16()
+    b = torch.randn(N, K, device=dev).bfloat16()
+    A, B = _store(a, a_kmaj), _store(b, b_kmaj)
+    z = torch.randn(M, N, device=dev).bfloat16()
+    lib = _lib.lib()
+    _lib.set_gemm_impl(25)
+    lib.dpc_gemm7_set_act_lds(act_lds)
+    try:
+        cs = torch.full((N,), 0.25, device=dev)
+        od = gemm(A, B, a_kmaj=a_kmaj, b_kmaj=b_kmaj, act_bwd=2, aux_in=z, colsum=cs)
+        of = gemm(A, B, a_kmaj=a_kmaj, b_kmaj=b_kmaj, act_bwd=2, aux_in=z, out_dtype=torch.float32, alpha=0.5)
+    finally:
+        _lib.set_gemm_impl(-1)
+        lib.dpc_gemm7_set_act_lds(-1)
+    od_r = torch.empty(M, N, device=dev)
+    cs_r = torch.full((N,), 0.25, device=dev)
+    _gemm_ref(a, b, True, True, od_r, None, 0, 2, z, None, None, 1.0, None, False, cs_r)
+    assert rel_err(od, od_r) < 1e-2
+    assert rel_err(cs, cs_r) < 2e-3
+    of_r = torch.empty(M, N, device=dev)
+    _gemm_ref(a, b, True, True, of_r, None, 0, 2, z, None, None, 0.5, None, False)
+    assert rel_err(of, of_r) < 2e-3
+
+
 @pytest.mark.parametrize("M,N,K", [(16000, 3072, 768), (12000, 2560, 1600), (10000, 2048, 576), (4096, 4352, 768),
                                    (65472, 3072, 768), (65472, 768, 3072), (9000, 1600, 2048)])
 def test_gemm_v7d_deferred_gelu_epilogues(M, N, K):
