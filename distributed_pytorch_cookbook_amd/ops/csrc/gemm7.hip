@@ -139,6 +139,8 @@ static bool g7d_launch(const GemmArgs* a, const G7Plan& pl, hipStream_t stream, 
 // zeros past it), N % 8 == 0, 16-B aligned C / bias / residual, 8-B aligned aux.
 static int g7_act_lds = -1;  // -1: DPC_G7_ACTLDS (default on); 0 / 1 forced (A/B sweeps)
 DPC_API void dpc_gemm7_set_act_lds(int v) { g7_act_lds = v; }
+static int g7_res_lds = -1;  // -1: DPC_G7_RESLDS (default on); 0 / 1 forced (A/B sweeps)
+DPC_API void dpc_gemm7_set_res_lds(int v) { g7_res_lds = v; }
 
 DPC_API int dpc_gemm7_ok(const GemmArgs* a) {
   const long long ab = g7_operand_bytes(a->a_r, a->a_c, a->lda);
@@ -309,7 +311,15 @@ DPC_API int dpc_gemm7(const GemmArgs* a, int persistent, int sched, int splits, 
     else if (sched == 2) g7_launch<0, 2>(a, pl, stream, ab, bb);
     else g7_launch<0, 0>(a, pl, stream, ab, bb);
   } else if (!a->act_bwd && !a->colsum) {
-    g7_launch_s<1>(a, pl, stream, ab, bb);
+    // forward epilogue with an f32 residual into an f32 output: the residual staged through LDS
+    // (g7_epilogue_res_lds; DPC_G7_RESLDS=0 or dpc_gemm7_set_res_lds(0) keeps the per-lane reads)
+    static int res_env = -1;
+    if (res_env < 0) res_env = getenv("DPC_G7_RESLDS") ? atoi(getenv("DPC_G7_RESLDS")) : 1;
+    const bool res_lds = (g7_res_lds >= 0 ? g7_res_lds : res_env) && s == 1 && a->residual && a->out_f32 &&
+                         !a->accumulate && a->ldr % 4 == 0 && ((uintptr_t)a->residual % 16) == 0 &&
+                         a->ldr <= (1 << 20);
+    if (res_lds) g7_launch_s<9>(a, pl, stream, ab, bb);
+    else g7_launch_s<1>(a, pl, stream, ab, bb);
   } else if (act_lds) {
     // column sums through the workspace ([2 tiles_m][N] partials + g7_colsum_reduce) when the
     // caller passed one large enough, else f32 atomics from the epilogue

@@ -551,6 +551,147 @@ __device__ __forceinline__ void g7_epilogue_act_lds(const GemmArgs& p, floatx4 (
   reads_done();  // both buffers are ring slots again: the next tile's bodies 0 / 1 refill them
 }
 
+// MODE 1 with an f32 residual and an f32 output on v7 (the FFN down-projection forward: bias +
+// GELU + pre-activation aux_out + residual), the residual staged through LDS as in
+// g7_epilogue_act_lds: eight 16-row "eighths" of the 256-KiB residual tile (row block i of both
+// wave rows, 32 rows x 1 KiB = one ring slot) by LDS-DMA into the two idle ring slots,
+// double-buffered; one piece = one 1-KiB row, 16-B chunk c of local row r at position
+// c ^ (r & 15).  GELU in packed f32.
+template <int NJ>
+__device__ __forceinline__ void g7_epilogue_res_lds(const GemmArgs& p, floatx4 (&acc)[8][NJ], int m0, int n0,
+                                                    int wid, int lane_in, bf16_t* buf0, bf16_t* buf1) {
+  static_assert(NJ == 8, "v7 tiles");
+  int lane;  // (opaque: tile-invariant per-lane addresses must not be hoisted out of the tile loop)
+  asm volatile("v_mov_b32 %0, %1" : "=v"(lane) : "v"(lane_in));
+  float alpha = p.alpha;
+  if (p.alpha_ptr) alpha *= *p.alpha_ptr;
+  const int g = lane >> 4, rl = lane & 15;
+  const int wr = wid >> 1, wc = wid & 1;
+  const int mw = m0 + wr * 128, nw = n0 + wc * 128;
+  const int coff = 16 * (g & 1) + 8 * (g >> 1);
+  const int ld = (int)p.ldr;
+  const long long org = (long long)m0 * ld + n0;
+  const long long rem = ((long long)(p.M - 1) * ld + p.N - org) * 4;
+  const unsigned nrec = rem <= 0 ? 0u : (rem >= 0xffffffffll ? 0xffffffffu : (unsigned)rem);
+  const __amdgpu_buffer_rsrc_t rr_ =
+      __builtin_amdgcn_make_buffer_rsrc((void*)(p.residual + org), 0, nrec, 0x00020000);
+  auto rdma = [&](int e, bf16_t* buf) G7_AI {  // eighth e: tile rows 16 e + (0..15) of both wave rows
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const int lr = wid * 8 + k;  // local row 0..31 (one piece each)
+      const int tr = ((lr & 16) ? 128 : 0) + 16 * e + (lr & 15);
+      const int c = lane ^ (lr & 15);
+      g7_piece(rr_, (tr * ld + c * 4) * 4, buf + lr * 512);
+    }
+  };
+  const bool full = m0 + 256 <= p.M && n0 + 256 <= p.N;
+  const bool has_aux = p.aux_out != nullptr;
+  bf16_t* aux_out = static_cast<bf16_t*>(p.aux_out);
+  float4 bias4[NJ];
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) {
+    const int n = nw + 16 * j + 4 * g;
+    bias4[j] = (p.bias && n < p.N) ? *reinterpret_cast<const float4*>(p.bias + n) : make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+  auto proc = [&](auto E, const bf16_t* buf) G7_AI {
+    constexpr int i = decltype(E)::value;
+    const int m = mw + 16 * i + rl;
+    const bool mok = m < p.M;
+    const float* rrow = reinterpret_cast<const float*>(buf + (wr * 16 + rl) * 512);
+    sfor<NJ / 2>([&](auto J) G7_AI {
+      constexpr int j = 2 * decltype(J)::value;
+      unsigned pa[2][2];
+      sfor<2>([&](auto H) G7_AI {
+        constexpr int h = decltype(H)::value;
+        constexpr int jj = j + h;
+        const int n = nw + 16 * jj + 4 * g;
+        const bool ok = mok && n < p.N;
+        const int c = wc * 32 + 4 * jj + g;
+        const float4 res = *reinterpret_cast<const float4*>(rrow + (c ^ rl) * 4);
+        float w[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) w[r] = acc[i][jj][r] * alpha;
+        w[0] += bias4[jj].x; w[1] += bias4[jj].y; w[2] += bias4[jj].z; w[3] += bias4[jj].w;
+        pa[h][0] = pack2bf(w[0], w[1]);
+        pa[h][1] = pack2bf(w[2], w[3]);
+        if (p.act == ACT_GELU) {
+          const dpc_f2_t g01 = gelu_tanh2(dpc_f2_t{w[0], w[1]}), g23 = gelu_tanh2(dpc_f2_t{w[2], w[3]});
+          w[0] = g01.x; w[1] = g01.y; w[2] = g23.x; w[3] = g23.y;
+        } else {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) w[r] = act_fwd(w[r], p.act);
+        }
+        if (ok)
+          *reinterpret_cast<float4*>(static_cast<float*>(p.C) + (long long)m * p.ldc + n) =
+              make_float4(w[0] + res.x, w[1] + res.y, w[2] + res.z, w[3] + res.w);
+      });
+      if (has_aux) {
+        const int n8 = nw + 16 * j + coff;
+        const auto s0 = __builtin_amdgcn_permlane16_swap(pa[0][0], pa[1][0], false, false);
+        const auto s1 = __builtin_amdgcn_permlane16_swap(pa[0][1], pa[1][1], false, false);
+        if (mok && n8 < p.N)
+          *reinterpret_cast<uint4*>(aux_out + (long long)m * p.ld_aux_out + n8) = make_uint4(s0[0], s1[0], s0[1], s1[1]);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    });
+  };
+  // eighth e landed: younger = eighth e-1's stores (8 f32 + 4 aux per lane, full tiles) + the
+  // next DMA (8 pieces) when issued
+  auto landed = [&](bool st, bool next) G7_AI {
+    if (st && full) {
+      if (has_aux) {
+        if (next) g7_wait<20>();
+        else g7_wait<12>();
+      } else {
+        if (next) g7_wait<16>();
+        else g7_wait<8>();
+      }
+    } else {
+      if (next) g7_wait<8>();
+      else g7_wait<0>();
+    }
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+  };
+  auto reads_done = [&]() G7_AI {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+  };
+  reads_done();
+  rdma(0, buf0);
+  rdma(1, buf1);
+  landed(false, true);
+  proc(std::integral_constant<int, 0>{}, buf0);
+  reads_done();
+  rdma(2, buf0);
+  landed(true, true);
+  proc(std::integral_constant<int, 1>{}, buf1);
+  reads_done();
+  rdma(3, buf1);
+  landed(true, true);
+  proc(std::integral_constant<int, 2>{}, buf0);
+  reads_done();
+  rdma(4, buf0);
+  landed(true, true);
+  proc(std::integral_constant<int, 3>{}, buf1);
+  reads_done();
+  rdma(5, buf1);
+  landed(true, true);
+  proc(std::integral_constant<int, 4>{}, buf0);
+  reads_done();
+  rdma(6, buf0);
+  landed(true, true);
+  proc(std::integral_constant<int, 5>{}, buf1);
+  reads_done();
+  rdma(7, buf1);
+  landed(true, true);
+  proc(std::integral_constant<int, 6>{}, buf0);
+  landed(true, false);
+  proc(std::integral_constant<int, 7>{}, buf1);
+  reads_done();
+}
+
 // split-K partial tile (non-swapped accumulators: lane l, register r of accumulator (i, j) holds
 // C[mw + 16 i + 4 (l >> 4) + r][nw + 16 j + (l & 15)]): f32 atomic adds, each wave-instruction
 // four rows x 64 contiguous bytes.  The host zeroes C first unless the product accumulates.
@@ -576,7 +717,8 @@ __device__ __forceinline__ void g7_epilogue_atomic(const GemmArgs& p, floatx4 (&
 // EPI: 0 = plain products (bf16 / f32 C), 1 = forward fused epilogues, 2 = split-K f32 atomics,
 // 3 = input-gradient fused epilogues (act', column sums), 4 = split-K partial tiles stored to
 // the workspace slab of their k-range (plain 16-B stores; g7_splitk_reduce sums the slabs),
-// 8 = EPI 3 with an act' operand staged through LDS (v7 only; g7_epilogue_act_lds).
+// 8 = EPI 3 with an act' operand staged through LDS (v7 only; g7_epilogue_act_lds), 9 = EPI 1
+// with an f32 residual and output, the residual staged through LDS (v7 only; g7_epilogue_res_lds).
 // WN: output columns per wave.  128 = v7 (a 256 x 256 tile, one workgroup per CU); 64 = v8 (a
 // 256 x 128 tile, 128 accumulator registers, TWO workgroups per CU, each with a 3-slot ring:
 // the two drift out of phase, so one's epilogue -- the bias / GELU / residual / act' VALU work
@@ -857,6 +999,10 @@ __global__ __launch_bounds__(256, WN == 128 ? 1 : 2) void gemm7_kernel(GemmArgs 
       g7_epilogue<0, NJ>(q, acc, m0 + ar, n0 + bc, lane);
     } else if constexpr (EPI == 0) {
       g7_epilogue<EPI, NJ, WN == 64 && AK>(p, acc, m0 + ar, n0 + bc, lane, pl.debug);
+    } else if constexpr (EPI == 9) {
+      static_assert(WN == 128, "v7 only");
+      g7_epilogue_res_lds<NJ>(p, acc, m0, n0, wid, lane, smem + ((rd_slot + 3) % NS) * SLOT,
+                              smem + ((rd_slot + 4) % NS) * SLOT);
     } else if constexpr (EPI == 8) {
       // (its own instantiation: beside g7_epilogue<3> in one kernel the register allocator
       // spilled ~120 registers, alone it spills 2)

@@ -202,6 +202,42 @@ def test_gemm_v7_act_grad_epilogue_paths(monkeypatch, act_lds, use_ws, a_kmaj, b
     assert rel_err(of, of_r) < 2e-3
 
 
+@pytest.mark.parametrize("res_lds", [0, 1])
+@pytest.mark.parametrize("act,with_aux,with_bias", [(2, True, True), (0, False, True), (1, True, False)])
+@pytest.mark.parametrize("a_kmaj,b_kmaj", [(True, True), (True, False)])
+@pytest.mark.parametrize("M,N,K", [(1023, 768, 768), (4096, 4352, 256), (300, 264, 96)])
+def test_gemm_v7_residual_epilogue_paths(res_lds, act, with_aux, with_bias, a_kmaj, b_kmaj, M, N, K):
+    """The v7 forward epilogue into an f32 output with an f32 residual (the FFN down-projection:
+    bias + GELU + pre-activation aux + residual) on both paths: the residual staged through LDS
+    in 16-row eighths (gemm7_kern.h g7_epilogue_res_lds, EPI 9) and the per-lane reads
+    (DPC_G7_RESLDS=0); the residual is also passed aliased to the output, as the model does."""
+    torch.manual_seed(6)
+    a = torch.randn(M, K, device=dev).bfloat16()
+    b = torch.randn(N, K, device=dev).bfloat16()
+    A, B = _store(a, a_kmaj), _store(b, b_kmaj)
+    bias = torch.randn(N, device=dev) if with_bias else None
+    res = torch.randn(M, N, device=dev)
+    lib = _lib.lib()
+    _lib.set_gemm_impl(25)
+    lib.dpc_gemm7_set_res_lds(res_lds)
+    try:
+        aux = torch.empty(M, N, device=dev, dtype=torch.bfloat16) if with_aux else None
+        out = gemm(A, B, a_kmaj=a_kmaj, b_kmaj=b_kmaj, bias=bias, act=act, aux_out=aux, residual=res,
+                   out_dtype=torch.float32, alpha=0.75)
+        inplace = res.clone()
+        gemm(A, B, a_kmaj=a_kmaj, b_kmaj=b_kmaj, bias=bias, act=act, residual=inplace, out=inplace, alpha=0.75)
+    finally:
+        _lib.set_gemm_impl(-1)
+        lib.dpc_gemm7_set_res_lds(-1)
+    ref = torch.empty(M, N, device=dev)
+    aux_r = torch.empty(M, N, device=dev, dtype=torch.bfloat16) if with_aux else None
+    _gemm_ref(a, b, True, True, ref, bias, act, 0, None, aux_r, res, 0.75, None, False)
+    assert rel_err(out, ref) < 2e-3
+    assert rel_err(inplace, ref) < 2e-3
+    if with_aux:
+        assert rel_err(aux, aux_r) < 1e-2
+
+
 @pytest.mark.parametrize("M,N,K", [(16000, 3072, 768), (12000, 2560, 1600), (10000, 2048, 576), (4096, 4352, 768),
                                    (65472, 3072, 768), (65472, 768, 3072), (9000, 1600, 2048)])
 def test_gemm_v7d_deferred_gelu_epilogues(M, N, K):
