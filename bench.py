@@ -2,8 +2,13 @@
 """Headline benchmark: GPT-2 training tokens/sec (whole node) on N MI355X GPUs.
 
     python bench.py [--gpus 1] [--steps 20] [--warmup 5]            # 1 GPU
+    python bench.py --gpus N --steps K --warmup W                     # N GPUs (self-launch)
     torchrun --nproc-per-node N --master-addr 127.0.0.1 --master-port P \
         bench.py --gpus N --steps K --warmup W                        # N GPUs
+
+Without torchrun (``WORLD_SIZE`` unset) and N > 1, this process starts the N ranks itself as a
+``torch.distributed.run`` child and relays rank 0's line; under torchrun, a ``WORLD_SIZE`` that
+differs from ``--gpus`` is an error (exit 2), never a silently relabelled run.
 
 Metric and config follow BASELINE.json ("tokens/sec (node) GPT-2 training per recipe"):
 default is the ``main-ddp.py`` north-star config -- GPT-2 small (untied lm_head, 163M
@@ -46,6 +51,34 @@ BASELINE_TOKS_PER_GPU = {("ddp", "gpt2-small", 32, 1024): 276672.6,
 DEFAULT_BATCH = {"ddp": 64, "fsdp": 64, "pipe": 64, "pipe_ddp": 64}
 
 
+def _free_port() -> int:
+    import socket
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _launch_ranks(n: int) -> int:
+    """``python bench.py --gpus N`` without torchrun: run the same command line under
+    ``torch.distributed.run`` (one fresh process per GPU, rendezvous on 127.0.0.1) as a CHILD
+    process -- this process touches no GPU and never execs -- relay its output (rank 0 prints
+    the JSON line) and return its exit code, non-zero if any rank failed.  The reference's
+    multi-GPU recipes are torchrun-launched (``/root/reference/main-ddp.py:1-6``)."""
+    import subprocess
+
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(n),
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+           os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    env.setdefault("OMP_NUM_THREADS", "4")
+    r = subprocess.run(cmd, env=env)
+    if r.returncode != 0:
+        print(f"bench.py: {n}-rank run failed with exit code {r.returncode}", file=sys.stderr)
+    return r.returncode if r.returncode > 0 else (1 if r.returncode else 0)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -58,6 +91,8 @@ def main():
     ap.add_argument("--seq_len", type=int, default=1024)
     ap.add_argument("--bucket_mb", type=float, default=128.0)
     ap.add_argument("--reduce_dtype", default="fp32", choices=["fp32", "bf16"])
+    ap.add_argument("--pp_comm_dtype", default="fp32", choices=["fp32", "bf16"],
+                    help="pipe / pipe_ddp: wire dtype of the stage-boundary activations and gradients")
     ap.add_argument("--num_microbatches", type=int, default=0)
     ap.add_argument("--schedule", default="1f1b", choices=["1f1b", "gpipe"])
     ap.add_argument("--dp_size", type=int, default=0)
@@ -72,6 +107,15 @@ def main():
     ap.add_argument("--json", default=None, help="also write the result line to this file")
     a = ap.parse_args()
 
+    env_ws = os.environ.get("WORLD_SIZE")
+    if env_ws is None and a.gpus > 1:
+        # launched as `python bench.py --gpus N` (no torchrun): start N fresh ranks and relay
+        sys.exit(_launch_ranks(a.gpus))
+    if env_ws is not None and int(env_ws) != a.gpus:
+        print(f"bench.py: --gpus {a.gpus} but WORLD_SIZE={env_ws}; refusing to report a "
+              f"{env_ws}-rank run as {a.gpus} GPUs", file=sys.stderr)
+        sys.exit(2)
+
     batch_given = a.batch_size is not None
     if not batch_given:
         a.batch_size = DEFAULT_BATCH[a.recipe]
@@ -85,7 +129,8 @@ def main():
     argv = ["--model", model_name, "--batch_size", str(a.batch_size), "--bucket_mb", str(a.bucket_mb),
             "--reduce_dtype", a.reduce_dtype, "--synthetic_data"]
     if rec in ("pipe", "pipe_ddp"):
-        argv += ["--schedule", a.schedule, "--num_microbatches", str(a.num_microbatches)]
+        argv += ["--schedule", a.schedule, "--num_microbatches", str(a.num_microbatches),
+                 "--pp_comm_dtype", a.pp_comm_dtype]
     if rec == "pipe_ddp" and a.dp_size:
         argv += ["--dp_size", str(a.dp_size)]
     if rec == "fsdp" and a.prefetch is not None:
@@ -101,8 +146,6 @@ def main():
     args.sequence_length = a.seq_len
 
     info = comm.init_dist(force_group=a.force_dist_path)
-    if info.world_size != a.gpus and info.is_main:
-        print(f"warning: --gpus {a.gpus} but WORLD_SIZE {info.world_size}", file=sys.stderr)
     from distributed_pytorch_cookbook_amd.recipes import build_engine, build_model
 
     vocab = 50257

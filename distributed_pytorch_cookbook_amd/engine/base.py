@@ -130,13 +130,9 @@ class GraphedStep:
             st["tg"].copy_(targets, non_blocking=True)
             if mask is not None:
                 st["mask"].copy_(mask, non_blocking=True)
-            self.graph.replay()
+            self._replay()
             for o in self.opts:
                 o.step_count += 1
-            # the collectives inside a replayed graph are watched as one unit
-            wd = self._watchdog()
-            if wd.watchdog_running():
-                wd.watchdog_track(torch.cuda.current_stream().cuda_stream, "hip-graph step replay")
             return None if self.loss is None else self.loss.clone()
         if self.key != key:  # first call for this signature: eager (warm-up)
             self.key = key
@@ -193,5 +189,13 @@ class GraphedStep:
             self._sync()
             return body(batch, targets)
         self.graph = g
-        g.replay()
+        self._replay()  # (the first replay right after the capture is watched too)
         return None if self.loss is None else self.loss.clone()
+
+    def _replay(self):
+        """Replay the step graph; the collectives inside it are watched as one unit by the
+        native watchdog (its event is recorded behind the replay)."""
+        self.graph.replay()
+        wd = self._watchdog()
+        if wd.watchdog_running():
+            wd.watchdog_track(torch.cuda.current_stream().cuda_stream, "hip-graph step replay")

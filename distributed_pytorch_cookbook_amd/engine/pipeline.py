@@ -39,7 +39,8 @@ class PipelineEngine(Engine):
     def __init__(self, model, device, lr: float, pp: int, dp: int = 1, num_microbatches: int = 0,
                  schedule: str = "1f1b", bucket_mb: float = 128.0, compute_dtype=None,
                  seq_len: int | None = None, grad_scaler: bool = False, comm_kind: str | None = None,
-                 wire_dtype=None, graph: bool = False, force_dist: bool = False):
+                 wire_dtype=None, graph: bool = False, force_dist: bool = False,
+                 reduce_dtype=torch.float32):
         self.device = torch.device(device)
         self.model = model
         if grad_scaler:
@@ -95,7 +96,8 @@ class PipelineEngine(Engine):
                         p.data = _placeholder(p.shape, self.device)
         if dp > 1 or force_dist:
             self.store = DDPStore(model, device, group=self.dp_group, bucket_mb=bucket_mb,
-                                  compute_dtype=compute_dtype, units=self.my_units, transport=self.dp_tp)
+                                  reduce_dtype=reduce_dtype, compute_dtype=compute_dtype,
+                                  units=self.my_units, transport=self.dp_tp)
         else:
             self.store = LocalStore(model, device, compute_dtype=compute_dtype, units=self.my_units)
         self.store.accum_steps = self.n_micro

@@ -142,8 +142,8 @@ def _layer_forward(x, mask, layer, store, N, S, act, training, drops, attend=Non
     qkv = linear_fwd(h1, _qkv_weight(store, attn), out_dtype=cdt)
     o, lse = attention_fwd(qkv, N, S, H, hd, mask, causal=True) if attend is None else attend(qkv)
     if x.is_cuda and cdt == torch.bfloat16 and _FUSE_OUT_LN:
-        # out-projection as a plain product (hipBLASLt, bf16 out -- the reference's autocast
-        # Linear output dtype) and its bias / dropout / residual add fused into LN2, which
+        # out-projection as a plain product (the hand-written v7 / v9 MFMA GEMM, bf16 out -- the
+        # reference's autocast Linear output dtype) and its bias / dropout / residual add fused into LN2, which
         # writes the new f32 residual stream x2: the residual is read and written once,
         # instead of by a memory-bound GEMM epilogue and again by LN2
         yo = linear_fwd(o, w(attn.to_out.weight), out_dtype=cdt)

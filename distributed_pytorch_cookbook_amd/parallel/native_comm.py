@@ -260,7 +260,18 @@ class NativeComm:
             _check(_lib().dpc_rccl_group_end(), "group_end")
 
     def split(self, color: int, key: int) -> "NativeComm":
-        """Sub-communicator of the ranks sharing ``color`` (ordered by ``key``), collective."""
+        """Sub-communicator of the ranks sharing ``color`` (ordered by ``key``), collective.
+
+        ncclCommSplit is itself a blocking collective on this communicator, so the ranks first
+        agree (through the bootstrap group) that every one of them can enter it: the parent is
+        alive and reports no asynchronous error.  A rank that fails INSIDE the split after that
+        leaves the others blocked in it; the native watchdog (``dpc_wd_*``) is what ends such a
+        hang (abort + non-zero exit).  A split that returns an error on some rank is agreed
+        afterwards: every rank keeps its split, or none does."""
+        pre_ok = bool(self.comm) and _lib().dpc_rccl_async_error(self.comm) == 0
+        if not _agree(pre_ok, self.group):
+            raise RuntimeError("ncclCommSplit not attempted: the parent communicator is down on "
+                               + ("this rank" if not pre_ok else "another rank"))
         out = ctypes.c_void_p()
         rc = _lib().dpc_rccl_split(self.comm, color, key, ctypes.byref(out))
         if not _agree(rc == 0, self.group):  # every rank keeps its split, or none does

@@ -354,8 +354,11 @@ class NativeTransport(Transport):
                     raise RuntimeError(f"stream-order check: {op} buffer {tuple(t.shape)} on {t.device} "
                                        f"(contiguous={t.is_contiguous()}) handed to the comm stream of {self.device}")
         capturing = _capturing()
-        if comm.coll_check_enabled() and not capturing:
-            # --coll_check on the production path: every rank's (sequence, op, shape, dtype)
+        if comm.coll_check_enabled() and not capturing and op != "sendrecv":
+            # --coll_check on the production path: every rank's (sequence, op, shape, dtype).
+            # Point-to-point exchanges are not lockstep over the group (1F1B posts M exchanges
+            # on the first stage, M + 1 on the last, other counts in between), so a group-wide
+            # fingerprint would pair up wrongly: skipped, as TorchTransport.sendrecv does
             comm.fingerprint(op, tensors[0] if tensors else None, self.group)
         desc = _desc(op, tensors)
         s = self.stream

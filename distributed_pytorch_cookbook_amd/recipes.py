@@ -51,6 +51,10 @@ def build_engine(recipe: str, model, info, args, force_dist: bool = False):
     communicator (bucketed DDP store, sharded FSDP store, replica DDP store of the pipeline) --
     bench.py --force_dist_path profiles it on one GPU."""
     compute_dtype = torch.float32 if args.disable_amp else None
+    # --reduce_dtype: the wire/reduction dtype of the gradient collectives of every recipe (DDP
+    # bucket all-reduce, FSDP reduce-scatter, the PP x DP replica all-reduce); the reference
+    # reduces fp32 (autocast keeps fp32 grads, /root/reference/main-fsdp.py:64-69)
+    reduce_dtype = torch.bfloat16 if getattr(args, "reduce_dtype", "fp32") == "bf16" else torch.float32
     comm_kind = "native" if force_dist else getattr(args, "comm", "auto")
     # the cookbook's "compile": capture the whole step into a HIP graph (dropout masks are
     # drawn per step on the host: not graph-replayable).  One rank by default; at N > 1 only
@@ -65,7 +69,7 @@ def build_engine(recipe: str, model, info, args, force_dist: bool = False):
 
         return DataParallelEngine(
             model, info.device, lr=args.learning_rate, bucket_mb=args.bucket_mb,
-            reduce_dtype=torch.bfloat16 if args.reduce_dtype == "bf16" else torch.float32,
+            reduce_dtype=reduce_dtype,
             overlap=not args.no_overlap, compute_dtype=compute_dtype, graph=graph,
             comm_kind=comm_kind, grad_scaler=getattr(args, "grad_scaler", False), force_ddp_store=force_dist,
         )
@@ -75,7 +79,7 @@ def build_engine(recipe: str, model, info, args, force_dist: bool = False):
         return FSDPEngine(model, info.device, lr=args.learning_rate, prefetch=args.prefetch,
                           reshard_after_forward=not args.no_reshard_after_forward,
                           cpu_offload=args.cpu_offload, compute_dtype=compute_dtype,
-                          grad_scaler=getattr(args, "grad_scaler", False), graph=graph, comm_kind=comm_kind,
+                          reduce_dtype=reduce_dtype, grad_scaler=getattr(args, "grad_scaler", False), graph=graph, comm_kind=comm_kind,
                           force_sharded=force_dist)
     if recipe in ("pipe", "pipe_ddp"):
         from .engine.pipeline import PipelineEngine
@@ -86,7 +90,8 @@ def build_engine(recipe: str, model, info, args, force_dist: bool = False):
                               num_microbatches=args.num_microbatches,
                               schedule=args.schedule, bucket_mb=args.bucket_mb,
                               compute_dtype=compute_dtype, grad_scaler=getattr(args, "grad_scaler", False),
-                              comm_kind=comm_kind, wire_dtype=wire, graph=graph, force_dist=force_dist)
+                              comm_kind=comm_kind, wire_dtype=wire, graph=graph, force_dist=force_dist,
+                              reduce_dtype=reduce_dtype)
     raise ValueError(recipe)
 
 

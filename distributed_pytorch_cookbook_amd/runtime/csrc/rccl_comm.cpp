@@ -144,7 +144,9 @@ DPC_API int dpc_rccl_split(void* comm, int color, int key, void** out) {
   return r;
 }
 
-DPC_API int dpc_rccl_destroy(void* comm) { return g.handle ? check(g.comm_destroy(comm), "ncclCommDestroy") : -1; }
+int wd_destroy_locked(void* comm);  // below: unregisters from the watchdog, then destroys
+
+DPC_API int dpc_rccl_destroy(void* comm) { return g.handle ? wd_destroy_locked(comm) : -1; }
 
 DPC_API int dpc_rccl_abort(void* comm) { return g.handle ? check(g.comm_abort(comm), "ncclCommAbort") : -1; }
 
@@ -225,6 +227,9 @@ struct Pending {
 
 struct Watchdog {
   std::mutex mu;
+  // held across "unregister + ncclCommDestroy" by the owner and across "copy + ncclCommAbort"
+  // by wd_fire: the watchdog never aborts a communicator that is being (or has been) destroyed
+  std::timed_mutex life;
   std::deque<Pending> q;
   std::vector<hipEvent_t> pool;  // completed events, re-recorded instead of re-created
   std::vector<ncclComm_t> comms;
@@ -244,8 +249,14 @@ Watchdog& wd = *new Watchdog;
   fprintf(stderr, "[dpc watchdog] rank %d: %s; aborting %zu RCCL communicator(s) and exiting with status %d\n",
           wd.rank, why.c_str(), wd.comms.size(), wd.exit_code);
   fflush(stderr);
-  // ncclCommAbort can itself wait on a wedged device: give it a bounded time, then leave anyway
-  std::vector<ncclComm_t> comms = wd.comms;
+  // ncclCommAbort can itself wait on a wedged device: give it a bounded time, then leave anyway.
+  // A destroy in progress on the main thread holds `life`; if it does not finish within 2 s the
+  // communicators are left to the process exit rather than aborted while being freed.
+  std::vector<ncclComm_t> comms;
+  if (wd.life.try_lock_for(std::chrono::seconds(2))) {
+    std::lock_guard<std::mutex> lk(wd.mu);
+    comms = wd.comms;
+  }  // (`life` stays held: this thread ends the process)
   std::atomic<bool> done{false};
   std::thread ab([&comms, &done] {
     for (ncclComm_t c : comms)
@@ -364,6 +375,12 @@ DPC_API void dpc_wd_unregister(void* comm) {
       wd.comms.erase(it);
       break;
     }
+}
+
+int wd_destroy_locked(void* comm) {
+  std::lock_guard<std::timed_mutex> life(wd.life);
+  dpc_wd_unregister(comm);
+  return check(g.comm_destroy(static_cast<ncclComm_t>(comm)), "ncclCommDestroy");
 }
 
 // Record an event behind the work just enqueued on `stream` and watch it.  Not during a

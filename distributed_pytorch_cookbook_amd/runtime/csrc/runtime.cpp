@@ -59,6 +59,7 @@ struct Loader {
   std::condition_variable cv_full, cv_space;
   std::deque<std::pair<uint64_t, std::vector<int64_t>>> ready;  // (batch index, data)
   uint64_t next_to_make = 0, next_to_take = 0;
+  uint64_t gen = 0;  // bumped by every seek: a batch made under an older generation is dropped
   std::atomic<bool> stop{false};
 
   void fill(uint64_t bi, int64_t* out) const {
@@ -73,18 +74,21 @@ struct Loader {
 
   void work() {
     for (;;) {
-      uint64_t bi;
+      uint64_t bi, my_gen;
       {
         std::unique_lock<std::mutex> lk(mu);
         cv_space.wait(lk, [&] { return stop.load() || next_to_make < next_to_take + depth; });
         if (stop) return;
         bi = next_to_make++;
+        my_gen = gen;
       }
       std::vector<int64_t> buf((size_t)B * (S + 1));
       fill(bi, buf.data());
       {
         std::lock_guard<std::mutex> lk(mu);
-        if (bi >= next_to_take) ready.emplace_back(bi, std::move(buf));  // (else: made before a seek)
+        // made before a seek (backward seeks included: the val loader's seek(0) every epoch):
+        // dropped, so `ready` never holds an index that next() will not take
+        if (my_gen == gen && bi >= next_to_take) ready.emplace_back(bi, std::move(buf));
       }
       cv_full.notify_all();
     }
@@ -178,6 +182,7 @@ API void dpc_loader_seek(void* h, int64_t bi) {
   {
     std::lock_guard<std::mutex> lk(L->mu);
     L->ready.clear();
+    L->gen++;
     L->next_to_make = L->next_to_take = (uint64_t)(bi < 0 ? 0 : bi);
   }
   L->cv_space.notify_all();

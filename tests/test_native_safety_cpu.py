@@ -16,7 +16,8 @@ import pytest
 import torch
 
 from dist_helpers import ROOT, free_port, run_workers
-from dist_workers import worker_capture_fallback, worker_native_agreement, worker_native_fingerprint
+from dist_workers import (worker_capture_fallback, worker_native_agreement, worker_native_fingerprint,
+                          worker_native_fingerprint_p2p)
 
 pytestmark = pytest.mark.slow
 
@@ -90,6 +91,13 @@ def test_coll_check_through_native_transport(fake_lib, tmp_path):
     run_workers(worker_native_fingerprint, 2, fake_lib, str(tmp_path / "log"))
     for r in range(2):
         assert (tmp_path / f"log.{r}").read_text().split() == ["all_reduce", "all_gather"]
+
+
+def test_coll_check_skips_p2p_on_native_transport(fake_lib, tmp_path):
+    run_workers(worker_native_fingerprint_p2p, 2, fake_lib, str(tmp_path / "log"))
+    for r in range(2):
+        ops = (tmp_path / f"log.{r}").read_text().split()
+        assert ops[-2:] == ["all_reduce", "all_gather"], ops
 
 
 @pytest.mark.parametrize("mode", ["uid", "init"])
