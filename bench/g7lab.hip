@@ -135,6 +135,16 @@ int main(int argc, char** argv) {
     vs.push_back({"no_read", [&] { launch<128 | 32, AK_, BK_>(a, pl, ab, bb); }, true, {}});              \
     vs.push_back({"no_read_no_dma", [&] { launch<128 | 32 | 2, AK_, BK_>(a, pl, ab, bb); }, true, {}});   \
     vs.push_back({"mfma_only", [&] { launch<128 | 32 | 16 | 2, AK_, BK_>(a, pl, ab, bb); }, true, {}});   \
+  } else if (set == "epi") {                                                                             \
+    vs.push_back({"v9", [&] { launch9<0, AK_, BK_>(a, pl, ab, bb); }, false, {}});                        \
+    vs.push_back({"v9_nt", [&] { launch9<1024, AK_, BK_>(a, pl, ab, bb); }, false, {}});                  \
+    vs.push_back({"v9_clk", [&] { launch9<128, AK_, BK_>(a, pl, ab, bb); }, true, {}});                   \
+    vs.push_back({"v9_nt_clk", [&] { launch9<128 | 1024, AK_, BK_>(a, pl, ab, bb); }, true, {}});         \
+    vs.push_back({"v9_no_epilogue", [&] { launch9<128, AK_, BK_>(a, noepi, ab, bb); }, true, {}});        \
+    vs.push_back({"v9_no_stores", [&] { launch9<128 | 512, AK_, BK_>(a, pl, ab, bb); }, true, {}});       \
+    vs.push_back({"v9_no_credit", [&] { launch9<128 | 2048, AK_, BK_>(a, pl, ab, bb); }, true, {}});      \
+    vs.push_back({"v9_no_dma", [&] { launch9<128 | 2, AK_, BK_>(a, pl, ab, bb); }, true, {}});            \
+    vs.push_back({"s6", [&] { launch<0, AK_, BK_, 6>(a, pl, ab, bb); }, false, {}});                      \
   } else {                                                                                                \
     vs.push_back({"s3", [&] { launch<0, AK_, BK_>(a, pl, ab, bb); }, false, {}});                         \
     vs.push_back({"s3_old", [&] { launch<256, AK_, BK_>(a, pl, ab, bb); }, false, {}});                   \

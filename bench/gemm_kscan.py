@@ -1,5 +1,5 @@
 """Time vs K at fixed M x N (forward layout): separates per-tile fixed cost (prologue /
-epilogue) from the per-k-slice main-loop cost.   python bench/gemm_kscan.py --impls 2 10 11"""
+epilogue) from the per-k-slice main-loop cost.   python bench/gemm_kscan.py --impls 2 10 20"""
 import argparse
 import os
 import sys
@@ -14,7 +14,7 @@ from distributed_pytorch_cookbook_amd.ops.gemm import gemm  # noqa: E402
 from kernels import timeit  # noqa: E402
 
 ap = argparse.ArgumentParser()
-ap.add_argument("--impls", type=int, nargs="+", default=[2, 10, 11])
+ap.add_argument("--impls", type=int, nargs="+", default=[2, 10, 20])
 ap.add_argument("--M", type=int, default=32736)
 ap.add_argument("--N", type=int, default=3072)
 ap.add_argument("--Ks", type=int, nargs="+", default=[256, 768, 1536, 3072, 6144])

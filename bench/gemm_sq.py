@@ -1,6 +1,6 @@
 """Square-GEMM ceiling check: our impls vs torch (hipBLASLt) at one large shape.
 
-    python bench/gemm_sq.py --n 8192 --impls 2 10 11
+    python bench/gemm_sq.py --n 8192 --impls 2 10 20
 """
 import argparse
 import os
@@ -17,7 +17,7 @@ from kernels import timeit  # noqa: E402
 
 ap = argparse.ArgumentParser()
 ap.add_argument("--n", type=int, nargs="+", default=[8192])
-ap.add_argument("--impls", type=int, nargs="+", default=[2, 10, 11])
+ap.add_argument("--impls", type=int, nargs="+", default=[2, 10, 20])
 a = ap.parse_args()
 for n in a.n:
     x = (torch.rand(n, n, device="cuda") * 2 - 1).bfloat16()

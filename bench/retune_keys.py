@@ -6,7 +6,7 @@ optionally write the winners into ``ops/gemm_tuned.json``.
 A signature (ops/gemm.py:_sig) is ``MxNxK:<a><b>:<f|h>:<act><act_bwd>:<flags>`` with layouts k / m
 (k-major / mn-major) and flags b(ias) x (aux_out) r(esidual) c(olsum) a(ccumulate); each entry is
 rebuilt from it on random data and timed (min of 3 x 5 calls) for the table's current choice and
-every listed implementation.
+every listed implementation, each reached through the table entry (0 = the dispatcher policy).
 """
 from __future__ import annotations
 
@@ -86,13 +86,17 @@ def main():
         cur = table["impl"][key]
         times = {}
         for impl in dict.fromkeys([cur] + a.impls):
-            _lib.set_gemm_impl(impl)
+            # the candidate goes through the table entry, exactly as a training step reaches the
+            # dispatcher: 0 = the dispatcher's own policy ("auto"), not a forced impl 0 (which
+            # set_gemm_impl would turn into the v1 register-staged kernel)
+            G._table[key] = impl
+            G._near_cache.clear()
             try:
                 times[impl] = timeit(fn)
             except RuntimeError:
                 pass
             finally:
-                _lib.set_gemm_impl(-1)
+                G._table[key] = cur
         best = min(times, key=times.get)
         row = {"key": key, "table": cur, "best": best,
                "tflops": {str(k): round(fl / v / 1e9) for k, v in times.items()}}

@@ -18,6 +18,7 @@ from ..parallel import comm
 from ..parallel.ddp import DDPStore
 from ..parallel.store import LocalStore
 from ..parallel.transport import check_drained
+from ..utils.profiling import mark
 from .base import Engine, GraphedStep
 
 
@@ -55,8 +56,14 @@ class DataParallelEngine(Engine):
     # ------------------------------------------------------------------ training
     def _step_body(self, batch, targets):
         self.store.zero_grad()
-        out = self.model(**batch, targets=targets)
-        self._scaled(out.loss).backward()
+        with mark("fwd"):
+            out = self.model(**batch, targets=targets)
+        with mark("bwd"):  # (the DDP bucket all-reduces are enqueued from inside it: "comm:*")
+            self._scaled(out.loss).backward()
+        with mark("optim"):
+            return self._optim(out)
+
+    def _optim(self, out):
         if self.scaler is not None:
             # the non-finite check needs every bucket reduced before any parameter moves;
             # all-reduced gradients are identical on every rank, so is the flag
@@ -74,7 +81,8 @@ class DataParallelEngine(Engine):
             st.launch_all()
             self.opt.begin_step()
             for bi in range(len(st.buckets)):
-                st.wait_bucket(bi)
+                with mark("comm:wait_bucket"):
+                    st.wait_bucket(bi)
                 lo, hi = st.bucket_range(bi)
                 self.opt.update(lo, hi, grad_scale=1.0 / self.dp_world)
             st.reset_buckets()

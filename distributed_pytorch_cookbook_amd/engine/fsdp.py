@@ -16,6 +16,7 @@ from ..ops.optim import FlatAdamW
 from ..parallel import comm
 from ..parallel.fsdp import FSDPStore
 from ..parallel.transport import check_drained
+from ..utils.profiling import mark
 from .base import Engine, GraphedStep
 
 # A/B switch (bench/offload.py): the synchronous offload step (D2H, host AdamW, H2D in turn)
@@ -62,9 +63,17 @@ class FSDPEngine(Engine):
     def _step_body(self, batch, targets):
         st = self.store
         st.zero_grad()
-        out = self.model(**batch, targets=targets)
-        self._scaled(out.loss).backward()
-        st.finish_grads()
+        with mark("fwd"):  # (unit all-gathers enqueued inside: "comm:all_gather")
+            out = self.model(**batch, targets=targets)
+        with mark("bwd"):  # (re-gathers and reduce-scatters enqueued inside)
+            self._scaled(out.loss).backward()
+        with mark("comm:finish_grads"):
+            st.finish_grads()
+        with mark("optim"):
+            return self._optim(out)
+
+    def _optim(self, out):
+        st = self.store
         if st.cpu_offload and self.scaler is None and not _OFFLOAD_SYNC:
             # pipelined host AdamW: overlaps the next step's forward (FSDPStore.host_step)
             st.host_step(self.opt, grad_scale=1.0 / self.dp_world)

@@ -29,6 +29,7 @@ from ..parallel.pipeline import P2P, partition, run_schedule, schedule_1f1b, sch
 from ..parallel.store import LocalStore
 from ..parallel.transport import TorchTransport, make_mesh_transports
 from ..parallel.transport import check_drained
+from ..utils.profiling import mark
 from .base import Engine, GraphedStep
 
 
@@ -178,7 +179,8 @@ class PipelineEngine(Engine):
         def forward(m, x):
             if x is not None:
                 x.requires_grad_(True)
-            out = self._fwd(micro[m], x, True)
+            with mark(f"fwd mb{m}"):
+                out = self._fwd(micro[m], x, True)
             inputs[m] = x
             if self.last:
                 loss, n_valid, _ = out
@@ -191,17 +193,23 @@ class PipelineEngine(Engine):
 
         def backward(m, g):
             y = outputs.pop(m)
-            if self.last:
-                self._scaled(y).backward()
-            else:
-                torch.autograd.backward(y, g)
+            with mark(f"bwd mb{m}"):
+                if self.last:
+                    self._scaled(y).backward()
+                else:
+                    torch.autograd.backward(y, g)
             x = inputs.pop(m)
             return None if x is None else x.grad
 
         order = (schedule_gpipe if self.schedule == "gpipe" else schedule_1f1b)(self.n_micro, self.stage, self.pp)
         run_schedule(order, self.first, self.last, forward, backward, self.p2p, shape)
         if isinstance(st, DDPStore):
-            st.finish_grads()
+            with mark("comm:finish_grads"):
+                st.finish_grads()
+        with mark("optim"):
+            return self._optim(acc)
+
+    def _optim(self, acc):
         if self.scaler is not None:
             # every stage holds different gradients: one skip decision for the whole job
             self.scaler.check(self.opt.grad)

@@ -37,6 +37,7 @@ class GemmArgs(ctypes.Structure):
         ("impl", c_int),    # 0 = dispatcher policy, else a measured per-shape choice
         ("aux_f32", c_int),  # dpc_gemm_f32: f32 aux_in / aux_out (else bf16)
         ("ws", P), ("ws_bytes", LL),  # split-K workspace (v7 slab split instead of atomics)
+        ("nt_store", c_int),  # dispatcher-owned (pass 0): non-temporal epilogue stores
     ]
 
 

@@ -40,7 +40,31 @@ struct GemmArgs {
   // f32 atomics into C (gemm7.hip: dpc_gemm7)
   void* ws;
   long long ws_bytes;
+  // set by the dispatcher (callers pass 0): epilogue stores with the non-temporal bit -- bit 0 the
+  // bf16 C / aux_out stores, bit 1 the f32 C stores (DPC_GEMM_NT, default 3).  The short-K
+  // forward products spent 20-35 % of their time in the tile-end store burst; with nt stores
+  // v9 runs the GPT-2 QKV / up / LM-head forward 947 / 964 / 1031 -> 1151 / 1150 / 1163 TF/s
+  // and 8192^3 1327 -> 1448 (bench/g7lab epi set, profiles/r4_gemm/lab_epi_nt.log)
+  int nt_store;
 };
+
+// 16-B epilogue stores, plain or non-temporal (GemmArgs::nt_store; the flag is a kernel
+// argument, so the branch is wave-uniform)
+__device__ __forceinline__ void st16(void* ptr, uint4 v, bool nt) {
+  typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+  if (nt) __builtin_nontemporal_store(u32x4{v.x, v.y, v.z, v.w}, reinterpret_cast<u32x4*>(ptr));
+  else *reinterpret_cast<uint4*>(ptr) = v;
+}
+__device__ __forceinline__ void st8(void* ptr, uint2 v, bool nt) {
+  typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+  if (nt) __builtin_nontemporal_store(u32x2{v.x, v.y}, reinterpret_cast<u32x2*>(ptr));
+  else *reinterpret_cast<uint2*>(ptr) = v;
+}
+__device__ __forceinline__ void st16(void* ptr, float4 v, bool nt) {
+  typedef float f32x4 __attribute__((ext_vector_type(4)));
+  if (nt) __builtin_nontemporal_store(f32x4{v.x, v.y, v.z, v.w}, reinterpret_cast<f32x4*>(ptr));
+  else *reinterpret_cast<float4*>(ptr) = v;
+}
 
 constexpr int BM = 128, BN = 128, BKT = 64, NT = 256;
 constexpr int TILE_ELEMS = BM * BKT;  // 8192 bf16 = 16 KiB per operand per stage

@@ -195,7 +195,7 @@ __device__ __forceinline__ void epi_tile(const GemmArgs& p, floatx4 (&acc)[FM][4
         uint2 w;
         w.x = pack2bf(v[0], v[1]);
         w.y = pack2bf(v[2], v[3]);
-        *reinterpret_cast<uint2*>(aux_out + (long long)m * p.ld_aux_out + n) = w;
+        st8(aux_out + (long long)m * p.ld_aux_out + n, w, p.nt_store & 1);
       }
       if (p.act == ACT_GELU) {  // packed-f32 math (common.h:gelu_tanh2)
         const dpc_f2_t g01 = gelu_tanh2(dpc_f2_t{v[0], v[1]}), g23 = gelu_tanh2(dpc_f2_t{v[2], v[3]});
@@ -215,12 +215,12 @@ __device__ __forceinline__ void epi_tile(const GemmArgs& p, floatx4 (&acc)[FM][4
           const float4 o = *C;
           v[0] += o.x; v[1] += o.y; v[2] += o.z; v[3] += o.w;
         }
-        *C = make_float4(v[0], v[1], v[2], v[3]);
+        st16(C, make_float4(v[0], v[1], v[2], v[3]), p.nt_store & 2);
       } else {
         uint2 w;
         w.x = pack2bf(v[0], v[1]);
         w.y = pack2bf(v[2], v[3]);
-        *reinterpret_cast<uint2*>(static_cast<bf16_t*>(p.C) + ci) = w;
+        st8(static_cast<bf16_t*>(p.C) + ci, w, p.nt_store & 1);
       }
     }
   }
@@ -620,131 +620,7 @@ __global__ __launch_bounds__((V3Cfg<BM_, BN_, WM, WN, KB, STAGES>::NTH), (V3Cfg<
 }
 
 // =====================================================================================
-// v4: 256x256 tile, 8 waves (2 x 4, 128x64 per wave), a ring of four 32-deep k-slices
-// (32 KiB each, 128 KiB) filled by LDS-DMA, with fragment reads software-pipelined across
-// the one barrier per slice.  Per slice and wave: 12 ds_read_b128 feed 32 MFMAs, split as
-//   A_hi(s) reads | 8 MFMA (s, rows 0-31) | vmcnt + barrier + DMA(s+3) + B(s+1) reads |
-//   8 MFMA (s, rows 32-63) | A_lo(s+1) reads | 16 MFMA (s, rows 64-127)
-// so every read has >= 8 MFMAs (128 cycles/wave, 256 per SIMD) in front of its first use,
-// and the DMA of slice s+3 (issued at barrier s+1) has two slices of MFMA work to land.
-// WAR: slot (s+3)%4 last held slice s-1, whose reads all retired before the MFMAs of
-// slice s-1's second half -- i.e. before every wave reached barrier s+1.
-// RAW: slice s+1 is read only after barrier s+1, which each wave enters after waiting for
-// its own DMAs of slice s+1 (counted vmcnt: slice s+2's 4 loads may stay in flight).
-template <bool AK>
-__device__ __forceinline__ void v4_read_a(bf16x8 (&a)[4], const bf16_t* la, int r0, int lane) {
-#pragma unroll
-  for (int i = 0; i < 4; ++i) a[i] = frag3<32, AK>(la, r0 + i * 16, 0, lane);
-}
-template <bool BK>
-__device__ __forceinline__ void v4_read_b(bf16x8 (&b)[4], const bf16_t* lb, int c0, int lane) {
-#pragma unroll
-  for (int j = 0; j < 4; ++j) b[j] = frag3<32, BK>(lb, c0 + j * 16, 0, lane);
-}
-__device__ __forceinline__ void v4_mma(floatx4 (&acc)[8][4], const bf16x8 (&a)[4], const bf16x8 (&b)[4],
-                                       int i0, int i1) {
-#pragma unroll
-  for (int i = i0; i < i1; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j)
-      acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i & 3], b[j], acc[i][j], 0, 0, 0);
-}
-
-template <bool AK, bool BK>
-__global__ __launch_bounds__(512, 1) void gemm4_kernel(GemmArgs p, unsigned long long a_bytes,
-                                                       unsigned long long b_bytes) {
-  using Cfg = V3Cfg<256, 256, 2, 4, 32, 4>;
-  constexpr int NS = 4, SLOT = Cfg::TA + Cfg::TB;
-  __shared__ __attribute__((aligned(16))) bf16_t smem[Cfg::SMEM];
-  const int tiles_m = (p.M + 255) / 256, tiles_n = (p.N + 255) / 256;
-  const int nwg = tiles_m * tiles_n;
-  const TileSlot ts = tile_slot(p, nwg);
-  const int bid = ts.bid;
-  const int group = GROUP_M * tiles_n;
-  const int gid = bid / group, first_m = gid * GROUP_M;
-  const int gsz = min(tiles_m - first_m, GROUP_M);
-  const int tm = first_m + (bid % group) % gsz;
-  const int tn = (bid % group) / gsz;
-  const int m0 = tm * 256, n0 = tn * 256;
-
-  const int lane = threadIdx.x & 63;
-  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int wr = wid >> 2, wc = wid & 3;
-  const int ar = wr * 128, bc = wc * 64;
-
-  int va[Cfg::NLA], vb[Cfg::NLB];  // 2 + 2 DMA instructions per wave per slice
-  dma_offsets3<32, AK, Cfg::NLA>(va, p.lda, wid, lane);
-  dma_offsets3<32, BK, Cfg::NLB>(vb, p.ldb, wid, lane);
-  const unsigned long long a_org = AK ? (unsigned long long)m0 * p.lda * 2 : (unsigned long long)m0 * 2;
-  const unsigned long long b_org = BK ? (unsigned long long)n0 * p.ldb * 2 : (unsigned long long)n0 * 2;
-  const unsigned long long a_step = AK ? 64ull : 32ull * p.lda * 2;
-  const unsigned long long b_step = BK ? 64ull : 32ull * p.ldb * 2;
-  floatx4 acc[8][4];
-#pragma unroll
-  for (int i = 0; i < 8; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
-
-  const int nk_all = (p.K + 31) / 32;
-  const int splits = ts.splits;
-  const int per = (nk_all + splits - 1) / splits;
-  const int kt0 = ts.split * per;
-  const int nk = max(0, min(nk_all, kt0 + per) - kt0);
-#define DPC_ISSUE4(s_)                                                                              \
-  do {                                                                                              \
-    bf16_t* base_ = smem + ((s_) % NS) * SLOT;                                                      \
-    const unsigned long long kg_ = (unsigned long long)(kt0 + (s_));                                \
-    issue_tile<Cfg::NLA>(p.A, a_bytes, a_org + a_step * kg_, va, base_, wid);                       \
-    issue_tile<Cfg::NLB>(p.B, b_bytes, b_org + b_step * kg_, vb, base_ + Cfg::TA, wid);             \
-  } while (0)
-
-  bf16x8 alo[4], ahi[4], b0[4], b1[4];
-  if (nk > 0) {
-    DPC_ISSUE4(0);
-    if (nk > 1) DPC_ISSUE4(1);
-    if (nk > 2) DPC_ISSUE4(2);
-    if (nk > 2) wait_vm<2 * (Cfg::NLA + Cfg::NLB)>();
-    else if (nk > 1) wait_vm<Cfg::NLA + Cfg::NLB>();
-    else wait_vm<0>();
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
-    v4_read_b<BK>(b0, smem + Cfg::TA, bc, lane);
-    v4_read_a<AK>(alo, smem, ar, lane);
-  }
-  // one k-slice; bc_/bn_ = current / next B fragments (alternating register sets)
-#define DPC_SLICE4(s_, bcur_, bnext_)                                                               \
-  do {                                                                                              \
-    const bf16_t* la_ = smem + ((s_) % NS) * SLOT;                                                  \
-    v4_read_a<AK>(ahi, la_, ar + 64, lane);                                                         \
-    v4_mma(acc, alo, bcur_, 0, 2);                                                                  \
-    const bool more_ = (s_) + 1 < nk;                                                               \
-    if (more_) {                                                                                    \
-      if ((s_) + 2 < nk) wait_vm<Cfg::NLA + Cfg::NLB>();                                            \
-      else wait_vm<0>();                                                                            \
-      __builtin_amdgcn_s_barrier();                                                                 \
-      asm volatile("" ::: "memory");                                                                \
-      if ((s_) + 3 < nk) DPC_ISSUE4((s_) + 3);                                                      \
-      v4_read_b<BK>(bnext_, smem + (((s_) + 1) % NS) * SLOT + Cfg::TA, bc, lane);                   \
-    }                                                                                               \
-    v4_mma(acc, alo, bcur_, 2, 4);                                                                  \
-    if (more_) v4_read_a<AK>(alo, smem + (((s_) + 1) % NS) * SLOT, ar, lane);                       \
-    v4_mma(acc, ahi, bcur_, 4, 8);                                                                  \
-  } while (0)
-  int s = 0;
-  for (; s + 1 < nk; s += 2) {
-    DPC_SLICE4(s, b0, b1);
-    DPC_SLICE4(s + 1, b1, b0);
-  }
-  if (s < nk) DPC_SLICE4(s, b0, b1);
-#undef DPC_SLICE4
-#undef DPC_ISSUE4
-
-  // ---------------- epilogue: four passes of 32 rows per wave through LDS (as v3)
-  epi_tile<8, false>(p, acc, reinterpret_cast<float*>(smem) + wid * 32 * 64, splits, m0 + ar, n0 + bc, lane);
-}
-
-// =====================================================================================
-// v5: 256x256 ping-pong.  Same 4-slot ring of 32-deep k-slices and LDS images as v4, but the
+// v5: 256x256 ping-pong.  A 4-slot ring of 32-deep k-slices (32 KiB each) filled by LDS-DMA, but the
 // two wave groups of the workgroup (waves 0-3 = rows 0-127, waves 4-7 = rows 128-255; waves
 // w and w+4 share a SIMD) run one barrier interval apart: while one group's MFMA segment
 // (16 x v_mfma_f32_16x16x32_bf16 = 256 cycles) runs, its SIMD partner is in a read segment
@@ -869,126 +745,6 @@ __global__ __launch_bounds__(512, 1) void gemm5_kernel(GemmArgs p, unsigned long
   epi_tile<8, false>(p, acc, reinterpret_cast<float*>(smem) + wid * 32 * 64, splits, m0 + ar, n0 + bc, lane);
 }
 
-// =====================================================================================
-// v6: the v5 ping-pong with the LDS-DMA issue spread over BOTH read segments of a k-slice
-// and an NS-slot ring (NS = 4: 128 KiB, NS = 5: the whole 160 KiB LDS, one more slice in
-// flight).  In v5 the (s,1) read segment issued all four 1-KiB DMA pieces of slice s+3 on
-// top of its fragment reads; a DMA piece costs ~60-185 issue cycles beside MFMA traffic
-// (MI355X_MICROARCH.md cycle constants), so that segment outlasted the partner group's
-// 256-cycle MFMA segment and the matrix pipe idled every other phase.  Here
-//   R(s,0): fragment reads B(s) + A rows 0-63 (s), then the B part of slice s+NS-1
-//   R(s,1): fragment reads A rows 64-127 (s), then the A part of slice s+NS-1, counted vmcnt
-// WAR (slot (s+NS-1)%NS last held slice s-1): B(s-1) was read in R(s-1,0) by both groups and
-// retired at the start of each group's M(s-1,0) -- at least two barriers before either group's
-// R(s,0).  A(s-1) rows 64-127 were read in R(s-1,1), retired at the start of M(s-1,1); the
-// lagging group's M(s-1,1) starts at the barrier that opens the leading group's R(s,0), so the
-// A part waits until R(s,1), which both groups enter after that barrier's successor.
-// RAW: slice s+1 is read in R(s+1,0); the youngest loads a wave may leave in flight after its
-// R(s,1) issue are slices s+2 .. s+NS-1 (4 pieces each) -> vmcnt(4 (NS-2)), then the barrier
-// (and for the leading group the lagging group's vmcnt precedes the barrier before R(s+1,0)).
-template <int NS, bool AK, bool BK>
-__global__ __launch_bounds__(512, 1) void gemm6_kernel(GemmArgs p, unsigned long long a_bytes,
-                                                       unsigned long long b_bytes) {
-  using Cfg = V3Cfg<256, 256, 2, 4, 32, 4>;
-  constexpr int SLOT = Cfg::TA + Cfg::TB;
-  constexpr int NLA = Cfg::NLA, NLB = Cfg::NLB;  // 2 + 2 DMA instructions per wave per slice
-  constexpr int SMEM = NS * SLOT > Cfg::SMEM ? NS * SLOT : Cfg::SMEM;
-  static_assert(SMEM * 2 <= 160 * 1024, "LDS");
-  __shared__ __attribute__((aligned(16))) bf16_t smem[SMEM];
-  const int tiles_m = (p.M + 255) / 256, tiles_n = (p.N + 255) / 256;
-  const int nwg = tiles_m * tiles_n;
-  const TileSlot ts = tile_slot(p, nwg);
-  const int bid = ts.bid;
-  const int group = GROUP_M * tiles_n;
-  const int gid = bid / group, first_m = gid * GROUP_M;
-  const int gsz = min(tiles_m - first_m, GROUP_M);
-  const int tm = first_m + (bid % group) % gsz;
-  const int tn = (bid % group) / gsz;
-  const int m0 = tm * 256, n0 = tn * 256;
-
-  const int lane = threadIdx.x & 63;
-  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int wr = wid >> 2, wc = wid & 3;
-  const int ar = wr * 128, bc = wc * 64;
-
-  int va[NLA], vb[NLB];
-  dma_offsets3<32, AK, NLA>(va, p.lda, wid, lane);
-  dma_offsets3<32, BK, NLB>(vb, p.ldb, wid, lane);
-  const unsigned long long a_org = AK ? (unsigned long long)m0 * p.lda * 2 : (unsigned long long)m0 * 2;
-  const unsigned long long b_org = BK ? (unsigned long long)n0 * p.ldb * 2 : (unsigned long long)n0 * 2;
-  const unsigned long long a_step = AK ? 64ull : 32ull * p.lda * 2;
-  const unsigned long long b_step = BK ? 64ull : 32ull * p.ldb * 2;
-  floatx4 acc[8][4];
-#pragma unroll
-  for (int i = 0; i < 8; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
-
-  const int nk_all = (p.K + 31) / 32;
-  const int splits = ts.splits;
-  const int per = (nk_all + splits - 1) / splits;
-  const int kt0 = ts.split * per;
-  const int nk = max(0, min(nk_all, kt0 + per) - kt0);
-#define DPC_ISSUE6A(s_)                                                                              \
-  issue_tile_v<NLA>(p.A, a_bytes, a_org + a_step * (unsigned long long)(kt0 + (s_)), (s_) < nk, va,  \
-                    smem + ((s_) % NS) * SLOT, wid)
-#define DPC_ISSUE6B(s_)                                                                              \
-  issue_tile_v<NLB>(p.B, b_bytes, b_org + b_step * (unsigned long long)(kt0 + (s_)), (s_) < nk, vb,  \
-                    smem + ((s_) % NS) * SLOT + Cfg::TA, wid)
-
-  if (nk > 0) {
-#pragma unroll
-    for (int s = 0; s < NS - 1; ++s) {
-      DPC_ISSUE6B(s);
-      DPC_ISSUE6A(s);
-    }
-    wait_vm<(NS - 2) * (NLA + NLB)>();  // slice 0 landed (slices 1 .. NS-2 in flight)
-    seg_barrier();
-    if (wr == 1) seg_barrier();  // the second group runs one barrier interval behind
-    bf16x8 alo[4], ahi[4], b[4];
-    for (int s = 0; s < nk; ++s) {
-      const bf16_t* la = smem + (s % NS) * SLOT;
-      const bf16_t* lb = la + Cfg::TA;
-      // ---- R(s,0)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) b[j] = frag3<32, BK>(lb, bc + j * 16, 0, lane);
-#pragma unroll
-      for (int i = 0; i < 4; ++i) alo[i] = frag3<32, AK>(la, ar + i * 16, 0, lane);
-      DPC_ISSUE6B(s + NS - 1);
-      seg_barrier();
-      // ---- M(s,0)
-      __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(alo[i], b[j], acc[i][j], 0, 0, 0);
-      __builtin_amdgcn_s_setprio(0);
-      seg_barrier();
-      // ---- R(s,1)
-#pragma unroll
-      for (int i = 0; i < 4; ++i) ahi[i] = frag3<32, AK>(la, ar + 64 + i * 16, 0, lane);
-      DPC_ISSUE6A(s + NS - 1);
-      wait_vm<(NS - 2) * (NLA + NLB)>();  // slice s+1 landed for this wave
-      seg_barrier();
-      // ---- M(s,1)
-      __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-          acc[4 + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ahi[i], b[j], acc[4 + i][j], 0, 0, 0);
-      __builtin_amdgcn_s_setprio(0);
-      seg_barrier();
-    }
-    if (wr == 0) seg_barrier();  // rebalance the barrier count of the two groups
-  }
-#undef DPC_ISSUE6A
-#undef DPC_ISSUE6B
-
-  epi_tile<8, false>(p, acc, reinterpret_cast<float*>(smem) + wid * 32 * 64, splits, m0 + ar, n0 + bc, lane);
-}
-
 }  // namespace dpc
 
 using namespace dpc;
@@ -999,23 +755,6 @@ static void launch_v5(const GemmArgs* a, dim3 grid, hipStream_t stream, unsigned
   else if (a->a_kmaj) hipLaunchKernelGGL((gemm5_kernel<true, false>), grid, dim3(512), 0, stream, *a, ab, bb);
   else if (!a->b_kmaj) hipLaunchKernelGGL((gemm5_kernel<false, false>), grid, dim3(512), 0, stream, *a, ab, bb);
   else hipLaunchKernelGGL((gemm5_kernel<false, true>), grid, dim3(512), 0, stream, *a, ab, bb);
-}
-
-template <int NS>
-static void launch_v6(const GemmArgs* a, dim3 grid, hipStream_t stream, unsigned long long ab,
-                      unsigned long long bb) {
-  if (a->a_kmaj && a->b_kmaj) hipLaunchKernelGGL((gemm6_kernel<NS, true, true>), grid, dim3(512), 0, stream, *a, ab, bb);
-  else if (a->a_kmaj) hipLaunchKernelGGL((gemm6_kernel<NS, true, false>), grid, dim3(512), 0, stream, *a, ab, bb);
-  else if (!a->b_kmaj) hipLaunchKernelGGL((gemm6_kernel<NS, false, false>), grid, dim3(512), 0, stream, *a, ab, bb);
-  else hipLaunchKernelGGL((gemm6_kernel<NS, false, true>), grid, dim3(512), 0, stream, *a, ab, bb);
-}
-
-static void launch_v4(const GemmArgs* a, dim3 grid, hipStream_t stream, unsigned long long ab,
-                      unsigned long long bb) {
-  if (a->a_kmaj && a->b_kmaj) hipLaunchKernelGGL((gemm4_kernel<true, true>), grid, dim3(512), 0, stream, *a, ab, bb);
-  else if (a->a_kmaj) hipLaunchKernelGGL((gemm4_kernel<true, false>), grid, dim3(512), 0, stream, *a, ab, bb);
-  else if (!a->b_kmaj) hipLaunchKernelGGL((gemm4_kernel<false, false>), grid, dim3(512), 0, stream, *a, ab, bb);
-  else hipLaunchKernelGGL((gemm4_kernel<false, true>), grid, dim3(512), 0, stream, *a, ab, bb);
 }
 
 template <int BM_, int BN_, int WM, int WN, int KB, int STAGES>
@@ -1095,6 +834,13 @@ static int policy_impl(const GemmArgs* a) {
 extern "C" int dpc_gemm7(const GemmArgs* a, int persistent, int sched, int splits, hipStream_t stream, int wn);
 extern "C" int dpc_gemm7_ok(const GemmArgs* a);
 
+// GemmArgs::nt_store for every product (DPC_GEMM_NT: bit 0 bf16 outputs, bit 1 f32 outputs)
+static int gemm_nt_mode() {
+  static int mode = -1;
+  if (mode < 0) mode = getenv("DPC_GEMM_NT") ? atoi(getenv("DPC_GEMM_NT")) : 3;
+  return mode;
+}
+
 DPC_API int dpc_gemm(const GemmArgs* a, hipStream_t stream) {
   if (a->M <= 0 || a->N <= 0) return 0;
   const int tiles = ((a->M + BM - 1) / BM) * ((a->N + BN - 1) / BN);
@@ -1152,6 +898,7 @@ DPC_API int dpc_gemm(const GemmArgs* a, hipStream_t stream) {
   if (impl >= 15 && impl <= 26) {  // v7 (gemm7.hip): 4-wave 256x256, split-K f32 products
     GemmArgs c = *a;
     c.ksplit = 0;
+    c.nt_store = gemm_nt_mode();
     // (25: the split DMA interleave forced for plain products, SCHED 6; 20 / 22 pick it for
     // products with an mn-major operand; 26: v9, the 64-deep-stage kernel, which every other v7
     // placement takes for plain nt products)
@@ -1165,6 +912,7 @@ DPC_API int dpc_gemm(const GemmArgs* a, hipStream_t stream) {
   if (impl >= 2 && !v2_ok) impl = 1;
   GemmArgs b = *a;  // dispatcher-owned copy: split-K mode is decided here
   b.ksplit = 0;
+  b.nt_store = gemm_nt_mode();
   if (impl >= 2) {
     int bm = BM, bn = BN;
     if (impl >= 6) {
@@ -1197,17 +945,10 @@ DPC_API int dpc_gemm(const GemmArgs* a, hipStream_t stream) {
     switch (impl) {
       case 3: launch_v2<64, 3>(&b, g, stream, ab, bb); break;
       case 4: launch_v2<32, 3>(&b, g, stream, ab, bb); break;
-      case 5: launch_v2<32, 4>(&b, g, stream, ab, bb); break;
-      case 6: launch_v3<256, 256, 2, 4, 64, 2>(&b, g, stream, ab, bb); break;
-      case 7: launch_v3<256, 256, 2, 4, 32, 4>(&b, g, stream, ab, bb); break;
-      case 8: launch_v3<256, 128, 4, 2, 64, 2>(&b, g, stream, ab, bb); break;
-      case 9: launch_v3<256, 128, 4, 2, 32, 4>(&b, g, stream, ab, bb); break;
       case 10: launch_v3<256, 128, 4, 2, 32, 3>(&b, g, stream, ab, bb); break;
-      case 11: launch_v4(&b, g, stream, ab, bb); break;
       case 12: launch_v5(&b, g, stream, ab, bb); break;
-      case 13: launch_v6<4>(&b, g, stream, ab, bb); break;
-      case 14: launch_v6<5>(&b, g, stream, ab, bb); break;
-      default: launch_v2<64, 2>(&b, g, stream, ab, bb); break;
+      case 2: launch_v2<64, 2>(&b, g, stream, ab, bb); break;
+      default: return 1;  // (5-9, 11, 13, 14: removed implementations, chosen by no table or policy)
     }
     return (int)hipGetLastError();
   }

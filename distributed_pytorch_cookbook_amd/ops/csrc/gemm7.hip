@@ -279,7 +279,7 @@ DPC_API int dpc_gemm7(const GemmArgs* a, int persistent, int sched, int splits, 
       const long long nq = (long long)a->M * (a->N / 4);
       const int blocks = (int)std::min<long long>((nq + 255) / 256, 4096);
       hipLaunchKernelGGL(g7_splitk_reduce, dim3(blocks), dim3(256), 0, stream, static_cast<float*>(a->C), a->ldc,
-                         static_cast<const float*>(a->ws), a->M, a->N, s, a->accumulate);
+                         static_cast<const float*>(a->ws), a->M, a->N, s, a->accumulate, a->nt_store & 2);
       return (int)hipGetLastError();
     }
   }
@@ -289,7 +289,7 @@ DPC_API int dpc_gemm7(const GemmArgs* a, int persistent, int sched, int splits, 
     const long long nq = (long long)a->M * (a->N / 4);
     const int blocks = (int)std::min<long long>((nq + 255) / 256, 4096);
     hipLaunchKernelGGL(g7_splitk_reduce, dim3(blocks), dim3(256), 0, stream, static_cast<float*>(a->C), a->ldc,
-                       static_cast<const float*>(a->ws), a->M, a->N, s, a->accumulate);
+                       static_cast<const float*>(a->ws), a->M, a->N, s, a->accumulate, a->nt_store & 2);
   } else if (s > 1) {
     if (!a->accumulate) hipMemset2DAsync(a->C, (size_t)a->ldc * 4, 0, (size_t)a->N * 4, (size_t)a->M, stream);
     g7_launch_s<2>(a, pl, stream, ab, bb);

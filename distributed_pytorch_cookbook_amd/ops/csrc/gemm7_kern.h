@@ -182,8 +182,8 @@ __device__ __forceinline__ void g7_epilogue(const GemmArgs& p, floatx4 (&acc)[8]
           const int m = mw + 16 * i + rr, n = nw + 16 * j + 4 * g + 16 * hi8;
           if (n < p.N) {
             float* C = static_cast<float*>(p.C) + (long long)m * p.ldc + n;
-            if (m < p.M) *reinterpret_cast<float4*>(C) = dA;
-            if (m + 8 < p.M) *reinterpret_cast<float4*>(C + 8 * p.ldc) = dB;
+            if (m < p.M) st16(C, dA, p.nt_store & 2);
+            if (m + 8 < p.M) st16(C + 8 * p.ldc, dB, p.nt_store & 2);
           }
         }
       }
@@ -221,8 +221,9 @@ __device__ __forceinline__ void g7_epilogue(const GemmArgs& p, floatx4 (&acc)[8]
           asm volatile("" ::"v"(dA.x), "v"(dA.y), "v"(dA.z), "v"(dA.w), "v"(dB.x), "v"(dB.y), "v"(dB.z), "v"(dB.w));
         } else if (n < p.N) {
           bf16_t* C = static_cast<bf16_t*>(p.C) + (long long)m * p.ldc + n;
-          if (m < p.M) *reinterpret_cast<uint4*>(C) = dA;
-          if (m + 8 < p.M) *reinterpret_cast<uint4*>(C + 8 * p.ldc) = dB;
+          const bool nt = (p.nt_store & 1) || (dbg & 16);  // (dbg 16: the lab's nt arm)
+          if (m < p.M) st16(C, dA, nt);
+          if (m + 8 < p.M) st16(C + 8 * p.ldc, dB, nt);
         }
       }
     }
@@ -326,7 +327,7 @@ __device__ __forceinline__ void g7_epilogue(const GemmArgs& p, floatx4 (&acc)[8]
               const float4 o = *C;
               w[0] += o.x; w[1] += o.y; w[2] += o.z; w[3] += o.w;
             }
-            *C = make_float4(w[0], w[1], w[2], w[3]);
+            st16(C, make_float4(w[0], w[1], w[2], w[3]), p.nt_store & 2);
           }
         } else {
           pc[h][0] = pack2bf(w[0], w[1]);
@@ -339,14 +340,14 @@ __device__ __forceinline__ void g7_epilogue(const GemmArgs& p, floatx4 (&acc)[8]
         const auto s0 = __builtin_amdgcn_permlane16_swap(pa[0][0], pa[1][0], false, false);
         const auto s1 = __builtin_amdgcn_permlane16_swap(pa[0][1], pa[1][1], false, false);
         if (ok8)
-          *reinterpret_cast<uint4*>(aux_out + (long long)m * p.ld_aux_out + n8) = make_uint4(s0[0], s1[0], s0[1], s1[1]);
+          st16(aux_out + (long long)m * p.ld_aux_out + n8, make_uint4(s0[0], s1[0], s0[1], s1[1]), p.nt_store & 1);
       }
       if (!p.out_f32) {
         const auto s0 = __builtin_amdgcn_permlane16_swap(pc[0][0], pc[1][0], false, false);
         const auto s1 = __builtin_amdgcn_permlane16_swap(pc[0][1], pc[1][1], false, false);
         if (ok8)
-          *reinterpret_cast<uint4*>(static_cast<bf16_t*>(p.C) + (long long)m * p.ldc + n8) =
-              make_uint4(s0[0], s1[0], s0[1], s1[1]);
+          st16(static_cast<bf16_t*>(p.C) + (long long)m * p.ldc + n8, make_uint4(s0[0], s1[0], s0[1], s1[1]),
+               p.nt_store & 1);
       }
     });
   });
@@ -461,8 +462,8 @@ __device__ __forceinline__ void g7_epilogue_act_lds(const GemmArgs& p, floatx4 (
             for (int r = 0; r < 4; ++r) cs[jj][r] += w[r];
           }
           if (p.out_f32) {
-            if (ok) *reinterpret_cast<float4*>(static_cast<float*>(p.C) + (long long)m * p.ldc + n) =
-                make_float4(w[0], w[1], w[2], w[3]);
+            if (ok) st16(static_cast<float*>(p.C) + (long long)m * p.ldc + n, make_float4(w[0], w[1], w[2], w[3]),
+                         p.nt_store & 2);
           } else {
             pc[h][0] = pack2bf(w[0], w[1]);
             pc[h][1] = pack2bf(w[2], w[3]);
@@ -473,8 +474,8 @@ __device__ __forceinline__ void g7_epilogue_act_lds(const GemmArgs& p, floatx4 (
           const auto s0 = __builtin_amdgcn_permlane16_swap(pc[0][0], pc[1][0], false, false);
           const auto s1 = __builtin_amdgcn_permlane16_swap(pc[0][1], pc[1][1], false, false);
           if (mok && n8 < p.N)
-            *reinterpret_cast<uint4*>(static_cast<bf16_t*>(p.C) + (long long)m * p.ldc + n8) =
-                make_uint4(s0[0], s1[0], s0[1], s1[1]);
+            st16(static_cast<bf16_t*>(p.C) + (long long)m * p.ldc + n8, make_uint4(s0[0], s1[0], s0[1], s1[1]),
+                 p.nt_store & 1);
         }
         __builtin_amdgcn_sched_barrier(0);  // one column pair at a time (else all are live: spills)
       });
@@ -622,15 +623,15 @@ __device__ __forceinline__ void g7_epilogue_res_lds(const GemmArgs& p, floatx4 (
           for (int r = 0; r < 4; ++r) w[r] = act_fwd(w[r], p.act);
         }
         if (ok)
-          *reinterpret_cast<float4*>(static_cast<float*>(p.C) + (long long)m * p.ldc + n) =
-              make_float4(w[0] + res.x, w[1] + res.y, w[2] + res.z, w[3] + res.w);
+          st16(static_cast<float*>(p.C) + (long long)m * p.ldc + n,
+               make_float4(w[0] + res.x, w[1] + res.y, w[2] + res.z, w[3] + res.w), p.nt_store & 2);
       });
       if (has_aux) {
         const int n8 = nw + 16 * j + coff;
         const auto s0 = __builtin_amdgcn_permlane16_swap(pa[0][0], pa[1][0], false, false);
         const auto s1 = __builtin_amdgcn_permlane16_swap(pa[0][1], pa[1][1], false, false);
         if (mok && n8 < p.N)
-          *reinterpret_cast<uint4*>(aux_out + (long long)m * p.ld_aux_out + n8) = make_uint4(s0[0], s1[0], s0[1], s1[1]);
+          st16(aux_out + (long long)m * p.ld_aux_out + n8, make_uint4(s0[0], s1[0], s0[1], s1[1]), p.nt_store & 1);
       }
       __builtin_amdgcn_sched_barrier(0);
     });
@@ -1057,7 +1058,7 @@ __global__ __launch_bounds__(256) void g7_colsum_reduce(float* colsum, const flo
 // C (=, or += when accumulating) the sum of the s workspace slabs [s][M][N]; 4 columns per
 // thread (N % 8 == 0, ldc % 8 == 0: 16-B rows)
 __global__ __launch_bounds__(256) void g7_splitk_reduce(float* C, long long ldc, const float* ws, int M, int N,
-                                                       int s, int accumulate) {
+                                                       int s, int accumulate, int nt = 0) {
   const long long nq = (long long)M * (N >> 2);
   const long long slab = (long long)M * N;
   for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < nq; i += (long long)gridDim.x * 256) {
@@ -1073,7 +1074,7 @@ __global__ __launch_bounds__(256) void g7_splitk_reduce(float* C, long long ldc,
       const float4 o = *c;
       v.x += o.x; v.y += o.y; v.z += o.z; v.w += o.w;
     }
-    *c = v;
+    st16(c, v, nt);
   }
 }
 
@@ -1150,7 +1151,7 @@ __device__ __forceinline__ float g7_bf(unsigned w, int hi) {
 // (bl = the bias vector) instead of the tile's LDS copy.
 template <bool BIAS, bool CHECK = false>
 __device__ __forceinline__ void g7_split_store(bf16_t* dst, long long ld, floatx4 (&acc)[8][8], int mw, int nw,
-                                               int lane, float alpha, const float* bl, int M = 0, int N = 0) {
+                                               int lane, float alpha, const float* bl, bool nt, int M = 0, int N = 0) {
   const int g = lane >> 4, rl = lane & 15;
   const int coff = 16 * (g & 1) + 8 * (g >> 1);
   const bool lo = rl < 8;
@@ -1193,8 +1194,8 @@ __device__ __forceinline__ void g7_split_store(bf16_t* dst, long long ld, floatx
       const uint4 dB = make_uint4(lo ? rcv.x : c1.x, lo ? rcv.y : c1.y, lo ? rcv.z : c1.z, lo ? rcv.w : c1.w);
       const int m = mw + 16 * i + rr, n = nw + 16 * j + coff + 32 * hi8;
       bf16_t* C = dst + (long long)m * ld + n;
-      if (!CHECK || (n < N && m < M)) *reinterpret_cast<uint4*>(C) = dA;
-      if (!CHECK || (n < N && m + 8 < M)) *reinterpret_cast<uint4*>(C + 8 * ld) = dB;
+      if (!CHECK || (n < N && m < M)) st16(C, dA, nt);
+      if (!CHECK || (n < N && m + 8 < M)) st16(C + 8 * ld, dB, nt);
     }
   }
 }
@@ -1224,10 +1225,10 @@ __device__ __forceinline__ void g7d_finish(const GemmArgs& p, int mw, int nw, in
           const float* R = p.residual + (long long)m * p.ldr + n;
           const float4 r0 = *reinterpret_cast<const float4*>(R), r1 = *reinterpret_cast<const float4*>(R + 4);
           float* Cf = static_cast<float*>(p.C) + (long long)m * p.ldc + n;
-          *reinterpret_cast<float4*>(Cf) = make_float4(r0.x + g7_gelu(g7_bf(x.x, 0)), r0.y + g7_gelu(g7_bf(x.x, 1)),
-                                                       r0.z + g7_gelu(g7_bf(x.y, 0)), r0.w + g7_gelu(g7_bf(x.y, 1)));
-          *reinterpret_cast<float4*>(Cf + 4) = make_float4(r1.x + g7_gelu(g7_bf(x.z, 0)), r1.y + g7_gelu(g7_bf(x.z, 1)),
-                                                           r1.z + g7_gelu(g7_bf(x.w, 0)), r1.w + g7_gelu(g7_bf(x.w, 1)));
+          st16(Cf, make_float4(r0.x + g7_gelu(g7_bf(x.x, 0)), r0.y + g7_gelu(g7_bf(x.x, 1)),
+                               r0.z + g7_gelu(g7_bf(x.y, 0)), r0.w + g7_gelu(g7_bf(x.y, 1))), p.nt_store & 2);
+          st16(Cf + 4, make_float4(r1.x + g7_gelu(g7_bf(x.z, 0)), r1.y + g7_gelu(g7_bf(x.z, 1)),
+                                   r1.z + g7_gelu(g7_bf(x.w, 0)), r1.w + g7_gelu(g7_bf(x.w, 1))), p.nt_store & 2);
           continue;
         } else if constexpr (EPI == 5) {
           const uint4 x = *reinterpret_cast<const uint4*>(static_cast<const bf16_t*>(p.aux_out) + (long long)m * p.ld_aux_out + n);
@@ -1248,7 +1249,7 @@ __device__ __forceinline__ void g7d_finish(const GemmArgs& p, int mw, int nw, in
             g7_setcomp(o, q, pack2bf(y0, y1));
           }
         }
-        *reinterpret_cast<uint4*>(C) = o;
+        st16(C, o, p.nt_store & 1);
       }
     }
     if (EPI == 6 && p.colsum) {
@@ -1490,10 +1491,10 @@ __global__ __launch_bounds__(256, 1) void gemm7d_kernel(GemmArgs p, unsigned lon
         const long long e_ = (long long)(pm0 + ar + 16 * i_ + rr + 8 * h_) * p.ldc + pn0 + bc + 64 * jb_ + \
                              coff + 32 * hi8;                                                       \
         if constexpr (EPI == 7) {                                                                   \
-          *reinterpret_cast<float4*>(static_cast<float*>(p.C) + e_) = of0[k];                       \
-          *reinterpret_cast<float4*>(static_cast<float*>(p.C) + e_ + 4) = of1[k];                   \
+          st16(static_cast<float*>(p.C) + e_, of0[k], p.nt_store & 2);                               \
+          st16(static_cast<float*>(p.C) + e_ + 4, of1[k], p.nt_store & 2);                           \
         } else {                                                                                    \
-          *reinterpret_cast<uint4*>(static_cast<bf16_t*>(p.C) + e_) = uo[k];                        \
+          st16(static_cast<bf16_t*>(p.C) + e_, uo[k], p.nt_store & 1);                               \
         }                                                                                           \
       }                                                                                             \
       tail = EPI == 7 ? 2 * NU : NU;                                                                \
@@ -1560,10 +1561,10 @@ __global__ __launch_bounds__(256, 1) void gemm7d_kernel(GemmArgs p, unsigned lon
     }
     if (defer_me) {
       if constexpr (FWD) {
-        if (p.bias) g7_split_store<true>(static_cast<bf16_t*>(p.aux_out), p.ld_aux_out, acc, m0 + ar, n0 + bc, lane, alpha, bl + bc);
-        else g7_split_store<false>(static_cast<bf16_t*>(p.aux_out), p.ld_aux_out, acc, m0 + ar, n0 + bc, lane, alpha, bl);
+        if (p.bias) g7_split_store<true>(static_cast<bf16_t*>(p.aux_out), p.ld_aux_out, acc, m0 + ar, n0 + bc, lane, alpha, bl + bc, p.nt_store & 1);
+        else g7_split_store<false>(static_cast<bf16_t*>(p.aux_out), p.ld_aux_out, acc, m0 + ar, n0 + bc, lane, alpha, bl, p.nt_store & 1);
       } else {
-        g7_split_store<false>(static_cast<bf16_t*>(p.C), p.ldc, acc, m0 + ar, n0 + bc, lane, alpha, bl);
+        g7_split_store<false>(static_cast<bf16_t*>(p.C), p.ldc, acc, m0 + ar, n0 + bc, lane, alpha, bl, p.nt_store & 1);
       }
       post += 32;
       pend = 1;
@@ -1572,10 +1573,10 @@ __global__ __launch_bounds__(256, 1) void gemm7d_kernel(GemmArgs p, unsigned lon
     } else {
       // partial or last tile: the same two halves back to back
       if constexpr (FWD) {
-        if (p.bias) g7_split_store<true, true>(static_cast<bf16_t*>(p.aux_out), p.ld_aux_out, acc, m0 + ar, n0 + bc, lane, alpha, p.bias, p.M, p.N);
-        else g7_split_store<false, true>(static_cast<bf16_t*>(p.aux_out), p.ld_aux_out, acc, m0 + ar, n0 + bc, lane, alpha, p.bias, p.M, p.N);
+        if (p.bias) g7_split_store<true, true>(static_cast<bf16_t*>(p.aux_out), p.ld_aux_out, acc, m0 + ar, n0 + bc, lane, alpha, p.bias, p.nt_store & 1, p.M, p.N);
+        else g7_split_store<false, true>(static_cast<bf16_t*>(p.aux_out), p.ld_aux_out, acc, m0 + ar, n0 + bc, lane, alpha, p.bias, p.nt_store & 1, p.M, p.N);
       } else {
-        g7_split_store<false, true>(static_cast<bf16_t*>(p.C), p.ldc, acc, m0 + ar, n0 + bc, lane, alpha, bl, p.M, p.N);
+        g7_split_store<false, true>(static_cast<bf16_t*>(p.C), p.ldc, acc, m0 + ar, n0 + bc, lane, alpha, bl, p.nt_store & 1, p.M, p.N);
       }
       g7_wait<0>();
       g7d_finish<EPI>(p, m0 + ar, n0 + bc, lane);

@@ -215,9 +215,11 @@ __global__ __launch_bounds__(256, 1) void gemm9_kernel(GemmArgs p, unsigned long
       q.out_f32 = 1;
       g7_epilogue<0, NJ>(q, acc, m0 + ar, n0 + bc, lane, 0);
     } else {
-      g7_epilogue<0, NJ>(p, acc, m0 + ar, n0 + bc, lane, 0);
+      // (ABL 512: the epilogue's VALU without its stores; ABL 1024: non-temporal stores -- lab only)
+      g7_epilogue<0, NJ>(p, acc, m0 + ar, n0 + bc, lane, (ABL & 512) ? 4 : ((ABL & 1024) ? 16 : 0));
     }
     credit = (pl.store_cnt > 0 && m0 + 256 <= p.M && n0 + 256 <= p.N) ? 1 : 0;
+    if constexpr ((ABL & 2048) != 0) credit = 0;  // (lab: the next tile waits for the stores at once)
   }
 #undef G9_G0
 #undef G9_G1

@@ -37,6 +37,7 @@ import torch
 import torch.distributed as dist
 
 from . import comm
+from ..utils.profiling import mark
 
 
 # ---------------------------------------------------------------- stream-order checks
@@ -346,8 +347,6 @@ class NativeTransport(Transport):
         return True
 
     def _enqueue(self, fn, tensors, async_op, op="collective"):
-        from . import native_comm
-
         if _STREAM_CHECK:
             for t in tensors:
                 if not t.is_contiguous() or t.device != self.device:
@@ -361,6 +360,12 @@ class NativeTransport(Transport):
             # fingerprint would pair up wrongly: skipped, as TorchTransport.sendrecv does
             comm.fingerprint(op, tensors[0] if tensors else None, self.group)
         desc = _desc(op, tensors)
+        with mark(f"comm:{op}"):
+            return self._launch(fn, tensors, async_op, desc, capturing)
+
+    def _launch(self, fn, tensors, async_op, desc, capturing):
+        from . import native_comm
+
         s = self.stream
         if s is None:  # host-side fake library
             fn(0)

@@ -162,3 +162,34 @@ def test_pipeline_default_microbatches_divide_the_batch():
     assert f(SimpleNamespace(n_micro_req=0, pp=5), 36) == 18
     assert f(SimpleNamespace(n_micro_req=0, pp=1), 64) == 1
     assert f(SimpleNamespace(n_micro_req=6, pp=2), 36) == 6
+
+
+def test_phase_ranges_cover_every_engine(monkeypatch):
+    """roctx ranges around the step phases (fwd / bwd / optim, comm waits) in
+    every engine's eager step -- recorded here by replacing the range helper."""
+    import contextlib
+
+    from distributed_pytorch_cookbook_amd.engine import data_parallel, fsdp, pipeline
+    from distributed_pytorch_cookbook_amd.engine.data_parallel import DataParallelEngine
+    from distributed_pytorch_cookbook_amd.engine.fsdp import FSDPEngine
+    from distributed_pytorch_cookbook_amd.engine.pipeline import PipelineEngine
+
+    from dist_workers import full_batch, make_model
+
+    seen = []
+
+    @contextlib.contextmanager
+    def rec(name):
+        seen.append(name)
+        yield
+
+    for mod in (data_parallel, fsdp, pipeline):
+        monkeypatch.setattr(mod, "mark", rec)
+    for build in (lambda m: DataParallelEngine(m, "cpu", lr=1e-3),
+                  lambda m: FSDPEngine(m, "cpu", lr=1e-3),
+                  lambda m: PipelineEngine(m, "cpu", lr=1e-3, pp=1)):
+        seen.clear()
+        eng = build(make_model())
+        eng.train_step(*full_batch())
+        names = {n.split(" ")[0] for n in seen}
+        assert {"fwd", "bwd", "optim"} <= names, seen
