@@ -61,10 +61,10 @@ template <int ABL, bool AK, bool BK, int SCHED = 3>
 static void launch(const GemmArgs& a, G7Plan pl, unsigned long long ab, unsigned long long bb) {
   hipLaunchKernelGGL((gemm7_kernel<0, SCHED, AK, BK, 128, ABL>), dim3(pl.grid), dim3(256), 0, 0, a, ab, bb, pl);
 }
-template <int ABL, bool AK, bool BK>
+template <int ABL, bool AK, bool BK, int ER = 0>
 static void launch9(const GemmArgs& a, G7Plan pl, unsigned long long ab, unsigned long long bb) {
   pl.nk = a.K / 64;  // (v9: 64-deep stages)
-  hipLaunchKernelGGL((gemm9_kernel<0, AK, BK, ABL>), dim3(pl.grid), dim3(256), 0, 0, a, ab, bb, pl);
+  hipLaunchKernelGGL((gemm9_kernel<0, AK, BK, ABL, ER>), dim3(pl.grid), dim3(256), 0, 0, a, ab, bb, pl);
 }
 
 int main(int argc, char** argv) {
@@ -135,6 +135,15 @@ int main(int argc, char** argv) {
     vs.push_back({"no_read", [&] { launch<128 | 32, AK_, BK_>(a, pl, ab, bb); }, true, {}});              \
     vs.push_back({"no_read_no_dma", [&] { launch<128 | 32 | 2, AK_, BK_>(a, pl, ab, bb); }, true, {}});   \
     vs.push_back({"mfma_only", [&] { launch<128 | 32 | 16 | 2, AK_, BK_>(a, pl, ab, bb); }, true, {}});   \
+  } else if (set == "er") {                                                                              \
+    vs.push_back({"v9", [&] { launch9<1024, AK_, BK_>(a, pl, ab, bb); }, false, {}});                     \
+    vs.push_back({"v9_er2", [&] { launch9<1024, AK_, BK_, 2>(a, pl, ab, bb); }, false, {}});              \
+    vs.push_back({"v9_er4", [&] { launch9<1024, AK_, BK_, 4>(a, pl, ab, bb); }, false, {}});              \
+    vs.push_back({"v9_clk", [&] { launch9<128 | 1024, AK_, BK_>(a, pl, ab, bb); }, true, {}});            \
+    vs.push_back({"v9_er2_clk", [&] { launch9<128 | 1024, AK_, BK_, 2>(a, pl, ab, bb); }, true, {}});     \
+    vs.push_back({"v9_er4_clk", [&] { launch9<128 | 1024, AK_, BK_, 4>(a, pl, ab, bb); }, true, {}});     \
+    vs.push_back({"v9_er2_noepi", [&] { launch9<128, AK_, BK_, 2>(a, noepi, ab, bb); }, true, {}});       \
+    vs.push_back({"v9_noepi", [&] { launch9<128, AK_, BK_>(a, noepi, ab, bb); }, true, {}});              \
   } else if (set == "epi") {                                                                             \
     vs.push_back({"v9", [&] { launch9<0, AK_, BK_>(a, pl, ab, bb); }, false, {}});                        \
     vs.push_back({"v9_nt", [&] { launch9<1024, AK_, BK_>(a, pl, ab, bb); }, false, {}});                  \

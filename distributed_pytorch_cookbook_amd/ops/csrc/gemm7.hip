@@ -259,7 +259,15 @@ DPC_API int dpc_gemm7(const GemmArgs* a, int persistent, int sched, int splits, 
       G7Plan p9 = pl;
       p9.nk = a->K / 64;
       p9.nk_all = p9.nk;
-      hipLaunchKernelGGL((gemm9_kernel<0, true, true>), dim3(p9.grid), dim3(256), 0, stream, *a, ab, bb, p9);
+      // early-release schedule (gemm9_kern.h ER): DPC_G9_ER = 0 / 2 / 4
+      static int er_env = -1;
+      if (er_env < 0) er_env = getenv("DPC_G9_ER") ? atoi(getenv("DPC_G9_ER")) : 0;
+      if (er_env == 2)
+        hipLaunchKernelGGL((gemm9_kernel<0, true, true, 0, 2>), dim3(p9.grid), dim3(256), 0, stream, *a, ab, bb, p9);
+      else if (er_env == 4)
+        hipLaunchKernelGGL((gemm9_kernel<0, true, true, 0, 4>), dim3(p9.grid), dim3(256), 0, stream, *a, ab, bb, p9);
+      else
+        hipLaunchKernelGGL((gemm9_kernel<0, true, true>), dim3(p9.grid), dim3(256), 0, stream, *a, ab, bb, p9);
       return (int)hipGetLastError();
     }
     // weight gradients (both operands mn-major, split K through workspace slabs) on v9, with the

@@ -39,10 +39,23 @@ constexpr int G9_NL = G9_TA / 512 / 4;      // 1-KiB pieces per wave per operand
 // EPI 0: plain products; EPI 4: split-K partial tiles into the f32 workspace slab of their
 // k-range (as v7 EPI 4: unit = split * tiles + tile, pl.nk = stages per split, pl.nk_all =
 // stages of the whole product -- whole stages past it are issued with empty descriptors).
-template <int EPI, bool AK, bool BK, int ABL = 0>
+// ER (early release, 0 = the schedule above): phase 0 reads ALL of stage t's k-step-1 fragments
+// in its first ER groups (16 / ER reads per group, one per MFMA gap), then lgkmcnt(0) + an extra
+// barrier -- every wave is done with stage t's buffer -- and the DMA of stage t+2 starts right
+// there (pairs in phase 0 groups ER..7, the rest in phase 1), instead of in phase 1.  A stage's
+// pieces then have ~1.5-1.75 bodies (3,000-3,600 MFMA cycles) to land before the mid wait that
+// needs them, instead of 0.5-1 body: the round-4 lab had v9's main loop at ~70 % MFMA use with
+// the DMA the only large ablation (no-DMA +57 % on the QKV forward).
+//   RAW: unchanged (mid wait = this wave's stage t+1 pieces; the stage t+2 pieces issued in
+//        phase 0 -- 2 (8 - ER) loads -- may stay in flight).
+//   WAR: stage t+2 lands in buffer t % 2 only after the early barrier, which every wave enters
+//        after lgkmcnt(0) on its last read of stage t (k-step 0 was read in body t-1).
+template <int EPI, bool AK, bool BK, int ABL = 0, int ER = 0>
 __global__ __launch_bounds__(256, 1) void gemm9_kernel(GemmArgs p, unsigned long long a_bytes,
                                                        unsigned long long b_bytes, G7Plan pl) {
   static_assert(EPI == 0 || EPI == 4, "v9: plain products, split-K slabs");
+  static_assert(ER == 0 || ER == 2 || ER == 4, "v9: early release over 2 or 4 groups");
+  constexpr int P0 = ER ? 8 - ER : 0;  // DMA pairs of stage t+2 issued in phase 0
   constexpr int NJ = 8;
   __shared__ __attribute__((aligned(16))) bf16_t smem[2 * G9_SLOT];
 
@@ -176,6 +189,81 @@ __global__ __launch_bounds__(256, 1) void gemm9_kernel(GemmArgs p, unsigned long
     G9_SB; mf(i, 6, a1, b1, false); G9_SB;                                                          \
     mf(i, 7, a1, b1, false); G9_SB;                                                                 \
   } while (0)
+  // early-release phase 0: group i < ER reads 16 / ER fragments of k-step 1 (one per MFMA gap);
+  // groups ER..7 carry the DMA pairs 0 .. P0-1 of stage t+2
+#define G9_E0(i, FIRST)                                                                             \
+  do {                                                                                              \
+    if constexpr ((i) < ER) {                                                                       \
+      constexpr int NR = 16 / ER, R0 = (i) * NR;                                                    \
+      _Pragma("unroll") for (int j_ = 0; j_ < 8; ++j_) {                                            \
+        mf(i, j_, a0, b0, FIRST); G9_SB;                                                            \
+        if (j_ < NR && !(ABL & 32)) {                                                               \
+          const int r_ = R0 + j_;                                                                   \
+          if (r_ < 8) a1[r_ & 7] = frag3<G9_KB, AK>(lc, ar + 16 * (r_ & 7), 1, lane);               \
+          else b1[r_ & 7] = frag3<G9_KB, BK>(lc + G9_TA, bc + 16 * (r_ & 7), 1, lane);              \
+        }                                                                                           \
+        G9_SB;                                                                                      \
+      }                                                                                             \
+      if constexpr ((i) == ER - 1) {                                                                \
+        /* every wave done reading stage t: its buffer may take stage t+2 */                      \
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");                                          \
+        G9_SB;                                                                                      \
+        if (!(ABL & 16)) __builtin_amdgcn_s_barrier();                                              \
+        asm volatile("" ::: "memory");                                                              \
+      }                                                                                             \
+    } else {                                                                                        \
+      mf(i, 0, a0, b0, FIRST); G9_SB; mf(i, 1, a0, b0, FIRST); G9_SB;                               \
+      mf(i, 2, a0, b0, FIRST); G9_SB;                                                               \
+      dma((i) - ER, 0);                                                                             \
+      G9_SB; mf(i, 3, a0, b0, FIRST); G9_SB;                                                        \
+      dma((i) - ER, 1);                                                                             \
+      G9_SB; mf(i, 4, a0, b0, FIRST); G9_SB;                                                        \
+      dma((i) - ER, 2);                                                                             \
+      G9_SB; mf(i, 5, a0, b0, FIRST); G9_SB; mf(i, 6, a0, b0, FIRST); G9_SB;                        \
+      mf(i, 7, a0, b0, FIRST); G9_SB;                                                               \
+    }                                                                                               \
+  } while (0)
+  // early-release phase 1: group i reads stage t+1's k-step-0 fragments; groups 0 .. 7-P0 carry the
+  // remaining DMA pairs P0 .. 7, and the group after the last pair advances the cursor
+#define G9_E1(i)                                                                                    \
+  do {                                                                                              \
+    mf(i, 0, a1, b1, false); G9_SB;                                                                 \
+    if (!(ABL & 32)) a0[i] = frag3<G9_KB, AK>(ln, ar + 16 * i, 0, lane);                            \
+    G9_SB; mf(i, 1, a1, b1, false); G9_SB;                                                          \
+    if (!(ABL & 32)) b0[i] = frag3<G9_KB, BK>(ln + G9_TA, bc + 16 * i, 0, lane);                    \
+    G9_SB; mf(i, 2, a1, b1, false); G9_SB;                                                          \
+    if constexpr ((i) < 8 - P0) dma(P0 + (i), 0);                                                   \
+    G9_SB; mf(i, 3, a1, b1, false); G9_SB;                                                          \
+    if constexpr ((i) < 8 - P0) dma(P0 + (i), 1);                                                   \
+    G9_SB; mf(i, 4, a1, b1, false); G9_SB;                                                          \
+    if constexpr ((i) < 8 - P0) dma(P0 + (i), 2);                                                   \
+    if constexpr ((i) == 8 - P0) advance();                                                         \
+    G9_SB; mf(i, 5, a1, b1, false); G9_SB;                                                          \
+    if constexpr ((i) == 8 - P0) prep();                                                            \
+    G9_SB; mf(i, 6, a1, b1, false); G9_SB;                                                          \
+    mf(i, 7, a1, b1, false); G9_SB;                                                                 \
+  } while (0)
+#define G9_EBODY(FIRST, CREDIT)                                                                     \
+  do {                                                                                              \
+    const bf16_t* lc = smem + rd * G9_SLOT;                                                         \
+    const bf16_t* ln = smem + (rd ^ 1) * G9_SLOT;                                                   \
+    G9_E0(0, FIRST); G9_E0(1, FIRST); G9_E0(2, FIRST); G9_E0(3, FIRST);                             \
+    G9_E0(4, FIRST); G9_E0(5, FIRST); G9_E0(6, FIRST); G9_E0(7, FIRST);                             \
+    /* mid: stage t+1 landed (younger: the 2 P0 pieces of stage t+2 issued in phase 0, and in  */ \
+    /* a tile's first body the last epilogue's stores between the two)                         */ \
+    if (ABL & 64) {                                                                                 \
+    } else if ((CREDIT) && credit > 0) {                                                            \
+      if (pl.store_cnt >= 48) g7_wait<63>(); /* (the counter's limit: stage t+1 still done) */       \
+      else g7_wait<31 + 2 * P0>();                                                                  \
+    } else {                                                                                        \
+      g7_wait<2 * P0>();                                                                            \
+    }                                                                                               \
+    G9_SB;                                                                                          \
+    if (!(ABL & 16)) __builtin_amdgcn_s_barrier();                                                  \
+    asm volatile("" ::: "memory");                                                                  \
+    G9_E1(0); G9_E1(1); G9_E1(2); G9_E1(3); G9_E1(4); G9_E1(5); G9_E1(6); G9_E1(7);                 \
+    rd ^= 1;                                                                                        \
+  } while (0)
 #define G9_BODY(FIRST, CREDIT)                                                                      \
   do {                                                                                              \
     const bf16_t* lc = smem + rd * G9_SLOT;                                                         \
@@ -201,9 +289,15 @@ __global__ __launch_bounds__(256, 1) void gemm9_kernel(GemmArgs p, unsigned long
   } while (0)
 
   for (int u = 0; u < nmine; ++u) {
-    G9_BODY(true, true);
-    credit = 0;
-    for (int k = 1; k < pl.nk; ++k) G9_BODY(false, false);
+    if constexpr (ER != 0) {
+      G9_EBODY(true, true);
+      credit = 0;
+      for (int k = 1; k < pl.nk; ++k) G9_EBODY(false, false);
+    } else {
+      G9_BODY(true, true);
+      credit = 0;
+      for (int k = 1; k < pl.nk; ++k) G9_BODY(false, false);
+    }
     const int uu = local + u * pl.grid;
     int m0, n0;
     g7_tile(pl, uu % ntiles, m0, n0);
@@ -224,6 +318,9 @@ __global__ __launch_bounds__(256, 1) void gemm9_kernel(GemmArgs p, unsigned long
 #undef G9_G0
 #undef G9_G1
 #undef G9_BODY
+#undef G9_E0
+#undef G9_E1
+#undef G9_EBODY
 #undef G9_SB
   g7_wait<0>();  // the empty-descriptor DMA issued past the end drained before exit
   if constexpr ((ABL & 128) != 0) {

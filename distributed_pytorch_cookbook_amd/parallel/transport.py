@@ -118,6 +118,33 @@ def cu_reserve_active() -> bool:
     return _comm_inflight > 0
 
 
+# ---------------------------------------------------------------- fake collectives (one GPU)
+# DPC_FAKE_COLL="<cus>,<bus GB/s>,<world>" (e.g. "16,300,8"): every collective of a native
+# transport is followed, on its comm stream, by an occupier kernel of <cus> workgroups (32 KiB LDS
+# each, so a CU hosting one cannot also host a persistent GEMM workgroup) that stays resident
+# for the time the collective would take on <world> GPUs at <bus GB/s> bus bandwidth
+# (all-reduce 2 (W-1) / W x bytes, reduce-scatter / all-gather (W-1) / W x the full buffer).
+# Run at one rank (bench.py --force_dist_path), it reproduces the CU co-residency of the
+# multi-GPU step -- the same launch points, sizes and overlap -- on a one-GPU box, to set
+# DPC_CU_RESERVE from measurements (bench/cu_corun.sh).
+_FAKE_COLL = os.environ.get("DPC_FAKE_COLL", "")
+_fake_sink = None
+
+
+def _fake_coll(op: str, tensors, stream) -> None:
+    global _fake_sink
+    from ..ops import _lib
+
+    cus, busbw, world = (float(v) for v in _FAKE_COLL.split(","))
+    nbytes = max((t.numel() * t.element_size() for t in tensors), default=0)
+    factor = {"all_reduce": 2.0 * (world - 1) / world, "reduce_scatter": (world - 1) / world,
+              "all_gather": (world - 1) / world}.get(op, 1.0)
+    ns = int(factor * nbytes / (busbw * 1e9) * 1e9)
+    if _fake_sink is None:
+        _fake_sink = torch.zeros(4096, dtype=torch.int32, device=tensors[0].device)
+    _lib.occupy(int(cus), ns, _fake_sink, stream)
+
+
 def check_drained(where: str = "end of step") -> None:
     """Raise if a collective issued with ``async_op=True`` was never waited on."""
     if not _STREAM_CHECK:
@@ -375,6 +402,8 @@ class NativeTransport(Transport):
         s.wait_stream(cur)
         with torch.cuda.stream(s):
             fn(s)
+            if _FAKE_COLL and tensors:
+                _fake_coll(desc.split("(")[0].split(" ")[0], tensors, s)
         for t in tensors:
             t.record_stream(s)
         done = torch.cuda.Event()
