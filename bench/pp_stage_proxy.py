@@ -62,8 +62,10 @@ def main():
     if stage < 0:
         mids = [s for s in range(a.pp) if 0 not in groups[s] and model.num_layers + 1 not in groups[s]] or list(range(a.pp))
         stage = max(mids, key=lambda s: sum(costs[u] for u in groups[s]))
-    units = groups[stage]
-    layers = [model.decoder.layers[u - 1] for u in units if 1 <= u <= model.num_layers]
+    # the stage's decoder layers (a pp2 stage also holds the embeddings or the head: those stay
+    # unmaterialised, the proxy times the layers)
+    units = [u for u in groups[stage] if 1 <= u <= model.num_layers]
+    layers = [model.decoder.layers[u - 1] for u in units]
     # materialise only the stage's parameters (the others stay on the meta device)
     for li in layers:
         li.to_empty(device=dev)

@@ -220,6 +220,8 @@ def lib() -> ctypes.CDLL:
             handle.dpc_occupy.restype = c_int
             handle.dpc_attn_set_dkdv2.argtypes = [c_int]
             handle.dpc_attn_set_dkdv2.restype = None
+            handle.dpc_attn_set_dq2.argtypes = [c_int]
+            handle.dpc_attn_set_dq2.restype = None
             handle.dpc_embedding_bwd_ws.argtypes = [c_int, c_int]
             handle.dpc_embedding_bwd_ws.restype = ctypes.c_ulonglong
             _lib = handle
@@ -258,6 +260,12 @@ def set_attn_dkdv2(on: int) -> None:
     """1: the persistent pair-stream dK / dV kernel (default), 0: one launch per key block,
     -1: back to DPC_ATTN_DKDV2 / the default."""
     lib().dpc_attn_set_dkdv2(int(on))
+
+
+def set_attn_dq2(on: int) -> None:
+    """1: the persistent pair-stream dQ (+ delta) kernel, 0: one launch per query block,
+    -1: back to DPC_ATTN_DQ2 / the default."""
+    lib().dpc_attn_set_dq2(int(on))
 
 
 def get_cu_reserve() -> int:

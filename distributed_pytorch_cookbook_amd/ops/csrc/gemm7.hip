@@ -259,15 +259,34 @@ DPC_API int dpc_gemm7(const GemmArgs* a, int persistent, int sched, int splits, 
       G7Plan p9 = pl;
       p9.nk = a->K / 64;
       p9.nk_all = p9.nk;
-      // early-release schedule (gemm9_kern.h ER): DPC_G9_ER = 0 / 2 / 4
+      // early-release schedule (gemm9_kern.h ER): DPC_G9_ER = 0 / 2 / 4.  Default 4: same-box
+      // bench/g7lab +2..5 % on the GPT-2 nt products (QKV 1142 -> 1169-1200, up 1166 -> 1200,
+      // 8192^3 1494 -> 1546-1563 TF/s) and the DDP step 940.4K -> 945.9K tok/s over two
+      // interleaved runs each (profiles/r4_er/)
       static int er_env = -1;
-      if (er_env < 0) er_env = getenv("DPC_G9_ER") ? atoi(getenv("DPC_G9_ER")) : 0;
+      if (er_env < 0) er_env = getenv("DPC_G9_ER") ? atoi(getenv("DPC_G9_ER")) : 4;
       if (er_env == 2)
         hipLaunchKernelGGL((gemm9_kernel<0, true, true, 0, 2>), dim3(p9.grid), dim3(256), 0, stream, *a, ab, bb, p9);
       else if (er_env == 4)
         hipLaunchKernelGGL((gemm9_kernel<0, true, true, 0, 4>), dim3(p9.grid), dim3(256), 0, stream, *a, ab, bb, p9);
       else
         hipLaunchKernelGGL((gemm9_kernel<0, true, true>), dim3(p9.grid), dim3(256), 0, stream, *a, ab, bb, p9);
+      return (int)hipGetLastError();
+    }
+    // forward epilogues that read nothing per element (bias / activation / aux_out, no residual or
+    // accumulate: the FFN up-projection) on v9 when the table asks for it (impl 26) or
+    // DPC_G9_FWD=1: the 2 x 32 bf16 stores of a tile stay in flight into the next tile's stages
+    // instead of draining beside the MFMAs of a 256 x 128 two-per-CU kernel (impl 10)
+    static int g9f_env = -1;
+    if (g9f_env < 0) g9f_env = getenv("DPC_G9_FWD") ? atoi(getenv("DPC_G9_FWD")) : 0;
+    const bool g9_fwd = !plain && !a->residual && !a->accumulate && !a->act_bwd && !a->colsum && s == 1 && !v8 &&
+                        a->a_kmaj && a->b_kmaj && a->K % 64 == 0 && a->K >= 192 && a->lda >= 64 && a->ldb >= 64 &&
+                        (!a->aux_out || (a->ld_aux_out % 8 == 0 && ((uintptr_t)a->aux_out % 16) == 0));
+    if (g9_fwd && (sched == 7 || g9f_env)) {
+      G7Plan p9 = pl;
+      p9.nk = a->K / 64;
+      p9.nk_all = p9.nk;
+      hipLaunchKernelGGL((gemm9_kernel<1, true, true>), dim3(p9.grid), dim3(256), 0, stream, *a, ab, bb, p9);
       return (int)hipGetLastError();
     }
     // weight gradients (both operands mn-major, split K through workspace slabs) on v9, with the

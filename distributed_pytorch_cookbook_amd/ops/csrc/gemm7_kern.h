@@ -134,6 +134,19 @@ __device__ __forceinline__ void sfor(F&& f) {
 
 #define G7_AI __attribute__((always_inline))
 
+// alpha x *alpha_ptr through the scalar cache.  As a vector load (what the compiler emits for
+// the plain dereference) the value is waited for with vmcnt(0) at the top of every epilogue of
+// the persistent kernels, which drains the next tile's already issued operand stages each tile.
+__device__ __forceinline__ float g7_alpha(const GemmArgs& p) {
+  float a = p.alpha;
+  if (p.alpha_ptr) {
+    float v;
+    asm volatile("s_load_dword %0, %1, 0x0\n\ts_waitcnt lgkmcnt(0)" : "=s"(v) : "s"(p.alpha_ptr) : "memory");
+    a *= v;
+  }
+  return a;
+}
+
 #ifndef G7_EPI_PF
 #define G7_EPI_PF 0  // 0 = the default depth per epilogue (A/B builds override)
 #endif
@@ -145,11 +158,15 @@ __device__ __forceinline__ unsigned g7_ror8(unsigned v) {
 __device__ __forceinline__ float g7_ror8(float v) { return __uint_as_float(g7_ror8(__float_as_uint(v))); }
 
 // PK: GELU / GELU' in packed-f32 math (v8 with a K-major A, v7's forward epilogues)
-template <int MODE, int NJ, bool PK = false>
+// NOLD: MODE 1 known at compile time to read nothing per element (no residual / accumulate --
+// v9's forward epilogue): no operand prefetch registers
+// lbias (NOLD only): the wave's 128 bias values in LDS (v9 stages them by DMA with the tile's
+// operands) -- no vector load in the epilogue, so nothing there waits on vmcnt, which would
+// drain the next tile's operand stages already in flight
+template <int MODE, int NJ, bool PK = false, bool NOLD = false>
 __device__ __forceinline__ void g7_epilogue(const GemmArgs& p, floatx4 (&acc)[8][NJ], int mw, int nw, int lane,
-                                            int dbg = 0) {
-  float alpha = p.alpha;
-  if (p.alpha_ptr) alpha *= *p.alpha_ptr;
+                                            int dbg = 0, const float* lbias = nullptr) {
+  const float alpha = g7_alpha(p);
   const int g = lane >> 4, rl = lane & 15;
   // bf16 outputs leave in 16-B stores: after v_permlane16_swap of fragments (j, j+1) lane
   // group g holds columns 16 j + {0, 16, 8, 24}[g] .. +7 (host: N % 8 == 0, ldc % 8 == 0,
@@ -235,13 +252,14 @@ __device__ __forceinline__ void g7_epilogue(const GemmArgs& p, floatx4 (&acc)[8]
   // is refilled with (i + PF, j)
   const bf16_t* aux_in = static_cast<const bf16_t*>(p.aux_in);
   bf16_t* aux_out = static_cast<bf16_t*>(p.aux_out);
-  const float* fsrc = FWD ? (p.residual ? p.residual : (p.out_f32 && p.accumulate ? static_cast<const float*>(p.C) : nullptr))
+  const float* fsrc = (FWD && !NOLD)
+                          ? (p.residual ? p.residual : (p.out_f32 && p.accumulate ? static_cast<const float*>(p.C) : nullptr))
                           : nullptr;
   const long long ldf = p.residual ? p.ldr : p.ldc;
   const bool has_ld = FWD ? fsrc != nullptr : p.act_bwd != 0;
   auto load_one = [&](int m, int n) G7_AI {
     uint4 r = make_uint4(0u, 0u, 0u, 0u);
-    if (has_ld && m < p.M && n < p.N) {
+    if (!NOLD && has_ld && m < p.M && n < p.N) {
       if constexpr (FWD) {
         r = *reinterpret_cast<const uint4*>(fsrc + (long long)m * ldf + n);
       } else {
@@ -257,6 +275,9 @@ __device__ __forceinline__ void g7_epilogue(const GemmArgs& p, floatx4 (&acc)[8]
   constexpr int PF = G7_EPI_PF > 0 ? G7_EPI_PF : (FWD || NJ > 4 ? 1 : 2);  // (v8; 3 - 4 spill there)
   uint4 ld[PF][NJ];
   float4 bias4[NJ];
+  // (NOLD: the lane's bias column base as an LDS address)
+  const float __attribute__((address_space(3)))* lb =
+      (const float __attribute__((address_space(3)))*)(lds_void_t)(lbias) + 4 * g;
   float cs[NJ][4];
   sfor<NJ>([&](auto J) G7_AI {
     constexpr int j = decltype(J)::value;
@@ -264,10 +285,13 @@ __device__ __forceinline__ void g7_epilogue(const GemmArgs& p, floatx4 (&acc)[8]
       constexpr int q = decltype(Q)::value;
       ld[q][j] = load_one(mw + 16 * q + rl, nw + 16 * j + 4 * g);
     });
-    if constexpr (FWD) {
+    if constexpr (FWD && NOLD) {
+      const floatx4 b = *reinterpret_cast<const floatx4 __attribute__((address_space(3)))*>(lb + 16 * j);
+      bias4[j] = make_float4(b[0], b[1], b[2], b[3]);
+    } else if constexpr (FWD) {
       const int n = nw + 16 * j + 4 * g;
       bias4[j] = (p.bias && n < p.N) ? *reinterpret_cast<const float4*>(p.bias + n) : make_float4(0.f, 0.f, 0.f, 0.f);
-    } else {
+    } else if constexpr (!FWD) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) cs[j][r] = 0.f;
     }
@@ -323,7 +347,7 @@ __device__ __forceinline__ void g7_epilogue(const GemmArgs& p, floatx4 (&acc)[8]
         if (p.out_f32) {
           if (ok) {
             float4* C = reinterpret_cast<float4*>(static_cast<float*>(p.C) + (long long)m * p.ldc + n);
-            if (FWD && p.accumulate && p.residual) {  // (no caller does both; C read late)
+            if (FWD && !NOLD && p.accumulate && p.residual) {  // (no caller does both; C read late)
               const float4 o = *C;
               w[0] += o.x; w[1] += o.y; w[2] += o.z; w[3] += o.w;
             }
@@ -400,8 +424,7 @@ __device__ __forceinline__ void g7_epilogue_act_lds(const GemmArgs& p, floatx4 (
   // hoisted out of the persistent tile loop they would stay live across the main loop (spills)
   int lane;
   asm volatile("v_mov_b32 %0, %1" : "=v"(lane) : "v"(lane_in));
-  float alpha = p.alpha;
-  if (p.alpha_ptr) alpha *= *p.alpha_ptr;
+  const float alpha = g7_alpha(p);
   const int g = lane >> 4, rl = lane & 15;
   const int wr = wid >> 1, wc = wid & 1;
   const int mw = m0 + wr * 128, nw = n0 + wc * 128;
@@ -564,8 +587,7 @@ __device__ __forceinline__ void g7_epilogue_res_lds(const GemmArgs& p, floatx4 (
   static_assert(NJ == 8, "v7 tiles");
   int lane;  // (opaque: tile-invariant per-lane addresses must not be hoisted out of the tile loop)
   asm volatile("v_mov_b32 %0, %1" : "=v"(lane) : "v"(lane_in));
-  float alpha = p.alpha;
-  if (p.alpha_ptr) alpha *= *p.alpha_ptr;
+  const float alpha = g7_alpha(p);
   const int g = lane >> 4, rl = lane & 15;
   const int wr = wid >> 1, wc = wid & 1;
   const int mw = m0 + wr * 128, nw = n0 + wc * 128;
@@ -698,8 +720,7 @@ __device__ __forceinline__ void g7_epilogue_res_lds(const GemmArgs& p, floatx4 (
 // four rows x 64 contiguous bytes.  The host zeroes C first unless the product accumulates.
 __device__ __forceinline__ void g7_epilogue_atomic(const GemmArgs& p, floatx4 (&acc)[8][8], int mw, int nw,
                                                    int lane) {
-  float alpha = p.alpha;
-  if (p.alpha_ptr) alpha *= *p.alpha_ptr;
+  const float alpha = g7_alpha(p);
   float* C = static_cast<float*>(p.C);
   const int g = lane >> 4, cl = lane & 15;
 #pragma unroll
@@ -1396,8 +1417,7 @@ __global__ __launch_bounds__(256, 1) void gemm7d_kernel(GemmArgs p, unsigned lon
   float yev[2], cs[8];
 #pragma unroll
   for (int v = 0; v < 8; ++v) cs[v] = 0.f;
-  float alpha = p.alpha;
-  if (p.alpha_ptr) alpha *= *p.alpha_ptr;
+  const float alpha = g7_alpha(p);
   const float* bl = reinterpret_cast<const float*>(smem + BOFF);
   auto ureg = [&](int r, int k, int q) G7_AI { return smem + UOFF + ((r * 4 + wid) * MAXU * DPU + k * DPU + q) * 512; };
   auto ugeo = [&](int u, long long ld) G7_AI {  // uniform byte offset of unit u in the tile

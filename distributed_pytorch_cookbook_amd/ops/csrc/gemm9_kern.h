@@ -24,8 +24,9 @@
 //        read of stage t (k-step 0 in phase 1 of body t-1, k-step 1 in phase 0 of body t) is
 //        older than that barrier, and each wave waits lgkmcnt(0) before entering it (the k-step-1
 //        fragments are consumed only after it, so the compiler's own waits would come too late).
-// Epilogue: v7's MODE 0 (plain bf16 / f32 products); the stores of a full tile may stay in
-// flight through the next tile's first mid wait (stage 1 was issued before them).
+// Epilogue: v7's MODE 0 (plain bf16 / f32 products) or MODE 1 without per-element reads (the
+// up-projection forward: bias + GELU + the pre-activation aux_out); the stores of a full tile may
+// stay in flight through the next tile's first mid wait (stage 1 was issued before them).
 #pragma once
 #include "gemm7_kern.h"
 
@@ -39,7 +40,7 @@ constexpr int G9_NL = G9_TA / 512 / 4;      // 1-KiB pieces per wave per operand
 // EPI 0: plain products; EPI 4: split-K partial tiles into the f32 workspace slab of their
 // k-range (as v7 EPI 4: unit = split * tiles + tile, pl.nk = stages per split, pl.nk_all =
 // stages of the whole product -- whole stages past it are issued with empty descriptors).
-// ER (early release, 0 = the schedule above): phase 0 reads ALL of stage t's k-step-1 fragments
+// ER (early release, 0 = the schedule above; the plain products default to 4): phase 0 reads ALL of stage t's k-step-1 fragments
 // in its first ER groups (16 / ER reads per group, one per MFMA gap), then lgkmcnt(0) + an extra
 // barrier -- every wave is done with stage t's buffer -- and the DMA of stage t+2 starts right
 // there (pairs in phase 0 groups ER..7, the rest in phase 1), instead of in phase 1.  A stage's
@@ -53,11 +54,15 @@ constexpr int G9_NL = G9_TA / 512 / 4;      // 1-KiB pieces per wave per operand
 template <int EPI, bool AK, bool BK, int ABL = 0, int ER = 0>
 __global__ __launch_bounds__(256, 1) void gemm9_kernel(GemmArgs p, unsigned long long a_bytes,
                                                        unsigned long long b_bytes, G7Plan pl) {
-  static_assert(EPI == 0 || EPI == 4, "v9: plain products, split-K slabs");
+  static_assert(EPI == 0 || EPI == 1 || EPI == 4, "v9: plain products, load-free forward epilogues, split-K slabs");
   static_assert(ER == 0 || ER == 2 || ER == 4, "v9: early release over 2 or 4 groups");
   constexpr int P0 = ER ? 8 - ER : 0;  // DMA pairs of stage t+2 issued in phase 0
   constexpr int NJ = 8;
   __shared__ __attribute__((aligned(16))) bf16_t smem[2 * G9_SLOT];
+  // EPI 1: the bias of a tile's 256 columns per wave, by unit parity -- DMA'd when the issue
+  // cursor enters the unit (two units ahead of its epilogue: the host requires >= 3 stages per
+  // unit so that unit u+2's copy lands after unit u's epilogue read the same buffer)
+  __shared__ __attribute__((aligned(16))) float sbias[EPI == 1 ? 2 * 4 * 256 : 4];
 
   const int lane = threadIdx.x & 63;
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -84,6 +89,18 @@ __global__ __launch_bounds__(256, 1) void gemm9_kernel(GemmArgs p, unsigned long
   int is_u = 0, is_k = 0, is_buf = 0, is_kt0 = 0;
   unsigned long long is_aoff = 0, is_boff = 0;
   const int ntiles = pl.tiles_m * pl.tiles_n;
+  // the bias copy of unit ui: one 1-KiB piece per wave (columns past N read as zeros); issued
+  // between operand pieces, it only adds a younger op to the counted waits before it
+  auto bias_dma = [&](int ui, int n0) G7_AI {
+    if constexpr (EPI == 1) {
+      // (no bias: an empty descriptor, the copy reads zeros -- the epilogue adds without a branch)
+      const long long rem = p.bias ? (long long)(p.N - n0) * 4 : 0;
+      const unsigned nb = rem <= 0 ? 0u : (rem > 1024 ? 1024u : (unsigned)rem);
+      const auto rs = __builtin_amdgcn_make_buffer_rsrc((void*)(p.bias + n0), 0, nb, 0x00020000);
+      g7_m0(reinterpret_cast<const bf16_t*>(sbias + ((ui & 1) * 4 + wid) * 256));
+      g7_ld<0>(rs, lane * 16);
+    }
+  };
   auto set_org = [&](int ui) {
     const int uu = local + ui * pl.grid;
     const int sp = uu / ntiles;
@@ -92,6 +109,7 @@ __global__ __launch_bounds__(256, 1) void gemm9_kernel(GemmArgs p, unsigned long
     is_kt0 = sp * pl.nk;
     is_aoff = (AK ? (unsigned long long)m0 * p.lda * 2 : (unsigned long long)m0 * 2) + a_step * is_kt0;
     is_boff = (BK ? (unsigned long long)n0 * p.ldb * 2 : (unsigned long long)n0 * 2) + b_step * is_kt0;
+    bias_dma(ui, n0);
   };
   set_org(0);
   __amdgpu_buffer_rsrc_t rsa, rsb;
@@ -174,9 +192,9 @@ __global__ __launch_bounds__(256, 1) void gemm9_kernel(GemmArgs p, unsigned long
 #define G9_G1(i)                                                                                    \
   do {                                                                                              \
     mf(i, 0, a1, b1, false); G9_SB;                                                                 \
-    if (!(ABL & 32)) a0[i] = frag3<G9_KB, AK>(ln, ar + 16 * i, 0, lane);                            \
+    if (!(ABL & 32) && !LASTB) a0[i] = frag3<G9_KB, AK>(ln, ar + 16 * i, 0, lane);                  \
     G9_SB; mf(i, 1, a1, b1, false); G9_SB;                                                          \
-    if (!(ABL & 32)) b0[i] = frag3<G9_KB, BK>(ln + G9_TA, bc + 16 * i, 0, lane);                    \
+    if (!(ABL & 32) && !LASTB) b0[i] = frag3<G9_KB, BK>(ln + G9_TA, bc + 16 * i, 0, lane);          \
     G9_SB; mf(i, 2, a1, b1, false); G9_SB;                                                          \
     dma(i, 0);                                                                                      \
     G9_SB; mf(i, 3, a1, b1, false); G9_SB;                                                          \
@@ -264,8 +282,9 @@ __global__ __launch_bounds__(256, 1) void gemm9_kernel(GemmArgs p, unsigned long
     G9_E1(0); G9_E1(1); G9_E1(2); G9_E1(3); G9_E1(4); G9_E1(5); G9_E1(6); G9_E1(7);                 \
     rd ^= 1;                                                                                        \
   } while (0)
-#define G9_BODY(FIRST, CREDIT)                                                                      \
+#define G9_BODY(FIRST, CREDIT, LASTB_)                                                              \
   do {                                                                                              \
+    constexpr bool LASTB = (LASTB_);                                                                \
     const bf16_t* lc = smem + rd * G9_SLOT;                                                         \
     const bf16_t* ln = smem + (rd ^ 1) * G9_SLOT;                                                   \
     G9_G0(0, FIRST); G9_G0(1, FIRST); G9_G0(2, FIRST); G9_G0(3, FIRST);                             \
@@ -294,9 +313,20 @@ __global__ __launch_bounds__(256, 1) void gemm9_kernel(GemmArgs p, unsigned long
       credit = 0;
       for (int k = 1; k < pl.nk; ++k) G9_EBODY(false, false);
     } else {
-      G9_BODY(true, true);
-      credit = 0;
-      for (int k = 1; k < pl.nk; ++k) G9_BODY(false, false);
+      if constexpr (EPI == 1) {
+        // the unit's last body reads no k-step-0 fragments of the next unit: those 64 registers
+        // stay free through the epilogue (its bias and GELU temporaries would spill otherwise,
+        // and a spill reload there is waited for with vmcnt(0) -- behind the stores); they are
+        // read after it (the host guarantees nk >= 3)
+        G9_BODY(true, true, false);
+        credit = 0;
+        for (int k = 1; k < pl.nk - 1; ++k) G9_BODY(false, false, false);
+        G9_BODY(false, false, true);
+      } else {
+        G9_BODY(true, true, false);
+        credit = 0;
+        for (int k = 1; k < pl.nk; ++k) G9_BODY(false, false, false);
+      }
     }
     const int uu = local + u * pl.grid;
     int m0, n0;
@@ -308,11 +338,32 @@ __global__ __launch_bounds__(256, 1) void gemm9_kernel(GemmArgs p, unsigned long
       q.ldc = p.N;
       q.out_f32 = 1;
       g7_epilogue<0, NJ>(q, acc, m0 + ar, n0 + bc, lane, 0);
+    } else if constexpr (EPI == 1) {
+      // forward epilogue that reads nothing per element (bias, activation, the pre-activation
+      // aux_out; no residual / accumulate): its 32 + 32 stores stay in flight into the next tile
+      // (the lane index recomputed by an opaque mbcnt: the epilogue's per-lane offsets are derived
+      // here, not hoisted out of the unit loop into registers the main loop would have to carry)
+      int elane;
+      asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(elane));
+      g7_epilogue<1, NJ, true, true>(p, acc, m0 + ar, n0 + bc, elane, 0, sbias + ((u & 1) * 4 + wid) * 256 + bc);
     } else {
       // (ABL 512: the epilogue's VALU without its stores; ABL 1024: non-temporal stores -- lab only)
       g7_epilogue<0, NJ>(p, acc, m0 + ar, n0 + bc, lane, (ABL & 512) ? 4 : ((ABL & 1024) ? 16 : 0));
     }
     credit = (pl.store_cnt > 0 && m0 + 256 <= p.M && n0 + 256 <= p.N) ? 1 : 0;
+    if constexpr (EPI == 1) {
+      if (u + 1 < nmine) {  // the next unit's stage 0 (buffer rd, retired by the last mid wait)
+        // (lane offsets from an opaque mbcnt again: a value kept from before the stores would be
+        // a spill reload here, waited for with vmcnt(0) behind all of them)
+        int flane;
+        asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(flane));
+        const bf16_t* lc = smem + rd * G9_SLOT;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) a0[i] = frag3<G9_KB, AK>(lc, ar + 16 * i, 0, flane);
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) b0[j] = frag3<G9_KB, BK>(lc + G9_TA, bc + 16 * j, 0, flane);
+      }
+    }
     if constexpr ((ABL & 2048) != 0) credit = 0;  // (lab: the next tile waits for the stores at once)
   }
 #undef G9_G0

@@ -2,6 +2,15 @@
 # GPU tests, GEMM table re-timing with nt stores (+ the chosen v9 schedule), recipe A/B old vs new
 # table, attention PMC counters
 [ -n "$ER" ] && export DPC_G9_ER=$ER
+scripts/gpu_step.sh "300:warm:python -u scripts/warm.py" "200:attn_tests_b:python -u -m pytest tests/test_kernels_gpu.py -x -q -k attention --timeout 120 --timeout-method thread" || exit $?
+for i in 1 2; do
+  scripts/gpu_step.sh "60:ab_bwd_00_$i:DPC_ATTN_DQ2=0 DPC_ATTN_DKDV2=0 python -u bench/attn_one.py --N 64 --S 1023 --H 12 --iters 20 --bwd" \
+    "60:ab_bwd_10_$i:DPC_ATTN_DQ2=1 DPC_ATTN_DKDV2=0 python -u bench/attn_one.py --N 64 --S 1023 --H 12 --iters 20 --bwd" \
+    "60:ab_bwd_11_$i:DPC_ATTN_DQ2=1 DPC_ATTN_DKDV2=1 python -u bench/attn_one.py --N 64 --S 1023 --H 12 --iters 20 --bwd" || exit $?
+done
+DPC_ATTN_DQ2=1 DPC_ATTN_DKDV2=1 timeout -k 10 120 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_dq2 -o run -- python -u bench/attn_one.py --N 64 --S 1023 --H 12 --iters 10 --bwd > gpurun_out/prof_dq2.log 2>&1 || exit $?
+[ -n "$DQ2" ] && export DPC_ATTN_DQ2=$DQ2
+[ -n "$DKDV2" ] && export DPC_ATTN_DKDV2=$DKDV2
 scripts/gpu_step.sh "500:gputests:python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread" || exit $?
 scripts/gpu_step.sh "900:retune:python -u bench/retune_keys.py --match . --impls 0 2 3 4 10 12 16 19 20 21 22 23 24 25 26 --write gpurun_out/gemm_tuned_r4.json" || exit $?
 for i in 1 2; do

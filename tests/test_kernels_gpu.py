@@ -163,6 +163,34 @@ def test_gemm_v7_v8_v9(impl, a_kmaj, b_kmaj, M, N, K):
     assert rel_err(og, og_r) < 1e-2
 
 
+@pytest.mark.parametrize("M,N,K", [(1023, 768, 768), (16384, 3072, 192), (3000, 2312, 320)])
+@pytest.mark.parametrize("with_bias", [True, False])
+@pytest.mark.parametrize("act", [0, 1, 2])
+@pytest.mark.parametrize("out_f32", [False, True])
+def test_gemm_v9_forward_epilogue(M, N, K, with_bias, act, out_f32):
+    """v9's load-free forward epilogue (gemm9_kern.h EPI 1: bias staged into LDS by the operand
+    DMA stream, activation, the pre-activation aux_out, 64 stores in flight into the next unit),
+    forced by impl 26 on nt products: ragged M and N, 768 tiles at K = 192 (three units per
+    persistent workgroup: the bias buffers of unit parity are reused), against f32 PyTorch."""
+    torch.manual_seed(5)
+    a = torch.randn(M, K, device=dev).bfloat16()
+    b = torch.randn(N, K, device=dev).bfloat16()
+    A, B = _store(a, True), _store(b, True)
+    bias = torch.randn(N, device=dev) if with_bias else None
+    aux = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+    _lib.set_gemm_impl(26)
+    try:
+        out = gemm(A, B, bias=bias, act=act, aux_out=aux, out_dtype=torch.float32 if out_f32 else torch.bfloat16)
+    finally:
+        _lib.set_gemm_impl(-1)
+    ref = torch.empty(M, N, device=dev)
+    aux_r = torch.empty_like(aux)
+    _gemm_ref(a, b, True, True, ref, bias, act, 0, None, aux_r, None, 1.0, None, False)
+    assert rel_err(out, ref) < (2e-3 if out_f32 else 1e-2)
+    assert rel_err(aux, aux_r) < 1e-2
+    assert _lib.is_loaded()
+
+
 @pytest.mark.parametrize("act_lds", [0, 1])
 @pytest.mark.parametrize("use_ws", [False, True])
 @pytest.mark.parametrize("a_kmaj,b_kmaj", [(True, False), (True, True), (False, False)])
@@ -756,9 +784,10 @@ def test_gemv_few_rows(M, Nw, N, K, epi):
 @pytest.mark.parametrize("S,N,H,causal,with_pad", [(1023, 16, 12, True, False), (1000, 3, 5, True, True),
                                                    (257, 2, 3, True, False), (200, 3, 5, False, True),
                                                    (64, 2, 2, True, False), (129, 4, 7, False, False)])
-def test_attention_dkdv_pair_stream_matches_per_block(S, N, H, causal, with_pad, hd):
-    """attn_bwd_dkdv2_kernel (one persistent LDS-DMA stream of key-block pairs per workgroup) does
-    the per-block kernel's arithmetic in the same order: dK / dV bitwise equal, dQ untouched --
+def test_attention_bwd_pair_streams_match_per_block(S, N, H, causal, with_pad, hd):
+    """attn_bwd_dkdv2_kernel / attn_bwd_dq2_kernel (one persistent LDS-DMA stream of block pairs
+    per workgroup) do the per-block kernels' arithmetic in the same order: dQ / dK / dV bitwise
+    equal in every combination --
     on ragged S (rows past S dropped by the buffer stores), odd block counts (a block paired with
     itself), key padding, the non-causal form, and more items than workgroups (16 x 12 x 4 = 768
     items on a 512-workgroup grid)."""
@@ -773,11 +802,14 @@ def test_attention_dkdv_pair_stream_matches_per_block(S, N, H, causal, with_pad,
     o, lse = attention_fwd(qkv, N, S, H, hd, pad, causal=causal)
     do = torch.randn(T, H * hd, device=dev).bfloat16()
     outs = []
-    for on in (0, 1):
-        _lib.set_attn_dkdv2(on)
+    for dq2, dkdv2 in ((0, 0), (0, 1), (1, 0), (1, 1)):
+        _lib.set_attn_dkdv2(dkdv2)
+        _lib.set_attn_dq2(dq2)
         try:
             outs.append(attention_bwd(do, qkv, o, lse, N, S, H, hd, pad, causal=causal).clone())
         finally:
             _lib.set_attn_dkdv2(-1)
-    assert torch.equal(outs[0], outs[1]), (outs[0].float() - outs[1].float()).abs().max().item()
+            _lib.set_attn_dq2(-1)
+    for k in range(1, 4):
+        assert torch.equal(outs[0], outs[k]), (k, (outs[0].float() - outs[k].float()).abs().max().item())
     assert _lib.is_loaded()
