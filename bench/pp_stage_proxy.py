@@ -46,6 +46,8 @@ def main():
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--graph", action="store_true", help="also time the step as a replayed HIP graph")
+    ap.add_argument("--only", default="both", choices=["both", "micro", "full"],
+                    help="run one of the two steps (a kernel profile of each on its own)")
     ap.add_argument("--json", default=None)
     a = ap.parse_args()
     dev = torch.device("cuda" if torch.cuda.is_available() else "cpu")
@@ -124,17 +126,20 @@ def main():
     out = {"model": a.model, "pp": a.pp, "stage": stage, "units": units, "layers": len(layers),
            "micro": a.micro, "mb": a.mb, "full": a.full, "wire": a.wire,
            "boundary_mb_per_micro": round(a.mb * (S - 1) * D * (4 if a.wire == "fp32" else 2) / 2**20, 1)}
-    body_m, tok_m = make_step(a.micro, a.mb)
-    body_f, tok_f = make_step(1, a.full)
-    for name, body, tok in (("micro", body_m, tok_m), ("full", body_f, tok_f)):
+    steps = []
+    if a.only in ("both", "micro"):
+        steps.append(("micro",) + make_step(a.micro, a.mb))
+    if a.only in ("both", "full"):
+        steps.append(("full",) + make_step(1, a.full))
+    for name, body, tok in steps:
         for graph in ([False, True] if a.graph else [False]):
             dt = timed(body, graph)
             key = f"{name}_{'graph' if graph else 'eager'}"
             out[key + "_ms"] = round(dt * 1e3, 3)
             out[key + "_us_per_ktok"] = round(dt * 1e6 / tok * 1000, 3)
-    ref = out["full_eager_us_per_ktok"]
+    ref = out.get("full_eager_us_per_ktok")
     for k in list(out):
-        if k.endswith("_us_per_ktok") and k != "full_eager_us_per_ktok":
+        if ref and k.endswith("_us_per_ktok") and k != "full_eager_us_per_ktok":
             out[k.replace("_us_per_ktok", "_vs_full")] = round(out[k] / ref, 3)
     line = json.dumps(out)
     print(line, flush=True)

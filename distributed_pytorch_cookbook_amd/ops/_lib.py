@@ -218,10 +218,6 @@ def lib() -> ctypes.CDLL:
             handle.dpc_get_cu_reserve.restype = c_int
             handle.dpc_occupy.argtypes = [c_int, ctypes.c_longlong, c_void_p, c_void_p]
             handle.dpc_occupy.restype = c_int
-            handle.dpc_attn_set_dkdv2.argtypes = [c_int]
-            handle.dpc_attn_set_dkdv2.restype = None
-            handle.dpc_attn_set_dq2.argtypes = [c_int]
-            handle.dpc_attn_set_dq2.restype = None
             handle.dpc_embedding_bwd_ws.argtypes = [c_int, c_int]
             handle.dpc_embedding_bwd_ws.restype = ctypes.c_ulonglong
             _lib = handle
@@ -254,18 +250,6 @@ def set_cu_reserve(r: int) -> None:
     """CUs the persistent GEMMs (v7 / v8) leave free for a kernel resident beside them -- an
     RCCL collective in flight on the comm stream (``parallel/transport.py`` drives it)."""
     lib().dpc_set_cu_reserve(int(r))
-
-
-def set_attn_dkdv2(on: int) -> None:
-    """1: the persistent pair-stream dK / dV kernel (default), 0: one launch per key block,
-    -1: back to DPC_ATTN_DKDV2 / the default."""
-    lib().dpc_attn_set_dkdv2(int(on))
-
-
-def set_attn_dq2(on: int) -> None:
-    """1: the persistent pair-stream dQ (+ delta) kernel, 0: one launch per query block,
-    -1: back to DPC_ATTN_DQ2 / the default."""
-    lib().dpc_attn_set_dq2(int(on))
 
 
 def get_cu_reserve() -> int:

@@ -965,506 +965,6 @@ __global__ __launch_bounds__(256, OCC) void attn_bwd_dkdv_kernel(AttnArgs p) {
   }
 }
 
-// dK, dV as ONE persistent stream per workgroup (the pair stream of attn_fwd2_kernel applied to
-// the backward).  attn_bwd_dkdv_kernel pays a prologue (K / V rows, ring fill) and an epilogue
-// (dK / dV stores) per 128-key block that nothing overlaps -- the lab measured 131 of its 420 us
-// with the tile loop removed (profiles/r3_attn/bwd_ablation_lab.log).  Here a workgroup runs
-// items of two key blocks of one (batch, head), the heaviest and the lightest left under the
-// causal mask (blocks pr and nkb-1-pr: equal query-tile counts), and every block is a run of
-// ring elements in ONE LDS-DMA stream: its K rows (element 0: rows 0-63 | 64-127 of the block),
-// its V rows (element 1), then its query tiles (Q | dO, + the lse / delta rows by wave 0).  So
-// the next block's K / V rows and first tiles land while the current block finishes, and its
-// dK / dV stores drain under the next block's work.  A persistent grid (two workgroups per CU)
-// walks the items; an XCD's workgroups hold a contiguous run of item ids (same heads: Q / dO
-// tiles shared in its L2).
-//   Counting: every element is 2 NPW pieces per wave (+ 2 row DMAs on wave 0, empty for K / V
-//   elements), so a step waits for element e with the two younger elements in flight; the
-//   step after a block end also leaves the 4 NDT dK / dV stores in flight -- buffer stores
-//   against a descriptor that ends at row S, so every wave issues all of them whatever S is
-//   (rows past S are dropped by the hardware) and the count is exact.
-//   WAR: element e's slot takes element e+4, issued after the barrier of step e+1; the K / V
-//   fragment reads of steps 0 / 1 complete (lgkmcnt(0)) before that barrier, the tile reads
-//   are consumed by MFMAs inside their step.
-template <int HD, int OCC>
-__global__ __launch_bounds__(256, OCC) void attn_bwd_dkdv2_kernel(AttnArgs p, int nitems) {
-  using A = AT<HD>;
-  __shared__ __attribute__((aligned(16))) bf16_t smem[NSLOT * 2 * A::TILE];  // [slot][Q|dO] / [K lo|hi]
-  __shared__ __attribute__((aligned(16))) float srow[NSLOT][2][KT];          // [slot][lse|delta]
-  const int S = p.S, H = p.H;
-  const int nkb = (S + QB - 1) / QB;
-  const int npr = (nkb + 1) / 2;
-  const int nqt = (S + KT - 1) / KT;
-  const int grid = gridDim.x;
-  const int local = g7_local_attn(blockIdx.x, grid);
-  const int lane = threadIdx.x & 63, hh = lane >> 5;
-  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  constexpr int NSTORE = 4 * A::NDT;  // dK + dV 16-B stores per lane at a block end
-  auto qt_begin = [&](int kb) { return p.causal ? (kb * QB) / KT : 0; };
-  auto blen = [&](int kb) { return 2 + nqt - qt_begin(kb); };  // elements of a block
-  auto item = [&](int k) {
-    PairItem it;
-    const int id = local + k * grid;
-    it.bh = id / npr;
-    const int pr = id - it.bh * npr;
-    it.blk0 = pr;            // most query tiles under the causal mask
-    it.blk1 = nkb - 1 - pr;  // fewest
-    it.len0 = blen(it.blk0);
-    it.len = it.len0 + (it.blk1 != it.blk0 ? blen(it.blk1) : 0);
-    return it;
-  };
-  const int nmine = local < nitems ? (nitems - local + grid - 1) / grid : 0;
-  if (nmine == 0) return;
-  int total = 0;
-  for (int k = 0; k < nmine; ++k) total += item(k).len;
-
-  int vq[A::NPW], vd[A::NPW];
-  dma_voff<HD>(vq, p.ld_qkv, wid, lane);
-  dma_voff<HD>(vd, p.ld_o, wid, lane);
-  // ---- issue cursor
-  int is_k = 0, is_off = 0;
-  PairItem is_it = item(0);
-  auto issue_next = [&](int e) {
-    const int slot = e % NSLOT;
-    bf16_t* st = smem + slot * 2 * A::TILE;
-    const bool valid = is_k < nmine;
-    const int n = is_it.bh / H, h = is_it.bh - n * H;
-    const long long tok0 = (long long)n * S;
-    const bool second = is_off >= is_it.len0;
-    const int i = is_off - (second ? is_it.len0 : 0);
-    const int kb = second ? is_it.blk1 : is_it.blk0;
-    const float* lse = p.delta + (long long)p.N * H * S + (long long)is_it.bh * S;  // log2 units
-    const float* delta = p.delta + (long long)is_it.bh * S;
-    int qt = 0;
-    bool tile = false;
-    if (i < 2) {  // K (i = 0) or V (i = 1) rows of the block: two 64-row images
-      const bf16_t* X = static_cast<const bf16_t*>(i == 0 ? p.k : p.v) + tok0 * p.ld_qkv + h * HD;
-      tile_dma<HD>(X, p.ld_qkv, kb * QB, S, valid, vq, st, wid);
-      tile_dma<HD>(X, p.ld_qkv, kb * QB + KT, S, valid, vq, st + A::TILE, wid);
-    } else {
-      qt = qt_begin(kb) + i - 2;
-      tile = true;
-      const bf16_t* Q = static_cast<const bf16_t*>(p.q) + tok0 * p.ld_qkv + h * HD;
-      const bf16_t* dO = static_cast<const bf16_t*>(p.dout) + tok0 * p.ld_o + h * HD;
-      tile_dma<HD>(Q, p.ld_qkv, qt * KT, S, valid, vq, st, wid);
-      tile_dma<HD>(dO, p.ld_o, qt * KT, S, valid, vd, st + A::TILE, wid);
-    }
-    if (wid == 0) {  // (issued for every element -- empty for K / V -- so the counts are uniform)
-      dma4(rows_rsrc(lse, 4, qt * KT, S, valid && tile), lane * 4, &srow[slot][0][0]);
-      dma4(rows_rsrc(delta, 4, qt * KT, S, valid && tile), lane * 4, &srow[slot][1][0]);
-    }
-    if (valid && ++is_off == is_it.len) {
-      is_off = 0;
-      if (++is_k < nmine) is_it = item(is_k);
-    }
-  };
-
-  const float c = p.scale * LOG2E;
-  bf16x8 kf[A::NST], vf[A::NST];
-  floatx16 dvt[A::NDT], dkt[A::NDT];
-  // ---- consume cursor: the block being accumulated
-  int c_k = 0, c_off = 0;
-  PairItem c_it = is_it;
-  int bh = 0, kb = 0, k0 = 0, key = 0, n = 0, h = 0;
-  bool key_ok = false, have_block = false;
-
-  auto store_block = [&]() {  // dK / dV of the finished block: NSTORE buffer stores per lane
-    const long long tok0 = (long long)n * S;
-    const __amdgpu_buffer_rsrc_t rk =
-        __builtin_amdgcn_make_buffer_rsrc((void*)(static_cast<bf16_t*>(p.dk) + tok0 * p.ld_dqkv + h * HD), 0,
-                                          (unsigned)((long long)(S - 1) * p.ld_dqkv * 2 + HD * 2), 0x00020000);
-    const __amdgpu_buffer_rsrc_t rv =
-        __builtin_amdgcn_make_buffer_rsrc((void*)(static_cast<bf16_t*>(p.dv) + tok0 * p.ld_dqkv + h * HD), 0,
-                                          (unsigned)((long long)(S - 1) * p.ld_dqkv * 2 + HD * 2), 0x00020000);
-    // (a key past S gets an offset past the descriptor's end: the store is dropped)
-    const int roff = (key < S ? key : S + 1) * (int)p.ld_dqkv * 2;
-    typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
-#pragma unroll
-    for (int d = 0; d < A::NDT; ++d)
-#pragma unroll
-      for (int g = 0; g < 4; g += 2) {
-        uint2 ka = make_uint2(0u, 0u), kb2 = ka, va = ka, vb = ka;
-        if (key_ok) {
-          ka.x = pack2bf(dkt[d][4 * g + 0] * p.scale, dkt[d][4 * g + 1] * p.scale);
-          ka.y = pack2bf(dkt[d][4 * g + 2] * p.scale, dkt[d][4 * g + 3] * p.scale);
-          kb2.x = pack2bf(dkt[d][4 * g + 4] * p.scale, dkt[d][4 * g + 5] * p.scale);
-          kb2.y = pack2bf(dkt[d][4 * g + 6] * p.scale, dkt[d][4 * g + 7] * p.scale);
-          va.x = pack2bf(dvt[d][4 * g + 0], dvt[d][4 * g + 1]);
-          va.y = pack2bf(dvt[d][4 * g + 2], dvt[d][4 * g + 3]);
-          vb.x = pack2bf(dvt[d][4 * g + 4], dvt[d][4 * g + 5]);
-          vb.y = pack2bf(dvt[d][4 * g + 6], dvt[d][4 * g + 7]);
-        }
-        // (store_pair16's lane trade, then one 16-B buffer store per lane)
-        const auto k0s = __builtin_amdgcn_permlane32_swap(ka.x, kb2.x, false, false);
-        const auto k1s = __builtin_amdgcn_permlane32_swap(ka.y, kb2.y, false, false);
-        const auto v0s = __builtin_amdgcn_permlane32_swap(va.x, vb.x, false, false);
-        const auto v1s = __builtin_amdgcn_permlane32_swap(va.y, vb.y, false, false);
-        const int coff = roff + (d * 32 + 8 * g + 8 * hh) * 2;
-        __builtin_amdgcn_raw_buffer_store_b128(u32x4{k0s[0], k1s[0], k0s[1], k1s[1]}, rk, coff, 0, 0);
-        __builtin_amdgcn_raw_buffer_store_b128(u32x4{v0s[0], v1s[0], v0s[1], v1s[1]}, rv, coff, 0, 0);
-      }
-  };
-
-  // one 32-query half of the tile in slot `slot` (query tile qt), key on the lane
-  auto half = [&](int slot, int qt, int hf) {
-    const bf16_t* lq = smem + slot * 2 * A::TILE;
-    const bf16_t* ldo = lq + A::TILE;
-    const int qt0 = qt * KT;
-    const int qs0 = qt0 + 32 * hf;
-    if (p.causal && qs0 + 31 < k0) return;  // wave-uniform: every query before every key
-    const bool diag = p.causal && qs0 < k0 + 31;
-    floatx16 sa, dp;
-    zero16(sa);
-    {
-      const float* drow = &srow[slot][1][0];
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const float4 d4 = *reinterpret_cast<const float4*>(drow + 32 * hf + 8 * g + 4 * hh);
-        dp[4 * g + 0] = -d4.x;
-        dp[4 * g + 1] = -d4.y;
-        dp[4 * g + 2] = -d4.z;
-        dp[4 * g + 3] = -d4.w;
-      }
-    }
-#pragma unroll
-    for (int st = 0; st < A::NST; ++st) {
-      sa = MFMA32(row_frag<HD>(lq, 32 * hf, st, lane), kf[st], sa);
-      dp = MFMA32(row_frag<HD>(ldo, 32 * hf, st, lane), vf[st], dp);
-    }
-#pragma unroll
-    for (int g = 0; g < 4; ++g) {
-      const int qi0 = 32 * hf + 8 * g + 4 * hh;
-      const float4 l4 = *reinterpret_cast<const float4*>(&srow[slot][0][qi0]);
-      const float lv[4] = {l4.x, l4.y, l4.z, l4.w};
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const int r = 4 * g + e;
-        float pv = fast_exp2(fmaf(sa[r], c, -lv[e]));
-        if (diag) pv = (key > qt0 + qi0 + e) ? 0.f : pv;
-        sa[r] = pv;
-        dp[r] = pv * dp[r];
-      }
-    }
-#pragma unroll
-    for (int ss = 0; ss < 2; ++ss) {
-      const bf16x8 pb = acc_frag(sa, ss);
-      const bf16x8 db = acc_frag(dp, ss);
-#pragma unroll
-      for (int d = 0; d < A::NDT; ++d) {
-        dvt[d] = MFMA32(tr_frag<HD>(ldo, 32 * hf, ss, d * 32, lane), pb, dvt[d]);
-        dkt[d] = MFMA32(tr_frag<HD>(lq, 32 * hf, ss, d * 32, lane), db, dkt[d]);
-      }
-    }
-  };
-
-  issue_next(0);
-  issue_next(1);
-  issue_next(2);
-  bool stored = false;  // the previous step issued a block's NSTORE stores
-  for (int e = 0; e < total; ++e) {
-    // element e landed; younger: elements e+1, e+2 (+ the previous step's stores)
-    if (stored) {
-      if (wid == 0) vm_wait<2 * (2 * A::NPW + 2) + NSTORE>();
-      else vm_wait<2 * 2 * A::NPW + NSTORE>();
-    } else {
-      if (wid == 0) vm_wait<2 * (2 * A::NPW + 2)>();
-      else vm_wait<2 * 2 * A::NPW>();
-    }
-    stored = false;
-    ring_barrier();  // every wave's pieces of e landed; every wave is done with element e-1's slot
-    issue_next(e + 3);
-    const int slot = e % NSLOT;
-    const PairItem cur = c_it;
-    const bool second = c_off >= cur.len0;
-    const int i = c_off - (second ? cur.len0 : 0);
-    if (++c_off == cur.len) {
-      c_off = 0;
-      if (++c_k < nmine) c_it = item(c_k);
-    }
-    if (i == 0) {  // a block starts: the previous one's dK / dV out, this one's K rows in
-      if (have_block) {
-        store_block();
-        stored = true;
-      }
-      have_block = true;
-      bh = cur.bh;
-      n = bh / H;
-      h = bh - n * H;
-      kb = second ? cur.blk1 : cur.blk0;
-      k0 = kb * QB + wid * 32;
-      key = k0 + (lane & 31);
-      key_ok = key < S && !(p.pad && p.pad[(long long)n * S + min(key, S - 1)]);
-      const bf16_t* sk = smem + slot * 2 * A::TILE + (wid >> 1) * A::TILE;
-#pragma unroll
-      for (int st = 0; st < A::NST; ++st) kf[st] = row_frag<HD>(sk, 32 * (wid & 1), st, lane);
-#pragma unroll
-      for (int d = 0; d < A::NDT; ++d) {
-        zero16(dvt[d]);
-        zero16(dkt[d]);
-      }
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // (WAR: done with the slot)
-      continue;
-    }
-    if (i == 1) {  // V rows
-      const bf16_t* sv = smem + slot * 2 * A::TILE + (wid >> 1) * A::TILE;
-#pragma unroll
-      for (int st = 0; st < A::NST; ++st) vf[st] = row_frag<HD>(sv, 32 * (wid & 1), st, lane);
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      continue;
-    }
-    const int qt = qt_begin(kb) + i - 2;
-#pragma unroll 1
-    for (int hf = 0; hf < 2; ++hf) half(slot, qt, hf);
-  }
-  if (have_block) store_block();
-  vm_wait<0>();  // (the elements issued past the end: empty descriptors) drained
-}
-
-// Bounded 16-B / 4-B stores of the stream kernels: a buffer descriptor that ends where the output
-// rows end, so a lane past the last row issues its store (the wave's vmcnt count stays exact)
-// and the hardware drops it.
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t out_rsrc(const void* base, long long bytes) {
-  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0,
-                                           (unsigned)(bytes > 0xffffffffll ? 0xffffffffll : bytes), 0x00020000);
-}
-// store_pair16 through a buffer descriptor (byte offset `off` of the lane's 16 B)
-__device__ __forceinline__ void store_pair16_b(__amdgpu_buffer_rsrc_t rs, int off, uint2 wa, uint2 wb) {
-  typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
-  const auto s0 = __builtin_amdgcn_permlane32_swap(wa.x, wb.x, false, false);
-  const auto s1 = __builtin_amdgcn_permlane32_swap(wa.y, wb.y, false, false);
-  __builtin_amdgcn_raw_buffer_store_b128(u32x4{s0[0], s1[0], s0[1], s1[1]}, rs, off, 0, 0);
-}
-
-// dQ (with the delta pre-pass) as ONE persistent stream per workgroup -- attn_bwd_dkdv2_kernel's
-// structure for the query side: items of two 128-query blocks of one (batch, head), the
-// heaviest and the lightest under the causal mask (blocks nqb-1-pr and pr), each block a run of
-// ring elements: its Q rows (+ its lse rows, wave 0), its dO rows, its O rows, then its K | V
-// tiles.  The query rows arrive by coalesced LDS-DMA instead of per-lane row loads, and the
-// per-block prologue (rows in) / epilogue (dQ out) overlaps the neighbouring blocks' tiles.
-// At the O element each lane forms delta = rowsum(dO * O) and stores delta and the log2-unit lse
-// for the dK / dV kernel (2 bounded stores); at a block end, the dQ rows (2 NDT bounded stores).
-template <int HD, int OCC>
-__global__ __launch_bounds__(256, OCC) void attn_bwd_dq2_kernel(AttnArgs p, int nitems) {
-  using A = AT<HD>;
-  __shared__ __attribute__((aligned(16))) bf16_t smem[NSLOT * 2 * A::TILE];  // [slot][K|V] / [rows lo|hi]
-  __shared__ __attribute__((aligned(16))) float srow[NSLOT][2][KT];          // [slot][lse lo|hi]
-  const int S = p.S, H = p.H;
-  const int nqb = (S + QB - 1) / QB;
-  const int npr = (nqb + 1) / 2;
-  const int grid = gridDim.x;
-  const int local = g7_local_attn(blockIdx.x, grid);
-  const int lane = threadIdx.x & 63, hh = lane >> 5;
-  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  constexpr int NSTQ = 2 * A::NDT;  // dQ 16-B stores per lane at a block end
-  auto ntiles_of = [&](int qb) {
-    const int kend = p.causal ? min(S, qb * QB + QB) : S;
-    return (kend + KT - 1) / KT;
-  };
-  auto item = [&](int k) {
-    PairItem it;
-    const int id = local + k * grid;
-    it.bh = id / npr;
-    const int pr = id - it.bh * npr;
-    it.blk0 = nqb - 1 - pr;  // most key tiles under the causal mask
-    it.blk1 = pr;
-    it.len0 = 3 + ntiles_of(it.blk0);
-    it.len = it.len0 + (it.blk1 != it.blk0 ? 3 + ntiles_of(it.blk1) : 0);
-    return it;
-  };
-  const int nmine = local < nitems ? (nitems - local + grid - 1) / grid : 0;
-  if (nmine == 0) return;
-  int total = 0;
-  for (int k = 0; k < nmine; ++k) total += item(k).len;
-
-  int vq[A::NPW], vo[A::NPW];
-  dma_voff<HD>(vq, p.ld_qkv, wid, lane);
-  dma_voff<HD>(vo, p.ld_o, wid, lane);
-  // ---- issue cursor
-  int is_k = 0, is_off = 0;
-  PairItem is_it = item(0);
-  auto issue_next = [&](int e) {
-    const int slot = e % NSLOT;
-    bf16_t* st = smem + slot * 2 * A::TILE;
-    const bool valid = is_k < nmine;
-    const int n = is_it.bh / H, h = is_it.bh - n * H;
-    const long long tok0 = (long long)n * S;
-    const bool second = is_off >= is_it.len0;
-    const int i = is_off - (second ? is_it.len0 : 0);
-    const int qb = second ? is_it.blk1 : is_it.blk0;
-    if (i < 3) {  // Q / dO / O rows of the block: two 64-row images
-      const bf16_t* X = i == 0 ? static_cast<const bf16_t*>(p.q) : static_cast<const bf16_t*>(i == 1 ? p.dout : p.o);
-      const long long ld = i == 0 ? p.ld_qkv : p.ld_o;
-      X += tok0 * ld + h * HD;
-      tile_dma<HD>(X, ld, qb * QB, S, valid, i == 0 ? vq : vo, st, wid);
-      tile_dma<HD>(X, ld, qb * QB + KT, S, valid, i == 0 ? vq : vo, st + A::TILE, wid);
-    } else {
-      const int t = i - 3;
-      const bf16_t* K = static_cast<const bf16_t*>(p.k) + tok0 * p.ld_qkv + h * HD;
-      const bf16_t* V = static_cast<const bf16_t*>(p.v) + tok0 * p.ld_qkv + h * HD;
-      tile_dma<HD>(K, p.ld_qkv, t * KT, S, valid, vq, st, wid);
-      tile_dma<HD>(V, p.ld_qkv, t * KT, S, valid, vq, st + A::TILE, wid);
-    }
-    if (wid == 0) {  // the block's lse rows with its Q element (empty for every other element)
-      const float* lse = p.lse + (long long)is_it.bh * S;
-      dma4(rows_rsrc(lse, 4, qb * QB, S, valid && i == 0), lane * 4, &srow[slot][0][0]);
-      dma4(rows_rsrc(lse, 4, qb * QB + KT, S, valid && i == 0), lane * 4, &srow[slot][1][0]);
-    }
-    if (valid && ++is_off == is_it.len) {
-      is_off = 0;
-      if (++is_k < nmine) is_it = item(is_k);
-    }
-  };
-
-  const float c = p.scale * LOG2E;
-  bf16x8 qf[A::NST], df[A::NST];
-  floatx16 dqt[A::NDT];
-  float lse2 = INFINITY, dl = 0.f;
-  int c_k = 0, c_off = 0;
-  PairItem c_it = is_it;
-  int bh = 0, n = 0, h = 0, q0 = 0, q = 0;
-  bool have_block = false;
-  const unsigned char* pad = nullptr;
-
-  auto store_block = [&]() {  // dQ rows of the finished block (NSTQ bounded stores per lane)
-    const long long tok0 = (long long)n * S;
-    const __amdgpu_buffer_rsrc_t rq =
-        out_rsrc(static_cast<bf16_t*>(p.dq) + tok0 * p.ld_dqkv + h * HD, (long long)(S - 1) * p.ld_dqkv * 2 + HD * 2);
-    const int roff = (q < S ? q : S + 1) * (int)p.ld_dqkv * 2;
-#pragma unroll
-    for (int d = 0; d < A::NDT; ++d)
-#pragma unroll
-      for (int g = 0; g < 4; g += 2) {
-        uint2 wa, wb;
-        wa.x = pack2bf(dqt[d][4 * g + 0] * p.scale, dqt[d][4 * g + 1] * p.scale);
-        wa.y = pack2bf(dqt[d][4 * g + 2] * p.scale, dqt[d][4 * g + 3] * p.scale);
-        wb.x = pack2bf(dqt[d][4 * g + 4] * p.scale, dqt[d][4 * g + 5] * p.scale);
-        wb.y = pack2bf(dqt[d][4 * g + 6] * p.scale, dqt[d][4 * g + 7] * p.scale);
-        store_pair16_b(rq, roff + (d * 32 + 8 * g + 8 * hh) * 2, wa, wb);
-      }
-  };
-  // one 32-key half of the K | V tile in `slot` (key tile t), query on the lane
-  auto half = [&](int slot, int t, int hf) {
-    const bf16_t* lk = smem + slot * 2 * A::TILE;
-    const int kt0 = t * KT;
-    const int ks0 = kt0 + 32 * hf;
-    if (p.causal && ks0 > q0 + 31) return;  // wave-uniform: every key after every query
-    const bool need_mask = (p.causal && ks0 + 31 > q0) || (ks0 + 32 > S) || pad;
-    floatx16 sa, dp;
-    zero16(sa);
-#pragma unroll
-    for (int r = 0; r < 16; ++r) dp[r] = -dl;
-#pragma unroll
-    for (int st = 0; st < A::NST; ++st) {
-      sa = MFMA32(row_frag<HD>(lk, 32 * hf, st, lane), qf[st], sa);
-      dp = MFMA32(row_frag<HD>(lk + A::TILE, 32 * hf, st, lane), df[st], dp);
-    }
-    if (need_mask) {
-      const unsigned long long pm = pad_bits(pad, kt0, S, lane);
-      const int lim = (p.causal ? min(q, S - 1) : S - 1) - kt0;
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int kl = 32 * hf + acc_row(r, lane);
-        float pv = fast_exp2(fmaf(sa[r], c, -lse2));
-        pv = (kl > lim || ((pm >> kl) & 1ull)) ? 0.f : pv;
-        dp[r] = pv * dp[r];
-      }
-    } else {
-#pragma unroll
-      for (int r = 0; r < 16; ++r) dp[r] = fast_exp2(fmaf(sa[r], c, -lse2)) * dp[r];
-    }
-#pragma unroll
-    for (int ss = 0; ss < 2; ++ss) {
-      const bf16x8 db = acc_frag(dp, ss);
-#pragma unroll
-      for (int d = 0; d < A::NDT; ++d) dqt[d] = MFMA32(tr_frag<HD>(lk, 32 * hf, ss, d * 32, lane), db, dqt[d]);
-    }
-  };
-
-  issue_next(0);
-  issue_next(1);
-  issue_next(2);
-  int stored = 0;  // stores the previous step issued: 0, 2 (delta / lse) or NSTQ (dQ)
-  for (int e = 0; e < total; ++e) {
-    // element e landed; younger: elements e+1, e+2 (+ the previous step's stores)
-    if (wid == 0) {
-      constexpr int P2 = 2 * (2 * A::NPW + 2);
-      if (stored == 2) vm_wait<P2 + 2>();
-      else if (stored) vm_wait<P2 + NSTQ>();
-      else vm_wait<P2>();
-    } else {
-      constexpr int P2 = 2 * 2 * A::NPW;
-      if (stored == 2) vm_wait<P2 + 2>();
-      else if (stored) vm_wait<P2 + NSTQ>();
-      else vm_wait<P2>();
-    }
-    stored = 0;
-    ring_barrier();
-    issue_next(e + 3);
-    const int slot = e % NSLOT;
-    const PairItem cur = c_it;
-    const bool second = c_off >= cur.len0;
-    const int i = c_off - (second ? cur.len0 : 0);
-    if (++c_off == cur.len) {
-      c_off = 0;
-      if (++c_k < nmine) c_it = item(c_k);
-    }
-    const bf16_t* rows = smem + slot * 2 * A::TILE + (wid >> 1) * A::TILE;  // (this wave's 32 rows)
-    if (i == 0) {  // a block starts: the previous one's dQ out, this one's Q rows and lse in
-      if (have_block) {
-        store_block();
-        stored = NSTQ;
-      }
-      have_block = true;
-      bh = cur.bh;
-      n = bh / H;
-      h = bh - n * H;
-      pad = p.pad ? p.pad + (long long)n * S : nullptr;
-      q0 = (second ? cur.blk1 : cur.blk0) * QB + wid * 32;
-      q = q0 + (lane & 31);
-#pragma unroll
-      for (int st = 0; st < A::NST; ++st) qf[st] = row_frag<HD>(rows, 32 * (wid & 1), st, lane);
-      const float lv = srow[slot][wid >> 1][32 * (wid & 1) + (lane & 31)];
-      lse2 = q < S ? lv * LOG2E : INFINITY;  // (+inf stays +inf: a fully masked row)
-#pragma unroll
-      for (int d = 0; d < A::NDT; ++d) zero16(dqt[d]);
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // (WAR: done with the slot)
-      continue;
-    }
-    if (i == 1) {  // dO rows
-#pragma unroll
-      for (int st = 0; st < A::NST; ++st) df[st] = row_frag<HD>(rows, 32 * (wid & 1), st, lane);
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      continue;
-    }
-    if (i == 2) {  // O rows: delta = rowsum(dO * O), stored with the log2-unit lse for dK / dV
-      float acc = 0.f;
-#pragma unroll
-      for (int st = 0; st < A::NST; ++st) {
-        const bf16x8 of = row_frag<HD>(rows, 32 * (wid & 1), st, lane);
-        float fo[8], fd[8];
-        unpack8(__builtin_bit_cast(uint4, of), fo);
-        unpack8(__builtin_bit_cast(uint4, df[st]), fd);
-#pragma unroll
-        for (int k = 0; k < 8; ++k) acc = fmaf(fo[k], fd[k], acc);
-      }
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      dl = acc + __shfl_xor(acc, 32, 64);  // (the row's other half on lane ^ 32)
-      const long long rbytes = (long long)S * 4;
-      const __amdgpu_buffer_rsrc_t rd = out_rsrc(p.delta + (long long)bh * S, rbytes);
-      const __amdgpu_buffer_rsrc_t rl = out_rsrc(p.delta + (long long)p.N * H * S + (long long)bh * S, rbytes);
-      const int off = (q < S ? q : S) * 4;
-      __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(dl), rd, off, 0, 0);
-      __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(lse2), rl, off, 0, 0);
-      stored = 2;
-      continue;
-    }
-    const int t = i - 3;
-#pragma unroll 1
-    for (int hf = 0; hf < 2; ++hf) half(slot, t, hf);
-  }
-  if (have_block) store_block();
-  vm_wait<0>();
-}
-
 // dQ: workgroup = 128 queries (4 waves x 32, query on the lane), sweeping the key tiles up to
 // the last query.  Per 32-key sub-block j: S^T, dP^T of j+1 overlap dS^T of j, then
 // dQ^T += K^T dS^T (2 x NDT MFMAs).
@@ -1673,39 +1173,20 @@ static int launch_fwd(const AttnArgs* a, hipStream_t stream) {
 // The shipped backward (variant 1 at hd 64, 2 at hd 32): the dQ kernel first, with the delta
 // pre-pass fused in (it writes delta / lse2 for the dK / dV kernel); DPC_ATTN_PRE=1 (or a forced
 // variant) keeps the separate pre-pass kernel and the dK / dV -> dQ order.
-static int g_dkdv2 = -1;  // (dpc_attn_set_dkdv2: tests A/B the two dK / dV kernels in one process)
-static int g_dq2 = -1;    // (dpc_attn_set_dq2: the same for the dQ kernels)
-
 template <int HD>
 static int launch_bwd(const AttnArgs* a, hipStream_t stream) {
   const int var = attn_var(HD, 1);
   static int pre_env = -1;
   if (pre_env < 0) pre_env = getenv("DPC_ATTN_PRE") ? atoi(getenv("DPC_ATTN_PRE")) : 0;
   dim3 grid((unsigned)(((a->S + QB - 1) / QB) * a->N * a->H));
-  // dK / dV as one persistent pair stream per workgroup (attn_bwd_dkdv2_kernel); DPC_ATTN_DKDV2=0
-  // keeps the one-launch-per-block kernel
-  if (g_dkdv2 < 0) g_dkdv2 = getenv("DPC_ATTN_DKDV2") ? atoi(getenv("DPC_ATTN_DKDV2")) : 0;
-  const int dkdv2_env = g_dkdv2;
-  if (g_dq2 < 0) g_dq2 = getenv("DPC_ATTN_DQ2") ? atoi(getenv("DPC_ATTN_DQ2")) : 0;
+  // (round 4 measured persistent pair-stream forms of both kernels -- one LDS-DMA stream of
+  // (heaviest, lightest) block pairs per workgroup -- bitwise equal but slower: bwd 754 -> 798 us
+  // with the dK / dV stream, 770 -> 954 us with the dQ stream, DDP step -0.8 % / -4 %
+  // (profiles/r4_attn/); removed)
   if (!pre_env && var == (HD == 32 ? 2 : 1)) {
-    if (g_dq2) {  // dQ + delta as one persistent pair stream per workgroup
-      const int nqb = (a->S + QB - 1) / QB;
-      const int nitems = ((nqb + 1) / 2) * a->N * a->H;
-      dim3 g2((unsigned)(nitems > 512 ? 512 : nitems));
-      hipLaunchKernelGGL((attn_bwd_dq2_kernel<HD, 2>), g2, dim3(256), 0, stream, *a, nitems);
-    } else if (HD == 32) {
-      hipLaunchKernelGGL((attn_bwd_dq_kernel<HD, false, 3, 0, true>), grid, dim3(256), 0, stream, *a);
-    } else {
-      hipLaunchKernelGGL((attn_bwd_dq_kernel<HD, false, 2, 0, true>), grid, dim3(256), 0, stream, *a);
-    }
-    if (dkdv2_env) {
-      const int nkb = (a->S + QB - 1) / QB;
-      const int nitems = ((nkb + 1) / 2) * a->N * a->H;
-      dim3 g2((unsigned)(nitems > 512 ? 512 : nitems));  // two workgroups per CU
-      hipLaunchKernelGGL((attn_bwd_dkdv2_kernel<HD, 2>), g2, dim3(256), 0, stream, *a, nitems);
-    } else {
-      DPC_ATTN_SWITCH(var, attn_bwd_dkdv_kernel, grid, dim3(256), 0, stream, *a);
-    }
+    if (HD == 32) hipLaunchKernelGGL((attn_bwd_dq_kernel<HD, false, 3, 0, true>), grid, dim3(256), 0, stream, *a);
+    else hipLaunchKernelGGL((attn_bwd_dq_kernel<HD, false, 2, 0, true>), grid, dim3(256), 0, stream, *a);
+    DPC_ATTN_SWITCH(var, attn_bwd_dkdv_kernel, grid, dim3(256), 0, stream, *a);
     return (int)hipGetLastError();
   }
   const long long rows = (long long)a->N * a->S * a->H;
@@ -1764,8 +1245,6 @@ DPC_API int dpc_attn_bwd_lab(const AttnArgs* a, int which, int abl, hipStream_t 
   return (int)hipGetLastError();
 }
 
-DPC_API void dpc_attn_set_dkdv2(int on) { g_dkdv2 = on; }
-DPC_API void dpc_attn_set_dq2(int on) { g_dq2 = on; }
 
 DPC_API int dpc_attn_bwd(const AttnArgs* a, hipStream_t stream) {
   if (!attn_args_ok(a, true)) return (int)hipErrorInvalidValue;

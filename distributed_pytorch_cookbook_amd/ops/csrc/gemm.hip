@@ -888,12 +888,14 @@ DPC_API int dpc_gemm(const GemmArgs* a, hipStream_t stream) {
   const bool plain = a->out_f32 && !a->bias && !a->residual && !a->aux_in && !a->aux_out &&
                      !a->colsum && !a->act && !a->act_bwd;
   if (g_gemm_impl < 0 && a->impl <= 0 && v2_ok && plain && !a->a_kmaj && !a->b_kmaj && policy_impl(a) <= 0) {
-    // weight gradient: the split-K persistent kernel (v7, chosen above when K % 64 == 0) or the
+    // weight gradient: the split-K persistent kernel (v7, chosen above when its requirements
+    // hold -- its own planner splits K to fill the chip however few tiles there are), else the
     // 256x256 ping-pong kernel (v5) once there are enough 128x128 tiles to spread over the
-    // k-splits, else the 2-stage 64-k kernel (768 x 768)
+    // k-splits, else the 2-stage 64-k kernel.  (Round 4: the pipeline stage proxy's micro-batch
+    // out-projection weight gradient, 1024 x 1024 x 16368, off the table, fell to the 2-stage
+    // kernel at 506 TF/s -- 8.7 ms of a 262 ms stage step, profiles/r4_pp/.)
     const int t128 = ((a->M + BM - 1) / BM) * ((a->N + BN - 1) / BN);
-    if (t128 < 100) impl = 2;
-    else if (impl != 20) impl = 12;
+    if (impl != 20) impl = t128 < 100 ? 2 : 12;
   }
   if (impl >= 15 && impl <= 26) {  // v7 (gemm7.hip): 4-wave 256x256, split-K f32 products
     GemmArgs c = *a;

@@ -1,8 +1,9 @@
 #!/bin/bash
 # Multi-GPU tuning sweep for a whole 8 x MI355X node (not runnable on the one-GPU boxes of this
 # project's CI): the DDP bucket size (SURVEY.md §5.8 design rule 2: 25 -> 256 MB) and the
-# gradient-reduction dtype at N = 2, 4, 8, the FSDP all-gather prefetch depth (1-3) at N = 8,
-# then the pipeline recipes' defaults at N = 8.  One JSON line per
+# gradient-reduction dtype at N = 2, 4, 8, the FSDP all-gather prefetch depth (1-3) and
+# reduce-scatter dtype at N = 8, then the pipeline recipes' boundary (p2p) dtype and the PP x DP
+# stage all-reduce dtype at N = 8.  One JSON line per
 # run in gpurun_out/scaling_sweep.jsonl.
 #   bash scripts/scaling_sweep.sh [max_gpus]
 set -u
@@ -27,7 +28,11 @@ for n in 2 4 8; do
   done
 done
 for pf in 1 2 3; do run "$MAXG" --recipe fsdp --prefetch $pf || exit $?; done  # FSDP all-gather depth
-for r in pipe pipe_ddp; do run "$MAXG" --recipe $r || exit $?; done
+for dt in fp32 bf16; do run "$MAXG" --recipe fsdp --reduce_dtype $dt || exit $?; done  # FSDP RS dtype
+for r in pipe pipe_ddp; do
+  for w in fp32 bf16; do run "$MAXG" --recipe $r --pp_comm_dtype $w || exit $?; done  # PP wire dtype
+done
+for dt in fp32 bf16; do run "$MAXG" --recipe pipe_ddp --reduce_dtype $dt || exit $?; done  # PP x DP AR dtype
 python3 - <<'PY'
 import json
 for l in open("gpurun_out/scaling_sweep.jsonl"):

@@ -778,38 +778,3 @@ def test_gemv_few_rows(M, Nw, N, K, epi):
     assert rel_err(y[:, :Nw], ref) < (2e-3 if odt == torch.float32 else 1e-2)
     if N > Nw:
         assert torch.count_nonzero(y[:, Nw:]) == 0
-
-
-@pytest.mark.parametrize("hd", [64, 32])
-@pytest.mark.parametrize("S,N,H,causal,with_pad", [(1023, 16, 12, True, False), (1000, 3, 5, True, True),
-                                                   (257, 2, 3, True, False), (200, 3, 5, False, True),
-                                                   (64, 2, 2, True, False), (129, 4, 7, False, False)])
-def test_attention_bwd_pair_streams_match_per_block(S, N, H, causal, with_pad, hd):
-    """attn_bwd_dkdv2_kernel / attn_bwd_dq2_kernel (one persistent LDS-DMA stream of block pairs
-    per workgroup) do the per-block kernels' arithmetic in the same order: dQ / dK / dV bitwise
-    equal in every combination --
-    on ragged S (rows past S dropped by the buffer stores), odd block counts (a block paired with
-    itself), key padding, the non-causal form, and more items than workgroups (16 x 12 x 4 = 768
-    items on a 512-workgroup grid)."""
-    torch.manual_seed(9)
-    T = N * S
-    qkv = torch.randn(T, 3 * H * hd, device=dev).bfloat16()
-    pad = None
-    if with_pad:
-        pad = torch.zeros(N, S, dtype=torch.bool, device=dev)
-        pad[0, S - S // 3:] = True
-        pad[-1, 3:11] = True
-    o, lse = attention_fwd(qkv, N, S, H, hd, pad, causal=causal)
-    do = torch.randn(T, H * hd, device=dev).bfloat16()
-    outs = []
-    for dq2, dkdv2 in ((0, 0), (0, 1), (1, 0), (1, 1)):
-        _lib.set_attn_dkdv2(dkdv2)
-        _lib.set_attn_dq2(dq2)
-        try:
-            outs.append(attention_bwd(do, qkv, o, lse, N, S, H, hd, pad, causal=causal).clone())
-        finally:
-            _lib.set_attn_dkdv2(-1)
-            _lib.set_attn_dq2(-1)
-    for k in range(1, 4):
-        assert torch.equal(outs[0], outs[k]), (k, (outs[0].float() - outs[k].float()).abs().max().item())
-    assert _lib.is_loaded()
