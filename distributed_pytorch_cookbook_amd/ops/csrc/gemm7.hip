@@ -273,6 +273,22 @@ DPC_API int dpc_gemm7(const GemmArgs* a, int persistent, int sched, int splits, 
         hipLaunchKernelGGL((gemm9_kernel<0, true, true>), dim3(p9.grid), dim3(256), 0, stream, *a, ab, bb, p9);
       return (int)hipGetLastError();
     }
+    // plain input gradients (A k-major, B mn-major) on v9 only when the table asks for it (impl
+    // 26): the A/B candidate for the dX products, which v7 schedule 6 serves by default
+    const bool g9_km = plain && !a->accumulate && s == 1 && !v8 && a->a_kmaj && !a->b_kmaj && a->K % 64 == 0 &&
+                       a->lda >= 64 && a->ldb >= 128;
+    if (g9_km && sched == 7) {
+      G7Plan p9 = pl;
+      p9.nk = a->K / 64;
+      p9.nk_all = p9.nk;
+      static int er_km = -1;
+      if (er_km < 0) er_km = getenv("DPC_G9_ER") ? atoi(getenv("DPC_G9_ER")) : 4;
+      if (er_km == 4)
+        hipLaunchKernelGGL((gemm9_kernel<0, true, false, 0, 4>), dim3(p9.grid), dim3(256), 0, stream, *a, ab, bb, p9);
+      else
+        hipLaunchKernelGGL((gemm9_kernel<0, true, false>), dim3(p9.grid), dim3(256), 0, stream, *a, ab, bb, p9);
+      return (int)hipGetLastError();
+    }
     // forward epilogues that read nothing per element (bias / activation / aux_out, no residual or
     // accumulate: the FFN up-projection) on v9 when the table asks for it (impl 26) or
     // DPC_G9_FWD=1: the 2 x 32 bf16 stores of a tile stay in flight into the next tile's stages
