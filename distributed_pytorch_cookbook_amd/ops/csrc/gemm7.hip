@@ -274,7 +274,9 @@ DPC_API int dpc_gemm7(const GemmArgs* a, int persistent, int sched, int splits, 
       return (int)hipGetLastError();
     }
     // plain input gradients (A k-major, B mn-major) on v9 only when the table asks for it (impl
-    // 26): the A/B candidate for the dX products, which v7 schedule 6 serves by default
+    // 26): same-box A/B against v7 schedule 6 (the default for dX) +4-5 % on the out-projection
+    // input gradients (K = N = D), -1..-3 % on the others (profiles/r4_g9/ab_*.log), so the
+    // table gives it the square ones
     const bool g9_km = plain && !a->accumulate && s == 1 && !v8 && a->a_kmaj && !a->b_kmaj && a->K % 64 == 0 &&
                        a->lda >= 64 && a->ldb >= 128;
     if (g9_km && sched == 7) {
@@ -302,7 +304,14 @@ DPC_API int dpc_gemm7(const GemmArgs* a, int persistent, int sched, int splits, 
       G7Plan p9 = pl;
       p9.nk = a->K / 64;
       p9.nk_all = p9.nk;
-      hipLaunchKernelGGL((gemm9_kernel<1, true, true>), dim3(p9.grid), dim3(256), 0, stream, *a, ab, bb, p9);
+      // the early-release schedule here too (DPC_G9_FWD_ER, default 4): same-box XL up-projection
+      // 1,023 -> 1,046 TF/s, DDP 945.1K -> 947.7K, FSDP XL 88.5K -> 90.1K (profiles/r4_g9/)
+      static int fer = -1;
+      if (fer < 0) fer = getenv("DPC_G9_FWD_ER") ? atoi(getenv("DPC_G9_FWD_ER")) : 4;
+      if (fer == 4)
+        hipLaunchKernelGGL((gemm9_kernel<1, true, true, 0, 4>), dim3(p9.grid), dim3(256), 0, stream, *a, ab, bb, p9);
+      else
+        hipLaunchKernelGGL((gemm9_kernel<1, true, true>), dim3(p9.grid), dim3(256), 0, stream, *a, ab, bb, p9);
       return (int)hipGetLastError();
     }
     // weight gradients (both operands mn-major, split K through workspace slabs) on v9, with the

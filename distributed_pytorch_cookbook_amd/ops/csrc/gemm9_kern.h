@@ -246,9 +246,9 @@ __global__ __launch_bounds__(256, 1) void gemm9_kernel(GemmArgs p, unsigned long
 #define G9_E1(i)                                                                                    \
   do {                                                                                              \
     mf(i, 0, a1, b1, false); G9_SB;                                                                 \
-    if (!(ABL & 32)) a0[i] = frag3<G9_KB, AK>(ln, ar + 16 * i, 0, lane);                            \
+    if (!(ABL & 32) && !LASTB) a0[i] = frag3<G9_KB, AK>(ln, ar + 16 * i, 0, lane);                  \
     G9_SB; mf(i, 1, a1, b1, false); G9_SB;                                                          \
-    if (!(ABL & 32)) b0[i] = frag3<G9_KB, BK>(ln + G9_TA, bc + 16 * i, 0, lane);                    \
+    if (!(ABL & 32) && !LASTB) b0[i] = frag3<G9_KB, BK>(ln + G9_TA, bc + 16 * i, 0, lane);          \
     G9_SB; mf(i, 2, a1, b1, false); G9_SB;                                                          \
     if constexpr ((i) < 8 - P0) dma(P0 + (i), 0);                                                   \
     G9_SB; mf(i, 3, a1, b1, false); G9_SB;                                                          \
@@ -261,8 +261,9 @@ __global__ __launch_bounds__(256, 1) void gemm9_kernel(GemmArgs p, unsigned long
     G9_SB; mf(i, 6, a1, b1, false); G9_SB;                                                          \
     mf(i, 7, a1, b1, false); G9_SB;                                                                 \
   } while (0)
-#define G9_EBODY(FIRST, CREDIT)                                                                     \
+#define G9_EBODY(FIRST, CREDIT, LASTB_)                                                             \
   do {                                                                                              \
+    constexpr bool LASTB = (LASTB_);                                                                \
     const bf16_t* lc = smem + rd * G9_SLOT;                                                         \
     const bf16_t* ln = smem + (rd ^ 1) * G9_SLOT;                                                   \
     G9_E0(0, FIRST); G9_E0(1, FIRST); G9_E0(2, FIRST); G9_E0(3, FIRST);                             \
@@ -309,9 +310,16 @@ __global__ __launch_bounds__(256, 1) void gemm9_kernel(GemmArgs p, unsigned long
 
   for (int u = 0; u < nmine; ++u) {
     if constexpr (ER != 0) {
-      G9_EBODY(true, true);
-      credit = 0;
-      for (int k = 1; k < pl.nk; ++k) G9_EBODY(false, false);
+      if constexpr (EPI == 1) {  // (the last body's fragment reads moved after the epilogue, below)
+        G9_EBODY(true, true, false);
+        credit = 0;
+        for (int k = 1; k < pl.nk - 1; ++k) G9_EBODY(false, false, false);
+        G9_EBODY(false, false, true);
+      } else {
+        G9_EBODY(true, true, false);
+        credit = 0;
+        for (int k = 1; k < pl.nk; ++k) G9_EBODY(false, false, false);
+      }
     } else {
       if constexpr (EPI == 1) {
         // the unit's last body reads no k-step-0 fragments of the next unit: those 64 registers
