@@ -197,109 +197,6 @@ __global__ __launch_bounds__(CE_NT) void ce_kernel(CEArgs p) {
   }
 }
 
-// ce_kernel with ONE exponential per logit (mode 3): the statistics pass keeps exp(f - chunk max)
-// as packed f16 in the chunk's registers (in place of the logits) plus the chunk max, and the
-// gradient is e * exp(chunk max - lse) * scale -- one v_exp per 8 logits there instead of per
-// logit.  (f16: 2^-11 relative, below the bf16 rounding of the stored gradient; values under
-// 2^-24 flush to zero -- a gradient of < 6e-8 * scale.)  Non-temporal gradient stores.
-typedef _Float16 dpc_h2_t __attribute__((ext_vector_type(2)));
-__device__ __forceinline__ unsigned pack2h(float a, float b) {
-  return __builtin_bit_cast(unsigned, __builtin_amdgcn_cvt_pkrtz(a, b));
-}
-__device__ __forceinline__ void unpack2h(unsigned w, float& a, float& b) {
-  const dpc_h2_t h = __builtin_bit_cast(dpc_h2_t, w);
-  a = (float)h.x;
-  b = (float)h.y;
-}
-
-// statistics of one chunk, leaving exp(f - chunk max) as packed f16 in its place
-__device__ __forceinline__ void ce1x_chunk_stats(uint4& raw, float& cmo, int c, int V, long long tgt, float& m,
-                                                 float& s, float& bv, int& bi, float* tval) {
-  float f[8];
-  unpack8(raw, f);
-  float cm = -INFINITY;
-#pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    const int idx = c * 8 + j;
-    if (idx >= V) f[j] = -INFINITY;
-    if (idx == tgt) *tval = f[j];
-    cm = fmaxf(cm, f[j]);
-    if (f[j] > bv) { bv = f[j]; bi = idx; }
-  }
-  cmo = cm;
-  if (cm == -INFINITY) {  // past the row end
-    raw = make_uint4(0u, 0u, 0u, 0u);
-    return;
-  }
-  float e[8], cs = 0.f;
-#pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    e[j] = __expf(f[j] - cm);
-    cs += e[j];
-  }
-  ms_combine(m, s, cm, cs);
-  raw = make_uint4(pack2h(e[0], e[1]), pack2h(e[2], e[3]), pack2h(e[4], e[5]), pack2h(e[6], e[7]));
-}
-
-__device__ __forceinline__ void ce1x_chunk_grad(const uint4& raw, float cm, int c, long long tgt, float lse,
-                                                float scale, uint4* dst) {
-  const float k = cm == -INFINITY ? 0.f : __expf(cm - lse) * scale;
-  float f[8];
-  unpack2h(raw.x, f[0], f[1]);
-  unpack2h(raw.y, f[2], f[3]);
-  unpack2h(raw.z, f[4], f[5]);
-  unpack2h(raw.w, f[6], f[7]);
-#pragma unroll
-  for (int j = 0; j < 8; ++j) f[j] = f[j] * k - (c * 8 + j == tgt ? scale : 0.f);
-  const uint4 o = pack8(f);
-  typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
-  __builtin_nontemporal_store(u32x4_t{o.x, o.y, o.z, o.w}, reinterpret_cast<u32x4_t*>(dst));
-}
-
-template <int NC>
-__global__ __launch_bounds__(CE_NT) void ce1x_kernel(CEArgs p) {
-  __shared__ float red_m[CE_NT / 64], red_s[CE_NT / 64], red_v[CE_NT / 64], tv;
-  __shared__ int red_i[CE_NT / 64];
-  const long long row = blockIdx.x;
-  const int tid = threadIdx.x;
-  const bf16_t* x = static_cast<const bf16_t*>(p.logits) + row * p.ld;
-  const uint4* xv = reinterpret_cast<const uint4*>(x);
-  const long long tgt = p.targets[row];
-  const bool valid = tgt != p.ignore_index && tgt >= 0 && tgt < p.V;
-  const int nch = (p.V + 7) >> 3;
-  uint4 raw[NC];
-  float cmx[NC];
-#pragma unroll
-  for (int u = 0; u < NC; ++u) {
-    const int c = tid + u * CE_NT;
-    raw[u] = c < nch ? xv[c] : make_uint4(0u, 0u, 0u, 0u);
-  }
-  float m = -INFINITY, s = 0.f, bv = -INFINITY, tval = 0.f;
-  int bi = 0x7fffffff;
-#pragma unroll
-  for (int u = 0; u < NC; ++u) {
-    const int c = tid + u * CE_NT;
-    cmx[u] = -INFINITY;
-    if (c < nch) ce1x_chunk_stats(raw[u], cmx[u], c, p.V, tgt, m, s, bv, bi, &tval);
-  }
-  if (valid && tgt / 8 % CE_NT == tid) tv = tval;
-  ce_block_reduce<CE_NT / 64>(m, s, bv, bi, red_m, red_s, red_v, red_i);  // (its barrier publishes tv)
-  const float lse = m + __logf(s);
-  if (tid == 0) {
-    p.row_loss[row] = valid ? lse - tv : 0.f;
-    if (p.row_correct) p.row_correct[row] = (valid && bi == tgt) ? 1.f : 0.f;
-  }
-  if (!p.write_grad) return;
-  const float scale = valid ? *p.inv_count : 0.f;
-  uint4* g = reinterpret_cast<uint4*>(static_cast<bf16_t*>(p.dlogits) + row * p.ld);
-  const int nchl = (int)(p.ld >> 3);
-#pragma unroll
-  for (int u = 0; u < NC; ++u) {
-    const int c = tid + u * CE_NT;
-    if (c < nchl) ce1x_chunk_grad(raw[u], cmx[u], c, tgt, lse, scale, g + c);
-  }
-}
-
 // Streaming fallback for rows longer than CE_NT * 16 chunks (V > 65536): CE_UNROLL chunks in
 // flight per thread per trip, the gradient pass re-reads the row.
 template <int CE_UNROLL>
@@ -623,8 +520,10 @@ DPC_API int dpc_embedding_bwd(const EmbArgs* a, hipStream_t stream) {
 }
 
 // 0: register-resident rows when they fit (default); 1 / 2: streaming with 1 / 4 chunks in
-// flight per thread; 3: register-resident with one exponential per logit (ce1x_kernel) (A/B
-// sweeps: bench/ce_one.py)
+// flight per thread (A/B sweeps: bench/ce_one.py).  Mode 0 runs at the speed of a plain in-place
+// copy of the logits (2.77 ms at GPT-2 small B = 64, 4.77 TB/s); a round-4 variant with one
+// exponential per logit (exp kept as f16 between the passes) measured 3.17 ms and was removed
+// (profiles/r4_ce/).
 static int g_ce_mode = -1;  // -1: DPC_CE_MODE (default 0)
 DPC_API void dpc_ce_set_mode(int m) { g_ce_mode = m; }
 
@@ -634,11 +533,6 @@ DPC_API int dpc_cross_entropy(const CEArgs* a, hipStream_t stream) {
   const long long nc = ((a->ld >> 3) + CE_NT - 1) / CE_NT;  // chunks per thread (ld >= V)
   const dim3 grid((unsigned)a->T);
   if (g_ce_mode < 0) g_ce_mode = getenv("DPC_CE_MODE") ? atoi(getenv("DPC_CE_MODE")) : 0;
-  if (g_ce_mode == 3 && nc <= 13) {
-    if (nc <= 8) hipLaunchKernelGGL(ce1x_kernel<8>, grid, dim3(CE_NT), 0, stream, *a);
-    else hipLaunchKernelGGL(ce1x_kernel<13>, grid, dim3(CE_NT), 0, stream, *a);
-    return (int)hipGetLastError();
-  }
   if (g_ce_mode == 1) hipLaunchKernelGGL(ce_stream_kernel<1>, grid, dim3(256), 0, stream, *a);
   else if (g_ce_mode == 2) hipLaunchKernelGGL(ce_stream_kernel<4>, grid, dim3(256), 0, stream, *a);
   else if (nc <= 1) hipLaunchKernelGGL(ce_kernel<1>, grid, dim3(CE_NT), 0, stream, *a);
