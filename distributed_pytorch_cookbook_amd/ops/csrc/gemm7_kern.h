@@ -1086,7 +1086,20 @@ __global__ __launch_bounds__(256) void g7_splitk_reduce(float* C, long long ldc,
     const long long m = i / (N >> 2), n = (i - m * (N >> 2)) << 2;
     const float* w = ws + m * N + n;
     float4 v = *reinterpret_cast<const float4*>(w);
-    for (int k = 1; k < s; ++k) {
+    // four slabs' loads in flight before their adds (the one-at-a-time loop waited for each:
+    // 2.9 TB/s), the adds in the same order as before (bitwise the same sums)
+    int k = 1;
+    for (; k + 3 < s; k += 4) {
+      const float4 u0 = *reinterpret_cast<const float4*>(w + k * slab);
+      const float4 u1 = *reinterpret_cast<const float4*>(w + (k + 1) * slab);
+      const float4 u2 = *reinterpret_cast<const float4*>(w + (k + 2) * slab);
+      const float4 u3 = *reinterpret_cast<const float4*>(w + (k + 3) * slab);
+      v.x += u0.x; v.y += u0.y; v.z += u0.z; v.w += u0.w;
+      v.x += u1.x; v.y += u1.y; v.z += u1.z; v.w += u1.w;
+      v.x += u2.x; v.y += u2.y; v.z += u2.z; v.w += u2.w;
+      v.x += u3.x; v.y += u3.y; v.z += u3.z; v.w += u3.w;
+    }
+    for (; k < s; ++k) {
       const float4 u = *reinterpret_cast<const float4*>(w + k * slab);
       v.x += u.x; v.y += u.y; v.z += u.z; v.w += u.w;
     }
