@@ -40,7 +40,8 @@ constexpr int G9_NL = G9_TA / 512 / 4;      // 1-KiB pieces per wave per operand
 // EPI 0: plain products; EPI 4: split-K partial tiles into the f32 workspace slab of their
 // k-range (as v7 EPI 4: unit = split * tiles + tile, pl.nk = stages per split, pl.nk_all =
 // stages of the whole product -- whole stages past it are issued with empty descriptors).
-// ER (early release, 0 = the schedule above; the plain products default to 4): phase 0 reads ALL of stage t's k-step-1 fragments
+// ER (early release; 0 = the schedule above, the library launches 4 -- DPC_G9_ER /
+// DPC_G9_FWD_ER): phase 0 reads ALL of stage t's k-step-1 fragments
 // in its first ER groups (16 / ER reads per group, one per MFMA gap), then lgkmcnt(0) + an extra
 // barrier -- every wave is done with stage t's buffer -- and the DMA of stage t+2 starts right
 // there (pairs in phase 0 groups ER..7, the rest in phase 1), instead of in phase 1.  A stage's
@@ -96,7 +97,7 @@ __global__ __launch_bounds__(256, 1) void gemm9_kernel(GemmArgs p, unsigned long
       // (no bias: an empty descriptor, the copy reads zeros -- the epilogue adds without a branch)
       const long long rem = p.bias ? (long long)(p.N - n0) * 4 : 0;
       const unsigned nb = rem <= 0 ? 0u : (rem > 1024 ? 1024u : (unsigned)rem);
-      const auto rs = __builtin_amdgcn_make_buffer_rsrc((void*)(p.bias + n0), 0, nb, 0x00020000);
+      const auto rs = __builtin_amdgcn_make_buffer_rsrc((void*)(p.bias ? p.bias + n0 : p.bias), 0, nb, 0x00020000);
       g7_m0(reinterpret_cast<const bf16_t*>(sbias + ((ui & 1) * 4 + wid) * 256));
       g7_ld<0>(rs, lane * 16);
     }
