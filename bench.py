@@ -230,6 +230,7 @@ def main():
                    "tokens_per_step": tokens_per_step, "final_loss": round(loss_v, 4),
                    "peak_mem_gib": round(float(peak.item()), 1),
                    "force_dist_path": bool(a.force_dist_path),
+                   "reduce_dtype": a.reduce_dtype, "pp_comm_dtype": a.pp_comm_dtype,
                    "mfu_per_gpu": round(mfu(value / n, train_flops_per_token(
                        args.dim, args.heads, args.head_dim, args.num_layers, vocab, S)), 4),
                    "baseline": ("stock PyTorch reference-default recipe (manual attention + torch.compile)"
