@@ -456,6 +456,11 @@ def _want_native(kind: str, device) -> bool:
     if kind == "torch":
         return False
     dev = torch.device(device) if device is not None else torch.device("cpu")
+    if dev.type == "cpu":
+        # `--comm native` on CPU runs only against a host-side RCCL stand-in named by
+        # DPC_RCCL_LIB (tests/fakes/fake_rccl_hip.cpp, which moves host buffers between the
+        # ranks): the CPU tests drive the production transport's multi-rank code through it
+        return kind == "native" and bool(os.environ.get("DPC_RCCL_LIB")) and dist.is_initialized()
     return (dev.type == "cuda" and dist.is_initialized() and dist.get_backend() == "nccl")
 
 

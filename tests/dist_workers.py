@@ -366,3 +366,75 @@ def worker_capture_fallback(rank, world, out, kind, inject, no_reset):
     sd = eng.full_state_dict()
     if rank == 0:
         torch.save({k: v.clone() for k, v in sd.items()}, out)
+
+
+def worker_fake_rccl_semantics(rank, world, fake, fake_dir):
+    """NativeComm over the data-moving fake RCCL (tests/fakes/fake_rccl_hip.cpp, FAKE_DIR):
+    every collective's result on every rank, grouped ring send/recv, and ncclCommSplit."""
+    import os
+
+    os.makedirs(fake_dir, exist_ok=True)
+    _use_fake(fake)
+    os.environ["FAKE_DIR"] = fake_dir
+    from distributed_pytorch_cookbook_amd.parallel import comm
+    from distributed_pytorch_cookbook_amd.parallel.native_comm import NativeComm
+
+    comm.init_dist(force_cpu=True)
+    c = NativeComm(None, device="cpu")
+    assert (c.rank, c.size) == (rank, world)
+    base = torch.arange(12, dtype=torch.float32) + 100 * rank
+    # all-reduce sum / max / avg, f32, bf16 and int64
+    t = base.clone()
+    c.all_reduce(t)
+    assert torch.equal(t, sum(torch.arange(12, dtype=torch.float32) + 100 * r for r in range(world)))
+    t = base.clone()
+    c.all_reduce(t, op="max")
+    assert torch.equal(t, torch.arange(12, dtype=torch.float32) + 100 * (world - 1))
+    t = base.clone()
+    c.all_reduce(t, op="avg")
+    assert torch.allclose(t, torch.arange(12, dtype=torch.float32) + 50 * (world - 1))
+    tb = base.bfloat16()
+    c.all_reduce(tb)
+    assert torch.equal(tb, sum(torch.arange(12, dtype=torch.float32) + 100 * r for r in range(world)).bfloat16())
+    ti = torch.full((3,), rank + 1, dtype=torch.int64)
+    c.all_reduce(ti)
+    assert ti.tolist() == [world * (world + 1) // 2] * 3
+    # reduce-scatter: chunk `rank` of the summed input
+    inp = torch.arange(4 * world, dtype=torch.float32) * (rank + 1)
+    out = torch.empty(4)
+    c.reduce_scatter(out, inp)
+    scale = world * (world + 1) / 2
+    assert torch.equal(out, torch.arange(4 * rank, 4 * rank + 4, dtype=torch.float32) * scale)
+    # all-gather / broadcast
+    g = torch.empty(3 * world)
+    c.all_gather(g, torch.full((3,), float(rank)))
+    assert g.tolist() == [float(r) for r in range(world) for _ in range(3)]
+    bc = torch.full((5,), float(rank))
+    c.broadcast(bc, src=2)
+    assert bc.tolist() == [2.0] * 5
+    # grouped ring exchange: send to the right, receive from the left (deadlock-free only
+    # because the group posts every send first)
+    right, left = (rank + 1) % world, (rank - 1) % world
+    rx = torch.empty(6)
+    for step in range(3):
+        tx = torch.full((6,), float(10 * rank + step))  # (alive until the group has run)
+        with c.grouped():
+            c.send(tx, right)
+            c.recv(rx, left)
+        assert rx.tolist() == [float(10 * left + step)] * 6
+    # 2 x 2 split: colour = rank // 2, key = -rank (reversed order inside a colour)
+    sub = c.split(color=rank // 2, key=-rank)
+    assert sub.size == 2 and sub.rank == 1 - rank % 2, (sub.rank, sub.size)
+    s = torch.tensor([float(rank)])
+    sub.all_reduce(s)
+    lo = 2 * (rank // 2)
+    assert s.item() == float(lo + lo + 1)
+    # p2p on the split communicator: peer numbers are sub-communicator ranks
+    peer = 1 - sub.rank
+    got, tx = torch.empty(2), torch.tensor([float(rank), 7.0])
+    with sub.grouped():
+        sub.send(tx, peer)
+        sub.recv(got, peer)
+    assert got.tolist() == [float(lo + (1 - rank % 2)), 7.0]
+    sub.destroy()
+    c.destroy()
