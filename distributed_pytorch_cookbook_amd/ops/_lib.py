@@ -208,6 +208,10 @@ def lib() -> ctypes.CDLL:
                 fn.restype = c_int
             handle.dpc_gemm_set_impl.argtypes = [c_int]
             handle.dpc_gemm_set_impl.restype = None
+            handle.dpc_gemm_set_variant.argtypes = [c_int, c_int]
+            handle.dpc_gemm_set_variant.restype = None
+            handle.dpc_gemm_last_kernel.argtypes = []
+            handle.dpc_gemm_last_kernel.restype = c_int
             handle.dpc_gemm_set_xcd_split.argtypes = [c_int]
             handle.dpc_gemm_set_xcd_split.restype = None
             handle.dpc_gemm_set_splits.argtypes = [c_int]
@@ -234,6 +238,18 @@ def set_gemm_impl(impl: int) -> None:
     global forced_gemm_impl
     forced_gemm_impl = int(impl)
     lib().dpc_gemm_set_impl(int(impl))
+
+
+def gemm_last_kernel() -> int:
+    """Family + epilogue of the last product the persistent-GEMM dispatcher launched (900 + EPI:
+    v9, 700 + EPI: v7, 750 + EPI: v8 / v7d; 0: it launched nothing -- a fallback ran)."""
+    return int(lib().dpc_gemm_last_kernel())
+
+
+def set_gemm_variant(key: int, value: int) -> None:
+    """Lab switch for same-process A/Bs of one kernel's variants (``gemm7.hip:g_variant``):
+    key 0 = v9 EPI 1 store layout (1: the round-4 half-line form); -1 = default."""
+    lib().dpc_gemm_set_variant(int(key), int(value))
 
 
 def set_gemm_splits(n: int) -> None:

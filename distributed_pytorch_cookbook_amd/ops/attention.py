@@ -6,12 +6,15 @@ f32, output heads merged back to ``[T, H*hd]``.  One deliberate difference: a qu
 whose every key is masked yields 0 here (the reference's finfo.min / -1e9 arithmetic
 yields an ill-defined average); such rows only occur for all-padding sequences.
 
-HIP path (bf16, head_dim 32 or 64 natively): ``dpc_attn_fwd`` / ``dpc_attn_bwd`` flash
+HIP path (bf16, head_dim 32, 64 or 128 natively): ``dpc_attn_fwd`` / ``dpc_attn_bwd`` flash
 kernels (``csrc/attention.hip``) -- O(S) memory, f32 log-sum-exp saved for the backward.
 f32 operands (``--disable_amp``) run ``dpc_attn_fwd_f32`` / ``dpc_attn_bwd_f32``
 (``csrc/attention_f32.hip``, f32 matrix cores), also O(S).
 head_dim 32 is the reference default config (``/root/reference/main-single.py:160``); other
-head sizes below 64 are zero-padded to the next kernel size on the way in.
+head sizes up to 128 are zero-padded to the next kernel size on the way in (16 -> 32, 48 -> 64,
+96 -> 128).  The reference's ``SelfAttention`` takes any ``--head_dim``
+(``/root/reference/models/gpt.py:44-66``): sizes above 128 run the reference math on the
+device (O(S^2) memory, correct but slow) rather than refusing.
 CPU / fp32 path: the same math with torch ops (test oracle).
 """
 from __future__ import annotations
@@ -22,20 +25,24 @@ import torch
 
 from . import _lib
 
-HD_KERNELS = (32, 64)
-HD_KERNEL = 64  # the largest
+HD_KERNELS = (32, 64, 128)
+HD_KERNEL = 128  # the largest
 
 
-def kernel_head_dim(head_dim: int) -> int:
-    """The kernel size a head of ``head_dim`` runs at (itself for 32 / 64, else padded up)."""
+def kernel_head_dim(head_dim: int) -> int | None:
+    """The kernel size a head of ``head_dim`` runs at (itself for 32 / 64 / 128, else padded
+    up); None above the largest kernel (the device then runs the reference math)."""
     for k in HD_KERNELS:
         if head_dim <= k:
             return k
-    raise NotImplementedError(f"attention kernel supports head_dim <= {HD_KERNEL}")
+    return None
 
 
-def _use_hip(t: torch.Tensor) -> bool:
-    """bf16 -> csrc/attention.hip; f32 (--disable_amp) -> csrc/attention_f32.hip."""
+def _use_hip(t: torch.Tensor, head_dim: int | None = None) -> bool:
+    """bf16 -> csrc/attention.hip; f32 (--disable_amp) -> csrc/attention_f32.hip; head sizes
+    past the largest kernel -> the reference math (on whatever device ``t`` is on)."""
+    if head_dim is not None and kernel_head_dim(head_dim) is None:
+        return False
     return t.is_cuda and t.dtype in (torch.bfloat16, torch.float32)
 
 
@@ -86,7 +93,7 @@ def attention_fwd(qkv: torch.Tensor, N: int, S: int, heads: int, head_dim: int,
                   out: torch.Tensor | None = None):
     """qkv [T = N*S, 3*H*hd] -> (o [T, H*hd], lse [N*H, S] f32)."""
     T = N * S
-    if not _use_hip(qkv):
+    if not _use_hip(qkv, head_dim):
         o, lse = attention_ref(qkv, N, S, heads, head_dim, pad_mask, causal)
         if out is not None:
             out.copy_(o)
@@ -142,7 +149,7 @@ def attention_bwd(dout: torch.Tensor, qkv: torch.Tensor, o: torch.Tensor, lse: t
                   dqkv: torch.Tensor | None = None) -> torch.Tensor:
     """Gradient w.r.t. the fused qkv buffer: returns dqkv [T, 3*H*hd] (qkv dtype)."""
     T = N * S
-    if not _use_hip(qkv):
+    if not _use_hip(qkv, head_dim):
         with torch.enable_grad():
             x = qkv.detach().float().requires_grad_(True)
             o_ref, _ = attention_ref(x, N, S, heads, head_dim, pad_mask, causal)

@@ -28,9 +28,11 @@ BUILD_DIR = HERE / "_build"
 LIB_PATH = HERE / "libdpc_kernels.so"
 ARCH = os.environ.get("DPC_OFFLOAD_ARCH", "gfx950")
 
+# gemm7_part*.hip: the persistent GEMM kernels' instantiations, dealt over several files that
+# compile in parallel (ops/gen_gemm_parts.py; gemm7.hip itself is the host-side dispatcher)
 SOURCES = ["gemm.hip", "gemm7.hip", "gemm_f32.hip", "attention.hip", "attention_f32.hip", "layernorm.hip", "misc.hip",
-           "decode.hip", "embed_bwd.hip"]
-HEADERS = ["common.h", "gemm.h", "gemm7_kern.h", "gemm9_kern.h"]
+           "decode.hip", "embed_bwd.hip"] + sorted(p.name for p in CSRC.glob("gemm7_part*.hip"))
+HEADERS = ["common.h", "gemm.h", "gemm7_kern.h", "gemm9_kern.h", "gemm7_extern.inc"]
 
 # code-object v5 keeps the library loadable by torch's bundled ROCm 7.0 runtime as
 # well as by the 7.2 toolchain in /opt/rocm.
@@ -90,18 +92,32 @@ def _compile(src: Path, obj: Path, verbose: bool) -> None:
         raise RuntimeError(f"hipcc failed for {src.name}:\n{r.stdout}\n{r.stderr}")
 
 
-def build(force: bool = False, jobs: int = 4, verbose: bool = False) -> Path:
+def _deps(name: str, seen=None) -> set:
+    """The local headers ``name`` includes, transitively."""
+    import re
+
+    seen = set() if seen is None else seen
+    for inc in re.findall(r'^#include "([^"]+)"', (CSRC / name).read_text(), re.M):
+        if inc not in seen and (CSRC / inc).exists():
+            seen.add(inc)
+            _deps(inc, seen)
+    return seen
+
+
+def build(force: bool = False, jobs: int = 8, verbose: bool = False) -> Path:
     if not force and not needs_build():
         return LIB_PATH
     BUILD_DIR.mkdir(exist_ok=True)
-    header_mtime = _newest([CSRC / h for h in HEADERS])
     todo = []
     objs = []
     for s in SOURCES:
         src, obj = CSRC / s, BUILD_DIR / (Path(s).stem + ".o")
         objs.append(obj)
-        if force or not obj.exists() or obj.stat().st_mtime < max(src.stat().st_mtime, header_mtime):
+        newest = _newest([src] + [CSRC / h for h in _deps(s)])
+        if force or not obj.exists() or obj.stat().st_mtime < newest:
             todo.append((src, obj))
+    # the longest compiles first (the GEMM parts), so the pool's tail is short
+    todo.sort(key=lambda so: 0 if "gemm7" in so[0].name else 1)
     with ThreadPoolExecutor(max_workers=max(1, jobs)) as ex:
         list(ex.map(lambda so: _compile(so[0], so[1], verbose), todo))
     tmp = LIB_PATH.with_suffix(".so.tmp")
@@ -119,7 +135,7 @@ def build(force: bool = False, jobs: int = 4, verbose: bool = False) -> Path:
 def main(argv=None) -> int:
     ap = argparse.ArgumentParser(description=__doc__)
     ap.add_argument("--force", action="store_true")
-    ap.add_argument("-j", "--jobs", type=int, default=4)
+    ap.add_argument("-j", "--jobs", type=int, default=8)
     ap.add_argument("-v", "--verbose", action="store_true")
     a = ap.parse_args(argv)
     path = build(force=a.force, jobs=a.jobs, verbose=a.verbose)

@@ -1,4 +1,4 @@
-// Flash attention (forward + backward) for gfx950: head_dim 32 or 64 natively (template HD),
+// Flash attention (forward + backward) for gfx950: head_dim 32, 64 or 128 natively (template HD),
 // bf16 in / bf16 out, f32 online softmax, causal + optional key-padding mask.
 //
 // Replaces the reference's materialised attention (/root/reference/models/gpt.py:75-100: q@k,
@@ -51,7 +51,7 @@ struct AttnArgs {
   int N, S, H;
   float scale;
   int causal;
-  int hd;                                       // head_dim: 32 or 64
+  int hd;                                       // head_dim: 32, 64 or 128
 };
 
 constexpr int KT = 64;       // keys (or queries) per staged tile
@@ -61,7 +61,7 @@ constexpr float LOG2E = 1.4426950408889634f;
 
 template <int HD>
 struct AT {
-  static_assert(HD == 32 || HD == 64, "head_dim 32 or 64");
+  static_assert(HD == 32 || HD == 64 || HD == 128, "head_dim 32, 64 or 128");
   static constexpr int TILE = KT * HD;   // elements of one 64-row tile
   static constexpr int NPW = HD / 32;    // 1-KiB DMA pieces per wave per tile (4 waves)
   static constexpr int NST = HD / 16;    // k-steps of a product over head_dim (32x32x16)
@@ -1155,6 +1155,22 @@ static int attn_var(int hd, int bwd) {
     default: hipLaunchKernelGGL((KERNEL<HD, false, 3>), __VA_ARGS__); break;                \
   }
 
+// head_dim 128 (e.g. main-single.py --head_dim 128; 96 and other sizes over 64 are padded up to
+// it): the same kernels at one workgroup per CU -- the 4-slot ring of K|V (or Q|dO) tiles is
+// 4 x 2 x 16 KiB = 128 KiB of LDS, and the doubled Q / O (K, V, dK, dV) register rows need the
+// 512-register budget.  (Correctness path; the GPT-2 presets run hd 64.)
+static int launch_fwd128(const AttnArgs* a, hipStream_t stream) {
+  dim3 grid((unsigned)(((a->S + QB - 1) / QB) * a->N * a->H));
+  hipLaunchKernelGGL((attn_fwd_kernel<128, 1, 1>), grid, dim3(256), 0, stream, *a);
+  return (int)hipGetLastError();
+}
+static int launch_bwd128(const AttnArgs* a, hipStream_t stream) {
+  dim3 grid((unsigned)(((a->S + QB - 1) / QB) * a->N * a->H));
+  hipLaunchKernelGGL((attn_bwd_dq_kernel<128, false, 1, 0, true>), grid, dim3(256), 0, stream, *a);
+  hipLaunchKernelGGL((attn_bwd_dkdv_kernel<128, false, 1>), grid, dim3(256), 0, stream, *a);
+  return (int)hipGetLastError();
+}
+
 template <int HD>
 static int launch_fwd(const AttnArgs* a, hipStream_t stream) {
   const int var = attn_var(HD, 0);
@@ -1201,9 +1217,9 @@ static int launch_bwd(const AttnArgs* a, hipStream_t stream) {
 
 using namespace dpc;
 
-// Host-side checks: the kernels assume 16-B aligned rows (ld % 8 == 0) and head_dim 32 / 64.
+// Host-side checks: the kernels assume 16-B aligned rows (ld % 8 == 0) and head_dim 32 / 64 / 128.
 static bool attn_args_ok(const AttnArgs* a, bool bwd) {
-  if (a->hd != 32 && a->hd != 64) return false;
+  if (a->hd != 32 && a->hd != 64 && a->hd != 128) return false;
   if (a->N <= 0 || a->S <= 0 || a->H <= 0) return false;
   if (a->ld_qkv % 8 || a->ld_o % 8 || (bwd && a->ld_dqkv % 8)) return false;
   return true;
@@ -1211,6 +1227,7 @@ static bool attn_args_ok(const AttnArgs* a, bool bwd) {
 
 DPC_API int dpc_attn_fwd(const AttnArgs* a, hipStream_t stream) {
   if (!attn_args_ok(a, false)) return (int)hipErrorInvalidValue;
+  if (a->hd == 128) return launch_fwd128(a, stream);
   return a->hd == 32 ? launch_fwd<32>(a, stream) : launch_fwd<64>(a, stream);
 }
 
@@ -1248,5 +1265,6 @@ DPC_API int dpc_attn_bwd_lab(const AttnArgs* a, int which, int abl, hipStream_t 
 
 DPC_API int dpc_attn_bwd(const AttnArgs* a, hipStream_t stream) {
   if (!attn_args_ok(a, true)) return (int)hipErrorInvalidValue;
+  if (a->hd == 128) return launch_bwd128(a, stream);
   return a->hd == 32 ? launch_bwd<32>(a, stream) : launch_bwd<64>(a, stream);
 }

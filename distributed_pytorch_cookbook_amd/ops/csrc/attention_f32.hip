@@ -88,7 +88,7 @@ __device__ __forceinline__ void xcd_work(int nblk, int& bh, int& i) {
 
 // ------------------------------------------------------------------ forward
 template <int HD>
-__global__ __launch_bounds__(256, 2) void fwd_kernel(AttnArgs p) {
+__global__ __launch_bounds__(256, HD >= 128 ? 1 : 2) void fwd_kernel(AttnArgs p) {
   constexpr int LK = HD + 2, LV = HD + 8, NDT = HD / 32;
   __shared__ float sk[2][T * LK];
   __shared__ float sv[2][T * LV];
@@ -234,7 +234,7 @@ __global__ __launch_bounds__(256) void pre_kernel(AttnArgs p) {
 }
 
 template <int HD>
-__global__ __launch_bounds__(256, HD == 64 ? 1 : 2) void dkdv_kernel(AttnArgs p) {
+__global__ __launch_bounds__(256, HD >= 64 ? 1 : 2) void dkdv_kernel(AttnArgs p) {
   constexpr int LQ = HD + 2, NDT = HD / 32;
   __shared__ float sq[2][T * LQ];
   __shared__ float sd[2][T * LQ];
@@ -352,7 +352,7 @@ __global__ __launch_bounds__(256, HD == 64 ? 1 : 2) void dkdv_kernel(AttnArgs p)
 }
 
 template <int HD>
-__global__ __launch_bounds__(256, 2) void dq_kernel(AttnArgs p) {
+__global__ __launch_bounds__(256, HD >= 128 ? 1 : 2) void dq_kernel(AttnArgs p) {
   constexpr int LK = HD + 2, NDT = HD / 32;
   __shared__ float sk[2][T * LK];
   __shared__ float sv[2][T * LK];
@@ -468,17 +468,19 @@ int bwd(const AttnArgs* a, hipStream_t stream) {
 using namespace dpc;
 
 static bool f32_attn_ok(const AttnArgs* a, bool bwd) {
-  if (a->hd != 32 && a->hd != 64) return false;
+  if (a->hd != 32 && a->hd != 64 && a->hd != 128) return false;
   if (a->N <= 0 || a->S <= 0 || a->H <= 0) return false;
   return !(a->ld_qkv % 4 || a->ld_o % 4 || (bwd && a->ld_dqkv % 4));
 }
 
 DPC_API int dpc_attn_fwd_f32(const AttnArgs* a, hipStream_t stream) {
   if (!f32_attn_ok(a, false)) return (int)hipErrorInvalidValue;
+  if (a->hd == 128) return f32a::fwd<128>(a, stream);
   return a->hd == 32 ? f32a::fwd<32>(a, stream) : f32a::fwd<64>(a, stream);
 }
 
 DPC_API int dpc_attn_bwd_f32(const AttnArgs* a, hipStream_t stream) {
   if (!f32_attn_ok(a, true)) return (int)hipErrorInvalidValue;
+  if (a->hd == 128) return f32a::bwd<128>(a, stream);
   return a->hd == 32 ? f32a::bwd<32>(a, stream) : f32a::bwd<64>(a, stream);
 }

@@ -32,6 +32,8 @@
 //        can be in body(q).
 // Reference: every nn.Linear of /root/reference/models/gpt.py:29-30,60-64,219.
 #include "gemm9_kern.h"
+// every kernel instantiation below is compiled in gemm7_part*.hip (ops/gen_gemm_parts.py)
+#include "gemm7_extern.inc"
 
 using namespace dpc;
 
@@ -65,10 +67,13 @@ static inline long long g7_operand_bytes(long long rows, long long cols, long lo
   return ((rows - 1) * ld + ((cols + 7) / 8) * 8) * 2;
 }
 
+static int g_last_kernel = 0;  // (dpc_gemm_last_kernel, below)
+
 template <int EPI, int SCHED, int WN = 128>
 static void g7_launch(const GemmArgs* a, const G7Plan& pl, hipStream_t stream, unsigned long long ab,
                       unsigned long long bb) {
   dim3 grid(pl.grid), block(256);
+  g_last_kernel = 700 + EPI + (WN == 64 ? 50 : 0);
   if (a->a_kmaj && a->b_kmaj) hipLaunchKernelGGL((gemm7_kernel<EPI, SCHED, true, true, WN>), grid, block, 0, stream, *a, ab, bb, pl);
   else if (a->a_kmaj) hipLaunchKernelGGL((gemm7_kernel<EPI, SCHED, true, false, WN>), grid, block, 0, stream, *a, ab, bb, pl);
   else if (!a->b_kmaj) hipLaunchKernelGGL((gemm7_kernel<EPI, SCHED, false, false, WN>), grid, block, 0, stream, *a, ab, bb, pl);
@@ -114,6 +119,7 @@ static bool g7d_launch(const GemmArgs* a, const G7Plan& pl, hipStream_t stream, 
                        unsigned long long bb) {
   dim3 grid(pl.grid), block(256);
   if (!g7_bias_ok(a)) return false;
+  g_last_kernel = 750 + EPI;
   if (EPI == 5 && a->a_kmaj && a->b_kmaj) {
     hipLaunchKernelGGL((gemm7d_kernel<5, 3, true, true>), grid, block, 0, stream, *a, ab, bb, pl);
     return true;
@@ -139,6 +145,16 @@ static bool g7d_launch(const GemmArgs* a, const G7Plan& pl, hipStream_t stream, 
 // zeros past it), N % 8 == 0, 16-B aligned C / bias / residual, 8-B aligned aux.
 static int g7_act_lds = -1;  // -1: DPC_G7_ACTLDS (default on); 0 / 1 forced (A/B sweeps)
 DPC_API void dpc_gemm7_set_act_lds(int v) { g7_act_lds = v; }
+// lab switches for interleaved same-process A/Bs (bench/epi_decomp.py): variant k = v, -1 default
+//   (none wired at the moment; round 5 used key 0 for the v9 EPI 1 store-layout A/B)
+static int g_variant[8] = {-1, -1, -1, -1, -1, -1, -1, -1};
+// the kernel family + epilogue of the last product dpc_gemm7 launched (tests assert a forced
+// implementation really ran instead of falling back): 900 + EPI for v9, 700 + EPI for v7
+// (+ 50 for v8), 750 + EPI for v7d
+DPC_API int dpc_gemm_last_kernel() { return g_last_kernel; }
+DPC_API void dpc_gemm_set_variant(int k, int v) {
+  if (k >= 0 && k < 8) g_variant[k] = v;
+}
 static int g7_res_lds = -1;  // -1: DPC_G7_RESLDS (default on); 0 / 1 forced (A/B sweeps)
 DPC_API void dpc_gemm7_set_res_lds(int v) { g7_res_lds = v; }
 
@@ -159,6 +175,7 @@ DPC_API int dpc_gemm7_ok(const GemmArgs* a) {
 // wn: 128 = v7 (256 x 256 tiles, one workgroup per CU), 64 = v8 (256 x 128 tiles, two per CU;
 // split-K through workspace slabs only)
 DPC_API int dpc_gemm7(const GemmArgs* a, int persistent, int sched, int splits, hipStream_t stream, int wn) {
+  g_last_kernel = 0;
   if (a->M <= 0 || a->N <= 0) return 0;
   if (!dpc_gemm7_ok(a)) return -1;
   const long long ab = g7_operand_bytes(a->a_r, a->a_c, a->lda);
@@ -266,11 +283,11 @@ DPC_API int dpc_gemm7(const GemmArgs* a, int persistent, int sched, int splits, 
       static int er_env = -1;
       if (er_env < 0) er_env = getenv("DPC_G9_ER") ? atoi(getenv("DPC_G9_ER")) : 4;
       if (er_env == 2)
-        hipLaunchKernelGGL((gemm9_kernel<0, true, true, 0, 2>), dim3(p9.grid), dim3(256), 0, stream, *a, ab, bb, p9);
+        { g_last_kernel = 900; hipLaunchKernelGGL((gemm9_kernel<0, true, true, 0, 2>), dim3(p9.grid), dim3(256), 0, stream, *a, ab, bb, p9); }
       else if (er_env == 4)
-        hipLaunchKernelGGL((gemm9_kernel<0, true, true, 0, 4>), dim3(p9.grid), dim3(256), 0, stream, *a, ab, bb, p9);
+        { g_last_kernel = 900; hipLaunchKernelGGL((gemm9_kernel<0, true, true, 0, 4>), dim3(p9.grid), dim3(256), 0, stream, *a, ab, bb, p9); }
       else
-        hipLaunchKernelGGL((gemm9_kernel<0, true, true>), dim3(p9.grid), dim3(256), 0, stream, *a, ab, bb, p9);
+        { g_last_kernel = 900; hipLaunchKernelGGL((gemm9_kernel<0, true, true>), dim3(p9.grid), dim3(256), 0, stream, *a, ab, bb, p9); }
       return (int)hipGetLastError();
     }
     // plain input gradients (A k-major, B mn-major) on v9 only when the table asks for it (impl
@@ -283,12 +300,14 @@ DPC_API int dpc_gemm7(const GemmArgs* a, int persistent, int sched, int splits, 
       G7Plan p9 = pl;
       p9.nk = a->K / 64;
       p9.nk_all = p9.nk;
+      // (this path is built for ER 4 and ER 0 only: DPC_G9_ER=2 runs ER 0 here, so an ER-2 A/B
+      // covers the nt forward products alone)
       static int er_km = -1;
       if (er_km < 0) er_km = getenv("DPC_G9_ER") ? atoi(getenv("DPC_G9_ER")) : 4;
       if (er_km == 4)
-        hipLaunchKernelGGL((gemm9_kernel<0, true, false, 0, 4>), dim3(p9.grid), dim3(256), 0, stream, *a, ab, bb, p9);
+        { g_last_kernel = 900; hipLaunchKernelGGL((gemm9_kernel<0, true, false, 0, 4>), dim3(p9.grid), dim3(256), 0, stream, *a, ab, bb, p9); }
       else
-        hipLaunchKernelGGL((gemm9_kernel<0, true, false>), dim3(p9.grid), dim3(256), 0, stream, *a, ab, bb, p9);
+        { g_last_kernel = 900; hipLaunchKernelGGL((gemm9_kernel<0, true, false>), dim3(p9.grid), dim3(256), 0, stream, *a, ab, bb, p9); }
       return (int)hipGetLastError();
     }
     // forward epilogues that read nothing per element (bias / activation / aux_out, no residual or
@@ -309,9 +328,9 @@ DPC_API int dpc_gemm7(const GemmArgs* a, int persistent, int sched, int splits, 
       static int fer = -1;
       if (fer < 0) fer = getenv("DPC_G9_FWD_ER") ? atoi(getenv("DPC_G9_FWD_ER")) : 4;
       if (fer == 4)
-        hipLaunchKernelGGL((gemm9_kernel<1, true, true, 0, 4>), dim3(p9.grid), dim3(256), 0, stream, *a, ab, bb, p9);
+        { g_last_kernel = 901; hipLaunchKernelGGL((gemm9_kernel<1, true, true, 0, 4>), dim3(p9.grid), dim3(256), 0, stream, *a, ab, bb, p9); }
       else
-        hipLaunchKernelGGL((gemm9_kernel<1, true, true>), dim3(p9.grid), dim3(256), 0, stream, *a, ab, bb, p9);
+        { g_last_kernel = 901; hipLaunchKernelGGL((gemm9_kernel<1, true, true>), dim3(p9.grid), dim3(256), 0, stream, *a, ab, bb, p9); }
       return (int)hipGetLastError();
     }
     // weight gradients (both operands mn-major, split K through workspace slabs) on v9, with the
@@ -327,7 +346,7 @@ DPC_API int dpc_gemm7(const GemmArgs* a, int persistent, int sched, int splits, 
       G7Plan p9 = pl;
       p9.nk_all = (a->K + 63) / 64;
       p9.nk = (p9.nk_all + s - 1) / s;
-      hipLaunchKernelGGL((gemm9_kernel<4, false, false>), dim3(p9.grid), dim3(256), 0, stream, *a, ab, bb, p9);
+      { g_last_kernel = 904; hipLaunchKernelGGL((gemm9_kernel<4, false, false>), dim3(p9.grid), dim3(256), 0, stream, *a, ab, bb, p9); }
       const long long nq = (long long)a->M * (a->N / 4);
       const int blocks = (int)std::min<long long>((nq + 255) / 256, 4096);
       hipLaunchKernelGGL(g7_splitk_reduce, dim3(blocks), dim3(256), 0, stream, static_cast<float*>(a->C), a->ldc,

@@ -750,7 +750,7 @@ __device__ __forceinline__ void g7_epilogue_atomic(const GemmArgs& p, floatx4 (&
 // that keep the instruction stream otherwise unchanged -- 16 = no workgroup barrier per slice,
 // 32 = no fragment reads (the prologue's fragments are reused), 64 = no counted vmcnt waits in
 // the loop, 128 = per-workgroup clock stamps into g7_clk (the in-kernel clock, DVFS check).
-__device__ unsigned long long g7_clk[2 * 2048];
+static __device__ unsigned long long g7_clk[2 * 2048];  // (per translation unit: lab only)
 
 template <int EPI, int SCHED, bool AK, bool BK, int WN = 128, int ABL = 0>
 __global__ __launch_bounds__(256, WN == 128 ? 1 : 2) void gemm7_kernel(GemmArgs p, unsigned long long a_bytes,
@@ -1060,7 +1060,7 @@ __global__ __launch_bounds__(256, WN == 128 ? 1 : 2) void gemm7_kernel(GemmArgs 
 // colsum[n] += sum over the R rows of ws [R][N] (g7_epilogue_act_lds's per-tile partial column
 // sums): 4 columns per thread, 16 rows per workgroup row (grid.y), one atomic per column per 16
 // rows
-__global__ __launch_bounds__(256) void g7_colsum_reduce(float* colsum, const float* ws, int R, int N) {
+static __global__ __launch_bounds__(256) void g7_colsum_reduce(float* colsum, const float* ws, int R, int N) {
   const int c4 = (blockIdx.x * 256 + threadIdx.x) * 4;
   if (c4 >= N) return;
   const int r0 = blockIdx.y * 16, r1 = min(R, r0 + 16);
@@ -1078,7 +1078,7 @@ __global__ __launch_bounds__(256) void g7_colsum_reduce(float* colsum, const flo
 
 // C (=, or += when accumulating) the sum of the s workspace slabs [s][M][N]; 4 columns per
 // thread (N % 8 == 0, ldc % 8 == 0: 16-B rows)
-__global__ __launch_bounds__(256) void g7_splitk_reduce(float* C, long long ldc, const float* ws, int M, int N,
+static __global__ __launch_bounds__(256) void g7_splitk_reduce(float* C, long long ldc, const float* ws, int M, int N,
                                                        int s, int accumulate, int nt = 0) {
   const long long nq = (long long)M * (N >> 2);
   const long long slab = (long long)M * N;

@@ -354,6 +354,9 @@ __global__ __launch_bounds__(256, 1) void gemm9_kernel(GemmArgs p, unsigned long
       // here, not hoisted out of the unit loop into registers the main loop would have to carry)
       int elane;
       asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(elane));
+      // (measured round 5: MODE 0's whole-line store layout for both outputs -- lanes l, l ^ 8
+      // trading a chunk so one store writes 8 rows x 128 B -- was SLOWER here than these 16-row
+      // x 64-B stores, 448.6 vs 405.5 us on the GPT-2 up-projection, bench/epi_decomp.py)
       g7_epilogue<1, NJ, true, true>(p, acc, m0 + ar, n0 + bc, elane, 0, sbias + ((u & 1) * 4 + wid) * 256 + bc);
     } else {
       // (ABL 512: the epilogue's VALU without its stores; ABL 1024: non-temporal stores -- lab only)

@@ -127,21 +127,26 @@ def cu_reserve_active() -> bool:
 # Run at one rank (bench.py --force_dist_path), it reproduces the CU co-residency of the
 # multi-GPU step -- the same launch points, sizes and overlap -- on a one-GPU box, to set
 # DPC_CU_RESERVE from measurements (bench/cu_corun.sh).
-_FAKE_COLL = os.environ.get("DPC_FAKE_COLL", "")
+# (parsed once at import; the occupier's sink is allocated when a NativeTransport is built --
+# outside any HIP-graph capture, so a captured step never owns it)
+_FAKE_COLL = tuple(float(v) for v in os.environ["DPC_FAKE_COLL"].split(",")) if os.environ.get("DPC_FAKE_COLL") else None
 _fake_sink = None
 
 
-def _fake_coll(op: str, tensors, stream) -> None:
+def _fake_sink_for(device) -> None:
     global _fake_sink
+    if _FAKE_COLL and _fake_sink is None and torch.device(device).type == "cuda":
+        _fake_sink = torch.zeros(4096, dtype=torch.int32, device=device)
+
+
+def _fake_coll(op: str, tensors, stream) -> None:
     from ..ops import _lib
 
-    cus, busbw, world = (float(v) for v in _FAKE_COLL.split(","))
+    cus, busbw, world = _FAKE_COLL
     nbytes = max((t.numel() * t.element_size() for t in tensors), default=0)
     factor = {"all_reduce": 2.0 * (world - 1) / world, "reduce_scatter": (world - 1) / world,
               "all_gather": (world - 1) / world}.get(op, 1.0)
     ns = int(factor * nbytes / (busbw * 1e9) * 1e9)
-    if _fake_sink is None:
-        _fake_sink = torch.zeros(4096, dtype=torch.int32, device=tensors[0].device)
     _lib.occupy(int(cus), ns, _fake_sink, stream)
 
 
@@ -365,6 +370,7 @@ class NativeTransport(Transport):
         # RCCL runs on its own high-priority stream, ordered with events (a CPU "device" is the
         # host-side fake library of the CPU tests: calls go straight through)
         self.stream = torch.cuda.Stream(device=self.device, priority=-1) if self.device.type == "cuda" else None
+        _fake_sink_for(self.device)
 
     def capturable(self) -> bool:
         return True

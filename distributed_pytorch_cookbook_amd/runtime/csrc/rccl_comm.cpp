@@ -250,13 +250,22 @@ Watchdog& wd = *new Watchdog;
           wd.rank, why.c_str(), wd.comms.size(), wd.exit_code);
   fflush(stderr);
   // ncclCommAbort can itself wait on a wedged device: give it a bounded time, then leave anyway.
-  // A destroy in progress on the main thread holds `life`; if it does not finish within 2 s the
-  // communicators are left to the process exit rather than aborted while being freed.
+  // A destroy in progress on the main thread holds `life` (so no communicator is aborted while
+  // it is being freed).  If that destroy does not finish within 2 s -- e.g. ncclCommDestroy
+  // waiting on the very collective that hung -- every OTHER registered communicator is still
+  // aborted: the one being destroyed was unregistered under `mu` before its destroy began (and
+  // the owner destroys one communicator at a time), so the copy below never holds it.
   std::vector<ncclComm_t> comms;
-  if (wd.life.try_lock_for(std::chrono::seconds(2))) {
+  const bool owned = wd.life.try_lock_for(std::chrono::seconds(2));
+  {
     std::lock_guard<std::mutex> lk(wd.mu);
     comms = wd.comms;
-  }  // (`life` stays held: this thread ends the process)
+  }  // (`life`, when taken, stays held: this thread ends the process)
+  if (!owned) {
+    fprintf(stderr, "[dpc watchdog] rank %d: a communicator destroy is stuck; aborting the other %zu\n", wd.rank,
+            comms.size());
+    fflush(stderr);
+  }
   std::atomic<bool> done{false};
   std::thread ab([&comms, &done] {
     for (ncclComm_t c : comms)

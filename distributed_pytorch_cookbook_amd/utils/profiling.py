@@ -16,19 +16,42 @@ import os
 import torch
 
 
+# roctx ranges (torch.cuda.nvtx maps to roctx on ROCm): usable or not is decided ONCE, at the
+# first range -- not per call on the hot path (every collective and pipeline micro-batch opens
+# one) -- and DPC_ROCTX=0 turns them off entirely.
+_ROCTX: bool | None = None if os.environ.get("DPC_ROCTX", "1") != "0" else False
+
+
+def _roctx_usable() -> bool:
+    global _ROCTX
+    if _ROCTX is None:
+        _ROCTX = False
+        if torch.cuda.is_available():
+            try:
+                torch.cuda.nvtx.range_push("dpc")
+                torch.cuda.nvtx.range_pop()
+                _ROCTX = True
+            except Exception:  # a build whose nvtx module is a stub
+                pass
+    return _ROCTX
+
+
 @contextlib.contextmanager
-def mark(name: str):
-    use = torch.cuda.is_available()
-    if use:
-        try:
-            torch.cuda.nvtx.range_push(name)
-        except Exception:
-            use = False
+def _range(name: str):
+    torch.cuda.nvtx.range_push(name)
     try:
         yield
     finally:
-        if use:
-            torch.cuda.nvtx.range_pop()
+        torch.cuda.nvtx.range_pop()
+
+
+_NULL = contextlib.nullcontext()
+
+
+def mark(name: str):
+    """A roctx range around a step phase (``rocprofv3 --marker-trace`` shows them), or a no-op
+    context when ranges are unavailable or disabled (DPC_ROCTX=0)."""
+    return _range(name) if _roctx_usable() else _NULL
 
 
 class StepProfiler:

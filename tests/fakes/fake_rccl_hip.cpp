@@ -28,6 +28,7 @@
 //   FAKE_ABORT_MARK=path ncclCommAbort appends "abort" to that file
 //   FAKE_LOG=path        every collective appends its name to that file
 //   FAKE_TIMEOUT_S=<s>   a rendezvous waits at most this long (default 120), then fails
+//   FAKE_DESTROY_SLEEP=<s> ncclCommDestroy blocks this long (a destroy stuck on a hung peer)
 #include <stdarg.h>
 #include <stdint.h>
 #include <stdio.h>
@@ -346,6 +347,7 @@ ncclResult_t ncclCommSplit(void* comm, int color, int key, void** out, void*) {
 }
 ncclResult_t ncclCommDestroy(void* comm) {
   log_op("destroy");
+  if (const char* v = getenv("FAKE_DESTROY_SLEEP")) sleep((unsigned)atoi(v));  // a hung destroy
   delete static_cast<Comm*>(comm);
   return 0;
 }

@@ -68,7 +68,7 @@ def test_gemm_f32_epilogues(act, aux_dtype):
     assert rel(out2, ref2) < 1e-5 and rel(cs, cs_ref) < 1e-5
 
 
-@pytest.mark.parametrize("hd", [64, 32])
+@pytest.mark.parametrize("hd", [64, 32, 128])
 @pytest.mark.parametrize("S,with_pad,causal", [(257, False, True), (200, True, True), (130, False, False)])
 def test_attention_f32(S, with_pad, causal, hd):
     torch.manual_seed(2)

@@ -181,8 +181,10 @@ def test_gemm_v9_forward_epilogue(M, N, K, with_bias, act, out_f32):
     _lib.set_gemm_impl(26)
     try:
         out = gemm(A, B, bias=bias, act=act, aux_out=aux, out_dtype=torch.float32 if out_f32 else torch.bfloat16)
+        ran = _lib.gemm_last_kernel()
     finally:
         _lib.set_gemm_impl(-1)
+    assert ran == 901, ran  # the v9 EPI 1 kernel itself, not a fallback
     ref = torch.empty(M, N, device=dev)
     aux_r = torch.empty_like(aux)
     _gemm_ref(a, b, True, True, ref, bias, act, 0, None, aux_r, None, 1.0, None, False)
@@ -374,11 +376,11 @@ def test_gemm_epilogues(act):
     assert rel_err(acc, ref2) < 2e-3
 
 
-@pytest.mark.parametrize("hd", [64, 32])
+@pytest.mark.parametrize("hd", [64, 32, 128])
 @pytest.mark.parametrize("S", [1023, 200, 64])
 @pytest.mark.parametrize("with_pad", [False, True])
 def test_attention_fwd_bwd(S, with_pad, hd, monkeypatch):
-    """Native head sizes 32 / 64 (no pad path) against the f32 O(S^2) reference."""
+    """Native head sizes 32 / 64 / 128 (no pad path) against the f32 O(S^2) reference."""
     import distributed_pytorch_cookbook_amd.ops.attention as attn_mod
 
     def _no_pad(*a, **k):
@@ -430,10 +432,11 @@ def test_attention_long_context(S, hd):
 
 
 @pytest.mark.parametrize("causal", [True, False])
-@pytest.mark.parametrize("hd", [16, 48, 32])
+@pytest.mark.parametrize("hd", [16, 48, 32, 96, 160])
 def test_attention_head_dim_other(hd, causal):
     """Head sizes without a kernel of their own run zero-padded to the next one (16 -> 32,
-    48 -> 64); also the non-causal form."""
+    48 -> 64, 96 -> 128); past the largest kernel (160) the device runs the reference math
+    (/root/reference/models/gpt.py:44-66 takes any head_dim); also the non-causal form."""
     torch.manual_seed(3)
     N, S, H = 2, 100, 4
     qkv = torch.randn(N * S, 3 * H * hd, device=dev).bfloat16()

@@ -136,13 +136,16 @@ def test_long_context_train_step():
     assert all(math.isfinite(l) for l in losses) and losses[-1] < losses[0], losses
 
 
-def test_main_single_recipe_gpu(tmp_path, monkeypatch):
+@pytest.mark.parametrize("head_dim", [64, 128])
+def test_main_single_recipe_gpu(tmp_path, monkeypatch, head_dim):
+    """main-single.py end to end on the GPU, including --head_dim 128 (the reference takes any
+    head size: /root/reference/main-single.py:160)."""
     from distributed_pytorch_cookbook_amd.recipes import run
 
     monkeypatch.chdir(tmp_path)
     trainer, path = run("single", ["--synthetic_data", "--batch_size", "8", "--epochs", "1",
                                    "--sequence_length", "128", "--dim", "128", "--heads", "2",
-                                   "--head_dim", "64", "--num_layers", "2", "--max_steps", "16",
+                                   "--head_dim", str(head_dim), "--num_layers", "2", "--max_steps", "16",
                                    "--train_samples", "256", "--val_samples", "16", "--num_workers", "0",
                                    "--learning_rate", "1e-3"])
     assert path is not None and path.exists()

@@ -141,3 +141,39 @@ def test_process_with_running_watchdog_exits_cleanly(fake_lib, tmp_path):
     r = subprocess.run([sys.executable, "-c", code], env=e, capture_output=True, text=True, timeout=120)
     assert r.returncode == 0 and "bye" in r.stdout, (r.returncode, r.stderr[-2000:])
     assert "terminate" not in r.stderr
+
+
+_DESTROY_STUCK = r"""
+import os, sys, time
+sys.path.insert(0, os.environ["ROOT"])
+import torch, torch.distributed as dist
+from distributed_pytorch_cookbook_amd.parallel.native_comm import NativeComm
+dist.init_process_group("gloo", init_method="tcp://127.0.0.1:%s" % os.environ["PORT"], rank=0, world_size=1)
+world = NativeComm(None, device="cpu")
+sub = world.split(color=0, key=0)
+world.all_reduce(torch.ones(4), stream=0)
+from distributed_pytorch_cookbook_amd.parallel import native_comm
+native_comm.watchdog_track(0, "all_reduce(4,)")   # stalls (fake event): the watchdog fires at 1 s
+print("destroying", flush=True)
+sub.destroy()                                     # ncclCommDestroy hangs (FAKE_DESTROY_SLEEP)
+print("destroy returned", flush=True)
+"""
+
+
+def test_watchdog_aborts_others_while_a_destroy_hangs(fake_lib, tmp_path):
+    """the watchdog fires while the main thread is stuck inside ncclCommDestroy (it
+    holds the `life` lock): after its 2 s grace the watchdog still aborts every OTHER registered
+    communicator (the parent here) and exits 17, instead of leaving them all live."""
+    mark = tmp_path / "abort.txt"
+    e = dict(os.environ, ROOT=ROOT, PORT=str(free_port()), DPC_RCCL_LIB=fake_lib, DPC_HIP_LIB=fake_lib,
+             DPC_COLL_TIMEOUT="1.0", DPC_WATCHDOG_POLL_MS="50", FAKE_ABORT_MARK=str(mark), FAKE_EVENT_STALL="1",
+             FAKE_DESTROY_SLEEP="60")
+    e.pop("DPC_WATCHDOG", None)
+    t0 = time.monotonic()
+    r = subprocess.run([sys.executable, "-c", _DESTROY_STUCK], env=e, capture_output=True, text=True, timeout=120)
+    dt = time.monotonic() - t0
+    assert r.returncode == 17, (r.returncode, r.stdout, r.stderr[-2000:])
+    assert "destroying" in r.stdout and "destroy returned" not in r.stdout
+    assert "destroy is stuck; aborting the other 1" in r.stderr, r.stderr[-2000:]
+    assert mark.read_text().count("abort") == 1  # the parent, not the communicator being destroyed
+    assert dt < 40, dt
