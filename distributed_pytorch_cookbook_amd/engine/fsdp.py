@@ -67,6 +67,12 @@ class FSDPEngine(Engine):
             out = self.model(**batch, targets=targets)
         with mark("bwd"):  # (re-gathers and reduce-scatters enqueued inside)
             self._scaled(out.loss).backward()
+        if self.scaler is None and not st.cpu_offload and st.sharded and st.tp.active:
+            # unit by unit: AdamW of the units already reduce-scattered on the compute stream
+            # while the remaining reduce-scatters are still on the comm stream
+            with mark("optim"):
+                st.finish_grads_and_update(self.opt, self.opt_rep, grad_scale=1.0 / self.dp_world)
+            return out.loss.detach()
         with mark("comm:finish_grads"):
             st.finish_grads()
         with mark("optim"):

@@ -198,15 +198,42 @@ class TransformerDecoderLM(nn.Module):
         # dropout: per-forward seeds = (dropout_seed_base << 32) | call counter
         self.dropout_seed_base = 0
         self._dropout_calls = 0
+        object.__setattr__(self, "_seed_dev", None)  # device counter (next_dropout_seed)
+        object.__setattr__(self, "_seed_dev_base", None)
+        object.__setattr__(self, "_seed_snaps", {})  # host seed -> its device snapshot
         self.recompute = False  # per-layer activation recompute in the backward
         for i, layer in enumerate(self.decoder.layers):
             layer._layer_index = i
 
     # ------------------------------------------------------------------ dropout
     def next_dropout_seed(self) -> int:
-        """Seed of the next training forward (each call advances the stream)."""
+        """Seed of the next training forward (each call advances the stream).
+
+        On a GPU the seed also lives in device memory: a snapshot of the device counter
+        (low word = forward count, high word = per-rank base) is taken and the counter is
+        advanced with device ops, so a captured step (the HIP-graph "compile") replays with a
+        new seed every time -- the kernels derive each site's key from the snapshot
+        (``ops/dropout.py:DropSpec``).  Eager, both counters advance together and give the
+        same masks as the host seed."""
         seed = ((self.dropout_seed_base & 0xFFFFFFFF) << 32) | (self._dropout_calls & 0xFFFFFFFF)
         self._dropout_calls += 1
+        dev = next((q.device for q in self.parameters() if q.device.type != "meta"), None)
+        if dev is not None and dev.type == "cuda":
+            import torch
+
+            def i32(v):
+                v &= 0xFFFFFFFF
+                return v - (1 << 32) if v >= (1 << 31) else v
+
+            base = i32(self.dropout_seed_base)
+            if self._seed_dev is None or self._seed_dev_base != base:
+                self._seed_dev = torch.tensor([i32(seed), base], dtype=torch.int32, device=dev)
+                self._seed_dev_base = base
+            snap = self._seed_dev.clone()
+            self._seed_dev[0:1].add_(1)  # (int32 wraps like the u32 word the kernels read)
+            self._seed_snaps[seed] = snap
+            while len(self._seed_snaps) > 256:  # (a pipeline step keeps at most M in flight)
+                self._seed_snaps.pop(next(iter(self._seed_snaps)))
         return seed
 
     def dropout_specs(self, layer, seed):
@@ -214,7 +241,9 @@ class TransformerDecoderLM(nn.Module):
         from ..ops.dropout import DropSpec
 
         i = layer._layer_index
-        return DropSpec.make(self.dropout, seed, 2 * i), DropSpec.make(self.dropout, seed, 2 * i + 1)
+        snap = self._seed_snaps.get(seed)
+        return (DropSpec.make(self.dropout, seed, 2 * i, snap),
+                DropSpec.make(self.dropout, seed, 2 * i + 1, snap))
 
     # ------------------------------------------------------------------ structure
     def units(self):

@@ -65,6 +65,7 @@ class LNArgs(ctypes.Structure):
         ("drop_key", c_uint), ("drop_thresh", c_uint), ("drop_scale", c_float),
         ("dy_bf16", c_int),
         ("add_y", P), ("add_bias", P), ("x_out", P), ("ld_add", LL), ("ld_xout", LL),
+        ("drop_seed", P), ("drop_site", c_uint),
     ]
 
 
@@ -119,6 +120,7 @@ class BiasActArgs(ctypes.Structure):
         ("T", c_int), ("N", c_int),
         ("act", c_int),
         ("drop_key", c_uint), ("drop_thresh", c_uint), ("drop_scale", c_float),
+        ("drop_seed", P), ("drop_site", c_uint),
     ]
 
 
@@ -129,6 +131,7 @@ class DropResArgs(ctypes.Structure):
         ("T", c_int), ("N", c_int),
         ("key", c_uint), ("thresh", c_uint),
         ("scale", c_float),
+        ("seed", P), ("site", c_uint),
     ]
 
 

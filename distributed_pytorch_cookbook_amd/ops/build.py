@@ -56,7 +56,11 @@ def hipcc() -> str:
 
 # per-file extras: attention never produces NaNs (masked scores are -inf), so maxnum needs
 # no canonicalisation of MFMA results and folds into v_max3_f32
-FILE_FLAGS = {"attention.hip": ["-fno-honor-nans"], "attention_f32.hip": ["-fno-honor-nans"]}
+# attention.hip: -fno-slp-vectorize -- at -O3 the SLP vectoriser packed the softmax row sums
+# into v_pk_add_f32 fed by v_mov_b32 pairs (32 moves + 13 packed adds per tile instead of 32
+# adds) and the dS products into v_pk_mul_f32; packed f32 VALU beside MFMAs costs extra issue
+# cycles (MI355X_MICROARCH.md: "an anti-lever beside MFMAs")
+FILE_FLAGS = {"attention.hip": ["-fno-honor-nans", "-fno-slp-vectorize"], "attention_f32.hip": ["-fno-honor-nans"]}
 
 
 def _newest(paths) -> float:

@@ -225,6 +225,16 @@ __device__ __forceinline__ bf16x8 load_row8(const bf16_t* p) {
 
 #define MFMA32(a, b, c) __builtin_amdgcn_mfma_f32_32x32x16_bf16((a), (b), (c), 0, 0, 0)
 
+// x *= a in place, element by element (inline asm with tied operands): written as plain C++
+// inside the lazy-rescale branch, hipcc gave the rescaled accumulator new registers and paid
+// 16 v_mov_b64 on EVERY tile to merge the two versions after the branch (round-5 asm of
+// attn_fwd2_kernel); a v_mul_f32 per element also avoids v_pk_mul_f32, which costs extra
+// issue cycles beside MFMAs (MI355X_MICROARCH.md, cycle constants)
+__device__ __forceinline__ void scale16(floatx16& x, float a) {
+#pragma unroll
+  for (int i = 0; i < 16; ++i) asm volatile("v_mul_f32 %0, %0, %1" : "+v"(x[i]) : "v"(a));
+}
+
 __device__ __forceinline__ void zero16(floatx16& x) {
 #pragma unroll
   for (int i = 0; i < 16; ++i) x[i] = 0.f;
@@ -372,9 +382,7 @@ __global__ __launch_bounds__(256, OCC) void attn_fwd_kernel(AttnArgs p) {
       m = mn;
       l *= alpha;
 #pragma unroll
-      for (int d = 0; d < A::NDT; ++d)
-#pragma unroll
-        for (int i = 0; i < 16; ++i) o[d][i] *= alpha;
+      for (int d = 0; d < A::NDT; ++d) scale16(o[d], alpha);
     }
     const float nmu = (m == -INFINITY) ? 0.f : -m;
     // ---- one basic block: next tile's S^T MFMAs || this tile's exponentials
@@ -688,9 +696,7 @@ __global__ __launch_bounds__(256, OCC) void attn_fwd2_kernel(AttnArgs p, int nit
       m = mn;
       if constexpr (!LMFMA) l *= alpha;
 #pragma unroll
-      for (int d = 0; d < NO; ++d)
-#pragma unroll
-        for (int k = 0; k < 16; ++k) o[d][k] *= alpha;
+      for (int d = 0; d < NO; ++d) scale16(o[d], alpha);
     }
     const float nmu = (m == -INFINITY) ? 0.f : -m;
     if (t + 1 <= last_w) qk(sn, lsn);  // next tile's scores beside this tile's exponentials

@@ -173,4 +173,13 @@ __device__ __forceinline__ float drop_factor(uint32_t idx, uint32_t key, uint32_
   return fmix32((idx * 0x9E3779B1u) ^ key) >= thresh ? scale : 0.f;
 }
 
+// The site key from a per-forward seed held in DEVICE memory (seed[0] = the model's forward
+// counter, seed[1] = the per-rank base: ops/dropout.py:DropSpec.make's hash, bit for bit), so a
+// replayed HIP graph draws fresh masks every step instead of the key frozen at capture.
+// seed == nullptr: the host-computed key.
+__device__ __forceinline__ uint32_t drop_key_of(const unsigned* seed, unsigned site, uint32_t host_key) {
+  if (!seed) return host_key;
+  return fmix32(fmix32(seed[0]) ^ fmix32(seed[1] + 0x632BE5ABu * (site + 1u)));
+}
+
 }  // namespace dpc

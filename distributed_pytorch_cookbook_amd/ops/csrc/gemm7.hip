@@ -245,7 +245,7 @@ DPC_API int dpc_gemm7(const GemmArgs* a, int persistent, int sched, int splits, 
     static int env = -1;
     if (env < 0) env = getenv("DPC_G7_ACTLDS") ? atoi(getenv("DPC_G7_ACTLDS")) : 1;
     const int on = g7_act_lds >= 0 ? g7_act_lds : env;
-    act_lds = on && !v8 && s == 1 && a->act_bwd && a->aux_in && a->ld_aux_in % 8 == 0 &&
+    act_lds = on && !v8 && s == 1 && a->act_bwd && a->aux_in && !a->out_f32 && a->ld_aux_in % 8 == 0 &&
               ((uintptr_t)a->aux_in % 16) == 0 && a->ld_aux_in <= (1 << 20);
   }
   // v7d: sched 5 (impl 24) takes the GELU / GELU' fused epilogues of full-depth products

@@ -133,6 +133,8 @@ __device__ __forceinline__ void sfor(F&& f) {
 }
 
 #define G7_AI __attribute__((always_inline))
+typedef unsigned g7_u32x4 __attribute__((ext_vector_type(4)));
+typedef float g7_f32x4 __attribute__((ext_vector_type(4)));
 
 // alpha x *alpha_ptr through the scalar cache.  As a vector load (what the compiler emits for
 // the plain dereference) the value is waited for with vmcnt(0) at the top of every epilogue of
@@ -163,9 +165,15 @@ __device__ __forceinline__ float g7_ror8(float v) { return __uint_as_float(g7_ro
 // lbias (NOLD only): the wave's 128 bias values in LDS (v9 stages them by DMA with the tile's
 // operands) -- no vector load in the epilogue, so nothing there waits on vmcnt, which would
 // drain the next tile's operand stages already in flight
-template <int MODE, int NJ, bool PK = false, bool NOLD = false>
+// FA / FULL (MODE 1 only): the activation known at compile time (-1: read p.act per element
+// group) and a full 256 x 256 tile with a bf16 output -- no per-element bounds checks.  The
+// round-5 asm of the v9 forward epilogue showed every element group wrapped in ~10 scalar
+// branches (the runtime activation switch, the m / n guards of each store): the bias-only form
+// ran 57 us over the plain product of the GPT-2 up-projection (bench/epi_decomp.py).
+template <int MODE, int NJ, bool PK = false, bool NOLD = false, int FA = -1, bool FULL = false>
 __device__ __forceinline__ void g7_epilogue(const GemmArgs& p, floatx4 (&acc)[8][NJ], int mw, int nw, int lane,
                                             int dbg = 0, const float* lbias = nullptr) {
+  static_assert(!FULL || MODE == 1, "full-tile fast path: forward epilogues");
   const float alpha = g7_alpha(p);
   const int g = lane >> 4, rl = lane & 15;
   // bf16 outputs leave in 16-B stores: after v_permlane16_swap of fragments (j, j+1) lane
@@ -296,10 +304,11 @@ __device__ __forceinline__ void g7_epilogue(const GemmArgs& p, floatx4 (&acc)[8]
       for (int r = 0; r < 4; ++r) cs[j][r] = 0.f;
     }
   });
+  const int fact = FA >= 0 ? FA : p.act;  // (a constant when FA >= 0)
   sfor<8>([&](auto I) G7_AI {
     constexpr int i = decltype(I)::value;
     const int m = mw + 16 * i + rl;
-    const bool mok = m < p.M;
+    const bool mok = FULL || m < p.M;
     sfor<NJ / 2>([&](auto J) G7_AI {
       constexpr int j = 2 * decltype(J)::value;
       unsigned pa[2][2], pc[2][2];
@@ -307,7 +316,7 @@ __device__ __forceinline__ void g7_epilogue(const GemmArgs& p, floatx4 (&acc)[8]
         constexpr int h = decltype(H)::value;
         constexpr int jj = j + h;
         const int n = nw + 16 * jj + 4 * g;
-        const bool ok = mok && n < p.N;
+        const bool ok = FULL || (mok && n < p.N);
         const uint4 cur = ld[i % PF][jj];
         if (i + PF < 8) ld[i % PF][jj] = load_one(m + 16 * PF, n);
         float w[4];
@@ -317,12 +326,12 @@ __device__ __forceinline__ void g7_epilogue(const GemmArgs& p, floatx4 (&acc)[8]
           w[0] += bias4[jj].x; w[1] += bias4[jj].y; w[2] += bias4[jj].z; w[3] += bias4[jj].w;
           pa[h][0] = pack2bf(w[0], w[1]);  // the pre-activation (aux_out)
           pa[h][1] = pack2bf(w[2], w[3]);
-          if (PK && p.act == ACT_GELU) {
+          if (PK && fact == ACT_GELU) {
             const dpc_f2_t g01 = gelu_tanh2(dpc_f2_t{w[0], w[1]}), g23 = gelu_tanh2(dpc_f2_t{w[2], w[3]});
             w[0] = g01.x; w[1] = g01.y; w[2] = g23.x; w[3] = g23.y;
-          } else {
+          } else if (FA != 0) {
 #pragma unroll
-            for (int r = 0; r < 4; ++r) w[r] = act_fwd(w[r], p.act);
+            for (int r = 0; r < 4; ++r) w[r] = act_fwd(w[r], fact);
           }
           if (fsrc) {
             w[0] += __uint_as_float(cur.x); w[1] += __uint_as_float(cur.y);
@@ -344,7 +353,7 @@ __device__ __forceinline__ void g7_epilogue(const GemmArgs& p, floatx4 (&acc)[8]
             for (int r = 0; r < 4; ++r) cs[jj][r] += w[r];
           }
         }
-        if (p.out_f32) {
+        if (!FULL && p.out_f32) {
           if (ok) {
             float4* C = reinterpret_cast<float4*>(static_cast<float*>(p.C) + (long long)m * p.ldc + n);
             if (FWD && !NOLD && p.accumulate && p.residual) {  // (no caller does both; C read late)
@@ -359,14 +368,14 @@ __device__ __forceinline__ void g7_epilogue(const GemmArgs& p, floatx4 (&acc)[8]
         }
       });
       const int n8 = nw + 16 * j + coff;
-      const bool ok8 = mok && n8 < p.N;
+      const bool ok8 = FULL || (mok && n8 < p.N);
       if (FWD && aux_out) {
         const auto s0 = __builtin_amdgcn_permlane16_swap(pa[0][0], pa[1][0], false, false);
         const auto s1 = __builtin_amdgcn_permlane16_swap(pa[0][1], pa[1][1], false, false);
         if (ok8)
           st16(aux_out + (long long)m * p.ld_aux_out + n8, make_uint4(s0[0], s1[0], s0[1], s1[1]), p.nt_store & 1);
       }
-      if (!p.out_f32) {
+      if (FULL || !p.out_f32) {
         const auto s0 = __builtin_amdgcn_permlane16_swap(pc[0][0], pc[1][0], false, false);
         const auto s1 = __builtin_amdgcn_permlane16_swap(pc[0][1], pc[1][1], false, false);
         if (ok8)
@@ -416,10 +425,13 @@ __device__ __forceinline__ void g7_epilogue(const GemmArgs& p, floatx4 (&acc)[8]
 // bank groups.  Waits are counted: a quarter's DMA is older than the previous quarter's stores
 // and the next DMA, which may stay in flight (full tiles; an edge tile, which may skip stores,
 // waits for everything but the next DMA).
+// (round 5: act' by a select, the next column pair's operand read ahead, bounded buffer stores --
+// no branch inside the element loop; ONE copy per kernel, see the call site)
 template <int NJ>
 __device__ __forceinline__ void g7_epilogue_act_lds(const GemmArgs& p, floatx4 (&acc)[8][NJ], int m0, int n0,
                                                     int wid, int lane_in, bf16_t* buf0, bf16_t* buf1) {
   static_assert(NJ == 8, "v7 tiles");
+  const int fab = p.act_bwd;
   // the lane id through an opaque move: every per-lane address below is tile-invariant, and
   // hoisted out of the persistent tile loop they would stay live across the main loop (spills)
   int lane;
@@ -444,79 +456,89 @@ __device__ __forceinline__ void g7_epilogue_act_lds(const GemmArgs& p, floatx4 (
       g7_piece(rz, (tr * ld + c * 8) * 2, buf + (wid * 8 + k) * 512);
     }
   };
-  const bool full = m0 + 256 <= p.M && n0 + 256 <= p.N;
   float cs[NJ][4];
 #pragma unroll
   for (int j = 0; j < NJ; ++j)
 #pragma unroll
     for (int r = 0; r < 4; ++r) cs[j][r] = 0.f;
+  // bf16 output through a buffer descriptor over the tile's span of C: a store whose row is past
+  // M lies past num_records and is dropped by the hardware, one whose columns are past N gets an
+  // out-of-range offset -- no per-store exec branch (the dispatcher sends f32 outputs to EPI 3)
+  const long long corg = (long long)m0 * p.ldc + n0;
+  const long long crem = ((long long)(p.M - 1) * p.ldc + p.N - corg) * 2;
+  const unsigned cnrec = crem <= 0 ? 0u : (crem >= 0xffffffffll ? 0xffffffffu : (unsigned)crem);
+  const __amdgpu_buffer_rsrc_t rc =
+      __builtin_amdgcn_make_buffer_rsrc((void*)(static_cast<bf16_t*>(p.C) + corg), 0, cnrec, 0x00020000);
+  const bool gelu = fab == ACT_GELU;  // (else ReLU: act_lds is taken only with an act')
   auto proc = [&](auto Q, const bf16_t* buf) G7_AI {
     constexpr int q = decltype(Q)::value;
     sfor<2>([&](auto II) G7_AI {
       constexpr int i = 2 * q + decltype(II)::value;
-      const int m = mw + 16 * i + rl;
-      const bool mok = m < p.M;
+      const int mt = wr * 128 + 16 * i + rl;  // row in the tile
+      const bool rok = m0 + mt < p.M;
       const bf16_t* zrow = buf + (wr * 32 + 16 * decltype(II)::value + rl) * 256;
+      auto zload = [&](int jj) G7_AI {
+        const int c = wc * 16 + 2 * jj + (g >> 1);
+        return *reinterpret_cast<const uint2*>(zrow + (c ^ rl) * 8 + 4 * (g & 1));
+      };
+      // the act' operand of the NEXT column pair is read before this pair's arithmetic: with
+      // one pair per scheduling region (the barrier below) its LDS latency was exposed 128 times
+      // per tile
+      uint2 zc0 = zload(0), zc1 = zload(1);
       sfor<NJ / 2>([&](auto J) G7_AI {
         constexpr int j = 2 * decltype(J)::value;
+        uint2 zn0 = zc0, zn1 = zc1;
+        if constexpr (j + 2 < NJ) {
+          zn0 = zload(j + 2);
+          zn1 = zload(j + 3);
+        }
         unsigned pc[2][2];
         sfor<2>([&](auto H) G7_AI {
           constexpr int h = decltype(H)::value;
           constexpr int jj = j + h;
-          const int n = nw + 16 * jj + 4 * g;
-          const bool ok = mok && n < p.N;
-          const int c = wc * 16 + 2 * jj + (g >> 1);
-          const uint2 z = *reinterpret_cast<const uint2*>(zrow + (c ^ rl) * 8 + 4 * (g & 1));
+          const uint2 z = h == 0 ? zc0 : zc1;
           float w[4];
 #pragma unroll
           for (int r = 0; r < 4; ++r) w[r] = acc[i][jj][r] * alpha;
-          if (p.act_bwd == ACT_GELU) {  // packed-f32 GELU' (half the VALU issue of the scalar form)
-            const dpc_f2_t g01 = gelu_tanh_grad2(dpc_f2_t{__uint_as_float(z.x << 16), __uint_as_float(z.x & 0xffff0000u)});
-            const dpc_f2_t g23 = gelu_tanh_grad2(dpc_f2_t{__uint_as_float(z.y << 16), __uint_as_float(z.y & 0xffff0000u)});
-            w[0] *= g01.x; w[1] *= g01.y; w[2] *= g23.x; w[3] *= g23.y;
-          } else {
-            w[0] *= act_grad(__uint_as_float(z.x << 16), p.act_bwd);
-            w[1] *= act_grad(__uint_as_float(z.x & 0xffff0000u), p.act_bwd);
-            w[2] *= act_grad(__uint_as_float(z.y << 16), p.act_bwd);
-            w[3] *= act_grad(__uint_as_float(z.y & 0xffff0000u), p.act_bwd);
-          }
-          if (ok) {
+          const float z0 = __uint_as_float(z.x << 16), z1 = __uint_as_float(z.x & 0xffff0000u);
+          const float z2 = __uint_as_float(z.y << 16), z3 = __uint_as_float(z.y & 0xffff0000u);
+          // GELU' in packed f32 (half the VALU issue of the scalar form), or ReLU' -- a select,
+          // not a branch
+          const dpc_f2_t g01 = gelu_tanh_grad2(dpc_f2_t{z0, z1}), g23 = gelu_tanh_grad2(dpc_f2_t{z2, z3});
+          w[0] *= gelu ? g01.x : (z0 > 0.f ? 1.f : 0.f);
+          w[1] *= gelu ? g01.y : (z1 > 0.f ? 1.f : 0.f);
+          w[2] *= gelu ? g23.x : (z2 > 0.f ? 1.f : 0.f);
+          w[3] *= gelu ? g23.y : (z3 > 0.f ? 1.f : 0.f);
+          // (rows past M: an M-major A reads the next k-row's data into acc there, and the act'
+          // operand's LDS rows were never written by the DMA; columns past N may read the next
+          // row's data: both are kept out of the column sums by a select)
+          const bool cok = rok && n0 + wc * 128 + 16 * jj + 4 * g < p.N;
 #pragma unroll
-            for (int r = 0; r < 4; ++r) cs[jj][r] += w[r];
-          }
-          if (p.out_f32) {
-            if (ok) st16(static_cast<float*>(p.C) + (long long)m * p.ldc + n, make_float4(w[0], w[1], w[2], w[3]),
-                         p.nt_store & 2);
-          } else {
-            pc[h][0] = pack2bf(w[0], w[1]);
-            pc[h][1] = pack2bf(w[2], w[3]);
-          }
+          for (int r = 0; r < 4; ++r) cs[jj][r] += cok ? w[r] : 0.f;
+          pc[h][0] = pack2bf(w[0], w[1]);
+          pc[h][1] = pack2bf(w[2], w[3]);
         });
-        if (!p.out_f32) {
-          const int n8 = nw + 16 * j + coff;
-          const auto s0 = __builtin_amdgcn_permlane16_swap(pc[0][0], pc[1][0], false, false);
-          const auto s1 = __builtin_amdgcn_permlane16_swap(pc[0][1], pc[1][1], false, false);
-          if (mok && n8 < p.N)
-            st16(static_cast<bf16_t*>(p.C) + (long long)m * p.ldc + n8, make_uint4(s0[0], s1[0], s0[1], s1[1]),
-                 p.nt_store & 1);
-        }
+        const int n8 = wc * 128 + 16 * j + coff;  // column in the tile
+        const auto s0 = __builtin_amdgcn_permlane16_swap(pc[0][0], pc[1][0], false, false);
+        const auto s1 = __builtin_amdgcn_permlane16_swap(pc[0][1], pc[1][1], false, false);
+        const unsigned off = (n0 + n8 < p.N) ? (unsigned)((mt * p.ldc + n8) * 2) : 0xfffffff0u;
+        __builtin_amdgcn_raw_buffer_store_b128(
+            __builtin_bit_cast(g7_u32x4, make_uint4(s0[0], s1[0], s0[1], s1[1])), rc, off, 0, 2 /* nt */);
+        zc0 = zn0;
+        zc1 = zn1;
         __builtin_amdgcn_sched_barrier(0);  // one column pair at a time (else all are live: spills)
       });
     });
   };
   // wait until quarter q's pieces landed (every wave's): younger ops = the previous quarter's
-  // stores (st, full tiles only) + the next quarter's DMA (8) when one was issued
+  // 8 stores (st; every tile issues all of them now -- out-of-range ones are dropped by the
+  // buffer descriptor, still counted) + the next quarter's DMA (8) when one was issued
   auto landed = [&](bool st, bool next) G7_AI {
     if (!next) {
-      if (st && full) {
-        if (p.out_f32) g7_wait<16>();
-        else g7_wait<8>();
-      } else {
-        g7_wait<0>();
-      }
-    } else if (st && full) {
-      if (p.out_f32) g7_wait<24>();
-      else g7_wait<16>();
+      if (st) g7_wait<8>();
+      else g7_wait<0>();
+    } else if (st) {
+      g7_wait<16>();
     } else {
       g7_wait<8>();
     }
@@ -581,10 +603,13 @@ __device__ __forceinline__ void g7_epilogue_act_lds(const GemmArgs& p, floatx4 (
 // wave rows, 32 rows x 1 KiB = one ring slot) by LDS-DMA into the two idle ring slots,
 // double-buffered; one piece = one 1-KiB row, 16-B chunk c of local row r at position
 // c ^ (r & 15).  GELU in packed f32.
+// (round 5: the activation by selects, the next column pair's residual read ahead, bounded buffer
+// stores -- no branch inside the element loop)
 template <int NJ>
 __device__ __forceinline__ void g7_epilogue_res_lds(const GemmArgs& p, floatx4 (&acc)[8][NJ], int m0, int n0,
                                                     int wid, int lane_in, bf16_t* buf0, bf16_t* buf1) {
   static_assert(NJ == 8, "v7 tiles");
+  const int fact = p.act;
   int lane;  // (opaque: tile-invariant per-lane addresses must not be hoisted out of the tile loop)
   asm volatile("v_mov_b32 %0, %1" : "=v"(lane) : "v"(lane_in));
   const float alpha = g7_alpha(p);
@@ -607,9 +632,19 @@ __device__ __forceinline__ void g7_epilogue_res_lds(const GemmArgs& p, floatx4 (
       g7_piece(rr_, (tr * ld + c * 4) * 4, buf + lr * 512);
     }
   };
-  const bool full = m0 + 256 <= p.M && n0 + 256 <= p.N;
-  const bool has_aux = p.aux_out != nullptr;
-  bf16_t* aux_out = static_cast<bf16_t*>(p.aux_out);
+  // outputs through buffer descriptors over the tile's span (rows past M lie past num_records
+  // and are dropped by the hardware; columns past N get an out-of-range offset; no aux_out:
+  // num_records 0): every store is issued, none sits behind an exec branch
+  auto span = [&](const void* base, long long ldo, int esz) G7_AI {
+    const long long o = (long long)m0 * ldo + n0;
+    const long long rem = base ? ((long long)(p.M - 1) * ldo + p.N - o) * esz : 0;
+    const unsigned nr = rem <= 0 ? 0u : (rem >= 0xffffffffll ? 0xffffffffu : (unsigned)rem);
+    return __builtin_amdgcn_make_buffer_rsrc((void*)(static_cast<const char*>(base) + (base ? o * esz : 0)), 0, nr,
+                                             0x00020000);
+  };
+  const __amdgpu_buffer_rsrc_t rco = span(p.C, p.ldc, 4);
+  const __amdgpu_buffer_rsrc_t rax = span(p.aux_out, p.ld_aux_out, 2);
+  const bool gelu = fact == ACT_GELU, relu = fact == ACT_RELU;
   float4 bias4[NJ];
 #pragma unroll
   for (int j = 0; j < NJ; ++j) {
@@ -618,57 +653,61 @@ __device__ __forceinline__ void g7_epilogue_res_lds(const GemmArgs& p, floatx4 (
   }
   auto proc = [&](auto E, const bf16_t* buf) G7_AI {
     constexpr int i = decltype(E)::value;
-    const int m = mw + 16 * i + rl;
-    const bool mok = m < p.M;
+    const int mt = wr * 128 + 16 * i + rl;  // row in the tile
     const float* rrow = reinterpret_cast<const float*>(buf + (wr * 16 + rl) * 512);
+    auto rload = [&](int jj) G7_AI {
+      const int c = wc * 32 + 4 * jj + g;
+      return *reinterpret_cast<const float4*>(rrow + (c ^ rl) * 4);
+    };
+    // the residual of the NEXT column pair is read before this pair's arithmetic (its LDS
+    // latency was exposed once per pair behind the scheduling barrier below)
+    float4 rc0 = rload(0), rc1 = rload(1);
     sfor<NJ / 2>([&](auto J) G7_AI {
       constexpr int j = 2 * decltype(J)::value;
+      float4 rn0 = rc0, rn1 = rc1;
+      if constexpr (j + 2 < NJ) {
+        rn0 = rload(j + 2);
+        rn1 = rload(j + 3);
+      }
       unsigned pa[2][2];
       sfor<2>([&](auto H) G7_AI {
         constexpr int h = decltype(H)::value;
         constexpr int jj = j + h;
-        const int n = nw + 16 * jj + 4 * g;
-        const bool ok = mok && n < p.N;
-        const int c = wc * 32 + 4 * jj + g;
-        const float4 res = *reinterpret_cast<const float4*>(rrow + (c ^ rl) * 4);
+        const int ntc = wc * 128 + 16 * jj + 4 * g;  // column in the tile
+        const float4 res = h == 0 ? rc0 : rc1;
         float w[4];
 #pragma unroll
         for (int r = 0; r < 4; ++r) w[r] = acc[i][jj][r] * alpha;
         w[0] += bias4[jj].x; w[1] += bias4[jj].y; w[2] += bias4[jj].z; w[3] += bias4[jj].w;
         pa[h][0] = pack2bf(w[0], w[1]);
         pa[h][1] = pack2bf(w[2], w[3]);
-        if (p.act == ACT_GELU) {
-          const dpc_f2_t g01 = gelu_tanh2(dpc_f2_t{w[0], w[1]}), g23 = gelu_tanh2(dpc_f2_t{w[2], w[3]});
-          w[0] = g01.x; w[1] = g01.y; w[2] = g23.x; w[3] = g23.y;
-        } else {
+        // the activation by selects (GELU in packed f32, ReLU, or none), not branches
+        const dpc_f2_t g01 = gelu_tanh2(dpc_f2_t{w[0], w[1]}), g23 = gelu_tanh2(dpc_f2_t{w[2], w[3]});
+        const float ga[4] = {g01.x, g01.y, g23.x, g23.y};
 #pragma unroll
-          for (int r = 0; r < 4; ++r) w[r] = act_fwd(w[r], p.act);
-        }
-        if (ok)
-          st16(static_cast<float*>(p.C) + (long long)m * p.ldc + n,
-               make_float4(w[0] + res.x, w[1] + res.y, w[2] + res.z, w[3] + res.w), p.nt_store & 2);
+        for (int r = 0; r < 4; ++r) w[r] = gelu ? ga[r] : (relu ? fmaxf(w[r], 0.f) : w[r]);
+        const unsigned off = (n0 + ntc < p.N) ? (unsigned)((mt * p.ldc + ntc) * 4) : 0xfffffff0u;
+        __builtin_amdgcn_raw_buffer_store_b128(
+            __builtin_bit_cast(g7_u32x4, make_float4(w[0] + res.x, w[1] + res.y, w[2] + res.z, w[3] + res.w)), rco,
+            off, 0, 2 /* nt */);
       });
-      if (has_aux) {
-        const int n8 = nw + 16 * j + coff;
-        const auto s0 = __builtin_amdgcn_permlane16_swap(pa[0][0], pa[1][0], false, false);
-        const auto s1 = __builtin_amdgcn_permlane16_swap(pa[0][1], pa[1][1], false, false);
-        if (mok && n8 < p.N)
-          st16(aux_out + (long long)m * p.ld_aux_out + n8, make_uint4(s0[0], s1[0], s0[1], s1[1]), p.nt_store & 1);
-      }
+      const int n8 = wc * 128 + 16 * j + coff;
+      const auto s0 = __builtin_amdgcn_permlane16_swap(pa[0][0], pa[1][0], false, false);
+      const auto s1 = __builtin_amdgcn_permlane16_swap(pa[0][1], pa[1][1], false, false);
+      const unsigned aoff = (n0 + n8 < p.N) ? (unsigned)((mt * p.ld_aux_out + n8) * 2) : 0xfffffff0u;
+      __builtin_amdgcn_raw_buffer_store_b128(
+          __builtin_bit_cast(g7_u32x4, make_uint4(s0[0], s1[0], s0[1], s1[1])), rax, aoff, 0, 2 /* nt */);
+      rc0 = rn0;
+      rc1 = rn1;
       __builtin_amdgcn_sched_barrier(0);
     });
   };
-  // eighth e landed: younger = eighth e-1's stores (8 f32 + 4 aux per lane, full tiles) + the
-  // next DMA (8 pieces) when issued
+  // eighth e landed: younger = eighth e-1's stores (8 f32 + 4 aux per lane: every tile issues
+  // all of them, out-of-range ones dropped by their descriptor) + the next DMA (8 pieces) when issued
   auto landed = [&](bool st, bool next) G7_AI {
-    if (st && full) {
-      if (has_aux) {
-        if (next) g7_wait<20>();
-        else g7_wait<12>();
-      } else {
-        if (next) g7_wait<16>();
-        else g7_wait<8>();
-      }
+    if (st) {
+      if (next) g7_wait<20>();
+      else g7_wait<12>();
     } else {
       if (next) g7_wait<8>();
       else g7_wait<0>();
@@ -1023,6 +1062,9 @@ __global__ __launch_bounds__(256, WN == 128 ? 1 : 2) void gemm7_kernel(GemmArgs 
       g7_epilogue<EPI, NJ, WN == 64 && AK>(p, acc, m0 + ar, n0 + bc, lane, pl.debug);
     } else if constexpr (EPI == 9) {
       static_assert(WN == 128, "v7 only");
+      // (ONE epilogue copy per v7 kernel: with act-specialised full-tile copies beside the
+      // generic one the allocator spilled 67 (EPI 9) / 304 (EPI 8) VGPRs into the main loop --
+      // down-projection 369 -> 568 us, act' input gradient 535 -> 749 us, round 5)
       g7_epilogue_res_lds<NJ>(p, acc, m0, n0, wid, lane, smem + ((rd_slot + 3) % NS) * SLOT,
                               smem + ((rd_slot + 4) % NS) * SLOT);
     } else if constexpr (EPI == 8) {

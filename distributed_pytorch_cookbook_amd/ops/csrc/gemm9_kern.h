@@ -357,7 +357,14 @@ __global__ __launch_bounds__(256, 1) void gemm9_kernel(GemmArgs p, unsigned long
       // (measured round 5: MODE 0's whole-line store layout for both outputs -- lanes l, l ^ 8
       // trading a chunk so one store writes 8 rows x 128 B -- was SLOWER here than these 16-row
       // x 64-B stores, 448.6 vs 405.5 us on the GPT-2 up-projection, bench/epi_decomp.py)
-      g7_epilogue<1, NJ, true, true>(p, acc, m0 + ar, n0 + bc, elane, 0, sbias + ((u & 1) * 4 + wid) * 256 + bc);
+      const float* lb = sbias + ((u & 1) * 4 + wid) * 256 + bc;
+      if (m0 + 256 <= p.M && n0 + 256 <= p.N && !p.out_f32) {  // full tile, bf16 output: check-free
+        if (p.act == ACT_GELU) g7_epilogue<1, NJ, true, true, ACT_GELU, true>(p, acc, m0 + ar, n0 + bc, elane, 0, lb);
+        else if (p.act == ACT_RELU) g7_epilogue<1, NJ, true, true, ACT_RELU, true>(p, acc, m0 + ar, n0 + bc, elane, 0, lb);
+        else g7_epilogue<1, NJ, true, true, 0, true>(p, acc, m0 + ar, n0 + bc, elane, 0, lb);
+      } else {
+        g7_epilogue<1, NJ, true, true>(p, acc, m0 + ar, n0 + bc, elane, 0, lb);
+      }
     } else {
       // (ABL 512: the epilogue's VALU without its stores; ABL 1024: non-temporal stores -- lab only)
       g7_epilogue<0, NJ>(p, acc, m0 + ar, n0 + bc, lane, (ABL & 512) ? 4 : ((ABL & 1024) ? 16 : 0));

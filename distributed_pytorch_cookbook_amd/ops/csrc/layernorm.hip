@@ -47,10 +47,13 @@ struct LNArgs {
   const float* add_bias;
   float* x_out;
   long long ld_add, ld_xout;
+  const unsigned* drop_seed;  // device seed of the forward (drop_key_of); null: drop_key
+  unsigned drop_site;
 };
 
 template <int NV>
 __global__ __launch_bounds__(256) void ln_fwd_kernel(LNArgs p) {
+  const uint32_t dkey = p.drop_scale != 0.f ? drop_key_of(p.drop_seed, p.drop_site, p.drop_key) : 0u;
   const int lane = threadIdx.x & 63;
   const long long row = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= p.T) return;
@@ -80,7 +83,7 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(LNArgs p) {
         if (p.drop_scale != 0.f) {
           const uint32_t idx = (uint32_t)(row * p.D + 4 * c);
 #pragma unroll
-          for (int e = 0; e < 4; ++e) a[e] *= drop_factor(idx + e, p.drop_key, p.drop_thresh, p.drop_scale);
+          for (int e = 0; e < 4; ++e) a[e] *= drop_factor(idx + e, dkey, p.drop_thresh, p.drop_scale);
         }
         v[i].x += a[0]; v[i].y += a[1]; v[i].z += a[2]; v[i].w += a[3];
         xo[c] = v[i];
@@ -136,6 +139,7 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(LNArgs p) {
 
 template <int NV>
 __global__ __launch_bounds__(256) void ln_bwd_kernel(LNArgs p) {
+  const uint32_t dkey = p.drop_scale != 0.f ? drop_key_of(p.drop_seed, p.drop_site, p.drop_key) : 0u;
   __shared__ float red[4][2][NV * 256];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int nv4 = p.D >> 2;
@@ -195,10 +199,10 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(LNArgs p) {
         if (gout) {
           if (p.drop_scale != 0.f) {
             const uint32_t idx = (uint32_t)(row * p.D + 4 * c);
-            o.x *= drop_factor(idx + 0, p.drop_key, p.drop_thresh, p.drop_scale);
-            o.y *= drop_factor(idx + 1, p.drop_key, p.drop_thresh, p.drop_scale);
-            o.z *= drop_factor(idx + 2, p.drop_key, p.drop_thresh, p.drop_scale);
-            o.w *= drop_factor(idx + 3, p.drop_key, p.drop_thresh, p.drop_scale);
+            o.x *= drop_factor(idx + 0, dkey, p.drop_thresh, p.drop_scale);
+            o.y *= drop_factor(idx + 1, dkey, p.drop_thresh, p.drop_scale);
+            o.z *= drop_factor(idx + 2, dkey, p.drop_thresh, p.drop_scale);
+            o.w *= drop_factor(idx + 3, dkey, p.drop_thresh, p.drop_scale);
           }
           uint2 wv;
           wv.x = pack2bf(o.x, o.y);

@@ -397,9 +397,12 @@ struct DropResArgs {
   int T, N;
   unsigned key, thresh;
   float scale;
+  const unsigned* seed;  // device seed of the forward (common.h:drop_key_of); null: key
+  unsigned site;
 };
 
 __global__ __launch_bounds__(256) void dropout_residual_kernel(DropResArgs p) {
+  const uint32_t key = drop_key_of(p.seed, p.site, p.key);
   const int nq = p.N >> 2;
   const long long total = (long long)p.T * nq;
   for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < total; i += (long long)gridDim.x * 256) {
@@ -409,10 +412,10 @@ __global__ __launch_bounds__(256) void dropout_residual_kernel(DropResArgs p) {
     const float4 r = *reinterpret_cast<const float4*>(p.res + t * p.ldr + c);
     const uint32_t idx = (uint32_t)(t * p.N + c);
     float4 o;
-    o.x = r.x + y.x * drop_factor(idx + 0, p.key, p.thresh, p.scale);
-    o.y = r.y + y.y * drop_factor(idx + 1, p.key, p.thresh, p.scale);
-    o.z = r.z + y.z * drop_factor(idx + 2, p.key, p.thresh, p.scale);
-    o.w = r.w + y.w * drop_factor(idx + 3, p.key, p.thresh, p.scale);
+    o.x = r.x + y.x * drop_factor(idx + 0, key, p.thresh, p.scale);
+    o.y = r.y + y.y * drop_factor(idx + 1, key, p.thresh, p.scale);
+    o.z = r.z + y.z * drop_factor(idx + 2, key, p.thresh, p.scale);
+    o.w = r.w + y.w * drop_factor(idx + 3, key, p.thresh, p.scale);
     *reinterpret_cast<float4*>(p.out + t * p.ldo + c) = o;
   }
 }
@@ -432,11 +435,14 @@ struct BiasActArgs {
   int act;
   unsigned drop_key, drop_thresh;
   float drop_scale;    // 0: no dropout
+  const unsigned* drop_seed;  // device seed of the forward (common.h:drop_key_of); null: drop_key
+  unsigned drop_site;
 };
 
 constexpr int BA_ROWS = 128;
 
 __global__ __launch_bounds__(256) void bias_act_bwd_kernel(BiasActArgs p) {
+  const uint32_t dkey = p.drop_scale != 0.f ? drop_key_of(p.drop_seed, p.drop_site, p.drop_key) : 0u;
   __shared__ float red[4][256];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int c = blockIdx.x * 256 + lane * 4;
@@ -475,7 +481,7 @@ __global__ __launch_bounds__(256) void bias_act_bwd_kernel(BiasActArgs p) {
         if (p.drop_scale != 0.f) {
           const uint32_t idx = (uint32_t)(t * p.N + c);
 #pragma unroll
-          for (int j = 0; j < 4; ++j) f[j] *= drop_factor(idx + j, p.drop_key, p.drop_thresh, p.drop_scale);
+          for (int j = 0; j < 4; ++j) f[j] *= drop_factor(idx + j, dkey, p.drop_thresh, p.drop_scale);
         }
 #pragma unroll
         for (int j = 0; j < 4; ++j) acc[j] += f[j];

@@ -43,23 +43,33 @@ def _fmix32_t(x: torch.Tensor) -> torch.Tensor:
     return x ^ (x >> 16)
 
 
-@dataclass(frozen=True)
+@dataclass(frozen=True, eq=False)
 class DropSpec:
-    """Dropout of one site for one forward: keep iff hash >= thresh, kept values * scale."""
+    """Dropout of one site for one forward: keep iff hash >= thresh, kept values * scale.
+
+    ``seed_t`` (optional): the forward's seed in device memory, int32 [2] = (low word, high
+    word).  The kernels then derive the key from it themselves (``common.h:drop_key_of``, the
+    same hash as ``key``), so a HIP-graph replay of the step draws fresh masks each step: the
+    model advances the device counter with a captured add (``gpt.py:next_dropout_seed``)."""
 
     key: int
     thresh: int
     scale: float
+    seed_t: "torch.Tensor | None" = None
+    site: int = 0
 
     @staticmethod
-    def make(p: float, seed: int, site: int) -> "DropSpec | None":
+    def make(p: float, seed: int, site: int, seed_t: "torch.Tensor | None" = None) -> "DropSpec | None":
         if p <= 0.0:
             return None
         if p >= 1.0:
             raise ValueError("dropout probability must be < 1")
         key = _fmix32_int(_fmix32_int(seed & M32) ^ _fmix32_int((seed >> 32) + 0x632BE5AB * (site + 1)))
         thresh = min(int(round(p * 2.0 ** 32)), M32)
-        return DropSpec(key, thresh, 1.0 / (1.0 - p))
+        return DropSpec(key, thresh, 1.0 / (1.0 - p), seed_t, site)
+
+    def seed_ptr(self):
+        return self.seed_t.data_ptr() if self.seed_t is not None and self.seed_t.is_cuda else None
 
 
 def keep_mask(spec: DropSpec, T: int, N: int, device=None) -> torch.Tensor:
@@ -86,7 +96,7 @@ def dropout_residual(y: torch.Tensor, res: torch.Tensor, spec: DropSpec,
     args = _lib.DropResArgs(
         y=y.data_ptr(), res=res.data_ptr(), out=out.data_ptr(),
         ldy=y.stride(0), ldr=res.stride(0), ldo=out.stride(0), T=T, N=N,
-        key=spec.key, thresh=spec.thresh, scale=spec.scale,
+        key=spec.key, thresh=spec.thresh, scale=spec.scale, seed=spec.seed_ptr(), site=spec.site,
     )
     _lib.call("dpc_dropout_residual", args, y.device)
     return out

@@ -49,6 +49,7 @@ def bias_act_bwd(dy: torch.Tensor, z: torch.Tensor | None, act, db: torch.Tensor
         if T * N >= 2 ** 32:
             raise ValueError("bias_act_bwd: dropout needs T * N < 2^32")
         args.drop_key, args.drop_thresh, args.drop_scale = drop.key, drop.thresh, drop.scale
+        args.drop_seed, args.drop_site = drop.seed_ptr(), drop.site
     _lib.call("dpc_bias_act_bwd", args, dy.device)
     return out
 

@@ -75,6 +75,7 @@ def layernorm_fwd(x: torch.Tensor, gamma: torch.Tensor, beta: torch.Tensor, eps:
             if T * D >= 2 ** 32:
                 raise ValueError("layernorm_fwd: dropout needs T * D < 2^32")
             args.drop_key, args.drop_thresh, args.drop_scale = drop.key, drop.thresh, drop.scale
+            args.drop_seed, args.drop_site = drop.seed_ptr(), drop.site
     _lib.call("dpc_layernorm_fwd", args, x.device)
     return out, mean, rstd
 
@@ -128,5 +129,6 @@ def layernorm_bwd(dy: torch.Tensor, x: torch.Tensor, mean: torch.Tensor, rstd: t
             if T * D >= 2 ** 32:
                 raise ValueError("layernorm_bwd: dropout needs T * D < 2^32")
             args.drop_key, args.drop_thresh, args.drop_scale = drop.key, drop.thresh, drop.scale
+            args.drop_seed, args.drop_site = drop.seed_ptr(), drop.site
     _lib.call("dpc_layernorm_bwd", args, x.device)
     return dx

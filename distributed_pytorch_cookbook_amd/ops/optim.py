@@ -88,8 +88,10 @@ class FlatAdamW:
             )
             _lib.call("dpc_adamw", args, p.device)
             return
-        if lo != 0 or hi != p.numel():
-            raise ValueError("FlatAdamW.update: sub-ranges need the HIP path (4-aligned)")
+        # (other paths: elements [lo, hi) through views -- FSDP updates unit shards one by one)
+        p, g = p[lo:hi], g[lo:hi]
+        m_, v_ = self.exp_avg[lo:hi], self.exp_avg_sq[lo:hi]
+        sh = None if self.shadow is None else self.shadow[lo:hi]
         if skip_t is not None:
             # non-HIP paths: a host-read flag (the CPU / offload paths synchronise anyway)
             if float(skip_t) != 0.0:
@@ -104,19 +106,19 @@ class FlatAdamW:
                 from .. import runtime
 
                 host_shadow = None
-                bf16_shadow = self.shadow is not None and self.shadow.dtype == torch.bfloat16
+                bf16_shadow = sh is not None and sh.dtype == torch.bfloat16
                 if bf16_shadow:
                     if getattr(self, "_host_shadow", None) is None:
-                        self._host_shadow = torch.empty(p.numel(), dtype=torch.bfloat16,
+                        self._host_shadow = torch.empty(self.param.numel(), dtype=torch.bfloat16,
                                                         pin_memory=torch.cuda.is_available())
-                    host_shadow = self._host_shadow
+                    host_shadow = self._host_shadow[lo:hi]
                 hstep = int(round(float(self.step_t))) if skip_t is not None else self.step_count
-                runtime.adamw_host(p, g, self.exp_avg, self.exp_avg_sq, self.lr, b1, b2, self.eps,
+                runtime.adamw_host(p, g, m_, v_, self.lr, b1, b2, self.eps,
                                    self.weight_decay, hstep, grad_scale, host_shadow)
                 if bf16_shadow:
-                    self.shadow.copy_(host_shadow, non_blocking=True)
-                elif self.shadow is not None:
-                    self.shadow.copy_(p, non_blocking=True)
+                    sh.copy_(host_shadow, non_blocking=True)
+                elif sh is not None:
+                    sh.copy_(p, non_blocking=True)
                 return
             except (ImportError, OSError, RuntimeError):
                 pass
@@ -124,9 +126,9 @@ class FlatAdamW:
         if grad_scale_t is not None:
             gs = gs * grad_scale_t
         p.mul_(1.0 - self.lr * self.weight_decay)
-        self.exp_avg.mul_(b1).add_(gs, alpha=1 - b1)
-        self.exp_avg_sq.mul_(b2).addcmul_(gs, gs, value=1 - b2)
-        denom = (self.exp_avg_sq.sqrt() / bc2s).add_(self.eps)
-        p.addcdiv_(self.exp_avg, denom, value=-self.lr / bc1)
-        if self.shadow is not None:
-            self.shadow.copy_(p)
+        m_.mul_(b1).add_(gs, alpha=1 - b1)
+        v_.mul_(b2).addcmul_(gs, gs, value=1 - b2)
+        denom = (v_.sqrt() / bc2s).add_(self.eps)
+        p.addcdiv_(m_, denom, value=-self.lr / bc1)
+        if sh is not None:
+            sh.copy_(p)

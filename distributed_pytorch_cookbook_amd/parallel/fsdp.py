@@ -35,6 +35,7 @@ from ..ops.elementwise import cast_f32_bf16
 from . import comm
 from .store import ALIGN, FlatLayout, ParamStore, default_compute_dtype
 from .transport import Transport, make_transport
+from ..utils.profiling import mark
 
 
 def _placeholder(shape, device):
@@ -306,6 +307,37 @@ class FSDPStore(ParamStore):
         for u in list(self._full):
             self._release(u)
 
+    def finish_grads_and_update(self, opt, opt_rep, grad_scale: float = 1.0):
+        """``finish_grads`` + both AdamW steps, unit by unit: each unit's shard is updated as
+        soon as its reduce-scatter has landed (units complete in backward order, the last
+        layer's first), while the earlier units' reduce-scatters are still on the comm stream --
+        as the DDP engine does bucket by bucket.  Only the last units' reduce-scatters remain on
+        the critical path.  Same arithmetic as ``finish_grads`` then ``opt.step`` (AdamW is
+        element-wise; the step count advances once)."""
+        rep_w = self.tp.all_reduce(self.rep_grads, async_op=True) if self.sharded else None
+        opt.begin_step()
+        done = set()
+        for u in sorted(self._rs, reverse=True):  # (reduce-scatters were issued last unit first)
+            for w, tmp in self._rs[u]:
+                with mark("comm:wait_unit"):
+                    w.wait()
+                if tmp is not None:
+                    self.shard(self.grads, u).add_(tmp.float())
+            lo = self.shard_off[u]
+            opt.update(lo, lo + self.shard_len[u], grad_scale=grad_scale)
+            done.add(u)
+        for u in self.units:  # (a unit without a reduce-scatter this step: one rank, or no grad)
+            if u not in done:
+                lo = self.shard_off[u]
+                opt.update(lo, lo + self.shard_len[u], grad_scale=grad_scale)
+        self._rs.clear()
+        if rep_w is not None:
+            rep_w.wait()
+        opt_rep.step(grad_scale=grad_scale)
+        self._in_backward = False
+        for u in list(self._full):
+            self._release(u)
+
     def reset_step_state(self):
         """After a failed HIP-graph capture: no gathered unit, gradient buffer or
         reduce-scatter the capture recorded exists (engine/base.py:Engine.reset_step_state)."""
@@ -334,9 +366,20 @@ class FSDPStore(ParamStore):
         rep_flat = self.rep_master if rep_flat is None else rep_flat
         out = {} if self.rank == dst_rank else None
         for u in self.units:
-            sh = self.shard(flat_shards, u).to(self.device)
-            full = torch.empty(self.unit_len[u], dtype=sh.dtype, device=self.device)
-            self.tp.all_gather(full, sh.contiguous())
+            sh = self.shard(flat_shards, u).to(self.device).contiguous()
+            if not self.sharded:
+                full = sh
+            elif self.rank == dst_rank:
+                # gathered to dst_rank ONLY (grouped point-to-point): the reference's
+                # FULL_STATE_DICT all-gathers every unit onto every rank (main-fsdp.py:193-194),
+                # W x the traffic a rank-0 checkpoint needs
+                L = self.shard_len[u]
+                full = torch.empty(self.unit_len[u], dtype=sh.dtype, device=self.device)
+                full[self.rank * L:(self.rank + 1) * L].copy_(sh)
+                self.tp.sendrecv(recvs=[(full[r * L:(r + 1) * L], r) for r in range(self.tp.size) if r != dst_rank])
+            else:
+                self.tp.sendrecv(sends=[(sh, dst_rank)])
+                continue
             if out is not None:
                 lo = self.layout.unit_ranges[u][0]
                 for e in self.layout.unit_entries(u):

@@ -24,14 +24,31 @@ from __future__ import annotations
 import torch
 
 
+# Rates of the three kinds of work one training step does per token, measured on MI355X in
+# the GPT-2 small DDP step (profiles/r4_final/ddp_kstats_final.md, pmc_ddp.md): GEMMs run
+# ~1.0 PF/s (forward + input gradient + weight gradient = 3 x the forward FLOPs), flash
+# attention ~0.4 PF/s (forward + backward = 3.5 x the forward FLOPs), the memory-bound
+# kernels (LayerNorm fwd/bwd, residual / bias / activation passes, cross-entropy, embedding
+# gather / scatter) ~5 TB/s.
+_GEMM_RATE, _ATTN_RATE, _MEM_RATE = 1.0e15, 0.4e15, 5.0e12
+
+
 def unit_costs(model, seq_len: int) -> list[float]:
-    """Relative forward FLOPs per unit (embeddings, layers..., head)."""
+    """Estimated seconds per token of one training step (forward + backward) for each unit
+    (embeddings, layers..., head) -- the stage balance of ``partition``.  Counts the backward
+    and the memory-bound passes, not only forward FLOPs: at GPT-2 small the head (LM-head GEMM
+    + the cross-entropy over V logits) comes out at ~4.4 layers, at GPT-2 medium ~3.5."""
     D = model.dim
     hd = model.heads * model.head_dim
     V = model.vocab_size
-    layer = 2 * (3 * D * hd + hd * D + 2 * 4 * D * D) + 2 * 2 * seq_len * hd / 2
-    head = 2 * D * V + 6 * V  # lm_head GEMM + CE passes
-    emb = 0.02 * layer
+    S = seq_len
+    gemm = 2 * (3 * D * hd + hd * D + 2 * 4 * D * D)  # forward FLOPs of the layer's projections
+    attn = 2 * S * hd  # causal: QK^T + PV over S / 2 keys on average
+    layer_bytes = 32 * D + 4 * 4 * D  # two LayerNorms fwd + bwd, residual / bias / act' passes
+    layer = 3 * gemm / _GEMM_RATE + 3.5 * attn / _ATTN_RATE + layer_bytes / _MEM_RATE
+    # head: LM-head GEMM (3 x), the fused cross-entropy (read + write the bf16 logits), norm_out
+    head = 3 * 2 * D * V / _GEMM_RATE + (4 * V + 16 * D) / _MEM_RATE
+    emb = (4 * 4 * D + 64) / _MEM_RATE  # gather-add forward, sorted segment-sum backward
     return [emb] + [layer] * model.num_layers + [head]
 
 

@@ -364,6 +364,8 @@ class NativeTransport(Transport):
 
         self.group = group
         self.device = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+        if self.device.type == "cuda" and self.device.index is None:  # ("cuda": the current device)
+            self.device = torch.device("cuda", torch.cuda.current_device())
         self.nc = native if native is not None else NativeComm(group, device=self.device)
         self.rank, self.size = self.nc.rank, self.nc.size
         _native_comms.append(self.nc)

@@ -56,12 +56,13 @@ def build_engine(recipe: str, model, info, args, force_dist: bool = False):
     # reduces fp32 (autocast keeps fp32 grads, /root/reference/main-fsdp.py:64-69)
     reduce_dtype = torch.bfloat16 if getattr(args, "reduce_dtype", "fp32") == "bf16" else torch.float32
     comm_kind = "native" if force_dist else getattr(args, "comm", "auto")
-    # the cookbook's "compile": capture the whole step into a HIP graph (dropout masks are
-    # drawn per step on the host: not graph-replayable).  One rank by default; at N > 1 only
-    # with --graph (RCCL inside a replayed graph has not been run on a multi-GPU node yet, and
-    # bench.py's scaling runs take the same eager path); never under --coll_check, whose
-    # fingerprints are host-synchronous collectives
-    graph = (not args.disable_compile and not args.disable_amp and not args.dropout
+    # the cookbook's "compile": capture the whole step into a HIP graph (dropout included: the
+    # per-forward seed is a device counter the mask kernels read, so replays draw fresh masks --
+    # models/gpt.py:next_dropout_seed).  One rank by default; at N > 1 only with --graph (RCCL
+    # inside a replayed graph has not been run on a multi-GPU node yet, and bench.py's scaling
+    # runs take the same eager path); never under --coll_check, whose fingerprints are
+    # host-synchronous collectives
+    graph = (not args.disable_compile and not args.disable_amp
              and (info.world_size == 1 or getattr(args, "graph", False))
              and not getattr(args, "coll_check", False))
     if recipe in ("single", "ddp"):

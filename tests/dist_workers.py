@@ -303,9 +303,12 @@ class _FailingCapture:
     def __enter__(self):
         st = self.eng.store
         tgt = st if hasattr(st, "finish_grads") and getattr(st, "tp", None) is not None else self.eng.p2p
-        name = "finish_grads" if tgt is st else "drain"
-        self.saved.append((tgt, name))
-        setattr(tgt, name, self._boom)
+        # FSDP's unit-wise path (finish_grads_and_update) fails at the same point
+        names = ["finish_grads", "finish_grads_and_update"] if tgt is st else ["drain"]
+        for name in names:
+            if hasattr(tgt, name):
+                self.saved.append((tgt, name))
+                setattr(tgt, name, self._boom)
         return self
 
     def __exit__(self, *exc):

@@ -127,3 +127,28 @@ def test_grad_scaler_skips_nonfinite_step():
     eng.scaler.check = real_check
     eng.train_step(*batch(2))
     assert float(eng.opt.step_t) == 2.0 and not torch.equal(eng.store.master, before)
+
+
+def test_dropout_step_graph_replays_fresh_masks():
+    """--dropout > 0 no longer forces eager steps: the per-forward seed lives in device memory
+    (models/gpt.py:next_dropout_seed) and the mask kernels derive their keys from it, so every
+    replay of the captured step draws the masks the eager step would.  Eager and graphed
+    engines agree over 4 steps (eager, capture + replay, replay, replay); with keys frozen at
+    capture, steps 3-4 would reuse step 2's masks and the weights would part."""
+
+    def mk():
+        torch.manual_seed(0)
+        with torch.device("cuda"):
+            m = TransformerDecoderLM(dim=256, head_dim=64, heads=4, num_layers=3, vocab_size=4000,
+                                     max_position_embeddings=128, activation="gelu", dropout=0.1)
+        m.dropout_seed_base = 7
+        return m
+
+    eager = DataParallelEngine(mk(), "cuda", lr=1e-3)
+    graphed = DataParallelEngine(mk(), "cuda", lr=1e-3, graph=True)
+    le, sde = run(eager, steps=4)
+    lg, sdg = run(graphed, steps=4)
+    assert graphed._stepper.graph is not None, "the dropout step was not captured"
+    for a, b in zip(le, lg):
+        assert abs(a - b) < 1e-3, (le, lg)
+    close(sdg, sde, tol=1e-3, steps=4)
