@@ -1,6 +1,6 @@
 """A/B the hand-written GEMM implementations against hipBLASLt (torch.mm) on random data.
 
-    python bench/gemm_ab.py [--impls 12 20 26] [--shapes square|gpt2s|all] [--rounds 3]
+    python bench/gemm_ab.py [--impls 20 26] [--shapes square|gpt2s|all] [--rounds 3]
 
 Every variant of a shape is timed in interleaved rounds inside one process (HIP events over
 ``--iters`` back-to-back launches, median over rounds), and checked once against an f32
@@ -111,7 +111,7 @@ def check(A, B, lay, out):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--impls", type=int, nargs="+", default=[12, 20, 26])
+    ap.add_argument("--impls", type=int, nargs="+", default=[20, 26])
     ap.add_argument("--shapes", default="all", choices=["square", "gpt2s", "all", "fused", "xl", "wgrad"])
     ap.add_argument("--only", nargs="*", default=None)
     ap.add_argument("--rounds", type=int, default=3)

@@ -236,8 +236,8 @@ forced_gemm_impl = -1
 
 def set_gemm_impl(impl: int) -> None:
     """Force a GEMM implementation (tests / sweeps): -1 auto (default), 1 register-staged v1,
-    2-5 LDS-DMA 128x128 v2 variants, 6-10 large-tile v3 variants, 11 pipelined 256x256 v4, 12 256x256 ping-pong v5
-    (table at the dispatcher, ``csrc/gemm.hip``)."""
+    2-4 LDS-DMA 128x128 v2 variants, 10 the 256x128 v3, 16-26 the persistent 256x256 v7 / v8 / v9
+    placements (table at the dispatcher, ``csrc/gemm.hip``)."""
     global forced_gemm_impl
     forced_gemm_impl = int(impl)
     lib().dpc_gemm_set_impl(int(impl))

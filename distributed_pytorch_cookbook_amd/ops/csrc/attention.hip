@@ -235,6 +235,16 @@ __device__ __forceinline__ void scale16(floatx16& x, float a) {
   for (int i = 0; i < 16; ++i) asm volatile("v_mul_f32 %0, %0, %1" : "+v"(x[i]) : "v"(a));
 }
 
+// x[r] = 0 if v > K, in place (v_cmp + v_cndmask on the element's own register: a C++ select in
+// one arm of a branch gave the element a new register and both arms a copy back)
+template <int K>
+__device__ __forceinline__ void zero_if_gt(floatx16& x, int r, int v) {
+  asm volatile("v_cmp_lt_i32_e32 vcc, %1, %2\n\tv_cndmask_b32_e64 %0, %0, 0, vcc"
+               : "+v"(x[r])
+               : "n"(K), "v"(v)
+               : "vcc");
+}
+
 __device__ __forceinline__ void zero16(floatx16& x) {
 #pragma unroll
   for (int i = 0; i < 16; ++i) x[i] = 0.f;
@@ -734,9 +744,10 @@ __global__ __launch_bounds__(256, OCC) void attn_fwd2_kernel(AttnArgs p, int nit
 }
 
 // ------------------------------------------------------------------ backward
-// delta[n,h,s] = sum_d dO * O   (one HD/8-lane group per (token, head)), and the second half of
-// the buffer the row's lse in log2 units (lse * log2 e) -- the kernels then form
-// p = 2^(s c - lse2) with one FMA and no per-element multiply
+// delta[n,h,s] = sum_d dO * O   (one HD/8-lane group per (token, head)), stored NEGATED (the
+// dK / dV kernel's dP accumulator starts at -delta: an LDS read straight into it, no per-element
+// sign flip), and the second half of the buffer the row's lse in log2 units (lse * log2 e) --
+// the kernels then form p = 2^(s c - lse2) with one FMA and no per-element multiply
 template <int HD>
 __global__ __launch_bounds__(256) void attn_bwd_pre_kernel(AttnArgs p) {
   constexpr int G = HD / 8;
@@ -762,7 +773,7 @@ __global__ __launch_bounds__(256) void attn_bwd_pre_kernel(AttnArgs p) {
   if (row < T * p.H && sub == 0) {
     const long long n = t / p.S, s = t % p.S;
     const long long i = (n * p.H + h) * p.S + s;
-    p.delta[i] = acc;
+    p.delta[i] = -acc;
     p.delta[T * p.H + i] = p.lse[i] * LOG2E;  // (+inf stays +inf: a fully masked row)
   }
 }
@@ -830,18 +841,19 @@ __global__ __launch_bounds__(256, OCC) void attn_bwd_dkdv_kernel(AttnArgs p) {
     }
   };
   // S = Q K^T, dP - delta = dO V^T - delta of the 32-query sub-block at row r0 of the slot
-  // (key on the lane): the dP accumulator starts at -delta of its query rows, so dS = P (dP -
-  // delta) needs no subtraction
+  // (key on the lane): the dP accumulator starts at -delta of its query rows (the buffer holds
+  // -delta: four LDS reads land in the accumulator as they are), so dS = P (dP - delta) needs no
+  // subtraction
   auto sdp = [&](floatx16& sa, floatx16& dp, const bf16_t* lq, int r0) {
     zero16(sa);
     const float* drow = &srow[((lq - smem) / (2 * A::TILE))][1][0];
 #pragma unroll
     for (int g = 0; g < 4; ++g) {
       const float4 d4 = *reinterpret_cast<const float4*>(drow + r0 + 8 * g + 4 * hh);
-      dp[4 * g + 0] = -d4.x;
-      dp[4 * g + 1] = -d4.y;
-      dp[4 * g + 2] = -d4.z;
-      dp[4 * g + 3] = -d4.w;
+      dp[4 * g + 0] = d4.x;
+      dp[4 * g + 1] = d4.y;
+      dp[4 * g + 2] = d4.z;
+      dp[4 * g + 3] = d4.w;
     }
 #pragma unroll
     for (int st = 0; st < A::NST; ++st) {
@@ -904,21 +916,28 @@ __global__ __launch_bounds__(256, OCC) void attn_bwd_dkdv_kernel(AttnArgs p) {
     // ---- one basic block: next S, dP MFMAs || this sub-block's P, dS
     if constexpr (PIPE) sdp(san, dpn, nq, nr0);
     else sdp(sa, dp, lq, 32 * hf);
-#pragma unroll
-    for (int g = 0; g < 4; ++g) {
-      const int qi0 = 32 * hf + 8 * g + 4 * hh;  // rows 8g+4h..+3: consecutive queries
-      const float4 l4 = *reinterpret_cast<const float4*>(&srow[slot][0][qi0]);
+    // P, dS.  The causal zeroing runs only on the sub-blocks that cross the diagonal, in place,
+    // between the exponentials and the dS products: written as a select inside the element loop,
+    // hipcc if-converted it into an add, a compare, an exec-mask AND and a select on EVERY element
+    // of every sub-block, and as two loop copies it gave P new registers plus copies at the join.
+    // Element (g, e) holds query qs0 + 8 g + 4 hh + e: masked when key - qs0 - 4 hh > 8 g + e.
+    sfor<4>([&](auto G) {
+      constexpr int g = decltype(G)::value;
+      const float4 l4 = *reinterpret_cast<const float4*>(&srow[slot][0][32 * hf + 8 * g + 4 * hh]);
       const float lv[4] = {l4.x, l4.y, l4.z, l4.w};
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const int r = 4 * g + e;
-        float pv = fast_exp2(fmaf(sa[r], c, -lv[e]));
-        // a padded key's P only reaches this lane's own dK / dV column: zeroed at the store
-        if (diag) pv = (key > qt0 + qi0 + e) ? 0.f : pv;
-        sa[r] = pv;
-        dp[r] = pv * dp[r];
-      }
+      for (int e = 0; e < 4; ++e) sa[4 * g + e] = fast_exp2(fmaf(sa[4 * g + e], c, -lv[e]));
+    });
+    if (diag) {
+      // (a padded key's P only reaches this lane's own dK / dV column: zeroed at the store)
+      const int kd = key - qs0 - 4 * hh;
+      sfor<16>([&](auto R) {
+        constexpr int r = decltype(R)::value;
+        zero_if_gt<8 * (r >> 2) + (r & 3)>(sa, r, kd);
+      });
     }
+#pragma unroll
+    for (int r = 0; r < 16; ++r) dp[r] = sa[r] * dp[r];
 #pragma unroll
     for (int ss = 0; ss < 2; ++ss) {
       const bf16x8 pb = acc_frag(sa, ss);
@@ -1025,12 +1044,12 @@ __global__ __launch_bounds__(256, OCC) void attn_bwd_dq_kernel(AttnArgs p) {
     // (+inf stays +inf: a fully masked row)
     lse2 = q < S ? p.lse[(long long)bh * S + q] * LOG2E : INFINITY;
     if (q < S && hh == 0) {
-      p.delta[(long long)bh * S + q] = dl;
+      p.delta[(long long)bh * S + q] = -dl;  // (negated: attn_bwd_pre_kernel)
       p.delta[(long long)p.N * H * S + (long long)bh * S + q] = lse2;
     }
   } else {
     lse2 = q < S ? p.delta[(long long)p.N * H * S + (long long)bh * S + q] : INFINITY;
-    dl = q < S ? p.delta[(long long)bh * S + q] : 0.f;
+    dl = q < S ? -p.delta[(long long)bh * S + q] : 0.f;
   }
   pin_loaded(qf);
   pin_loaded(df);

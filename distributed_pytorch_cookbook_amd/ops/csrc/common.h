@@ -14,6 +14,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <utility>
+
 #define DPC_API extern "C" __attribute__((visibility("default")))
 
 typedef unsigned short bf16_t;  // raw bf16 payload
@@ -23,6 +25,17 @@ typedef float floatx4 __attribute__((ext_vector_type(4)));
 typedef float floatx16 __attribute__((ext_vector_type(16)));
 
 namespace dpc {
+
+// sfor<N>(f): f(integral_constant<int, 0>) ... f(integral_constant<int, N-1>) -- a loop whose index
+// is a compile-time constant in the body (template arguments, register-array indices)
+template <int... Is, class F>
+__device__ __forceinline__ void sfor_seq(std::integer_sequence<int, Is...>, F&& f) {
+  (f(std::integral_constant<int, Is>{}), ...);
+}
+template <int N, class F>
+__device__ __forceinline__ void sfor(F&& f) {
+  sfor_seq(std::make_integer_sequence<int, N>{}, f);
+}
 
 __device__ __forceinline__ float bf2f(bf16_t v) {
   return __uint_as_float(((unsigned)v) << 16);

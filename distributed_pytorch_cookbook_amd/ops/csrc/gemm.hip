@@ -92,7 +92,7 @@ __device__ __forceinline__ void colsum_flush(float (&cs)[4], float* colsum, int 
   if (nb + lane < N) atomicAdd(colsum + nb + lane, v);
 }
 
-// ---- Shared epilogue of the LDS-DMA kernels (v2-v5).  A wave owns FM x 4 fragments of
+// ---- Shared epilogue of the LDS-DMA kernels (v2, v3).  A wave owns FM x 4 fragments of
 // 16x16 (FM/2 passes of 32 rows x 64 columns).  Each pass stages its f32 rows through LDS
 // ([32][64] per wave, columns XOR-swizzled by ((row >> 2) & 3) << 4) so that bias /
 // residual / aux / C move 16 B (f32) or 8 B (bf16) per lane along rows.  Every global READ
@@ -619,143 +619,12 @@ __global__ __launch_bounds__((V3Cfg<BM_, BN_, WM, WN, KB, STAGES>::NTH), (V3Cfg<
   epi_tile<FM, (FM == 4 && Cfg::WGS == 1)>(p, acc, reinterpret_cast<float*>(smem) + wid * 32 * 64, splits, m0 + wr * Cfg::WTM, n0 + wc * 64, lane);
 }
 
-// =====================================================================================
-// v5: 256x256 ping-pong.  A 4-slot ring of 32-deep k-slices (32 KiB each) filled by LDS-DMA, but the
-// two wave groups of the workgroup (waves 0-3 = rows 0-127, waves 4-7 = rows 128-255; waves
-// w and w+4 share a SIMD) run one barrier interval apart: while one group's MFMA segment
-// (16 x v_mfma_f32_16x16x32_bf16 = 256 cycles) runs, its SIMD partner is in a read segment
-// (fragment ds_reads, LDS-DMA issue, counted vmcnt, lgkmcnt(0)) and vice versa, so the
-// matrix pipe of every SIMD alternates between two waves instead of stalling on one wave's
-// reads.  Per k-slice s each wave runs two phases:
-//   phase (s,0): read B(s) + A rows 0-63 (s)                        | MFMA rows 0-63
-//   phase (s,1): read A rows 64-127 (s); DMA slice s+3; wait slice s+1 | MFMA rows 64-127
-// A read segment only issues its ds_reads; they are retired by lgkmcnt waits at the start of
-// the following MFMA segment.  RAW: slice s+1 is read in phase (s+1,0), after every wave's
-// counted vmcnt in its phase (s,1) read segment and the barrier that ends it (the lagging
-// group's wait precedes the barrier before the leading group's next read segment).  WAR:
-// slot (s+3)%4 last held slice s-1, last read in phase (s-1,1) -- two phases before the DMA,
-// so even the lagging group's reads were retired (start of its MFMA segment) before a barrier
-// the issuing wave has passed.  Slices past the end are issued with an empty descriptor (they
-// land as zeros in a slot nobody reads) so every vmcnt in the loop is the same constant.
-
-__device__ __forceinline__ void seg_barrier() {
-  __builtin_amdgcn_sched_barrier(0);
-  __builtin_amdgcn_s_barrier();
-  asm volatile("" ::: "memory");
-  __builtin_amdgcn_sched_barrier(0);
-}
-
-template <bool AK, bool BK>
-__global__ __launch_bounds__(512, 1) void gemm5_kernel(GemmArgs p, unsigned long long a_bytes,
-                                                       unsigned long long b_bytes) {
-  using Cfg = V3Cfg<256, 256, 2, 4, 32, 4>;
-  constexpr int NS = 4, SLOT = Cfg::TA + Cfg::TB;
-  constexpr int NLA = Cfg::NLA, NLB = Cfg::NLB;  // 2 + 2 DMA instructions per wave per slice
-  __shared__ __attribute__((aligned(16))) bf16_t smem[Cfg::SMEM];
-  const int tiles_m = (p.M + 255) / 256, tiles_n = (p.N + 255) / 256;
-  const int nwg = tiles_m * tiles_n;
-  const TileSlot ts = tile_slot(p, nwg);
-  const int bid = ts.bid;
-  const int group = GROUP_M * tiles_n;
-  const int gid = bid / group, first_m = gid * GROUP_M;
-  const int gsz = min(tiles_m - first_m, GROUP_M);
-  const int tm = first_m + (bid % group) % gsz;
-  const int tn = (bid % group) / gsz;
-  const int m0 = tm * 256, n0 = tn * 256;
-
-  const int lane = threadIdx.x & 63;
-  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int wr = wid >> 2, wc = wid & 3;
-  const int ar = wr * 128, bc = wc * 64;
-
-  int va[NLA], vb[NLB];
-  dma_offsets3<32, AK, NLA>(va, p.lda, wid, lane);
-  dma_offsets3<32, BK, NLB>(vb, p.ldb, wid, lane);
-  const unsigned long long a_org = AK ? (unsigned long long)m0 * p.lda * 2 : (unsigned long long)m0 * 2;
-  const unsigned long long b_org = BK ? (unsigned long long)n0 * p.ldb * 2 : (unsigned long long)n0 * 2;
-  const unsigned long long a_step = AK ? 64ull : 32ull * p.lda * 2;
-  const unsigned long long b_step = BK ? 64ull : 32ull * p.ldb * 2;
-  floatx4 acc[8][4];
-#pragma unroll
-  for (int i = 0; i < 8; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
-
-  const int nk_all = (p.K + 31) / 32;
-  const int splits = ts.splits;
-  const int per = (nk_all + splits - 1) / splits;
-  const int kt0 = ts.split * per;
-  const int nk = max(0, min(nk_all, kt0 + per) - kt0);
-#define DPC_ISSUE5A(s_)                                                                              \
-  issue_tile_v<NLA>(p.A, a_bytes, a_org + a_step * (unsigned long long)(kt0 + (s_)), (s_) < nk, va,  \
-                    smem + ((s_) % NS) * SLOT, wid)
-#define DPC_ISSUE5B(s_)                                                                              \
-  issue_tile_v<NLB>(p.B, b_bytes, b_org + b_step * (unsigned long long)(kt0 + (s_)), (s_) < nk, vb,  \
-                    smem + ((s_) % NS) * SLOT + Cfg::TA, wid)
-
-  if (nk > 0) {
-    DPC_ISSUE5A(0); DPC_ISSUE5B(0);
-    DPC_ISSUE5A(1); DPC_ISSUE5B(1);
-    DPC_ISSUE5A(2); DPC_ISSUE5B(2);
-    wait_vm<2 * (NLA + NLB)>();  // slice 0 landed (slices 1, 2 in flight)
-    seg_barrier();
-    if (wr == 1) seg_barrier();  // the second group runs one barrier interval behind
-    bf16x8 alo[4], ahi[4], b[4];
-    for (int s = 0; s < nk; ++s) {
-      const bf16_t* la = smem + (s % NS) * SLOT;
-      const bf16_t* lb = la + Cfg::TA;
-      // ---- phase (s,0): read segment
-#pragma unroll
-      for (int j = 0; j < 4; ++j) b[j] = frag3<32, BK>(lb, bc + j * 16, 0, lane);
-#pragma unroll
-      for (int i = 0; i < 4; ++i) alo[i] = frag3<32, AK>(la, ar + i * 16, 0, lane);
-      seg_barrier();
-      // ---- phase (s,0): MFMA segment (the compiler's counted lgkmcnt waits retire the reads)
-      __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(alo[i], b[j], acc[i][j], 0, 0, 0);
-      __builtin_amdgcn_s_setprio(0);
-      seg_barrier();
-      // ---- phase (s,1): read segment
-#pragma unroll
-      for (int i = 0; i < 4; ++i) ahi[i] = frag3<32, AK>(la, ar + 64 + i * 16, 0, lane);
-      DPC_ISSUE5A(s + 3);
-      DPC_ISSUE5B(s + 3);
-      wait_vm<2 * (NLA + NLB)>();  // slice s+1 landed for this wave
-      seg_barrier();
-      // ---- phase (s,1): MFMA segment
-      __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-          acc[4 + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ahi[i], b[j], acc[4 + i][j], 0, 0, 0);
-      __builtin_amdgcn_s_setprio(0);
-      seg_barrier();
-    }
-    if (wr == 0) seg_barrier();  // rebalance the barrier count of the two groups
-  }
-#undef DPC_ISSUE5A
-#undef DPC_ISSUE5B
-
-  // ---------------- epilogue: four passes of 32 rows per wave through LDS (as v4)
-  epi_tile<8, false>(p, acc, reinterpret_cast<float*>(smem) + wid * 32 * 64, splits, m0 + ar, n0 + bc, lane);
-}
+// (v5, the 256x256 eight-wave ping-pong kernel, was removed in round 5: no tuned-table entry and
+// no policy branch chose it once v7 took the weight gradients)
 
 }  // namespace dpc
 
 using namespace dpc;
-
-static void launch_v5(const GemmArgs* a, dim3 grid, hipStream_t stream, unsigned long long ab,
-                      unsigned long long bb) {
-  if (a->a_kmaj && a->b_kmaj) hipLaunchKernelGGL((gemm5_kernel<true, true>), grid, dim3(512), 0, stream, *a, ab, bb);
-  else if (a->a_kmaj) hipLaunchKernelGGL((gemm5_kernel<true, false>), grid, dim3(512), 0, stream, *a, ab, bb);
-  else if (!a->b_kmaj) hipLaunchKernelGGL((gemm5_kernel<false, false>), grid, dim3(512), 0, stream, *a, ab, bb);
-  else hipLaunchKernelGGL((gemm5_kernel<false, true>), grid, dim3(512), 0, stream, *a, ab, bb);
-}
 
 template <int BM_, int BN_, int WM, int WN, int KB, int STAGES>
 static void launch_v3(const GemmArgs* a, dim3 grid, hipStream_t stream, unsigned long long ab,
@@ -788,8 +657,7 @@ static void launch_v2(const GemmArgs* a, dim3 grid, hipStream_t stream, unsigned
 
 // -1: auto; 1: v1; 2: v2 KB64 x2 stages; 3: KB64 x3; 4: KB32 x3; 5: KB32 x4;
 // 6-10: v3 (6: 256x256 KB64 x2, 7: 256x256 KB32 x4, 8: 256x128 KB64 x2, 9: 256x128 KB32 x4,
-// 10: 256x128 KB32 x3); 11: v4 (256x256, pipelined k32 ring); 12: v5 (256x256 ping-pong);
-// 13 / 14: v6 (v5 with the DMA spread over both read segments; 4- / 5-slot ring);
+// 10: 256x128 KB32 x3); (11-14: v4 / v5 / v6, removed);
 // 16 / 19 / 20: v7 (gemm7.hip: persistent one-wave-per-SIMD 256x256, 5-slot ring; DMA
 // placement 0 / 1 / 2); 17: v7, one unit per workgroup; plain f32 products split K
 static int g_gemm_impl = -1;
@@ -890,12 +758,10 @@ DPC_API int dpc_gemm(const GemmArgs* a, hipStream_t stream) {
   if (g_gemm_impl < 0 && a->impl <= 0 && v2_ok && plain && !a->a_kmaj && !a->b_kmaj && policy_impl(a) <= 0) {
     // weight gradient: the split-K persistent kernel (v7, chosen above when its requirements
     // hold -- its own planner splits K to fill the chip however few tiles there are), else the
-    // 256x256 ping-pong kernel (v5) once there are enough 128x128 tiles to spread over the
-    // k-splits, else the 2-stage 64-k kernel.  (Round 4: the pipeline stage proxy's micro-batch
+    // 2-stage 64-k kernel.  (Round 4: the pipeline stage proxy's micro-batch
     // out-projection weight gradient, 1024 x 1024 x 16368, off the table, fell to the 2-stage
     // kernel at 506 TF/s -- 8.7 ms of a 262 ms stage step, profiles/r4_pp/.)
-    const int t128 = ((a->M + BM - 1) / BM) * ((a->N + BN - 1) / BN);
-    if (impl != 20) impl = t128 < 100 ? 2 : 12;
+    if (impl != 20) impl = 2;
   }
   if (impl >= 15 && impl <= 26) {  // v7 (gemm7.hip): 4-wave 256x256, split-K f32 products
     GemmArgs c = *a;
@@ -948,9 +814,8 @@ DPC_API int dpc_gemm(const GemmArgs* a, hipStream_t stream) {
       case 3: launch_v2<64, 3>(&b, g, stream, ab, bb); break;
       case 4: launch_v2<32, 3>(&b, g, stream, ab, bb); break;
       case 10: launch_v3<256, 128, 4, 2, 32, 3>(&b, g, stream, ab, bb); break;
-      case 12: launch_v5(&b, g, stream, ab, bb); break;
       case 2: launch_v2<64, 2>(&b, g, stream, ab, bb); break;
-      default: return 1;  // (5-9, 11, 13, 14: removed implementations, chosen by no table or policy)
+      default: return 1;  // (5-9, 11-14: removed implementations, chosen by no table or policy)
     }
     return (int)hipGetLastError();
   }

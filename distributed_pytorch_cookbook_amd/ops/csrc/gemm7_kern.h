@@ -121,16 +121,9 @@ __device__ __forceinline__ void g7_wait() {
 // keeps each epilogue's live set (operand prefetch + bias or column sums) small enough that
 // nothing of the main loop spills: a spill reload in the loop is a vector-memory op, which
 // breaks the counted DMA waits.
-// sfor<N>: compile-time loop -- the fused row body is beyond clang's full-unroll threshold and
-// a rolled loop indexes acc[i] dynamically, which moves all 256 accumulators to scratch.
-template <int... Is, class F>
-__device__ __forceinline__ void sfor_seq(std::integer_sequence<int, Is...>, F&& f) {
-  (f(std::integral_constant<int, Is>{}), ...);
-}
-template <int N, class F>
-__device__ __forceinline__ void sfor(F&& f) {
-  sfor_seq(std::make_integer_sequence<int, N>{}, f);
-}
+// (sfor<N>, the compile-time loop: common.h -- the fused row body is beyond clang's full-unroll
+// threshold and a rolled loop indexes acc[i] dynamically, which moves all 256 accumulators to
+// scratch)
 
 #define G7_AI __attribute__((always_inline))
 typedef unsigned g7_u32x4 __attribute__((ext_vector_type(4)));

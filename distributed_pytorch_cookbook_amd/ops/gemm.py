@@ -74,14 +74,15 @@ _TUNE_PATH = os.environ.get("DPC_GEMM_TABLE_PATH") or os.path.join(
 _TUNE = os.environ.get("DPC_GEMM_TUNE", "0") == "1"
 _USE_TABLE = os.environ.get("DPC_GEMM_TABLE", "1") == "1"
 # 0 = the dispatcher policy; 2 / 3 / 4 = v2 (128 x 128, 64-deep x 2 / 3 stages, 32-deep x 3),
-# 10 = v3 (256 x 128, 8 waves, two per CU), 12 = v5 (256 x 256 ping-pong, weight gradients);
+# 10 = v3 (256 x 128, 8 waves, two per CU);
 # 16 / 17 / 19 / 20 / 22 / 23 = the 4-wave 256x256 kernel (gemm7.hip;
 # 16 / 20 / 22 run the paired-M0 DMA issue, 19 / 23 the quad form), 21 = v8 (two per CU),
 # 24 = v7d (the GELU / GELU' epilogues deferred into the next tile's main loop), 25 = v7 with the
 # split DMA interleave forced (20 / 22 already take it when an operand is mn-major), 26 = v9 (64-deep
 # stages; 16 / 20 / 22 / 23 already take it for plain nt products).  (5-9, 11, 13, 14 -- v3 / v4 /
-# v6 variants that neither the table nor the policy chose -- were removed in round 4.)
-_CANDIDATES = (0, 2, 3, 4, 10, 12, 16, 17, 19, 20, 21, 22, 23, 24, 25, 26)
+# v6 variants that neither the table nor the policy chose -- were removed in round 4, 12 = v5 in
+# round 5.)
+_CANDIDATES = (0, 2, 3, 4, 10, 16, 17, 19, 20, 21, 22, 23, 24, 25, 26)
 _TUNE_MAX_OUT_BYTES = 16 << 30  # (the GPT-2 small LM-head logits are 6.6 GB)
 
 
