@@ -32,7 +32,7 @@ from ..ops.attention import DECODE_MAX_S, attention_bwd, attention_fwd, decode_a
 from ..ops.elementwise import bias_act_bwd
 from ..ops.dropout import dropout_residual
 from ..ops.embedding import embedding_bwd, embedding_fwd
-from ..ops.gemm import (ACT_GELU, ACT_RELU, act_code, linear_dgrad, linear_fwd, linear_wgrad,
+from ..ops.gemm import (ACT_GELU, ACT_NONE, ACT_RELU, act_code, linear_dgrad, linear_fwd, linear_wgrad,
                         register_side_stream)
 from ..ops.loss import cross_entropy_fused, cross_entropy_rows
 from ..ops.norm import layernorm_bwd, layernorm_fwd
@@ -176,6 +176,41 @@ def _layer_forward(x, mask, layer, store, N, S, act, training, drops, attend=Non
     return x3, saved
 
 
+class _FfnTail:
+    """A layer's FFN down projection seen from the LayerNorm that consumes its output (the next
+    layer's LN1, or the final norm).  The reference's FFN ends in ``drop(act(z2))`` added to the
+    residual, so the first backward op of a layer is ``dz2 = bf16(dx3 * keep * act'(z2))`` plus
+    the bias column sums -- one pass over the f32 residual gradient dx3 that the consumer's
+    LayerNorm backward has just written.  The consumer does it in that pass instead
+    (layernorm_bwd's gout / gz) and leaves dz2 and the bias-gradient partial here; the layer's
+    own backward then starts from them.  Filled in the forward only when the layer keeps its
+    activations (no recompute: z2 must exist when the consumer's backward runs)."""
+
+    __slots__ = ("z2", "act", "drop", "dz2", "db")
+
+    def __init__(self):
+        self.z2 = self.act = self.drop = self.dz2 = self.db = None
+
+    def consume(self, ln_bwd_kwargs, T, D, device, cdt):
+        """Extend a LayerNorm backward call with this tail's fused consumer (if it has one)."""
+        if self.z2 is None:
+            return
+        self.dz2 = torch.empty(T, D, device=device, dtype=cdt)
+        self.db = torch.zeros(D, device=device, dtype=torch.float32)
+        ln_bwd_kwargs.update(gout=self.dz2, gsum=self.db, drop=self.drop)
+        if self.act != ACT_NONE:
+            ln_bwd_kwargs.update(gz=self.z2, gact=self.act)
+        self.z2 = None
+
+
+# the fused consumer needs a bf16 operand on the GPU (the kernel's gout); off: DPC_FUSE_FFN_TAIL=0
+_FUSE_TAIL = os.environ.get("DPC_FUSE_FFN_TAIL", "1") == "1"
+
+
+def _tail_ok(x, cdt):
+    return _FUSE_TAIL and (cdt == torch.bfloat16 or not x.is_cuda)
+
+
 class _LayerFn(torch.autograd.Function):
     """One decoder layer.  With ``recompute`` only the layer input is kept and the forward
     is re-run at the start of the backward (activation recompute: the saved activations of
@@ -183,7 +218,8 @@ class _LayerFn(torch.autograd.Function):
     bytes of its f32 input, for one extra forward)."""
 
     @staticmethod
-    def forward(ctx, x, mask, layer, store, N, S, act, training, drops=(None, None), recompute=False):
+    def forward(ctx, x, mask, layer, store, N, S, act, training, drops=(None, None), recompute=False,
+                prev_tail=None, tail=None):
         u = layer._unit_id
         store.pre_forward(u)
         x3, saved = _layer_forward(x, mask, layer, store, N, S, act, training and not recompute, drops)
@@ -192,6 +228,9 @@ class _LayerFn(torch.autograd.Function):
             ctx.save_for_backward(x, mask, *(saved or ()))
             ctx.layer, ctx.store, ctx.dims, ctx.act = layer, store, (N, S), act
             ctx.drops, ctx.recompute = drops, recompute
+            ctx.prev_tail, ctx.tail = prev_tail, tail
+            if tail is not None and saved is not None and _tail_ok(x, store.compute_dtype):
+                tail.z2, tail.act, tail.drop = saved[-1], act, drops[1]
         return x3
 
     @staticmethod
@@ -203,9 +242,10 @@ class _LayerFn(torch.autograd.Function):
         store.pre_backward(layer._unit_id)
         if ctx.recompute:
             _, saved = _layer_forward(x, mask, layer, store, N, S, act, True, ctx.drops)
-        dx = _layer_backward(dx3, x, mask, saved, layer, store, N, S, H, hd, act, ctx.drops)
+        dx = _layer_backward(dx3, x, mask, saved, layer, store, N, S, H, hd, act, ctx.drops,
+                             ctx.prev_tail, ctx.tail)
         store.post_backward(layer._unit_id)
-        return dx, None, None, None, None, None, None, None, None, None
+        return dx, None, None, None, None, None, None, None, None, None, None, None
 
 
 # Weight gradients of a layer run on a side HIP stream, concurrently with the input-gradient
@@ -247,8 +287,10 @@ class _SideWork:
             torch.cuda.current_stream(self.stream.device).wait_stream(self.stream)
 
 
-def _layer_backward(dx3, x, mask, saved, layer, store, N, S, H, hd, act, drops):
-    """Hand-written backward of ``_layer_forward``; weight grads go into the store."""
+def _layer_backward(dx3, x, mask, saved, layer, store, N, S, H, hd, act, drops, prev_tail=None, tail=None):
+    """Hand-written backward of ``_layer_forward``; weight grads go into the store.  ``tail``:
+    this layer's _FfnTail (dz2 already formed by the consumer's LayerNorm backward);
+    ``prev_tail``: the previous layer's, served by this layer's LN1 backward."""
     (h1, mu1, rs1, qkv, o, lse, x2, h2, mu2, rs2, zup, uact, z2) = saved
     attn, fc = layer.attn, layer.fc
     w, g = store.weight, store.grad
@@ -257,7 +299,12 @@ def _layer_backward(dx3, x, mask, saved, layer, store, N, S, H, hd, act, drops):
     dx = dx3.contiguous()  # becomes dx2 then dx (in place)
     # FFN down projection: x3 = x2 + drop(act(z2)), z2 = u W2^T + b2
     side = _SideWork(dx.device)
-    dz2 = bias_act_bwd(dx, z2, act, g(fc.down_proj.bias), out_dtype=cdt, drop=drop_ffn)
+    if tail is not None and tail.dz2 is not None:  # formed by the consumer's LayerNorm backward
+        dz2 = tail.dz2
+        g(fc.down_proj.bias).add_(tail.db)
+        tail.dz2 = tail.db = None
+    else:
+        dz2 = bias_act_bwd(dx, z2, act, g(fc.down_proj.bias), out_dtype=cdt, drop=drop_ffn)
     side.run(lambda: linear_wgrad(dz2, uact, out=g(fc.down_proj.weight)), dz2, uact)
     # up projection gradient with act' fused (relu' from its output, gelu' from z1)
     dz1 = linear_dgrad(dz2, w(fc.down_proj.weight), act_bwd=act, aux_in=zup, out_dtype=cdt,
@@ -283,8 +330,11 @@ def _layer_backward(dx3, x, mask, saved, layer, store, N, S, H, hd, act, drops):
 
     side.run(qkv_wgrad, dqkv, h1, gqkv)
     dh1 = linear_dgrad(dqkv, _qkv_weight(store, attn), out_dtype=_dh_dtype(cdt))
+    kw = {}
+    if prev_tail is not None:  # the previous layer's down-projection bias / act / dropout backward
+        prev_tail.consume(kw, x.shape[0], x.shape[1], x.device, cdt)
     layernorm_bwd(dh1, x, mu1, rs1, w(layer.norm1.weight), dx, g(layer.norm1.weight),
-                  g(layer.norm1.bias))
+                  g(layer.norm1.bias), **kw)
     side.join()
     return dx
 
@@ -293,7 +343,7 @@ class _HeadFn(torch.autograd.Function):
     """norm_out -> lm_head -> fused cross-entropy (reference gpt.py:229-231 + main-*.py loss)."""
 
     @staticmethod
-    def forward(ctx, x, targets, norm, head, store, unit, training, want_correct):
+    def forward(ctx, x, targets, norm, head, store, unit, training, want_correct, prev_tail=None):
         store.pre_forward(unit)
         w = store.weight
         cdt = store.compute_dtype
@@ -328,6 +378,7 @@ class _HeadFn(torch.autograd.Function):
         if training:
             ctx.save_for_backward(x, hf, mu, rs, buf)
             ctx.mods, ctx.store, ctx.unit, ctx.V = (norm, head), store, unit, V
+            ctx.prev_tail = prev_tail
         ctx.mark_non_differentiable(n_valid)
         if n_correct is None:
             n_correct = torch.zeros((), device=x.device)
@@ -347,9 +398,12 @@ class _HeadFn(torch.autograd.Function):
         dhf = linear_dgrad(dlogits, _head_weight_padded(store, head, dlogits.shape[1]),
                            out_dtype=_dh_dtype(store.compute_dtype), alpha_t=scale)
         dx = torch.zeros_like(x)
-        layernorm_bwd(dhf, x, mu, rs, w(norm.weight), dx, g(norm.weight), g(norm.bias))
+        kw = {}
+        if ctx.prev_tail is not None:  # the last layer's down-projection bias / act / dropout backward
+            ctx.prev_tail.consume(kw, x.shape[0], x.shape[1], x.device, store.compute_dtype)
+        layernorm_bwd(dhf, x, mu, rs, w(norm.weight), dx, g(norm.weight), g(norm.bias), **kw)
         store.post_backward(unit)
-        return dx, None, None, None, None, None, None, None
+        return dx, None, None, None, None, None, None, None, None
 
 
 def head_logits(model, x, store):
@@ -391,15 +445,20 @@ def run_layers(model, store, x, mask, N, S, layers, training, dropout_seed=None)
     if use_drop and dropout_seed is None:
         dropout_seed = model.next_dropout_seed()
     recompute = bool(getattr(model, "recompute", False)) and training
+    prev = None
     for layer in layers:
         drops = model.dropout_specs(layer, dropout_seed) if use_drop else (None, None)
-        x = _LayerFn.apply(x, mask, layer, store, N, S, act, training, drops, recompute)
+        tail = _FfnTail() if training else None
+        x = _LayerFn.apply(x, mask, layer, store, N, S, act, training, drops, recompute, prev, tail)
+        prev = tail
+    if prev is not None:
+        x._dpc_ffn_tail = prev  # (run_head's final norm consumes the last layer's output)
     return x
 
 
 def run_head(model, store, x, targets, training, want_correct):
     return _HeadFn.apply(x, targets.reshape(-1), model.norm_out, model.lm_head, store,
-                         model._head_unit_id, training, want_correct)
+                         model._head_unit_id, training, want_correct, getattr(x, "_dpc_ffn_tail", None))
 
 
 def last_rows(x, N, S):

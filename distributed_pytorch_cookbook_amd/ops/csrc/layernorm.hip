@@ -49,6 +49,12 @@ struct LNArgs {
   long long ld_add, ld_xout;
   const unsigned* drop_seed;  // device seed of the forward (drop_key_of); null: drop_key
   unsigned drop_site;
+  // bwd, the fused consumer with an activation in front of the dropout (the FFN down projection
+  // of the PREVIOUS layer: x3 = x2 + drop(act(z2)), its bias / act / dropout backward fused into
+  // the LayerNorm that consumes x3): g = dx * keep * act'(gz)  (gz bf16 [T][ld_gz], act per Act)
+  const void* gz;
+  long long ld_gz;
+  int gact;
 };
 
 template <int NV>
@@ -157,6 +163,17 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(LNArgs p) {
     const float4* dyr = reinterpret_cast<const float4*>(p.dy + row * p.lddy);
     const uint2* dyb = reinterpret_cast<const uint2*>(static_cast<const bf16_t*>((const void*)p.dy) + row * p.lddy);
     const float mu = p.mean[row], rs = p.rstd[row];
+    // the act' operand of the fused consumer, loaded with the row (it is used after the row's
+    // reductions)
+    uint2 zz[NV];
+    if (gout && p.gz) {
+      const uint2* zr = reinterpret_cast<const uint2*>(static_cast<const bf16_t*>(p.gz) + row * p.ld_gz);
+#pragma unroll
+      for (int i = 0; i < NV; ++i) {
+        const int c = lane + i * 64;
+        zz[i] = c < nv4 ? zr[c] : make_uint2(0u, 0u);
+      }
+    }
     float4 xh[NV], dg[NV];
     float s1 = 0.f, s2 = 0.f;
 #pragma unroll
@@ -197,6 +214,12 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(LNArgs p) {
         o.w += rs * (dg[i].w - s1 - xh[i].w * s2);
         dxr[c] = o;
         if (gout) {
+          if (p.gz) {
+            o.x *= act_grad(__uint_as_float(zz[i].x << 16), p.gact);
+            o.y *= act_grad(__uint_as_float(zz[i].x & 0xffff0000u), p.gact);
+            o.z *= act_grad(__uint_as_float(zz[i].y << 16), p.gact);
+            o.w *= act_grad(__uint_as_float(zz[i].y & 0xffff0000u), p.gact);
+          }
           if (p.drop_scale != 0.f) {
             const uint32_t idx = (uint32_t)(row * p.D + 4 * c);
             o.x *= drop_factor(idx + 0, dkey, p.drop_thresh, p.drop_scale);

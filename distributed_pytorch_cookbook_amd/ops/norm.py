@@ -11,6 +11,7 @@ import torch
 
 from . import _lib
 from .dropout import keep_mask
+from .gemm import act_grad_ref
 
 
 def _use_hip(x: torch.Tensor, y_dtype: torch.dtype, add=None) -> bool:
@@ -83,7 +84,7 @@ def layernorm_fwd(x: torch.Tensor, gamma: torch.Tensor, beta: torch.Tensor, eps:
 def layernorm_bwd(dy: torch.Tensor, x: torch.Tensor, mean: torch.Tensor, rstd: torch.Tensor,
                   gamma: torch.Tensor, dx: torch.Tensor, dgamma: torch.Tensor, dbeta: torch.Tensor,
                   gout: torch.Tensor | None = None, gsum: torch.Tensor | None = None,
-                  drop=None):
+                  drop=None, gz: torch.Tensor | None = None, gact=None):
     """dx += LN'(dy); dgamma += sum dy*xhat; dbeta += sum dy.  x, dx f32 [T, D]; dy f32 or
     bf16 (the input gradient of the Linear that consumed the LayerNorm's output -- bf16 under
     the reference's autocast too).
@@ -91,7 +92,9 @@ def layernorm_bwd(dy: torch.Tensor, x: torch.Tensor, mean: torch.Tensor, rstd: t
     Optional fused consumer of the updated dx (the backward of the bias + dropout of the
     projection whose output fed this LayerNorm's residual): ``gout = dx * keep`` (bf16,
     the next GEMM's operand) and ``gsum += colsum(dx * keep)`` (that projection's bias
-    gradient), saving a separate pass over the f32 dx.
+    gradient), saving a separate pass over the f32 dx.  With ``gz`` (bf16 [T, D]) and ``gact``
+    the projection's output went through an activation first (the reference's FFN applies it
+    after the down projection too): ``gout = dx * keep * act'(gz)``.
     """
     T, D = x.shape
     if not (x.is_cuda and dy.dtype in (torch.float32, torch.bfloat16) and gamma.dtype == torch.float32
@@ -106,6 +109,8 @@ def layernorm_bwd(dy: torch.Tensor, x: torch.Tensor, mean: torch.Tensor, rstd: t
         dbeta.add_(dyf.sum(0))
         if gout is not None:
             g = dx if drop is None else dx * keep_mask(drop, T, D, dx.device)
+            if gz is not None:
+                g = g * act_grad_ref(gz.float(), gact)
             gout.copy_(g)
             if gsum is not None:
                 gsum.add_(g.sum(0))
@@ -125,6 +130,11 @@ def layernorm_bwd(dy: torch.Tensor, x: torch.Tensor, mean: torch.Tensor, rstd: t
         if gout.dtype != torch.bfloat16 or gout.stride(1) != 1 or gout.stride(0) % 4 or D % 4:
             raise ValueError("layernorm_bwd: gout must be bf16 with 8-B aligned contiguous rows")
         args.gout, args.gsum, args.ld_gout = gout.data_ptr(), _lib.ptr(gsum), gout.stride(0)
+        if gz is not None:
+            if (gz.dtype != torch.bfloat16 or gz.shape != x.shape or gz.stride(1) != 1 or gz.stride(0) % 4
+                    or gz.data_ptr() % 8):
+                raise ValueError("layernorm_bwd: gz must be bf16 [T, D] with 8-B aligned contiguous rows")
+            args.gz, args.ld_gz, args.gact = gz.data_ptr(), gz.stride(0), int(gact)
         if drop is not None:
             if T * D >= 2 ** 32:
                 raise ValueError("layernorm_bwd: dropout needs T * D < 2^32")

@@ -484,6 +484,22 @@ def test_layernorm(D):
         ref = dx2 if drop is None else dx2 * keep_mask(drop, T, D, dev)
         assert rel_err(gout, ref) < 5e-3
         assert rel_err(gsum - 1, ref.sum(0)) < 1e-4
+    # ... with an activation in front of the dropout (the previous layer's FFN tail):
+    # gout = bf16(dx * keep * act'(z))
+    from distributed_pytorch_cookbook_amd.ops.gemm import act_grad_ref
+    z = (torch.randn(T, D, device=dev) * 2).bfloat16()
+    for act in (1, 2):
+        for drop in (None, DropSpec.make(0.2, seed=7, site=1)):
+            dx2 = dres.clone()
+            gout = torch.empty(T, D, device=dev, dtype=torch.bfloat16)
+            gsum = torch.zeros(D, device=dev)
+            layernorm_bwd(dy, x, mean, rstd, g, dx2, torch.zeros(D, device=dev), torch.zeros(D, device=dev),
+                          gout=gout, gsum=gsum, drop=drop, gz=z, gact=act)
+            ref = dx2 * act_grad_ref(z.float(), act)
+            if drop is not None:
+                ref = ref * keep_mask(drop, T, D, dev)
+            assert rel_err(gout, ref) < 5e-3, act
+            assert rel_err(gsum, ref.sum(0)) < 1e-4, act
     # bf16 dy (the input gradient of the next Linear): same math on the rounded values
     dyb = dy.bfloat16()
     dx3 = dres.clone()

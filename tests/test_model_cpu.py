@@ -94,6 +94,40 @@ def test_fused_backward_matches_autograd(act, pad):
         assert err < 1e-4, (n, err.item())
 
 
+@pytest.mark.parametrize("act", ["relu", "gelu"])
+@pytest.mark.parametrize("dropout", [0.0, 0.2])
+def test_ffn_tail_fused_into_consumer_layernorm(monkeypatch, act, dropout):
+    """Every layer's down-projection bias / act' / dropout backward runs inside the LayerNorm
+    backward that consumes its output (the next layer's LN1, the final norm: models/fused.py
+    _FfnTail) -- no separate bias_act_bwd pass -- with the gradients of the unfused path."""
+    import distributed_pytorch_cookbook_amd.models.fused as fz
+
+    calls = []
+    real = fz.bias_act_bwd
+    monkeypatch.setattr(fz, "bias_act_bwd", lambda *a, **k: calls.append(1) or real(*a, **k))
+
+    def grads(fuse):
+        monkeypatch.setattr(fz, "_FUSE_TAIL", fuse)
+        torch.manual_seed(0)
+        m = TransformerDecoderLM(dim=64, head_dim=16, heads=4, num_layers=3, vocab_size=97,
+                                 max_position_embeddings=24, activation=act, dropout=dropout)
+        m.train()
+        ids, pos, mask, tg = batch(pad=True)
+        store = LocalStore(m, "cpu")
+        store.zero_grad()
+        m(ids, pos, mask, targets=tg, dropout_seed=1234).loss.backward()
+        return {n: p.grad.clone() for n, p in m.named_parameters()}
+
+    calls.clear()
+    fused = grads(True)
+    assert calls == []  # all three layers fused
+    plain = grads(False)
+    assert len(calls) == 3
+    for n in plain:
+        err = (fused[n] - plain[n]).norm() / plain[n].norm().clamp_min(1e-12)
+        assert err < 1e-5, (n, err.item())
+
+
 def test_causality():
     m = tiny()
     ids, pos, _, _ = batch(pad=False)
