@@ -197,6 +197,99 @@ __global__ __launch_bounds__(CE_NT) void ce_kernel(CEArgs p) {
   }
 }
 
+// Register-resident row with the per-logit vector-ALU work cut to what the math needs (round 5;
+// ce_kernel above measured ~24 VALU per logit -- per-element end-of-row, target and argmax
+// compares -- and ran VALU-bound at 4.4 TB/s): per 16-B chunk one v_max3 tree, then
+// 2^(x log2e - max log2e) by one FMA + v_exp_f32 per logit; the tail chunk (V % 8) masked in a
+// branch only its thread takes; the target logit read by one lane from memory (before any
+// gradient store: dlogits may alias logits); the argmax tracked per chunk (chunk max) and resolved
+// inside the winning chunk by its owner after the block reduction; the gradient pass one FMA,
+// v_exp_f32 and multiply per logit, the target's -1 applied by the chunk's owner only.
+template <int NC>
+__global__ __launch_bounds__(CE_NT) void ce_kernel2(CEArgs p) {
+  __shared__ float red_m[CE_NT / 64], red_s[CE_NT / 64], red_v[CE_NT / 64], tv;
+  __shared__ int red_i[CE_NT / 64];
+  constexpr float L2E = 1.4426950408889634f;
+  const long long row = blockIdx.x;
+  const int tid = threadIdx.x;
+  const bf16_t* x = static_cast<const bf16_t*>(p.logits) + row * p.ld;
+  const uint4* xv = reinterpret_cast<const uint4*>(x);
+  const long long tgt = p.targets[row];
+  const bool valid = tgt != p.ignore_index && tgt >= 0 && tgt < p.V;
+  const int nch = (p.V + 7) >> 3;
+  const int tail = p.V & 7;  // valid logits of the last chunk (0: the chunk is full)
+  uint4 raw[NC];
+#pragma unroll
+  for (int u = 0; u < NC; ++u) {
+    const int c = tid + u * CE_NT;
+    raw[u] = c < nch ? xv[c] : make_uint4(0u, 0u, 0u, 0u);
+  }
+  if (tid == 0) tv = valid ? bf2f(x[tgt]) : 0.f;  // (published by the reduction's barrier)
+  float m = -INFINITY, s = 0.f, bv = -INFINITY;
+  int bc = 0x7fffffff;
+#pragma unroll
+  for (int u = 0; u < NC; ++u) {
+    const int c = tid + u * CE_NT;
+    if (c < nch) {
+      float f[8];
+      unpack8(raw[u], f);
+      if (tail && c == nch - 1) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) f[j] = j < tail ? f[j] : -INFINITY;
+      }
+      const float cm = fmaxf(fmaxf(fmaxf(f[0], f[1]), fmaxf(f[2], f[3])), fmaxf(fmaxf(f[4], f[5]), fmaxf(f[6], f[7])));
+      const float cml = cm * L2E;
+      float cs = 0.f;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) cs += __builtin_amdgcn_exp2f(fmaf(f[j], L2E, -cml));
+      ms_combine(m, s, cm, cs);
+      if (cm > bv) {  // (chunks visited in increasing order: the first maximal chunk)
+        bv = cm;
+        bc = c;
+      }
+    }
+  }
+  ce_block_reduce<CE_NT / 64>(m, s, bv, bc, red_m, red_s, red_v, red_i);
+  const float lse = m + __logf(s);
+  if (tid == 0) p.row_loss[row] = valid ? lse - tv : 0.f;
+  if (p.row_correct && tid == (bc & (CE_NT - 1)) && bc < nch) {
+    // the owner of the first maximal chunk finds the first maximal logit in it, re-reading the
+    // chunk (only its owner writes it, later: safe under dlogits == logits; a select over raw[]
+    // by a run-time index moved the whole row array to scratch)
+    float f[8];
+    unpack8(xv[bc], f);
+    int bi = 0x7fffffff;
+#pragma unroll
+    for (int j = 7; j >= 0; --j) bi = f[j] == bv ? bc * 8 + j : bi;
+    p.row_correct[row] = (valid && bi == tgt) ? 1.f : 0.f;
+  }
+  if (!p.write_grad) return;
+  const float scale = valid ? *p.inv_count : 0.f;
+  const float lsel = lse * L2E;
+  uint4* g = reinterpret_cast<uint4*>(static_cast<bf16_t*>(p.dlogits) + row * p.ld);
+  const int nchl = (int)(p.ld >> 3);
+  const int tc = valid ? (int)(tgt >> 3) : -1;
+#pragma unroll
+  for (int u = 0; u < NC; ++u) {
+    const int c = tid + u * CE_NT;
+    if (c < nchl) {
+      float f[8];
+      unpack8(raw[u], f);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) f[j] = __builtin_amdgcn_exp2f(fmaf(f[j], L2E, -lsel)) * scale;
+      if (c >= nch - 1 && (c >= nch || tail)) {  // past the vocabulary: zeros
+#pragma unroll
+        for (int j = 0; j < 8; ++j) f[j] = (c * 8 + j < p.V) ? f[j] : 0.f;
+      }
+      if (c == tc) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) f[j] -= (j == (int)(tgt & 7)) ? scale : 0.f;
+      }
+      g[c] = pack8(f);
+    }
+  }
+}
+
 // Streaming fallback for rows longer than CE_NT * 16 chunks (V > 65536): CE_UNROLL chunks in
 // flight per thread per trip, the gradient pass re-reads the row.
 template <int CE_UNROLL>
@@ -284,29 +377,48 @@ __global__ __launch_bounds__(256) void adamw_kernel(AdamArgs a) {
   a.bias_correction2_sqrt = bc2s;
   const float step = a.lr / bc1;
   const float decay = 1.f - a.lr * a.weight_decay;
-  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n4; i += (long long)gridDim.x * 256) {
-    float4 p = reinterpret_cast<float4*>(a.param)[i];
-    const float4 g = reinterpret_cast<const float4*>(a.grad)[i];
-    float4 m = reinterpret_cast<float4*>(a.exp_avg)[i];
-    float4 v = reinterpret_cast<float4*>(a.exp_avg_sq)[i];
-    float pp[4] = {p.x, p.y, p.z, p.w}, gg[4] = {g.x, g.y, g.z, g.w};
-    float mm[4] = {m.x, m.y, m.z, m.w}, vv[4] = {v.x, v.y, v.z, v.w};
+  const float inv_bc2s = 1.f / bc2s;
+  // two float4 groups per thread per trip, all eight loads issued before any math (16 B per lane
+  // per array in flight was 3.4 TB/s on the GPT-2 small step: 1.1 ms for 124M parameters), and
+  // non-temporal accesses: the 1.9 GB of optimizer state streams once per step
+  const long long stride = (long long)gridDim.x * 256;
+  floatx4* P = reinterpret_cast<floatx4*>(a.param);
+  const floatx4* G = reinterpret_cast<const floatx4*>(a.grad);
+  floatx4* M = reinterpret_cast<floatx4*>(a.exp_avg);
+  floatx4* V = reinterpret_cast<floatx4*>(a.exp_avg_sq);
+  for (long long i0 = (long long)blockIdx.x * 256 + threadIdx.x; i0 < n4; i0 += 2 * stride) {
+    const long long idx[2] = {i0, i0 + stride};
+    const bool has1 = idx[1] < n4;
+    floatx4 p[2], g[2], m[2], v[2];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const float gj = gg[j] * gs;
-      mm[j] = b1 * mm[j] + (1.f - b1) * gj;
-      vv[j] = b2 * vv[j] + (1.f - b2) * gj * gj;
-      const float denom = sqrtf(vv[j]) / a.bias_correction2_sqrt + a.eps;
-      pp[j] = pp[j] * decay - step * mm[j] / denom;
+    for (int u = 0; u < 2; ++u) {
+      if (u == 1 && !has1) break;
+      p[u] = __builtin_nontemporal_load(P + idx[u]);
+      g[u] = __builtin_nontemporal_load(G + idx[u]);
+      m[u] = __builtin_nontemporal_load(M + idx[u]);
+      v[u] = __builtin_nontemporal_load(V + idx[u]);
     }
-    reinterpret_cast<float4*>(a.param)[i] = make_float4(pp[0], pp[1], pp[2], pp[3]);
-    reinterpret_cast<float4*>(a.exp_avg)[i] = make_float4(mm[0], mm[1], mm[2], mm[3]);
-    reinterpret_cast<float4*>(a.exp_avg_sq)[i] = make_float4(vv[0], vv[1], vv[2], vv[3]);
-    if (a.shadow) {
-      uint2 w;
-      w.x = pack2bf(pp[0], pp[1]);
-      w.y = pack2bf(pp[2], pp[3]);
-      reinterpret_cast<uint2*>(a.shadow)[i] = w;
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      if (u == 1 && !has1) break;
+      floatx4 pp = p[u], mm = m[u], vv = v[u];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float gj = g[u][j] * gs;
+        mm[j] = b1 * mm[j] + (1.f - b1) * gj;
+        vv[j] = b2 * vv[j] + (1.f - b2) * gj * gj;
+        const float denom = sqrtf(vv[j]) * inv_bc2s + a.eps;
+        pp[j] = pp[j] * decay - step * mm[j] / denom;
+      }
+      __builtin_nontemporal_store(pp, P + idx[u]);
+      __builtin_nontemporal_store(mm, M + idx[u]);
+      __builtin_nontemporal_store(vv, V + idx[u]);
+      if (a.shadow) {
+        uint2 w;
+        w.x = pack2bf(pp[0], pp[1]);
+        w.y = pack2bf(pp[2], pp[3]);
+        reinterpret_cast<uint2*>(a.shadow)[idx[u]] = w;
+      }
     }
   }
 }
@@ -525,10 +637,12 @@ DPC_API int dpc_embedding_bwd(const EmbArgs* a, hipStream_t stream) {
   return (int)hipGetLastError();
 }
 
-// 0: register-resident rows when they fit (default); 1 / 2: streaming with 1 / 4 chunks in
-// flight per thread (A/B sweeps: bench/ce_one.py).  Mode 0 runs at the speed of a plain in-place
-// copy of the logits (2.77 ms at GPT-2 small B = 64, 4.77 TB/s); a round-4 variant with one
-// exponential per logit (exp kept as f16 between the passes) measured 3.17 ms and was removed
+// 0: register-resident rows when they fit (default, ce_kernel2); 1 / 2: streaming with 1 / 4
+// chunks in flight per thread; 3: the round-4 register-resident kernel (A/B sweeps:
+// bench/ce_one.py).  GPT-2 small B = 64 (65472 x 50257 bf16 logits, in place), one MI355X:
+// mode 0 2.52-2.54 ms (5.2 TB/s, the float4 copy roofline of profiles/r4_copylab/), mode 3
+// 2.77 ms, torch's device copy of the same bytes 2.85 ms (profiles/r5_ce/); a round-4 variant with
+// one exponential per logit (exp kept as f16 between the passes) measured 3.17 ms and was removed
 // (profiles/r4_ce/).
 static int g_ce_mode = -1;  // -1: DPC_CE_MODE (default 0)
 DPC_API void dpc_ce_set_mode(int m) { g_ce_mode = m; }
@@ -541,12 +655,13 @@ DPC_API int dpc_cross_entropy(const CEArgs* a, hipStream_t stream) {
   if (g_ce_mode < 0) g_ce_mode = getenv("DPC_CE_MODE") ? atoi(getenv("DPC_CE_MODE")) : 0;
   if (g_ce_mode == 1) hipLaunchKernelGGL(ce_stream_kernel<1>, grid, dim3(256), 0, stream, *a);
   else if (g_ce_mode == 2) hipLaunchKernelGGL(ce_stream_kernel<4>, grid, dim3(256), 0, stream, *a);
-  else if (nc <= 1) hipLaunchKernelGGL(ce_kernel<1>, grid, dim3(CE_NT), 0, stream, *a);
-  else if (nc <= 2) hipLaunchKernelGGL(ce_kernel<2>, grid, dim3(CE_NT), 0, stream, *a);
-  else if (nc <= 4) hipLaunchKernelGGL(ce_kernel<4>, grid, dim3(CE_NT), 0, stream, *a);
-  else if (nc <= 8) hipLaunchKernelGGL(ce_kernel<8>, grid, dim3(CE_NT), 0, stream, *a);
-  else if (nc <= 13) hipLaunchKernelGGL(ce_kernel<13>, grid, dim3(CE_NT), 0, stream, *a);
-  else if (nc <= 16) hipLaunchKernelGGL(ce_kernel<16>, grid, dim3(CE_NT), 0, stream, *a);
+  else if (g_ce_mode == 3 && nc <= 13) hipLaunchKernelGGL(ce_kernel<13>, grid, dim3(CE_NT), 0, stream, *a);
+  else if (nc <= 1) hipLaunchKernelGGL(ce_kernel2<1>, grid, dim3(CE_NT), 0, stream, *a);
+  else if (nc <= 2) hipLaunchKernelGGL(ce_kernel2<2>, grid, dim3(CE_NT), 0, stream, *a);
+  else if (nc <= 4) hipLaunchKernelGGL(ce_kernel2<4>, grid, dim3(CE_NT), 0, stream, *a);
+  else if (nc <= 8) hipLaunchKernelGGL(ce_kernel2<8>, grid, dim3(CE_NT), 0, stream, *a);
+  else if (nc <= 13) hipLaunchKernelGGL(ce_kernel2<13>, grid, dim3(CE_NT), 0, stream, *a);
+  else if (nc <= 16) hipLaunchKernelGGL(ce_kernel2<16>, grid, dim3(CE_NT), 0, stream, *a);
   else hipLaunchKernelGGL(ce_stream_kernel<4>, grid, dim3(256), 0, stream, *a);
   return (int)hipGetLastError();
 }
