@@ -3,6 +3,7 @@ piece at a time (plain -> bias -> + one stream of GELU -> + the aux stream), eac
 interleaved with the others in rounds on one box (median).
 
     python bench/epi_decomp.py [--tokens 65472] [--dim 768] [--rounds 5] [--iters 10]
+                               [--only up_full ...] [--sweep 16 21 25 ...]
 
 Cases (GPT-2 FFN, T tokens, D model dim):
   up_*   : [T, D] x [4D, D]^T forward (v9 EPI 1 when an epilogue is present: impl 26)
@@ -43,6 +44,8 @@ def main():
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--only", nargs="*", default=None)
     ap.add_argument("--json", default=None)
+    ap.add_argument("--sweep", type=int, nargs="*", default=[],
+                    help="also time up_full / dg_full / dn_full with these implementations forced")
     a = ap.parse_args()
     T, D = a.tokens, a.dim
     dev = "cuda"
@@ -81,8 +84,10 @@ def main():
         ("dn_full", -1, lambda: gemm(xu, w_down, bias=b_d, act=ACT_GELU, residual=res, aux_out=aux_d, out=out_f,
                                      **dn_kw)),
     ]
+    for im in a.sweep:
+        cases += [(f"{name}@{im}", im, fn) for name, _, fn in cases if name in ("up_full", "dg_full", "dn_full")]
     if a.only:
-        cases = [c for c in cases if c[0] in a.only]
+        cases = [c for c in cases if c[0].split("@")[0] in a.only]
     fns = {}
     for name, impl, fn in cases:
         # impl: forced implementation (-1 = table), or (impl, {lab variant key: value})
