@@ -50,14 +50,16 @@ __global__ __launch_bounds__(256) void eb_keys_kernel(const long long* src, int 
 }
 
 // Runs are cut at every EB_CH-th sorted position so no wave sums more than EB_CH rows (a
-// frequent token of real text has thousands).  One wave per sorted position i that starts a
+// frequent token of real text has thousands; the position table's runs are one row per sequence:
+// 64 at GPT-2 small B = 64, where EB_CH = 64 left 1,023 waves summing 64 rows each, latency-bound:
+// 230 us per step against 125 at EB_CH = 8, bench/emb_bwd_time.py, profiles/r5_emb/).  One wave per sorted position i that starts a
 // piece (a run start, or a chunk boundary inside a run).  A run that fits in its chunk is added
 // to the table by its start wave; a run that crosses boundaries leaves per-chunk partial sums
 // -- part[2 c] its first piece (the last run starting in chunk c), part[2 c + 1] the piece
 // continuing at chunk c's first position -- and eb_runsum_kernel adds them in chunk order.
 // Rows are read RB at a time, all loads issued before the adds, and added in row order, so
 // every sum has a fixed order: bitwise reproducible.
-constexpr int EB_CH = 64;
+constexpr int EB_CH = 8;
 
 template <int NV>
 __device__ __forceinline__ void eb_add_rows(float4 (&acc)[NV], const int* keys, const int* rows, const float* dout,
