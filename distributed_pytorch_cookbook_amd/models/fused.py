@@ -182,22 +182,23 @@ class _FfnTail:
     residual, so the first backward op of a layer is ``dz2 = bf16(dx3 * keep * act'(z2))`` plus
     the bias column sums -- one pass over the f32 residual gradient dx3 that the consumer's
     LayerNorm backward has just written.  The consumer does it in that pass instead
-    (layernorm_bwd's gout / gz) and leaves dz2 and the bias-gradient partial here; the layer's
-    own backward then starts from them.  Filled in the forward only when the layer keeps its
+    (layernorm_bwd's gout / gz): it leaves dz2 here and adds the column sums straight into the
+    bias gradient (a 1-D parameter: the stores keep those gradients valid for the whole backward,
+    and no bucket holding it is reduced before the layer's own backward ends); the layer's own
+    backward then starts from dz2.  Filled in the forward only when the layer keeps its
     activations (no recompute: z2 must exist when the consumer's backward runs)."""
 
-    __slots__ = ("z2", "act", "drop", "dz2", "db")
+    __slots__ = ("z2", "act", "drop", "dz2", "bias_grad")
 
     def __init__(self):
-        self.z2 = self.act = self.drop = self.dz2 = self.db = None
+        self.z2 = self.act = self.drop = self.dz2 = self.bias_grad = None
 
     def consume(self, ln_bwd_kwargs, T, D, device, cdt):
         """Extend a LayerNorm backward call with this tail's fused consumer (if it has one)."""
         if self.z2 is None:
             return
         self.dz2 = torch.empty(T, D, device=device, dtype=cdt)
-        self.db = torch.zeros(D, device=device, dtype=torch.float32)
-        ln_bwd_kwargs.update(gout=self.dz2, gsum=self.db, drop=self.drop)
+        ln_bwd_kwargs.update(gout=self.dz2, gsum=self.bias_grad(), drop=self.drop)
         if self.act != ACT_NONE:
             ln_bwd_kwargs.update(gz=self.z2, gact=self.act)
         self.z2 = None
@@ -231,6 +232,8 @@ class _LayerFn(torch.autograd.Function):
             ctx.prev_tail, ctx.tail = prev_tail, tail
             if tail is not None and saved is not None and _tail_ok(x, store.compute_dtype):
                 tail.z2, tail.act, tail.drop = saved[-1], act, drops[1]
+                bias = layer.fc.down_proj.bias
+                tail.bias_grad = lambda: store.grad(bias)
         return x3
 
     @staticmethod
@@ -300,9 +303,8 @@ def _layer_backward(dx3, x, mask, saved, layer, store, N, S, H, hd, act, drops, 
     # FFN down projection: x3 = x2 + drop(act(z2)), z2 = u W2^T + b2
     side = _SideWork(dx.device)
     if tail is not None and tail.dz2 is not None:  # formed by the consumer's LayerNorm backward
-        dz2 = tail.dz2
-        g(fc.down_proj.bias).add_(tail.db)
-        tail.dz2 = tail.db = None
+        dz2 = tail.dz2  # (its bias column sums are already in the gradient)
+        tail.dz2 = None
     else:
         dz2 = bias_act_bwd(dx, z2, act, g(fc.down_proj.bias), out_dtype=cdt, drop=drop_ffn)
     side.run(lambda: linear_wgrad(dz2, uact, out=g(fc.down_proj.weight)), dz2, uact)
@@ -397,11 +399,11 @@ class _HeadFn(torch.autograd.Function):
         # K = padded vocab: the CE kernel zeroed dlogits' pad columns, W_lm rows >= V read as 0
         dhf = linear_dgrad(dlogits, _head_weight_padded(store, head, dlogits.shape[1]),
                            out_dtype=_dh_dtype(store.compute_dtype), alpha_t=scale)
-        dx = torch.zeros_like(x)
+        dx = torch.empty_like(x)  # (written, not accumulated: dx_set)
         kw = {}
         if ctx.prev_tail is not None:  # the last layer's down-projection bias / act / dropout backward
             ctx.prev_tail.consume(kw, x.shape[0], x.shape[1], x.device, store.compute_dtype)
-        layernorm_bwd(dhf, x, mu, rs, w(norm.weight), dx, g(norm.weight), g(norm.bias), **kw)
+        layernorm_bwd(dhf, x, mu, rs, w(norm.weight), dx, g(norm.weight), g(norm.bias), dx_set=True, **kw)
         store.post_backward(unit)
         return dx, None, None, None, None, None, None, None, None
 

@@ -67,6 +67,7 @@ class LNArgs(ctypes.Structure):
         ("add_y", P), ("add_bias", P), ("x_out", P), ("ld_add", LL), ("ld_xout", LL),
         ("drop_seed", P), ("drop_site", c_uint),
         ("gz", P), ("ld_gz", LL), ("gact", c_int),
+        ("dx_set", c_int),
     ]
 
 

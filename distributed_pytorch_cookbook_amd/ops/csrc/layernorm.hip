@@ -55,6 +55,7 @@ struct LNArgs {
   const void* gz;
   long long ld_gz;
   int gact;
+  int dx_set;  // bwd: dx = LN'(dy) (dx not read) instead of dx += LN'(dy)
 };
 
 template <int NV>
@@ -207,7 +208,7 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(LNArgs p) {
     for (int i = 0; i < NV; ++i) {
       const int c = lane + i * 64;
       if (c < nv4) {
-        float4 o = dxr[c];
+        float4 o = p.dx_set ? make_float4(0.f, 0.f, 0.f, 0.f) : dxr[c];
         o.x += rs * (dg[i].x - s1 - xh[i].x * s2);
         o.y += rs * (dg[i].y - s1 - xh[i].y * s2);
         o.z += rs * (dg[i].z - s1 - xh[i].z * s2);

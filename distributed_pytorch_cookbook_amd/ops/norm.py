@@ -84,7 +84,7 @@ def layernorm_fwd(x: torch.Tensor, gamma: torch.Tensor, beta: torch.Tensor, eps:
 def layernorm_bwd(dy: torch.Tensor, x: torch.Tensor, mean: torch.Tensor, rstd: torch.Tensor,
                   gamma: torch.Tensor, dx: torch.Tensor, dgamma: torch.Tensor, dbeta: torch.Tensor,
                   gout: torch.Tensor | None = None, gsum: torch.Tensor | None = None,
-                  drop=None, gz: torch.Tensor | None = None, gact=None):
+                  drop=None, gz: torch.Tensor | None = None, gact=None, dx_set: bool = False):
     """dx += LN'(dy); dgamma += sum dy*xhat; dbeta += sum dy.  x, dx f32 [T, D]; dy f32 or
     bf16 (the input gradient of the Linear that consumed the LayerNorm's output -- bf16 under
     the reference's autocast too).
@@ -94,7 +94,8 @@ def layernorm_bwd(dy: torch.Tensor, x: torch.Tensor, mean: torch.Tensor, rstd: t
     the next GEMM's operand) and ``gsum += colsum(dx * keep)`` (that projection's bias
     gradient), saving a separate pass over the f32 dx.  With ``gz`` (bf16 [T, D]) and ``gact``
     the projection's output went through an activation first (the reference's FFN applies it
-    after the down projection too): ``gout = dx * keep * act'(gz)``.
+    after the down projection too): ``gout = dx * keep * act'(gz)``.  ``dx_set``: dx = LN'(dy),
+    dx's old contents neither read nor needed (the final norm's backward: no zero fill).
     """
     T, D = x.shape
     if not (x.is_cuda and dy.dtype in (torch.float32, torch.bfloat16) and gamma.dtype == torch.float32
@@ -104,7 +105,11 @@ def layernorm_bwd(dy: torch.Tensor, x: torch.Tensor, mean: torch.Tensor, rstd: t
         dg = dyf * gamma.float()
         s1 = dg.mean(-1, keepdim=True)
         s2 = (dg * xh).mean(-1, keepdim=True)
-        dx.add_(rstd[:, None] * (dg - s1 - xh * s2))
+        g_ln = rstd[:, None] * (dg - s1 - xh * s2)
+        if dx_set:
+            dx.copy_(g_ln)
+        else:
+            dx.add_(g_ln)
         dgamma.add_((dyf * xh).sum(0))
         dbeta.add_(dyf.sum(0))
         if gout is not None:
@@ -124,7 +129,7 @@ def layernorm_bwd(dy: torch.Tensor, x: torch.Tensor, mean: torch.Tensor, rstd: t
         x=x.data_ptr(), gamma=gamma.data_ptr(), mean=mean.data_ptr(), rstd=rstd.data_ptr(),
         dy=dy.data_ptr(), dx=dx.data_ptr(), dgamma=dgamma.data_ptr(), dbeta=dbeta.data_ptr(),
         ldx=x.stride(0), lddy=dy.stride(0), lddx=dx.stride(0), T=T, D=D, eps=0.0,
-        dy_bf16=int(dy.dtype == torch.bfloat16),
+        dy_bf16=int(dy.dtype == torch.bfloat16), dx_set=int(dx_set),
     )
     if gout is not None:
         if gout.dtype != torch.bfloat16 or gout.stride(1) != 1 or gout.stride(0) % 4 or D % 4:

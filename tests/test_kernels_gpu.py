@@ -466,11 +466,14 @@ def test_layernorm(D):
     dg = torch.zeros(D, device=dev)
     db = torch.zeros(D, device=dev)
     layernorm_bwd(dy, x, mean, rstd, g, dx, dg, db)
+    dx_only = torch.full_like(dx, float("nan"))  # dx_set: the old contents are never read
+    layernorm_bwd(dy, x, mean, rstd, g, dx_only, torch.zeros(D, device=dev), torch.zeros(D, device=dev), dx_set=True)
     xx = x.clone().requires_grad_(True)
     gg = g.clone().requires_grad_(True)
     bb = b.clone().requires_grad_(True)
     torch.nn.functional.layer_norm(xx, (D,), gg, bb, 1e-5).backward(dy)
     assert rel_err(dx - dres, xx.grad) < 1e-4
+    assert rel_err(dx_only, xx.grad) < 1e-4
     assert rel_err(dg, gg.grad) < 1e-4
     assert rel_err(db, bb.grad) < 1e-4
     # fused consumer: gout = bf16(dx * keep), gsum += colsum(dx * keep)
