@@ -55,6 +55,21 @@ __device__ __forceinline__ void st16(void* ptr, uint4 v, bool nt) {
   if (nt) __builtin_nontemporal_store(u32x4{v.x, v.y, v.z, v.w}, reinterpret_cast<u32x4*>(ptr));
   else *reinterpret_cast<uint4*>(ptr) = v;
 }
+// the same with the epilogue's cache scope (GemmArgs::nt_store bits 2-3, default 3: gemm.hip
+// gemm_nt_mode): 0 = st16's nt / plain, 1 = sc0 nt, 2 = sc1 nt, 3 = sc0 sc1 nt
+__device__ __forceinline__ void st16p(void* ptr, uint4 v, bool nt, int pol) {
+  typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+  const u32x4 w{v.x, v.y, v.z, v.w};
+  if (pol == 1) asm volatile("global_store_dwordx4 %0, %1, off sc0 nt" ::"v"(ptr), "v"(w) : "memory");
+  else if (pol == 2) asm volatile("global_store_dwordx4 %0, %1, off sc1 nt" ::"v"(ptr), "v"(w) : "memory");
+  else if (pol == 3) asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1 nt" ::"v"(ptr), "v"(w) : "memory");
+  else if (nt) __builtin_nontemporal_store(w, reinterpret_cast<u32x4*>(ptr));
+  else *reinterpret_cast<uint4*>(ptr) = v;
+}
+__device__ __forceinline__ void st16p(void* ptr, float4 v, bool nt, int pol) {
+  st16p(ptr, make_uint4(__float_as_uint(v.x), __float_as_uint(v.y), __float_as_uint(v.z), __float_as_uint(v.w)), nt,
+        pol);
+}
 __device__ __forceinline__ void st8(void* ptr, uint2 v, bool nt) {
   typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
   if (nt) __builtin_nontemporal_store(u32x2{v.x, v.y}, reinterpret_cast<u32x2*>(ptr));

@@ -702,10 +702,16 @@ static int policy_impl(const GemmArgs* a) {
 extern "C" int dpc_gemm7(const GemmArgs* a, int persistent, int sched, int splits, hipStream_t stream, int wn);
 extern "C" int dpc_gemm7_ok(const GemmArgs* a);
 
-// GemmArgs::nt_store for every product (DPC_GEMM_NT: bit 0 bf16 outputs, bit 1 f32 outputs)
+// GemmArgs::nt_store for every product (DPC_GEMM_NT: bit 0 bf16 outputs, bit 1 f32 outputs
+// non-temporal; bits 2-3 the cache scope of the v7 / v9 epilogue stores: 0 none, 1 sc0, 2 sc1,
+// 3 sc0 sc1).  Default 15 = nt + sc0 sc1: the epilogue's stores retire sooner, and the next
+// tile's counted DMA waits -- which CDNA4's one in-order vmcnt makes wait for them too -- stall
+// less.  Same box against nt alone (round 5, profiles/r5_epi/store_policy.log): up-projection
+// fused 402 -> 384 us, down-projection fused 367 -> 349, plain up 283 -> 274, plain input
+// gradient 300 -> 290; DDP 960.8K -> 971.6K (two runs each).
 static int gemm_nt_mode() {
   static int mode = -1;
-  if (mode < 0) mode = getenv("DPC_GEMM_NT") ? atoi(getenv("DPC_GEMM_NT")) : 3;
+  if (mode < 0) mode = getenv("DPC_GEMM_NT") ? atoi(getenv("DPC_GEMM_NT")) : 15;
   return mode;
 }
 

@@ -127,6 +127,14 @@ __device__ __forceinline__ void g7_wait() {
 
 #define G7_AI __attribute__((always_inline))
 typedef unsigned g7_u32x4 __attribute__((ext_vector_type(4)));
+// 16-B buffer store with the epilogue's cache policy (GemmArgs::nt_store bits 2-3, wave-uniform):
+// 0 nt, 1 sc0 nt, 2 sc1 nt, 3 sc0 sc1 nt
+__device__ __forceinline__ void g7_bst16(g7_u32x4 v, __amdgpu_buffer_rsrc_t rs, unsigned off, int pol) {
+  if (pol == 2) __builtin_amdgcn_raw_buffer_store_b128(v, rs, off, 0, 18);
+  else if (pol == 3) __builtin_amdgcn_raw_buffer_store_b128(v, rs, off, 0, 19);
+  else if (pol == 1) __builtin_amdgcn_raw_buffer_store_b128(v, rs, off, 0, 3);
+  else __builtin_amdgcn_raw_buffer_store_b128(v, rs, off, 0, 2);
+}
 typedef float g7_f32x4 __attribute__((ext_vector_type(4)));
 
 // alpha x *alpha_ptr through the scalar cache.  As a vector load (what the compiler emits for
@@ -200,8 +208,8 @@ __device__ __forceinline__ void g7_epilogue(const GemmArgs& p, floatx4 (&acc)[8]
           const int m = mw + 16 * i + rr, n = nw + 16 * j + 4 * g + 16 * hi8;
           if (n < p.N) {
             float* C = static_cast<float*>(p.C) + (long long)m * p.ldc + n;
-            if (m < p.M) st16(C, dA, p.nt_store & 2);
-            if (m + 8 < p.M) st16(C + 8 * p.ldc, dB, p.nt_store & 2);
+            if (m < p.M) st16p(C, dA, p.nt_store & 2, (p.nt_store >> 2) & 3);
+            if (m + 8 < p.M) st16p(C + 8 * p.ldc, dB, p.nt_store & 2, (p.nt_store >> 2) & 3);
           }
         }
       }
@@ -240,8 +248,8 @@ __device__ __forceinline__ void g7_epilogue(const GemmArgs& p, floatx4 (&acc)[8]
         } else if (n < p.N) {
           bf16_t* C = static_cast<bf16_t*>(p.C) + (long long)m * p.ldc + n;
           const bool nt = (p.nt_store & 1) || (dbg & 16);  // (dbg 16: the lab's nt arm)
-          if (m < p.M) st16(C, dA, nt);
-          if (m + 8 < p.M) st16(C + 8 * p.ldc, dB, nt);
+          if (m < p.M) st16p(C, dA, nt, (p.nt_store >> 2) & 3);
+          if (m + 8 < p.M) st16p(C + 8 * p.ldc, dB, nt, (p.nt_store >> 2) & 3);
         }
       }
     }
@@ -353,7 +361,7 @@ __device__ __forceinline__ void g7_epilogue(const GemmArgs& p, floatx4 (&acc)[8]
               const float4 o = *C;
               w[0] += o.x; w[1] += o.y; w[2] += o.z; w[3] += o.w;
             }
-            st16(C, make_float4(w[0], w[1], w[2], w[3]), p.nt_store & 2);
+            st16p(C, make_float4(w[0], w[1], w[2], w[3]), p.nt_store & 2, (p.nt_store >> 2) & 3);
           }
         } else {
           pc[h][0] = pack2bf(w[0], w[1]);
@@ -366,14 +374,15 @@ __device__ __forceinline__ void g7_epilogue(const GemmArgs& p, floatx4 (&acc)[8]
         const auto s0 = __builtin_amdgcn_permlane16_swap(pa[0][0], pa[1][0], false, false);
         const auto s1 = __builtin_amdgcn_permlane16_swap(pa[0][1], pa[1][1], false, false);
         if (ok8)
-          st16(aux_out + (long long)m * p.ld_aux_out + n8, make_uint4(s0[0], s1[0], s0[1], s1[1]), p.nt_store & 1);
+          st16p(aux_out + (long long)m * p.ld_aux_out + n8, make_uint4(s0[0], s1[0], s0[1], s1[1]), p.nt_store & 1,
+                (p.nt_store >> 2) & 3);
       }
       if (FULL || !p.out_f32) {
         const auto s0 = __builtin_amdgcn_permlane16_swap(pc[0][0], pc[1][0], false, false);
         const auto s1 = __builtin_amdgcn_permlane16_swap(pc[0][1], pc[1][1], false, false);
         if (ok8)
-          st16(static_cast<bf16_t*>(p.C) + (long long)m * p.ldc + n8, make_uint4(s0[0], s1[0], s0[1], s1[1]),
-               p.nt_store & 1);
+          st16p(static_cast<bf16_t*>(p.C) + (long long)m * p.ldc + n8, make_uint4(s0[0], s1[0], s0[1], s1[1]),
+                p.nt_store & 1, (p.nt_store >> 2) & 3);
       }
     });
   });
@@ -463,6 +472,7 @@ __device__ __forceinline__ void g7_epilogue_act_lds(const GemmArgs& p, floatx4 (
   const __amdgpu_buffer_rsrc_t rc =
       __builtin_amdgcn_make_buffer_rsrc((void*)(static_cast<bf16_t*>(p.C) + corg), 0, cnrec, 0x00020000);
   const bool gelu = fab == ACT_GELU;  // (else ReLU: act_lds is taken only with an act')
+  const int spol = (p.nt_store >> 2) & 3;
   auto proc = [&](auto Q, const bf16_t* buf) G7_AI {
     constexpr int q = decltype(Q)::value;
     sfor<2>([&](auto II) G7_AI {
@@ -515,8 +525,7 @@ __device__ __forceinline__ void g7_epilogue_act_lds(const GemmArgs& p, floatx4 (
         const auto s0 = __builtin_amdgcn_permlane16_swap(pc[0][0], pc[1][0], false, false);
         const auto s1 = __builtin_amdgcn_permlane16_swap(pc[0][1], pc[1][1], false, false);
         const unsigned off = (n0 + n8 < p.N) ? (unsigned)((mt * p.ldc + n8) * 2) : 0xfffffff0u;
-        __builtin_amdgcn_raw_buffer_store_b128(
-            __builtin_bit_cast(g7_u32x4, make_uint4(s0[0], s1[0], s0[1], s1[1])), rc, off, 0, 2 /* nt */);
+        g7_bst16(__builtin_bit_cast(g7_u32x4, make_uint4(s0[0], s1[0], s0[1], s1[1])), rc, off, spol);
         zc0 = zn0;
         zc1 = zn1;
         __builtin_amdgcn_sched_barrier(0);  // one column pair at a time (else all are live: spills)
@@ -638,6 +647,7 @@ __device__ __forceinline__ void g7_epilogue_res_lds(const GemmArgs& p, floatx4 (
   const __amdgpu_buffer_rsrc_t rco = span(p.C, p.ldc, 4);
   const __amdgpu_buffer_rsrc_t rax = span(p.aux_out, p.ld_aux_out, 2);
   const bool gelu = fact == ACT_GELU, relu = fact == ACT_RELU;
+  const int spol = (p.nt_store >> 2) & 3;
   float4 bias4[NJ];
 #pragma unroll
   for (int j = 0; j < NJ; ++j) {
@@ -680,16 +690,14 @@ __device__ __forceinline__ void g7_epilogue_res_lds(const GemmArgs& p, floatx4 (
 #pragma unroll
         for (int r = 0; r < 4; ++r) w[r] = gelu ? ga[r] : (relu ? fmaxf(w[r], 0.f) : w[r]);
         const unsigned off = (n0 + ntc < p.N) ? (unsigned)((mt * p.ldc + ntc) * 4) : 0xfffffff0u;
-        __builtin_amdgcn_raw_buffer_store_b128(
-            __builtin_bit_cast(g7_u32x4, make_float4(w[0] + res.x, w[1] + res.y, w[2] + res.z, w[3] + res.w)), rco,
-            off, 0, 2 /* nt */);
+        g7_bst16(__builtin_bit_cast(g7_u32x4, make_float4(w[0] + res.x, w[1] + res.y, w[2] + res.z, w[3] + res.w)),
+                 rco, off, spol);
       });
       const int n8 = wc * 128 + 16 * j + coff;
       const auto s0 = __builtin_amdgcn_permlane16_swap(pa[0][0], pa[1][0], false, false);
       const auto s1 = __builtin_amdgcn_permlane16_swap(pa[0][1], pa[1][1], false, false);
       const unsigned aoff = (n0 + n8 < p.N) ? (unsigned)((mt * p.ld_aux_out + n8) * 2) : 0xfffffff0u;
-      __builtin_amdgcn_raw_buffer_store_b128(
-          __builtin_bit_cast(g7_u32x4, make_uint4(s0[0], s1[0], s0[1], s1[1])), rax, aoff, 0, 2 /* nt */);
+      g7_bst16(__builtin_bit_cast(g7_u32x4, make_uint4(s0[0], s1[0], s0[1], s1[1])), rax, aoff, spol);
       rc0 = rn0;
       rc1 = rn1;
       __builtin_amdgcn_sched_barrier(0);
