@@ -10,6 +10,8 @@
 //
 // One wave per row, NV float4 per lane (D <= 256 * NV), 4 rows (waves) per workgroup.
 #include <algorithm>
+#include <cstdlib>
+#include <type_traits>
 
 #include "common.h"
 
@@ -144,7 +146,21 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(LNArgs p) {
   }
 }
 
-template <int NV>
+// One row's operands, loaded together (all of them before the row's reductions: the old
+// dx += form read dx after the two wave sums, a second full memory latency per row, and the
+// conditional read of the dx_set form was never hoisted above them by the compiler).
+template <int NV, bool DYB>
+struct LnBwdRow {
+  float4 x[NV];
+  typename std::conditional<DYB, uint2, float4>::type dy[NV];
+  uint2 zz[NV];    // act' operand of the fused consumer (p.gz)
+  float4 dold[NV]; // dx before this kernel (unless dx_set)
+  float mu, rs;
+};
+
+// PF: the next row's operands are issued before this row's arithmetic (one row in flight
+// behind the one being reduced), so a wave never waits a full memory latency per row.
+template <int NV, bool DYB, bool PF>
 __global__ __launch_bounds__(256) void ln_bwd_kernel(LNArgs p) {
   const uint32_t dkey = p.drop_scale != 0.f ? drop_key_of(p.drop_seed, p.drop_site, p.drop_key) : 0u;
   __shared__ float red[4][2][NV * 256];
@@ -159,47 +175,60 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(LNArgs p) {
     gam[i] = c < nv4 ? g4[c] : make_float4(0.f, 0.f, 0.f, 0.f);
   }
   bf16_t* gout = static_cast<bf16_t*>(p.gout);
-  for (long long row = (long long)blockIdx.x * 4 + w; row < p.T; row += (long long)gridDim.x * 4) {
+  const bool use_z = gout && p.gz;
+  using Row = LnBwdRow<NV, DYB>;
+  // Branch-free loads (a load under a branch made the compiler wait for everything in flight at
+  // the join, one memory latency per column chunk): a lane past the row end re-reads the row's
+  // last chunk, and an operand the launch does not use is read from gamma with row stride 0
+  // (L1-resident, D * 4 bytes >= what one row reads).  The results are ignored in those cases.
+  const bf16_t* zbase = use_z ? static_cast<const bf16_t*>(p.gz) : reinterpret_cast<const bf16_t*>(p.gamma);
+  const long long zld = use_z ? p.ld_gz : 0;
+  const float* obase = p.dx_set ? p.gamma : p.dx;
+  const long long old = p.dx_set ? 0 : p.lddx;
+  const float keep_old = p.dx_set ? 0.f : 1.f;  // (gamma is finite: 0 * it is 0)
+  auto load = [&](long long row, Row& r) {
+    r.mu = p.mean[row];
+    r.rs = p.rstd[row];
     const float4* xr = reinterpret_cast<const float4*>(p.x + row * p.ldx);
-    const float4* dyr = reinterpret_cast<const float4*>(p.dy + row * p.lddy);
-    const uint2* dyb = reinterpret_cast<const uint2*>(static_cast<const bf16_t*>((const void*)p.dy) + row * p.lddy);
-    const float mu = p.mean[row], rs = p.rstd[row];
-    // the act' operand of the fused consumer, loaded with the row (it is used after the row's
-    // reductions)
-    uint2 zz[NV];
-    if (gout && p.gz) {
-      const uint2* zr = reinterpret_cast<const uint2*>(static_cast<const bf16_t*>(p.gz) + row * p.ld_gz);
+    const float4* dor = reinterpret_cast<const float4*>(obase + row * old);
+    const uint2* zr = reinterpret_cast<const uint2*>(zbase + row * zld);
 #pragma unroll
-      for (int i = 0; i < NV; ++i) {
-        const int c = lane + i * 64;
-        zz[i] = c < nv4 ? zr[c] : make_uint2(0u, 0u);
-      }
+    for (int i = 0; i < NV; ++i) {
+      const int c = min(lane + i * 64, nv4 - 1);
+      r.x[i] = xr[c];
+      if constexpr (DYB) r.dy[i] = reinterpret_cast<const uint2*>(static_cast<const bf16_t*>((const void*)p.dy) + row * p.lddy)[c];
+      else r.dy[i] = reinterpret_cast<const float4*>(p.dy + row * p.lddy)[c];
+      r.zz[i] = zr[c];
+      r.dold[i] = dor[c];
     }
+  };
+  // compute: every operand is consumed outside any branch (a value used only under `c < nv4`
+  // let the compiler sink its load into that branch, behind a vmcnt(0)); lanes past the row end
+  // see dy = 0 (no contribution to the sums) and only their stores are skipped.
+  auto compute = [&](long long row, const Row& r) {
+    const float mu = r.mu, rs = r.rs;
     float4 xh[NV], dg[NV];
     float s1 = 0.f, s2 = 0.f;
 #pragma unroll
     for (int i = 0; i < NV; ++i) {
-      const int c = lane + i * 64;
-      if (c < nv4) {
-        const float4 xv = xr[c];
-        float4 d;
-        if (p.dy_bf16) {
-          const uint2 z = dyb[c];
-          d = make_float4(__uint_as_float(z.x << 16), __uint_as_float(z.x & 0xffff0000u),
-                          __uint_as_float(z.y << 16), __uint_as_float(z.y & 0xffff0000u));
-        } else {
-          d = dyr[c];
-        }
-        xh[i] = make_float4((xv.x - mu) * rs, (xv.y - mu) * rs, (xv.z - mu) * rs, (xv.w - mu) * rs);
-        dg[i] = make_float4(d.x * gam[i].x, d.y * gam[i].y, d.z * gam[i].z, d.w * gam[i].w);
-        s1 += dg[i].x + dg[i].y + dg[i].z + dg[i].w;
-        s2 += dg[i].x * xh[i].x + dg[i].y * xh[i].y + dg[i].z * xh[i].z + dg[i].w * xh[i].w;
-        gacc[i].x += d.x * xh[i].x; gacc[i].y += d.y * xh[i].y;
-        gacc[i].z += d.z * xh[i].z; gacc[i].w += d.w * xh[i].w;
-        bacc[i].x += d.x; bacc[i].y += d.y; bacc[i].z += d.z; bacc[i].w += d.w;
+      const bool ok = lane + i * 64 < nv4;
+      const float4 xv = r.x[i];
+      float4 d;
+      if constexpr (DYB) {
+        const uint2 z = r.dy[i];
+        d = make_float4(__uint_as_float(z.x << 16), __uint_as_float(z.x & 0xffff0000u),
+                        __uint_as_float(z.y << 16), __uint_as_float(z.y & 0xffff0000u));
       } else {
-        xh[i] = dg[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+        d = r.dy[i];
       }
+      if (!ok) d = make_float4(0.f, 0.f, 0.f, 0.f);
+      xh[i] = make_float4((xv.x - mu) * rs, (xv.y - mu) * rs, (xv.z - mu) * rs, (xv.w - mu) * rs);
+      dg[i] = make_float4(d.x * gam[i].x, d.y * gam[i].y, d.z * gam[i].z, d.w * gam[i].w);
+      s1 += dg[i].x + dg[i].y + dg[i].z + dg[i].w;
+      s2 += dg[i].x * xh[i].x + dg[i].y * xh[i].y + dg[i].z * xh[i].z + dg[i].w * xh[i].w;
+      gacc[i].x += d.x * xh[i].x; gacc[i].y += d.y * xh[i].y;
+      gacc[i].z += d.z * xh[i].z; gacc[i].w += d.w * xh[i].w;
+      bacc[i].x += d.x; bacc[i].y += d.y; bacc[i].z += d.z; bacc[i].w += d.w;
     }
     s1 = wave_sum(s1) / p.D;
     s2 = wave_sum(s2) / p.D;
@@ -207,34 +236,76 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(LNArgs p) {
 #pragma unroll
     for (int i = 0; i < NV; ++i) {
       const int c = lane + i * 64;
-      if (c < nv4) {
-        float4 o = p.dx_set ? make_float4(0.f, 0.f, 0.f, 0.f) : dxr[c];
-        o.x += rs * (dg[i].x - s1 - xh[i].x * s2);
-        o.y += rs * (dg[i].y - s1 - xh[i].y * s2);
-        o.z += rs * (dg[i].z - s1 - xh[i].z * s2);
-        o.w += rs * (dg[i].w - s1 - xh[i].w * s2);
+      const bool ok = c < nv4;
+      // (a multiply, not a select: a select on the uniform flag became a branch with dx's load
+      // sunk into it)
+      float4 o = make_float4(r.dold[i].x * keep_old, r.dold[i].y * keep_old, r.dold[i].z * keep_old,
+                             r.dold[i].w * keep_old);
+      o.x += rs * (dg[i].x - s1 - xh[i].x * s2);
+      o.y += rs * (dg[i].y - s1 - xh[i].y * s2);
+      o.z += rs * (dg[i].z - s1 - xh[i].z * s2);
+      o.w += rs * (dg[i].w - s1 - xh[i].w * s2);
+      float4 og = o;
+      if (use_z) {
+        og.x *= act_grad(__uint_as_float(r.zz[i].x << 16), p.gact);
+        og.y *= act_grad(__uint_as_float(r.zz[i].x & 0xffff0000u), p.gact);
+        og.z *= act_grad(__uint_as_float(r.zz[i].y << 16), p.gact);
+        og.w *= act_grad(__uint_as_float(r.zz[i].y & 0xffff0000u), p.gact);
+      }
+      if (gout && p.drop_scale != 0.f) {
+        const uint32_t idx = (uint32_t)(row * p.D + 4 * c);
+        og.x *= drop_factor(idx + 0, dkey, p.drop_thresh, p.drop_scale);
+        og.y *= drop_factor(idx + 1, dkey, p.drop_thresh, p.drop_scale);
+        og.z *= drop_factor(idx + 2, dkey, p.drop_thresh, p.drop_scale);
+        og.w *= drop_factor(idx + 3, dkey, p.drop_thresh, p.drop_scale);
+      }
+      if (!ok) og = make_float4(0.f, 0.f, 0.f, 0.f);
+      cacc[i].x += og.x; cacc[i].y += og.y; cacc[i].z += og.z; cacc[i].w += og.w;
+      if (ok) {
         dxr[c] = o;
         if (gout) {
-          if (p.gz) {
-            o.x *= act_grad(__uint_as_float(zz[i].x << 16), p.gact);
-            o.y *= act_grad(__uint_as_float(zz[i].x & 0xffff0000u), p.gact);
-            o.z *= act_grad(__uint_as_float(zz[i].y << 16), p.gact);
-            o.w *= act_grad(__uint_as_float(zz[i].y & 0xffff0000u), p.gact);
-          }
-          if (p.drop_scale != 0.f) {
-            const uint32_t idx = (uint32_t)(row * p.D + 4 * c);
-            o.x *= drop_factor(idx + 0, dkey, p.drop_thresh, p.drop_scale);
-            o.y *= drop_factor(idx + 1, dkey, p.drop_thresh, p.drop_scale);
-            o.z *= drop_factor(idx + 2, dkey, p.drop_thresh, p.drop_scale);
-            o.w *= drop_factor(idx + 3, dkey, p.drop_thresh, p.drop_scale);
-          }
           uint2 wv;
-          wv.x = pack2bf(o.x, o.y);
-          wv.y = pack2bf(o.z, o.w);
+          wv.x = pack2bf(og.x, og.y);
+          wv.y = pack2bf(og.z, og.w);
           *reinterpret_cast<uint2*>(gout + row * p.ld_gout + 4 * c) = wv;
-          cacc[i].x += o.x; cacc[i].y += o.y; cacc[i].z += o.z; cacc[i].w += o.w;
         }
       }
+    }
+  };
+  const long long stride = (long long)gridDim.x * 4;
+  long long row = (long long)blockIdx.x * 4 + w;
+  if constexpr (PF) {
+    // two rows per trip so the in-flight row alternates between ra and rb without copies; the
+    // prefetch is unconditional (past the end it re-reads the last row): a load under a branch
+    // would make the compiler wait for everything in flight before the current row's math
+    Row ra, rb;
+    const long long last = p.T - 1;
+    if (row < p.T) {
+      load(row, ra);
+      // (scheduling barriers keep each row's loads issued as one group ahead of the other row's
+      // math: interleaved, the waits for the row being reduced also covered the row in flight)
+      while (true) {
+        load(min(row + stride, last), rb);
+        __builtin_amdgcn_sched_barrier(0);
+        compute(row, ra);
+        __builtin_amdgcn_sched_barrier(0);
+        row += stride;
+        if (row >= p.T) break;
+        load(min(row + stride, last), ra);
+        __builtin_amdgcn_sched_barrier(0);
+        compute(row, rb);
+        __builtin_amdgcn_sched_barrier(0);
+        row += stride;
+        if (row >= p.T) break;
+      }
+    }
+  } else {
+    for (; row < p.T; row += stride) {
+      Row r;
+      load(row, r);
+      __builtin_amdgcn_sched_barrier(0);  // (all of the row's loads issued before any wait)
+      compute(row, r);
+      __builtin_amdgcn_sched_barrier(0);
     }
   }
   // reduce dgamma / dbeta across the 4 waves, then one atomic per column per workgroup
@@ -292,19 +363,54 @@ DPC_API int dpc_layernorm_fwd(const LNArgs* a, hipStream_t stream) {
 // (dgamma / dbeta), so the best grid shrinks as D grows: bench/ln_grid.py on MI355X, 1024 at
 // D = 768 (5.2 TB/s; 512: 4.6, 2048: 4.3) and 512 at D = 1600 (4.4 TB/s; 1024: 4.1) -- i.e.
 // ~786K column-atomics per launch, and at most one workgroup per 32 rows.  0 = that rule; > 0
-// forces a size (sweeps).
+// forces a size (sweeps).  The grid is also capped at what is resident at once (a second
+// partial wave of workgroups would double the tail).
 static int g_ln_bwd_blocks = 0;
 DPC_API void dpc_layernorm_set_bwd_blocks(int n) { g_ln_bwd_blocks = n > 0 ? n : 0; }
+// 1: the row-prefetch kernel (default), 0: one row at a time (DPC_LN_BWD_PF)
+static int g_ln_bwd_pf = -1;
+DPC_API void dpc_layernorm_set_bwd_prefetch(int v) { g_ln_bwd_pf = v; }
+
+template <int NV, bool DYB, bool PF>
+static int ln_bwd_launch(const LNArgs* a, long long cap, hipStream_t stream) {
+  static int resident = 0;
+  if (!resident) {
+    int per_cu = 0, dev = 0, ncu = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, ln_bwd_kernel<NV, DYB, PF>, 256, 0) != hipSuccess)
+      per_cu = 1;
+    (void)hipGetDevice(&dev);
+    if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) ncu = 256;
+    resident = std::max(1, per_cu) * std::max(1, ncu);
+  }
+  const long long blocks = std::min<long long>((a->T + 3) / 4, std::min<long long>(cap, resident));
+  hipLaunchKernelGGL((ln_bwd_kernel<NV, DYB, PF>), dim3((unsigned)blocks), dim3(256), 0, stream, *a);
+  return (int)hipGetLastError();
+}
+
+template <int NV>
+static int ln_bwd_nv(const LNArgs* a, long long cap, bool pf, hipStream_t stream) {
+  if (a->dy_bf16) return pf ? ln_bwd_launch<NV, true, true>(a, cap, stream) : ln_bwd_launch<NV, true, false>(a, cap, stream);
+  return pf ? ln_bwd_launch<NV, false, true>(a, cap, stream) : ln_bwd_launch<NV, false, false>(a, cap, stream);
+}
 
 DPC_API int dpc_layernorm_bwd(const LNArgs* a, hipStream_t stream) {
   if (a->T <= 0) return 0;
   if (a->D % 4) return (int)hipErrorInvalidValue;
-  const long long blocks = (a->T + 3) / 4;
+  if (g_ln_bwd_pf < 0) g_ln_bwd_pf = getenv("DPC_LN_BWD_PF") ? atoi(getenv("DPC_LN_BWD_PF")) : 1;
   // (also at most one workgroup per 32 rows: the reference-default shape T = 16320, D = 256 ran
   // 36 us at 1024 workgroups, 25.6 us at 256-512 -- bench/ln_grid.py)
   long long cap = g_ln_bwd_blocks > 0 ? g_ln_bwd_blocks : std::min<long long>(786432 / a->D, (a->T + 31) / 32);
   cap = cap < 256 ? 256 : (cap > 1024 && g_ln_bwd_blocks <= 0 ? 1024 : cap);
-  dim3 grid((unsigned)(blocks < cap ? blocks : cap));
-  LN_DISPATCH(ln_bwd_kernel, grid);
-  return (int)hipGetLastError();
+  const bool pf = g_ln_bwd_pf != 0;
+  switch ((a->D + 255) / 256) {
+    case 1: return ln_bwd_nv<1>(a, cap, pf, stream);
+    case 2: return ln_bwd_nv<2>(a, cap, pf, stream);
+    case 3: return ln_bwd_nv<3>(a, cap, pf, stream);
+    case 4: return ln_bwd_nv<4>(a, cap, pf, stream);
+    case 5: return ln_bwd_nv<5>(a, cap, pf, stream);
+    case 6: return ln_bwd_nv<6>(a, cap, pf, stream);
+    case 7: return ln_bwd_nv<7>(a, cap, pf, stream);
+    case 8: return ln_bwd_nv<8>(a, cap, pf, stream);
+    default: return (int)hipErrorInvalidValue;
+  }
 }

@@ -10,7 +10,7 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/prof_$tag -o
 cd $R
 db=$(ls gpurun_out/prof_$tag/*/b_results.db 2>/dev/null | head -1 || true)
 [ -z "$db" ] && db=$(find gpurun_out/prof_$tag -name "*.db" | head -1)
-python3 scripts/step_gaps.py $db --steps 8 > gpurun_out/prof_${tag}_steps.md
+python3 scripts/step_gaps.py $db --steps 8 --seq gpurun_out/prof_${tag}_seq.txt > gpurun_out/prof_${tag}_steps.md
 python3 scripts/kstats.py $db "bench $tag" > gpurun_out/prof_${tag}_kstats.md
 tail -3 gpurun_out/prof_$tag.log
 head -12 gpurun_out/prof_${tag}_steps.md

@@ -5,7 +5,10 @@ last ``--steps`` steps it prints, per step, the wall time between consecutive Ad
 the union of kernel intervals inside it (GPU busy) and the idle gap, then the mean, and the
 per-kernel time of one mean step.
 
-    python scripts/step_gaps.py gpurun_out/prof/b_results.db [--steps 8] [--delim adamw]
+    python scripts/step_gaps.py gpurun_out/prof/b_results.db [--steps 8] [--delim adamw] [--seq out.txt]
+
+--seq writes the last step's dispatches in launch order (duration, grid, name) to a file: the
+per-call view (which GEMM shape costs what) that the per-kernel totals hide.
 """
 import sqlite3
 import sys
@@ -54,6 +57,16 @@ for i in range(nsteps):
     print(f"step {i}: wall {wall / 1e6:.3f} ms  busy {busy / 1e6:.3f} ms  idle {(wall - busy) / 1e6:.3f} ms")
 print(f"mean: wall {tot_wall / nsteps / 1e6:.3f} ms  busy {tot_busy / nsteps / 1e6:.3f} ms  "
       f"idle {(tot_wall - tot_busy) / nsteps / 1e6:.3f} ms")
+if "--seq" in sys.argv:
+    lo, hi = marks[-2], marks[-1]
+    gcol = [c for c in cols if c in ("grid_size", "grid_x", "grid_size_x", "workgroup_count")]
+    sel = f'select name, "{s_col}", "{e_col}"' + (f', "{gcol[0]}"' if gcol else "") + " from kernels"
+    seq = sorted((r for r in con.execute(sel) if r[2] > lo and r[1] < hi), key=lambda r: r[1])
+    with open(sys.argv[sys.argv.index("--seq") + 1], "w") as f:
+        f.write(f"# columns: {cols}\n")
+        for r in seq:
+            g = r[3] if gcol else ""
+            f.write(f"{(r[2] - r[1]) / 1e3:9.1f} us  {g}  {r[0][:110]}\n")
 print("\n| kernel | ms per step |\n|---|---|")
 for n, t in sorted(per_kernel.items(), key=lambda kv: -kv[1])[:30]:
     n = n if len(n) < 100 else n[:97] + "..."
