@@ -57,52 +57,71 @@ __global__ __launch_bounds__(256) void eb_keys_kernel(const long long* src, int 
 // to the table by its start wave; a run that crosses boundaries leaves per-chunk partial sums
 // -- part[2 c] its first piece (the last run starting in chunk c), part[2 c + 1] the piece
 // continuing at chunk c's first position -- and eb_runsum_kernel adds them in chunk order.
-// Rows are read RB at a time, all loads issued before the adds, and added in row order, so
+// Rows are read in groups of 8 / 4 / 2 / 1, all of a group's loads issued before its adds, in row order, so
 // every sum has a fixed order: bitwise reproducible.
 constexpr int EB_CH = 8;
 
+// G rows (sorted positions j .. j+G-1, all of the run) summed into acc in row order: all G x NV
+// loads issued before the first add, none under a branch (a load under a branch is waited for
+// with vmcnt(0) at the join: G x NV serialized round trips); a lane past the row end re-reads
+// the last chunk and never stores it
+template <int NV, int G>
+__device__ __forceinline__ void eb_add_group(float4 (&acc)[NV], const int* rows, const float* dout, int j, int D,
+                                             int lane) {
+  const int nv4 = D >> 2;
+  float4 x[G][NV];
+#pragma unroll
+  for (int u = 0; u < G; ++u) {
+    const float4* src = reinterpret_cast<const float4*>(dout + (long long)rows[j + u] * D);
+#pragma unroll
+    for (int v = 0; v < NV; ++v) x[u][v] = src[min(lane + 64 * v, nv4 - 1)];
+  }
+#pragma unroll
+  for (int u = 0; u < G; ++u)
+#pragma unroll
+    for (int v = 0; v < NV; ++v) {
+      acc[v].x += x[u][v].x; acc[v].y += x[u][v].y; acc[v].z += x[u][v].z; acc[v].w += x[u][v].w;
+    }
+}
+
+// the rows of key k at sorted positions j0 .. jend-1 (a run's piece: <= EB_CH positions), in
+// groups of 8 / 4 / 2 / 1 by the piece's length -- a random token's run is mostly ONE row, and
+// a fixed group of 8 loaded 8 (the old form: conditionally, one round trip each)
 template <int NV>
 __device__ __forceinline__ void eb_add_rows(float4 (&acc)[NV], const int* keys, const int* rows, const float* dout,
                                             int j0, int jend, int k, int D, int lane) {
-  constexpr int RB = NV <= 4 ? 8 : 4;
-  const int nv4 = D >> 2;
-  for (int j = j0; j < jend; j += RB) {
-    int rr[RB];
-#pragma unroll
-    for (int u = 0; u < RB; ++u) rr[u] = (j + u < jend && keys[j + u] == k) ? rows[j + u] : -1;
-    float4 x[RB][NV];
-#pragma unroll
-    for (int u = 0; u < RB; ++u)
-#pragma unroll
-      for (int v = 0; v < NV; ++v) {
-        const int c = lane + 64 * v;
-        x[u][v] = (rr[u] >= 0 && c < nv4) ? reinterpret_cast<const float4*>(dout + (long long)rr[u] * D)[c]
-                                           : make_float4(0.f, 0.f, 0.f, 0.f);
-      }
-#pragma unroll
-    for (int u = 0; u < RB; ++u)
-#pragma unroll
-      for (int v = 0; v < NV; ++v) {
-        acc[v].x += x[u][v].x; acc[v].y += x[u][v].y; acc[v].z += x[u][v].z; acc[v].w += x[u][v].w;
-      }
-    if (rr[RB - 1] < 0) break;
+  int n = 0;
+  while (j0 + n < jend && keys[j0 + n] == k) ++n;  // (wave-uniform: scalar loads)
+  int j = j0;
+  const int end = j0 + n;
+  if constexpr (NV <= 4) {
+    for (; j + 8 <= end; j += 8) eb_add_group<NV, 8>(acc, rows, dout, j, D, lane);
   }
+  for (; j + 4 <= end; j += 4) eb_add_group<NV, 4>(acc, rows, dout, j, D, lane);
+  if (j + 2 <= end) {
+    eb_add_group<NV, 2>(acc, rows, dout, j, D, lane);
+    j += 2;
+  }
+  if (j < end) eb_add_group<NV, 1>(acc, rows, dout, j, D, lane);
 }
 
 template <int NV>
 __device__ __forceinline__ void eb_store_add(float* dst_row, const float4 (&acc)[NV], int D, int lane, bool add) {
   float4* dst = reinterpret_cast<float4*>(dst_row);
+  const int nv4 = D >> 2;
+  float4 t[NV];
+  if (add) {  // (all of the row's reads issued before the first add: unconditional, clamped)
+#pragma unroll
+    for (int v = 0; v < NV; ++v) t[v] = dst[min(lane + 64 * v, nv4 - 1)];
+  }
 #pragma unroll
   for (int v = 0; v < NV; ++v) {
     const int c = lane + 64 * v;
-    if (c < (D >> 2)) {
-      float4 o = acc[v];
-      if (add) {
-        const float4 t = dst[c];
-        o.x += t.x; o.y += t.y; o.z += t.z; o.w += t.w;
-      }
-      dst[c] = o;
+    float4 o = acc[v];
+    if (add) {
+      o.x += t[v].x; o.y += t[v].y; o.z += t[v].z; o.w += t[v].w;
     }
+    if (c < nv4) dst[c] = o;
   }
 }
 
@@ -145,18 +164,13 @@ __global__ __launch_bounds__(256) void eb_runsum_kernel(const int* keys, const f
   const int nv4 = D >> 2;
   float4 acc[NV];
 #pragma unroll
-  for (int v = 0; v < NV; ++v) {
-    const int cc = lane + 64 * v;
-    acc[v] = cc < nv4 ? reinterpret_cast<const float4*>(part + (long long)(2 * c) * D)[cc] : make_float4(0.f, 0.f, 0.f, 0.f);
-  }
+  for (int v = 0; v < NV; ++v)  // (clamped, unconditional loads; lanes past the row end never store)
+    acc[v] = reinterpret_cast<const float4*>(part + (long long)(2 * c) * D)[min(lane + 64 * v, nv4 - 1)];
   for (++c; c * EB_CH < T && keys[c * EB_CH] == k; ++c) {
 #pragma unroll
     for (int v = 0; v < NV; ++v) {
-      const int cc = lane + 64 * v;
-      if (cc < nv4) {
-        const float4 t = reinterpret_cast<const float4*>(part + (long long)(2 * c + 1) * D)[cc];
-        acc[v].x += t.x; acc[v].y += t.y; acc[v].z += t.z; acc[v].w += t.w;
-      }
+      const float4 t = reinterpret_cast<const float4*>(part + (long long)(2 * c + 1) * D)[min(lane + 64 * v, nv4 - 1)];
+      acc[v].x += t.x; acc[v].y += t.y; acc[v].z += t.z; acc[v].w += t.w;
     }
   }
   eb_store_add<NV>(table + (long long)k * D, acc, D, lane, true);
