@@ -57,6 +57,23 @@ def timeit(fn):
     return s.elapsed_time(e) / a.iters * 1e3
 
 
+# the forward forms: LN1 (plain) and LN2 (fused residual add of the attention projection + bias)
+yb = torch.randn(T, D, device=dev).bfloat16()
+bias = torch.randn(D, device=dev)
+xo = torch.empty(T, D, device=dev)
+fwd = {
+    "fwd_ln1": (lambda: layernorm_fwd(x, g, b), 4 + 2),
+    "fwd_ln2_add": (lambda: layernorm_fwd(x, g, b, add=(yb, bias, None), x_out=xo), 4 + 2 + 4 + 2),
+}
+try:
+    fwd["fwd_ln2_add"][0]()
+except TypeError:  # (a tree whose layernorm_fwd has other keywords)
+    fwd.pop("fwd_ln2_add")
+for r in range(a.rounds):
+    for name, (fn, bpe) in fwd.items():
+        us = timeit(fn)
+        print(json.dumps({"case": name, "us": round(us, 1), "TBps": round(T * D * bpe / us / 1e6, 2)}), flush=True)
+
 res = {}
 for r in range(a.rounds):
     for pf in (0, 1):

@@ -60,52 +60,62 @@ struct LNArgs {
   int dx_set;  // bwd: dx = LN'(dy) (dx not read) instead of dx += LN'(dy)
 };
 
-template <int NV>
+// Every load of the row (x, the fused add's y and bias, gamma, beta) is issued up front and
+// unconditionally (a load under a branch is waited for with vmcnt(0) at the join): a lane past
+// the row end re-reads the last chunk and is zeroed before the sums, and the add's operands read
+// gamma (row stride 0, L1-resident) when the add has no bias.  ADD: the launch has the fused add
+// (a template parameter: the plain form loads nothing of it).
+template <int NV, bool ADD>
 __global__ __launch_bounds__(256) void ln_fwd_kernel(LNArgs p) {
   const uint32_t dkey = p.drop_scale != 0.f ? drop_key_of(p.drop_seed, p.drop_site, p.drop_key) : 0u;
   const int lane = threadIdx.x & 63;
   const long long row = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= p.T) return;
-  const float4* xr = reinterpret_cast<const float4*>(p.x + row * p.ldx);
   const int nv4 = p.D >> 2;
-  float4 v[NV];
-  float s = 0.f;
-  if (p.add_y) {
-    // all loads of the row first (x f32, y bf16, bias), then the fused residual add
-    const uint2* yr = reinterpret_cast<const uint2*>(static_cast<const bf16_t*>(p.add_y) + row * p.ld_add);
-    const float4* b4 = reinterpret_cast<const float4*>(p.add_bias);
-    uint2 yv[NV];
+  constexpr bool has_add = ADD;
+  const float4* xr = reinterpret_cast<const float4*>(p.x + row * p.ldx);
+  const uint2* yr = reinterpret_cast<const uint2*>(has_add ? static_cast<const bf16_t*>(p.add_y) + row * p.ld_add
+                                                           : nullptr);
+  const bool has_bias = has_add && p.add_bias;
+  const float4* ab4 = reinterpret_cast<const float4*>(has_bias ? p.add_bias : p.gamma);
+  const float bsc = has_bias ? 1.f : 0.f;
+  const float4* g4 = reinterpret_cast<const float4*>(p.gamma);
+  const float4* b4 = reinterpret_cast<const float4*>(p.beta);
+  float4 v[NV], ab[NV], gm[NV], bt[NV];
+  uint2 yv[NV];
 #pragma unroll
-    for (int i = 0; i < NV; ++i) {
-      const int c = lane + i * 64;
-      v[i] = c < nv4 ? xr[c] : make_float4(0.f, 0.f, 0.f, 0.f);
-      yv[i] = c < nv4 ? yr[c] : make_uint2(0u, 0u);
+  for (int i = 0; i < NV; ++i) {
+    const int c = min(lane + i * 64, nv4 - 1);
+    v[i] = xr[c];
+    if constexpr (ADD) {
+      yv[i] = yr[c];
+      ab[i] = ab4[c];
     }
-    float4* xo = reinterpret_cast<float4*>(p.x_out + row * p.ld_xout);
+    gm[i] = g4[c];
+    bt[i] = b4[c];
+  }
+  __builtin_amdgcn_sched_barrier(0);
+  float s = 0.f;
+  float4* xo = reinterpret_cast<float4*>(p.x_out + row * p.ld_xout);
 #pragma unroll
-    for (int i = 0; i < NV; ++i) {
-      const int c = lane + i * 64;
-      if (c < nv4) {
-        const float4 b = p.add_bias ? b4[c] : make_float4(0.f, 0.f, 0.f, 0.f);
-        float a[4] = {__uint_as_float(yv[i].x << 16) + b.x, __uint_as_float(yv[i].x & 0xffff0000u) + b.y,
-                      __uint_as_float(yv[i].y << 16) + b.z, __uint_as_float(yv[i].y & 0xffff0000u) + b.w};
-        if (p.drop_scale != 0.f) {
-          const uint32_t idx = (uint32_t)(row * p.D + 4 * c);
+  for (int i = 0; i < NV; ++i) {
+    const int c = lane + i * 64;
+    const bool ok = c < nv4;
+    if (!ok) v[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+    if constexpr (ADD) {  // the fused residual add (no loads in here)
+      float a[4] = {__uint_as_float(yv[i].x << 16) + ab[i].x * bsc, __uint_as_float(yv[i].x & 0xffff0000u) + ab[i].y * bsc,
+                    __uint_as_float(yv[i].y << 16) + ab[i].z * bsc, __uint_as_float(yv[i].y & 0xffff0000u) + ab[i].w * bsc};
+      if (p.drop_scale != 0.f) {
+        const uint32_t idx = (uint32_t)(row * p.D + 4 * c);
 #pragma unroll
-          for (int e = 0; e < 4; ++e) a[e] *= drop_factor(idx + e, dkey, p.drop_thresh, p.drop_scale);
-        }
+        for (int e = 0; e < 4; ++e) a[e] *= drop_factor(idx + e, dkey, p.drop_thresh, p.drop_scale);
+      }
+      if (ok) {
         v[i].x += a[0]; v[i].y += a[1]; v[i].z += a[2]; v[i].w += a[3];
         xo[c] = v[i];
       }
-      s += v[i].x + v[i].y + v[i].z + v[i].w;
     }
-  } else {
-#pragma unroll
-    for (int i = 0; i < NV; ++i) {
-      const int c = lane + i * 64;
-      v[i] = c < nv4 ? xr[c] : make_float4(0.f, 0.f, 0.f, 0.f);
-      s += v[i].x + v[i].y + v[i].z + v[i].w;
-    }
+    s += v[i].x + v[i].y + v[i].z + v[i].w;
   }
   const float mu = wave_sum(s) / p.D;
   float ss = 0.f;
@@ -118,13 +128,11 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(LNArgs p) {
     }
   }
   const float rs = rsqrtf(wave_sum(ss) / p.D + p.eps);
-  const float4* g4 = reinterpret_cast<const float4*>(p.gamma);
-  const float4* b4 = reinterpret_cast<const float4*>(p.beta);
 #pragma unroll
   for (int i = 0; i < NV; ++i) {
     const int c = lane + i * 64;
     if (c < nv4) {
-      const float4 g = g4[c], b = b4[c];
+      const float4 g = gm[i], b = bt[i];
       float4 o;
       o.x = (v[i].x - mu) * rs * g.x + b.x;
       o.y = (v[i].y - mu) * rs * g.y + b.y;
@@ -338,24 +346,27 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(LNArgs p) {
 
 using namespace dpc;
 
-#define LN_DISPATCH(KERNEL, GRID)                                                     \
-  switch ((a->D + 255) / 256) {                                                        \
-    case 1: hipLaunchKernelGGL(KERNEL<1>, GRID, dim3(256), 0, stream, *a); break;      \
-    case 2: hipLaunchKernelGGL(KERNEL<2>, GRID, dim3(256), 0, stream, *a); break;      \
-    case 3: hipLaunchKernelGGL(KERNEL<3>, GRID, dim3(256), 0, stream, *a); break;      \
-    case 4: hipLaunchKernelGGL(KERNEL<4>, GRID, dim3(256), 0, stream, *a); break;      \
-    case 5: hipLaunchKernelGGL(KERNEL<5>, GRID, dim3(256), 0, stream, *a); break;      \
-    case 6: hipLaunchKernelGGL(KERNEL<6>, GRID, dim3(256), 0, stream, *a); break;      \
-    case 7: hipLaunchKernelGGL(KERNEL<7>, GRID, dim3(256), 0, stream, *a); break;      \
-    case 8: hipLaunchKernelGGL(KERNEL<8>, GRID, dim3(256), 0, stream, *a); break;      \
-    default: return (int)hipErrorInvalidValue;                                         \
-  }
+template <int NV>
+static void ln_fwd_nv(const LNArgs* a, dim3 grid, hipStream_t stream) {
+  if (a->add_y) hipLaunchKernelGGL((ln_fwd_kernel<NV, true>), grid, dim3(256), 0, stream, *a);
+  else hipLaunchKernelGGL((ln_fwd_kernel<NV, false>), grid, dim3(256), 0, stream, *a);
+}
 
 DPC_API int dpc_layernorm_fwd(const LNArgs* a, hipStream_t stream) {
   if (a->T <= 0) return 0;
   if (a->D % 4) return (int)hipErrorInvalidValue;
   dim3 grid((unsigned)((a->T + 3) / 4));
-  LN_DISPATCH(ln_fwd_kernel, grid);
+  switch ((a->D + 255) / 256) {
+    case 1: ln_fwd_nv<1>(a, grid, stream); break;
+    case 2: ln_fwd_nv<2>(a, grid, stream); break;
+    case 3: ln_fwd_nv<3>(a, grid, stream); break;
+    case 4: ln_fwd_nv<4>(a, grid, stream); break;
+    case 5: ln_fwd_nv<5>(a, grid, stream); break;
+    case 6: ln_fwd_nv<6>(a, grid, stream); break;
+    case 7: ln_fwd_nv<7>(a, grid, stream); break;
+    case 8: ln_fwd_nv<8>(a, grid, stream); break;
+    default: return (int)hipErrorInvalidValue;
+  }
   return (int)hipGetLastError();
 }
 
