@@ -87,25 +87,23 @@ __device__ __forceinline__ int toff(int row, int chunk) {
 // ---- LDS-DMA from inline asm (buffer_load ... lds; M0 = the wave's LDS destination).
 // Issued from asm so that the compiler does not wait for it before every LDS read: the
 // kernels wait with explicit counted s_waitcnt at the ring boundary.
+// M0 is written without saving / restoring it: the compiler uses M0 for nothing in this file's
+// kernels (their gfx950 asm has no M0 access but these; check with
+// `hipcc -S attention.hip && grep m0`), and the save / restore pair was 2 of the ~13 scalar
+// instructions per MFMA the forward issues (rocprofv3 SQ_INSTS_SALU, profiles/r5_attn/pmc_final.txt).
 __device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t rs, int voff, const void* lds) {
   const unsigned la = (unsigned)(uintptr_t)(lds_void_t)lds;
-  unsigned keep;
-  asm volatile(
-      "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds\n\t"
-      "s_mov_b32 m0, %0"
-      : "=&s"(keep)
-      : "v"(voff), "s"(rs), "s"(la)
-      : "memory");
+  asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tbuffer_load_dwordx4 %0, %1, 0 offen lds"
+               :
+               : "v"(voff), "s"(rs), "s"(la)
+               : "memory");
 }
 __device__ __forceinline__ void dma4(__amdgpu_buffer_rsrc_t rs, int voff, const void* lds) {
   const unsigned la = (unsigned)(uintptr_t)(lds_void_t)lds;
-  unsigned keep;
-  asm volatile(
-      "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dword %1, %2, 0 offen lds\n\t"
-      "s_mov_b32 m0, %0"
-      : "=&s"(keep)
-      : "v"(voff), "s"(rs), "s"(la)
-      : "memory");
+  asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tbuffer_load_dword %0, %1, 0 offen lds"
+               :
+               : "v"(voff), "s"(rs), "s"(la)
+               : "memory");
 }
 template <int N>
 __device__ __forceinline__ void vm_wait() {
@@ -127,12 +125,18 @@ __device__ __forceinline__ void ring_barrier() {
   asm volatile("" ::: "memory");
 }
 
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t rows_rsrc(const void* base, long long ld_bytes, int row0, int S,
+// Descriptor of rows row0 .. S-1 of a [S][ld] operand (rows past S, or all of them if !valid, read
+// as zeros).  32-bit offsets: the host guarantees (S + 256) * ld_bytes < 2^32 (attn_args_ok) --
+// the 64-bit form (multiplies, a 64-bit clamp through VALU compares) was ~20 scalar instructions
+// per descriptor, two descriptors per tile step.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rows_rsrc(const void* base, unsigned ld_bytes, int row0, int S,
                                                            bool valid) {
-  const long long left = valid ? (long long)(S - row0) * ld_bytes : 0;
-  const unsigned nrec = left <= 0 ? 0u : (left > 0xffffffffll ? 0xffffffffu : (unsigned)left);
-  return __builtin_amdgcn_make_buffer_rsrc((void*)((const char*)base + (long long)row0 * ld_bytes), 0, nrec,
-                                           0x00020000);
+  const unsigned span = (unsigned)S * ld_bytes;
+  const unsigned off = (unsigned)row0 * ld_bytes;
+  // (readfirstlane: left alone, the compiler forms the clamp as a VALU saturating subtract and the
+  // whole descriptor in VGPRs, which the DMA asm's "s" operand cannot take)
+  const unsigned nrec = __builtin_amdgcn_readfirstlane((valid && off < span) ? span - off : 0u);
+  return __builtin_amdgcn_make_buffer_rsrc((void*)((const char*)base + off), 0, nrec, 0x00020000);
 }
 
 // The DMA writes lane-linearly -- piece g (wave wid, instruction i: g = wid * NPW + i) fills
@@ -154,7 +158,7 @@ __device__ __forceinline__ void dma_voff(int (&v)[AT<HD>::NPW], long long ld, in
 template <int HD>
 __device__ __forceinline__ void tile_dma(const bf16_t* base, long long ld, int row0, int S, bool valid,
                                          const int (&v)[AT<HD>::NPW], bf16_t* lds, int wid) {
-  const __amdgpu_buffer_rsrc_t rs = rows_rsrc(base, ld * 2, row0, S, valid);
+  const __amdgpu_buffer_rsrc_t rs = rows_rsrc(base, (unsigned)(ld * 2), row0, S, valid);
 #pragma unroll
   for (int i = 0; i < AT<HD>::NPW; ++i) dma16(rs, v[i], lds + (wid * AT<HD>::NPW + i) * 512);
 }
@@ -555,30 +559,39 @@ __global__ __launch_bounds__(256, OCC) void attn_fwd2_kernel(AttnArgs p, int nit
 
   int dv[A::NPW];
   dma_voff<HD>(dv, p.ld_qkv, wid, lane);
-  // ---- issue cursor: (item, offset), wave-uniform
+  // ---- issue cursor: (item, offset), wave-uniform.  The item's (batch, head) offset is formed
+  // when the cursor enters the item (a division by H): per step it was ~20 of the ~200 scalar
+  // instructions of a tile (rocprofv3 SQ_INSTS_SALU, profiles/r5_attn/pmc_final.txt)
   int is_k = 0, is_off = 0;
   PairItem is_it = item(0);
+  long long is_hoff = 0;  // elements from q / k / v to row 0 of the item's (batch, head)
+  auto enter = [&]() {
+    const int n = is_it.bh / H, h = is_it.bh - n * H;
+    is_hoff = (long long)n * S * p.ld_qkv + h * HD;
+  };
+  enter();
   auto issue_next = [&](int e) {
     bf16_t* st = smem + (e % NSLOT) * 2 * A::TILE;
     const bool valid = is_k < nmine;
-    const int n = is_it.bh / H, h = is_it.bh - n * H;
-    const long long tok0 = (long long)n * S;
-    const bf16_t* base = static_cast<const bf16_t*>(p.q) + tok0 * p.ld_qkv + h * HD;
     const bool second = is_off >= is_it.len0;
     const int i = is_off - (second ? is_it.len0 : 0);
     if (i == 0 || !valid) {  // Q rows of the block (or an empty element past the end)
+      const bf16_t* base = static_cast<const bf16_t*>(p.q) + is_hoff;
       const int r0 = (second ? is_it.blk1 : is_it.blk0) * QB;
       tile_dma<HD>(base, p.ld_qkv, r0, S, valid, dv, st, wid);
       tile_dma<HD>(base, p.ld_qkv, r0 + KT, S, valid, dv, st + A::TILE, wid);
     } else {
-      const bf16_t* K = static_cast<const bf16_t*>(p.k) + tok0 * p.ld_qkv + h * HD;
-      const bf16_t* V = static_cast<const bf16_t*>(p.v) + tok0 * p.ld_qkv + h * HD;
+      const bf16_t* K = static_cast<const bf16_t*>(p.k) + is_hoff;
+      const bf16_t* V = static_cast<const bf16_t*>(p.v) + is_hoff;
       tile_dma<HD>(K, p.ld_qkv, (i - 1) * KT, S, true, dv, st, wid);
       tile_dma<HD>(V, p.ld_qkv, (i - 1) * KT, S, true, dv, st + A::TILE, wid);
     }
     if (valid && ++is_off == is_it.len) {
       is_off = 0;
-      if (++is_k < nmine) is_it = item(is_k);
+      if (++is_k < nmine) {
+        is_it = item(is_k);
+        enter();
+      }
     }
   };
 
@@ -1253,6 +1266,9 @@ static bool attn_args_ok(const AttnArgs* a, bool bwd) {
   if (a->hd != 32 && a->hd != 64 && a->hd != 128) return false;
   if (a->N <= 0 || a->S <= 0 || a->H <= 0) return false;
   if (a->ld_qkv % 8 || a->ld_o % 8 || (bwd && a->ld_dqkv % 8)) return false;
+  // (rows_rsrc's 32-bit offsets: one sequence's rows of Q / K / V / O / dO span < 4 GiB)
+  const long long ld = a->ld_qkv > a->ld_o ? a->ld_qkv : a->ld_o;
+  if (((long long)a->S + 256) * ld * 2 >= 0xffffffffll) return false;
   return true;
 }
 
