@@ -50,6 +50,14 @@ def _suffix(t: torch.Tensor) -> str:
     return "_f32" if t.dtype == torch.float32 else ""
 
 
+def _check_span(t: torch.Tensor, S: int, *lds: int) -> None:
+    """The bf16 kernels address one sequence's rows with 32-bit offsets (attention.hip:rows_rsrc):
+    (S + 256) rows of every strided operand must span < 4 GiB."""
+    if t.dtype != torch.float32 and (S + 256) * max(lds) * t.element_size() >= 0xFFFFFFFF:
+        raise ValueError(f"attention: one sequence's rows span >= 4 GiB (S={S}, row strides {lds}); "
+                         "split the sequence or run the reference path")
+
+
 def split_qkv(qkv: torch.Tensor, heads: int, head_dim: int):
     """Views q, k, v [T, H*hd] out of the fused [T, 3*H*hd] projection."""
     hd = heads * head_dim
@@ -139,6 +147,7 @@ def _attn_fwd_hip(qkv, N, S, heads, kd, pad_mask, causal, scale, out):
         pad=_lib.ptr(pad), ld_qkv=qkv.stride(0), ld_o=out.stride(0), ld_dqkv=0,
         N=N, S=S, H=heads, scale=float(scale), causal=int(causal), hd=kd,
     )
+    _check_span(qkv, S, qkv.stride(0), out.stride(0))
     _lib.call("dpc_attn_fwd" + _suffix(qkv), args, qkv.device)
     return out, lse
 
@@ -204,6 +213,7 @@ def _attn_bwd_hip(dout, qkv, o, lse, N, S, heads, kd, pad_mask, causal, scale, d
         ld_qkv=qkv.stride(0), ld_o=o.stride(0), ld_dqkv=dqkv.stride(0),
         N=N, S=S, H=heads, scale=float(scale), causal=int(causal), hd=kd,
     )
+    _check_span(qkv, S, qkv.stride(0), o.stride(0))
     _lib.call("dpc_attn_bwd" + _suffix(qkv), args, qkv.device)
     return dqkv
 

@@ -193,3 +193,19 @@ def test_phase_ranges_cover_every_engine(monkeypatch):
         eng.train_step(*full_batch())
         names = {n.split(" ")[0] for n in seen}
         assert {"fwd", "bwd", "optim"} <= names, seen
+
+
+def test_attention_span_check_rejects_4gib_sequences():
+    """The bf16 attention kernels use 32-bit row offsets per sequence (attention.hip:rows_rsrc):
+    a sequence whose rows would span >= 4 GiB is refused with a clear error before any launch;
+    the f32 kernels keep 64-bit offsets and are not limited."""
+    import pytest
+
+    from distributed_pytorch_cookbook_amd.ops.attention import _check_span
+
+    bf = torch.empty(1, dtype=torch.bfloat16)
+    _check_span(bf, 1023, 2304, 768)  # GPT-2 small: ~4.7 MB per sequence
+    _check_span(bf, 131072, 3 * 4096, 4096)  # 128K tokens of a 4096-wide model: ~3.2 GB
+    with pytest.raises(ValueError, match="4 GiB"):
+        _check_span(bf, 200000, 3 * 4096, 4096)
+    _check_span(torch.empty(1), 200000, 3 * 4096, 4096)
