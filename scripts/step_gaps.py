@@ -34,6 +34,9 @@ for e in ends:
         marks[-1] = e
     else:
         marks.append(e)
+if len(marks) < nsteps + 1:  # (fewer steps traced than asked: use what there is)
+    print(f"(only {len(marks) - 1} step boundaries found; using them)")
+    nsteps = len(marks) - 1
 marks = marks[-(nsteps + 1):]
 per_kernel = defaultdict(float)
 tot_wall = tot_busy = 0.0
