@@ -50,7 +50,6 @@ class AttnArgs(ctypes.Structure):
         ("scale", c_float),
         ("causal", c_int),
         ("hd", c_int),
-        ("spol", c_int),  # (attention.hip's launchers set it: DPC_ATTN_SPOL)
     ]
 
 

@@ -52,7 +52,6 @@ struct AttnArgs {
   float scale;
   int causal;
   int hd;                                       // head_dim: 32, 64 or 128
-  int spol;                                     // output stores: 0 plain, 1 nt, 2 sc0 sc1 nt (set by the launcher)
 };
 
 constexpr int KT = 64;       // keys (or queries) per staged tile
@@ -204,15 +203,12 @@ __device__ __forceinline__ int acc_row(int r, int lane) { return (r & 3) + 8 * (
 // pair leaves in one 16-B store per lane instead of two 8-B ones: half the store instructions
 // of a store-issue-bound tail (cdna_hip_programming.md T21).  Lanes l and l + 32 hold the same
 // row, so a row guard (key / query < S) keeps both or neither active.
-__device__ __forceinline__ void store_pair16(bf16_t* row, int g, int hh, uint2 wa, uint2 wb, int spol) {
+// (plain stores: the nt / sc0 sc1 nt scopes that speed up the GEMM epilogues measured 5-10 %
+// slower here -- O, dQ, dK, dV are re-read at once by the next GEMM; profiles/r5_epi/attn_store_policy.log)
+__device__ __forceinline__ void store_pair16(bf16_t* row, int g, int hh, uint2 wa, uint2 wb) {
   const auto s0 = __builtin_amdgcn_permlane32_swap(wa.x, wb.x, false, false);
   const auto s1 = __builtin_amdgcn_permlane32_swap(wa.y, wb.y, false, false);
-  typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
-  const u32x4 w{s0[0], s1[0], s0[1], s1[1]};
-  u32x4* dst = reinterpret_cast<u32x4*>(row + 8 * g + 8 * hh);
-  if (spol == 2) asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1 nt" ::"v"(dst), "v"(w) : "memory");
-  else if (spol == 1) __builtin_nontemporal_store(w, dst);
-  else *dst = w;
+  *reinterpret_cast<uint4*>(row + 8 * g + 8 * hh) = make_uint4(s0[0], s1[0], s0[1], s1[1]);
 }
 
 // raw v_exp_f32 (2^x): inputs here are <= ~8 or -inf, no denormal range reduction needed
@@ -491,7 +487,7 @@ __global__ __launch_bounds__(256, OCC) void attn_fwd_kernel(AttnArgs p) {
         wa.y = pack2bf(o[d][4 * g + 2] * inv, o[d][4 * g + 3] * inv);
         wb.x = pack2bf(o[d][4 * g + 4] * inv, o[d][4 * g + 5] * inv);
         wb.y = pack2bf(o[d][4 * g + 6] * inv, o[d][4 * g + 7] * inv);
-        store_pair16(O + d * 32, g, hh, wa, wb, p.spol);
+        store_pair16(O + d * 32, g, hh, wa, wb);
       }
     if (hh == 0) {
       const float lse = (l > 0.f) ? (m + log2f(l)) / LOG2E : INFINITY;
@@ -635,7 +631,7 @@ __global__ __launch_bounds__(256, OCC) void attn_fwd2_kernel(AttnArgs p, int nit
           wa.y = pack2bf(o[d][4 * g + 2] * inv, o[d][4 * g + 3] * inv);
           wb.x = pack2bf(o[d][4 * g + 4] * inv, o[d][4 * g + 5] * inv);
           wb.y = pack2bf(o[d][4 * g + 6] * inv, o[d][4 * g + 7] * inv);
-          store_pair16(O + d * 32, g, hh, wa, wb, p.spol);
+          store_pair16(O + d * 32, g, hh, wa, wb);
         }
       if (hh == 0) p.lse[(long long)bh * S + q] = (l > 0.f) ? (m + log2f(l)) / LOG2E : INFINITY;
     }
@@ -1003,8 +999,8 @@ __global__ __launch_bounds__(256, OCC) void attn_bwd_dkdv_kernel(AttnArgs p) {
     for (int d = 0; d < A::NDT; ++d)
 #pragma unroll
       for (int g = 0; g < 4; g += 2) {
-        store_pair16(dK + d * 32, g, hh, wk(d, g), wk(d, g + 1), p.spol);
-        store_pair16(dV + d * 32, g, hh, wv(d, g), wv(d, g + 1), p.spol);
+        store_pair16(dK + d * 32, g, hh, wk(d, g), wk(d, g + 1));
+        store_pair16(dV + d * 32, g, hh, wv(d, g), wv(d, g + 1));
       }
   }
 }
@@ -1168,7 +1164,7 @@ __global__ __launch_bounds__(256, OCC) void attn_bwd_dq_kernel(AttnArgs p) {
         wa.y = pack2bf(dqt[d][4 * g + 2] * p.scale, dqt[d][4 * g + 3] * p.scale);
         wb.x = pack2bf(dqt[d][4 * g + 4] * p.scale, dqt[d][4 * g + 5] * p.scale);
         wb.y = pack2bf(dqt[d][4 * g + 6] * p.scale, dqt[d][4 * g + 7] * p.scale);
-        store_pair16(dQ + d * 32, g, hh, wa, wb, p.spol);
+        store_pair16(dQ + d * 32, g, hh, wa, wb);
       }
   }
 }
@@ -1272,17 +1268,7 @@ static bool attn_args_ok(const AttnArgs* a, bool bwd) {
   return true;
 }
 
-// output store policy of every attention kernel (DPC_ATTN_SPOL: 0 plain, 1 nt, 2 sc0 sc1 nt)
-static int attn_spol() {
-  static int v = -1;
-  if (v < 0) v = getenv("DPC_ATTN_SPOL") ? atoi(getenv("DPC_ATTN_SPOL")) : 0;
-  return v;
-}
-
-DPC_API int dpc_attn_fwd(const AttnArgs* a_in, hipStream_t stream) {
-  AttnArgs b = *a_in;
-  b.spol = attn_spol();
-  const AttnArgs* a = &b;
+DPC_API int dpc_attn_fwd(const AttnArgs* a, hipStream_t stream) {
   if (!attn_args_ok(a, false)) return (int)hipErrorInvalidValue;
   if (a->hd == 128) return launch_fwd128(a, stream);
   return a->hd == 32 ? launch_fwd<32>(a, stream) : launch_fwd<64>(a, stream);
@@ -1320,10 +1306,7 @@ DPC_API int dpc_attn_bwd_lab(const AttnArgs* a, int which, int abl, hipStream_t 
 }
 
 
-DPC_API int dpc_attn_bwd(const AttnArgs* a_in, hipStream_t stream) {
-  AttnArgs b = *a_in;
-  b.spol = attn_spol();
-  const AttnArgs* a = &b;
+DPC_API int dpc_attn_bwd(const AttnArgs* a, hipStream_t stream) {
   if (!attn_args_ok(a, true)) return (int)hipErrorInvalidValue;
   if (a->hd == 128) return launch_bwd128(a, stream);
   return a->hd == 32 ? launch_bwd<32>(a, stream) : launch_bwd<64>(a, stream);

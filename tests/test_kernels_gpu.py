@@ -450,8 +450,20 @@ def test_attention_head_dim_other(hd, causal):
     assert rel_err(d, g) < 2e-2
 
 
-@pytest.mark.parametrize("D", [256, 768, 1600])
-def test_layernorm(D):
+@pytest.mark.parametrize("pf", [1, 0])
+@pytest.mark.parametrize("D", [100, 256, 768, 1600])
+def test_layernorm(D, pf):
+    """pf: the backward's next-row prefetch on / off (DPC_LN_BWD_PF); D = 100 and 1600 leave lanes
+    past the row end (the clamped, unconditional loads)."""
+    from distributed_pytorch_cookbook_amd.ops import _lib
+    _lib.lib().dpc_layernorm_set_bwd_prefetch(pf)
+    try:
+        _test_layernorm(D)
+    finally:
+        _lib.lib().dpc_layernorm_set_bwd_prefetch(-1)
+
+
+def _test_layernorm(D):
     torch.manual_seed(4)
     T = 517
     x = torch.randn(T, D, device=dev) * 3 + 1
