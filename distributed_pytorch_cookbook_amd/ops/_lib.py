@@ -50,6 +50,7 @@ class AttnArgs(ctypes.Structure):
         ("scale", c_float),
         ("causal", c_int),
         ("hd", c_int),
+        ("order", c_int),  # (attention.hip's backward launcher sets it: DPC_ATTN_ORDER)
     ]
 
 

@@ -52,6 +52,7 @@ struct AttnArgs {
   float scale;
   int causal;
   int hd;                                       // head_dim: 32, 64 or 128
+  int order;                                    // backward block order (set by the launcher: DPC_ATTN_ORDER)
 };
 
 constexpr int KT = 64;       // keys (or queries) per staged tile
@@ -263,6 +264,14 @@ __device__ __forceinline__ void zero16(floatx16& x) {
 __device__ __forceinline__ int g7_local_attn(int b, int grid) {
   const int xcd = b & 7, q = grid >> 3, r = grid & 7;
   return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (b >> 3);
+}
+// order 1 (the backward kernels' default, DPC_ATTN_ORDER): block-major over the whole grid in launch
+// order -- every (batch, head)'s heaviest causal block first, the lightest last, so the grid's
+// tail is light blocks -- at the cost of the L2 sharing of one head's rows across its blocks
+__device__ __forceinline__ void work_order1(int nblk, int& bh, int& i) {
+  const int nbh = gridDim.x / nblk;
+  i = blockIdx.x / nbh;
+  bh = blockIdx.x - i * nbh;
 }
 __device__ __forceinline__ void xcd_work(int nblk, int& bh, int& i) {
   const int b = blockIdx.x, nwg = gridDim.x, xcd = b & 7, q = nwg >> 3, r = nwg & 7;
@@ -807,7 +816,8 @@ __global__ __launch_bounds__(256, OCC) void attn_bwd_dkdv_kernel(AttnArgs p) {
   const int S = p.S, H = p.H;
   const int nkb = (S + QB - 1) / QB;
   int bh, kb;
-  xcd_work(nkb, bh, kb);  // kb = 0 (the most queries under the causal mask) first
+  if (p.order == 1) work_order1(nkb, bh, kb);
+  else xcd_work(nkb, bh, kb);  // kb = 0 (the most queries under the causal mask) first
   const int n = bh / H, h = bh % H;
   const int lane = threadIdx.x & 63, hh = lane >> 5;
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -1019,7 +1029,8 @@ __global__ __launch_bounds__(256, OCC) void attn_bwd_dq_kernel(AttnArgs p) {
   const int S = p.S, H = p.H;
   const int nqb = (S + QB - 1) / QB;
   int bh, bi;
-  xcd_work(nqb, bh, bi);
+  if (p.order == 1) work_order1(nqb, bh, bi);
+  else xcd_work(nqb, bh, bi);
   const int qb = nqb - 1 - bi;
   const int n = bh / H, h = bh % H;
   const int lane = threadIdx.x & 63, hh = lane >> 5;
@@ -1306,7 +1317,22 @@ DPC_API int dpc_attn_bwd_lab(const AttnArgs* a, int which, int abl, hipStream_t 
 }
 
 
-DPC_API int dpc_attn_bwd(const AttnArgs* a, hipStream_t stream) {
+// backward block order (DPC_ATTN_ORDER: 1 heaviest-first over the grid, the default; 0 per-XCD
+// head-major).  Measured round 5 (profiles/r5_attn/bwd_order.log, same box, interleaved): dQ + dK/dV
+// 601-608 -> 556-563 us, DDP 982.6K / 984.8K -> 994.3K / 993.0K.  Head-major left heavy blocks
+// (the first key block of a head sweeps all 16 query tiles, the last one 2) among the last
+// launched, a tail of up to one heavy block per slot; the lost L2 sharing of a head's Q / dO
+// rows costs less (they stay in the 256 MB Infinity Cache).
+static int attn_order() {
+  static int v = -1;
+  if (v < 0) v = getenv("DPC_ATTN_ORDER") ? atoi(getenv("DPC_ATTN_ORDER")) : 1;
+  return v;
+}
+
+DPC_API int dpc_attn_bwd(const AttnArgs* a_in, hipStream_t stream) {
+  AttnArgs b = *a_in;
+  b.order = attn_order();
+  const AttnArgs* a = &b;
   if (!attn_args_ok(a, true)) return (int)hipErrorInvalidValue;
   if (a->hd == 128) return launch_bwd128(a, stream);
   return a->hd == 32 ? launch_bwd<32>(a, stream) : launch_bwd<64>(a, stream);
