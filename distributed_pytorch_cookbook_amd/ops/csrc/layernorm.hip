@@ -376,7 +376,7 @@ DPC_API int dpc_layernorm_fwd(const LNArgs* a, hipStream_t stream) {
 // ~786K column-atomics per launch, and at most one workgroup per 32 rows.  0 = that rule; > 0
 // forces a size (sweeps).  The grid is also capped at what is resident at once (a second
 // partial wave of workgroups would double the tail).
-static int g_ln_bwd_blocks = 0;
+static int g_ln_bwd_blocks = getenv("DPC_LN_BWD_BLOCKS") ? atoi(getenv("DPC_LN_BWD_BLOCKS")) : 0;
 DPC_API void dpc_layernorm_set_bwd_blocks(int n) { g_ln_bwd_blocks = n > 0 ? n : 0; }
 // 1: the row-prefetch kernel (default), 0: one row at a time (DPC_LN_BWD_PF)
 static int g_ln_bwd_pf = -1;
