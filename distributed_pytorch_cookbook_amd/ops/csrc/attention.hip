@@ -1323,11 +1323,12 @@ DPC_API int dpc_attn_bwd_lab(const AttnArgs* a, int which, int abl, hipStream_t 
 // (the first key block of a head sweeps all 16 query tiles, the last one 2) among the last
 // launched, a tail of up to one heavy block per slot; the lost L2 sharing of a head's Q / dO
 // rows costs less (they stay in the 256 MB Infinity Cache).
+static int g_attn_order = -1;
 static int attn_order() {
-  static int v = -1;
-  if (v < 0) v = getenv("DPC_ATTN_ORDER") ? atoi(getenv("DPC_ATTN_ORDER")) : 1;
-  return v;
+  if (g_attn_order < 0) g_attn_order = getenv("DPC_ATTN_ORDER") ? atoi(getenv("DPC_ATTN_ORDER")) : 1;
+  return g_attn_order;
 }
+DPC_API void dpc_attn_set_order(int v) { g_attn_order = v; }  // (tests / A/B; -1: the env again)
 
 DPC_API int dpc_attn_bwd(const AttnArgs* a_in, hipStream_t stream) {
   AttnArgs b = *a_in;

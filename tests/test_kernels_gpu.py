@@ -450,6 +450,26 @@ def test_attention_head_dim_other(hd, causal):
     assert rel_err(d, g) < 2e-2
 
 
+def test_attention_bwd_block_order_bitwise():
+    """The backward's block order (DPC_ATTN_ORDER: 1 heaviest-first over the grid, 0 per-XCD
+    head-major) only changes WHEN each workgroup runs, not what it sums: dQ / dK / dV are bitwise
+    equal under both."""
+    from distributed_pytorch_cookbook_amd.ops import _lib
+    torch.manual_seed(21)
+    N, S, H, hd = 2, 300, 3, 64
+    qkv = (torch.randn(N * S, 3 * H * hd, device=dev) * 0.5).bfloat16()
+    o, lse = attention_fwd(qkv, N, S, H, hd, causal=True)
+    do = torch.randn_like(o)
+    outs = []
+    try:
+        for order in (1, 0):
+            _lib.lib().dpc_attn_set_order(order)
+            outs.append(attention_bwd(do, qkv, o, lse, N, S, H, hd, causal=True).clone())
+    finally:
+        _lib.lib().dpc_attn_set_order(-1)
+    assert torch.equal(outs[0], outs[1])
+
+
 @pytest.mark.parametrize("pf", [1, 0])
 @pytest.mark.parametrize("D", [100, 256, 768, 1600])
 def test_layernorm(D, pf):
