@@ -57,6 +57,15 @@ __device__ __forceinline__ void st16(void* ptr, uint4 v, bool nt) {
 }
 // the same with the epilogue's cache scope (GemmArgs::nt_store bits 2-3, default 3: gemm.hip
 // gemm_nt_mode): 0 = st16's nt / plain, 1 = sc0 nt, 2 = sc1 nt, 3 = sc0 sc1 nt
+// the f32 outputs' store scope: GemmArgs::nt_store bits 4-5 when bit 6 is set, else the bf16
+// outputs' scope (bits 2-3).  (f32 outputs -- the residual stream, split-K slabs -- are re-read
+// soon by the next kernel; A/B of a separate scope for them)
+// With bit 6: 0 = plain stores (-1 here), 1 sc0 nt, 2 sc1 nt, 3 sc0 sc1 nt.
+__device__ __forceinline__ int g_f32_pol(int nt_store) {
+  if (!(nt_store & 64)) return (nt_store >> 2) & 3;
+  const int v = (nt_store >> 4) & 3;
+  return v == 0 ? -1 : v;
+}
 __device__ __forceinline__ void st16p(void* ptr, uint4 v, bool nt, int pol) {
   typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
   const u32x4 w{v.x, v.y, v.z, v.w};

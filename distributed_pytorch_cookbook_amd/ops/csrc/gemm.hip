@@ -708,10 +708,14 @@ extern "C" int dpc_gemm7_ok(const GemmArgs* a);
 // tile's counted DMA waits -- which CDNA4's one in-order vmcnt makes wait for them too -- stall
 // less.  Same box against nt alone (round 5, profiles/r5_epi/store_policy.log): up-projection
 // fused 402 -> 384 us, down-projection fused 367 -> 349, plain up 283 -> 274, plain input
-// gradient 300 -> 290; DDP 960.8K -> 971.6K (two runs each).
+// gradient 300 -> 290; DDP 960.8K -> 971.6K (two runs each).  Bits 4-6: a separate scope for
+// the f32 outputs (gemm.h:g_f32_pol) -- default 77 = the above for bf16 outputs, PLAIN stores for
+// the f32 ones (the residual stream and the split-K slabs, which the next LayerNorm / the slab
+// reduction read back at once from the Infinity Cache): DDP +0.45 % same box, three interleaved
+// rounds (984.1 / 981.2 / 981.7K -> 989.7 / 984.5 / 985.5K, profiles/r5_epi/f32_store_scope.log).
 static int gemm_nt_mode() {
   static int mode = -1;
-  if (mode < 0) mode = getenv("DPC_GEMM_NT") ? atoi(getenv("DPC_GEMM_NT")) : 15;
+  if (mode < 0) mode = getenv("DPC_GEMM_NT") ? atoi(getenv("DPC_GEMM_NT")) : 77;
   return mode;
 }
 

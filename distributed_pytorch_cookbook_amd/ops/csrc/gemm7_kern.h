@@ -133,6 +133,7 @@ __device__ __forceinline__ void g7_bst16(g7_u32x4 v, __amdgpu_buffer_rsrc_t rs, 
   if (pol == 2) __builtin_amdgcn_raw_buffer_store_b128(v, rs, off, 0, 18);
   else if (pol == 3) __builtin_amdgcn_raw_buffer_store_b128(v, rs, off, 0, 19);
   else if (pol == 1) __builtin_amdgcn_raw_buffer_store_b128(v, rs, off, 0, 3);
+  else if (pol < 0) __builtin_amdgcn_raw_buffer_store_b128(v, rs, off, 0, 0);  // (g_f32_pol: plain)
   else __builtin_amdgcn_raw_buffer_store_b128(v, rs, off, 0, 2);
 }
 typedef float g7_f32x4 __attribute__((ext_vector_type(4)));
@@ -208,8 +209,8 @@ __device__ __forceinline__ void g7_epilogue(const GemmArgs& p, floatx4 (&acc)[8]
           const int m = mw + 16 * i + rr, n = nw + 16 * j + 4 * g + 16 * hi8;
           if (n < p.N) {
             float* C = static_cast<float*>(p.C) + (long long)m * p.ldc + n;
-            if (m < p.M) st16p(C, dA, p.nt_store & 2, (p.nt_store >> 2) & 3);
-            if (m + 8 < p.M) st16p(C + 8 * p.ldc, dB, p.nt_store & 2, (p.nt_store >> 2) & 3);
+            if (m < p.M) st16p(C, dA, p.nt_store & 2, g_f32_pol(p.nt_store));
+            if (m + 8 < p.M) st16p(C + 8 * p.ldc, dB, p.nt_store & 2, g_f32_pol(p.nt_store));
           }
         }
       }
@@ -361,7 +362,7 @@ __device__ __forceinline__ void g7_epilogue(const GemmArgs& p, floatx4 (&acc)[8]
               const float4 o = *C;
               w[0] += o.x; w[1] += o.y; w[2] += o.z; w[3] += o.w;
             }
-            st16p(C, make_float4(w[0], w[1], w[2], w[3]), p.nt_store & 2, (p.nt_store >> 2) & 3);
+            st16p(C, make_float4(w[0], w[1], w[2], w[3]), p.nt_store & 2, g_f32_pol(p.nt_store));
           }
         } else {
           pc[h][0] = pack2bf(w[0], w[1]);
@@ -647,7 +648,7 @@ __device__ __forceinline__ void g7_epilogue_res_lds(const GemmArgs& p, floatx4 (
   const __amdgpu_buffer_rsrc_t rco = span(p.C, p.ldc, 4);
   const __amdgpu_buffer_rsrc_t rax = span(p.aux_out, p.ld_aux_out, 2);
   const bool gelu = fact == ACT_GELU, relu = fact == ACT_RELU;
-  const int spol = (p.nt_store >> 2) & 3;
+  const int spol = (p.nt_store >> 2) & 3, fpol = g_f32_pol(p.nt_store);  // (bf16 aux / f32 C)
   float4 bias4[NJ];
 #pragma unroll
   for (int j = 0; j < NJ; ++j) {
@@ -691,7 +692,7 @@ __device__ __forceinline__ void g7_epilogue_res_lds(const GemmArgs& p, floatx4 (
         for (int r = 0; r < 4; ++r) w[r] = gelu ? ga[r] : (relu ? fmaxf(w[r], 0.f) : w[r]);
         const unsigned off = (n0 + ntc < p.N) ? (unsigned)((mt * p.ldc + ntc) * 4) : 0xfffffff0u;
         g7_bst16(__builtin_bit_cast(g7_u32x4, make_float4(w[0] + res.x, w[1] + res.y, w[2] + res.z, w[3] + res.w)),
-                 rco, off, spol);
+                 rco, off, fpol);
       });
       const int n8 = wc * 128 + 16 * j + coff;
       const auto s0 = __builtin_amdgcn_permlane16_swap(pa[0][0], pa[1][0], false, false);
