@@ -27,8 +27,7 @@ G._table = _Spy(G._table)
 @atexit.register
 def _report():
     for k, n in sorted(seen.items()):
-        print(f"{n:5d}  {k}  table={G._table.get.__func__(G._table, k) if False else dict.get(G._table, k)}",
-              file=sys.stderr)
+        print(f"{n:5d}  {k}  table={dict.get(G._table, k)}", file=sys.stderr)
 
 
 root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
