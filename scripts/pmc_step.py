@@ -4,6 +4,9 @@
 
 Columns: dispatches, mean wall (us), effective clock (GRBM_GUI_ACTIVE / 8 XCDs / wall), MFMA
 busy = SQ_VALU_MFMA_BUSY_CYCLES / (clock cycles x 1024 SIMDs), VALU instructions per MFMA.
+When the pass holds SQ_WAVE_CYCLES, two more columns: the share of wave cycles spent waiting on
+any counter (SQ_WAIT_ANY, mostly vmcnt / lgkmcnt) and waiting for instruction issue
+(SQ_WAIT_INST_ANY). Columns whose counters are absent from the pass print "-".
 """
 import sqlite3
 import sys
@@ -25,14 +28,27 @@ for name, ds in disp.items():
     c = vals[name]
     cyc = c.get("GRBM_GUI_ACTIVE", 0.0) / 8.0
     clock = cyc / wall_ns if wall_ns else 0.0
-    mfma = c.get("SQ_VALU_MFMA_BUSY_CYCLES", 0.0) / (cyc * 1024) if cyc else 0.0
-    vpm = c.get("SQ_INSTS_VALU", 0.0) / c["SQ_INSTS_MFMA"] if c.get("SQ_INSTS_MFMA") else float("nan")
-    rows.append((wall_ns, name, n, clock, mfma, vpm))
+    mfma = (c["SQ_VALU_MFMA_BUSY_CYCLES"] / (cyc * 1024)
+            if cyc and "SQ_VALU_MFMA_BUSY_CYCLES" in c else None)
+    vpm = (c["SQ_INSTS_VALU"] / c["SQ_INSTS_MFMA"]
+           if c.get("SQ_INSTS_MFMA") and "SQ_INSTS_VALU" in c else None)
+    wc = c.get("SQ_WAVE_CYCLES", 0.0)
+    wait = c["SQ_WAIT_ANY"] / wc if wc and "SQ_WAIT_ANY" in c else None
+    iwait = c["SQ_WAIT_INST_ANY"] / wc if wc and "SQ_WAIT_INST_ANY" in c else None
+    rows.append((wall_ns, name, n, clock, mfma, vpm, wait, iwait))
 rows.sort(reverse=True)
 total = sum(r[0] for r in rows)
 print(f"# {title}\n")
-print("| kernel | calls | mean us | % time | clock GHz | MFMA busy | VALU / MFMA |")
-print("|---|---|---|---|---|---|---|")
-for wall, name, n, clock, mfma, vpm in rows[:top]:
+
+
+def pct(v):
+    return "-" if v is None else f"{100 * v:.0f} %"
+
+
+print("| kernel | calls | mean us | % time | clock GHz | MFMA busy | VALU / MFMA | wait any | wait inst |")
+print("|---|---|---|---|---|---|---|---|---|")
+for wall, name, n, clock, mfma, vpm, wait, iwait in rows[:top]:
     nm = name if len(name) < 90 else name[:87] + "..."
-    print(f"| `{nm}` | {n} | {wall / n / 1e3:.1f} | {100 * wall / total:.1f} | {clock:.2f} | {100 * mfma:.0f} % | {vpm:.1f} |")
+    v = "-" if vpm is None else f"{vpm:.1f}"
+    print(f"| `{nm}` | {n} | {wall / n / 1e3:.1f} | {100 * wall / total:.1f} | {clock:.2f} | "
+          f"{pct(mfma)} | {v} | {pct(wait)} | {pct(iwait)} |")
