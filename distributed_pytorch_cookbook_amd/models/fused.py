@@ -32,7 +32,7 @@ from ..ops.attention import DECODE_MAX_S, attention_bwd, attention_fwd, decode_a
 from ..ops.elementwise import bias_act_bwd
 from ..ops.dropout import dropout_residual
 from ..ops.embedding import embedding_bwd, embedding_fwd
-from ..ops.gemm import (ACT_GELU, ACT_NONE, ACT_RELU, act_code, linear_dgrad, linear_fwd, linear_wgrad,
+from ..ops.gemm import (ACT_GELU, ACT_MUL, ACT_NONE, ACT_RELU, act_code, linear_dgrad, linear_fwd, linear_wgrad,
                         register_side_stream)
 from ..ops.loss import cross_entropy_fused, cross_entropy_rows
 from ..ops.norm import layernorm_bwd, layernorm_fwd
@@ -159,9 +159,12 @@ def _layer_forward(x, mask, layer, store, N, S, act, training, drops, attend=Non
             dropout_residual(x2, x, drop_attn, out=x2)
         h2, mu2, rs2 = layernorm_fwd(x2, w(layer.norm2.weight), w(layer.norm2.bias), LN_EPS, cdt)
     F4 = w(fc.up_proj.weight).shape[0]
-    z1 = torch.empty(T, F4, device=x.device, dtype=cdt) if (training and act == ACT_GELU) else None
-    uact = linear_fwd(h2, w(fc.up_proj.weight), bias=w(fc.up_proj.bias), act=act, aux_out=z1,
-                      out_dtype=cdt)
+    # GELU: the up-projection's second output is GELU'(z1) (bf16), so the backward's input
+    # gradient is dz1 = (dz2 @ W2) * g1 -- a plain multiply in its epilogue (ACT_MUL) instead of
+    # the tanh-derivative math there; ReLU's act' comes from its own output (uact > 0)
+    g1 = torch.empty(T, F4, device=x.device, dtype=cdt) if (training and act == ACT_GELU) else None
+    uact = linear_fwd(h2, w(fc.up_proj.weight), bias=w(fc.up_proj.bias), act=act, aux_out=g1,
+                      out_dtype=cdt, aux_deriv=g1 is not None)
     z2 = torch.empty(T, D, device=x.device, dtype=cdt) if training else None
     if drop_ffn is None:
         x3 = linear_fwd(uact, w(fc.down_proj.weight), bias=w(fc.down_proj.bias), act=act,
@@ -172,7 +175,7 @@ def _layer_forward(x, mask, layer, store, N, S, act, training, drops, attend=Non
         dropout_residual(x3, x2, drop_ffn, out=x3)
     saved = None
     if training:
-        saved = (h1, mu1, rs1, qkv, o, lse, x2, h2, mu2, rs2, z1 if z1 is not None else uact, uact, z2)
+        saved = (h1, mu1, rs1, qkv, o, lse, x2, h2, mu2, rs2, g1 if g1 is not None else uact, uact, z2)
     return x3, saved
 
 
@@ -308,9 +311,10 @@ def _layer_backward(dx3, x, mask, saved, layer, store, N, S, H, hd, act, drops, 
     else:
         dz2 = bias_act_bwd(dx, z2, act, g(fc.down_proj.bias), out_dtype=cdt, drop=drop_ffn)
     side.run(lambda: linear_wgrad(dz2, uact, out=g(fc.down_proj.weight)), dz2, uact)
-    # up projection gradient with act' fused (relu' from its output, gelu' from z1)
-    dz1 = linear_dgrad(dz2, w(fc.down_proj.weight), act_bwd=act, aux_in=zup, out_dtype=cdt,
-                       colsum=g(fc.up_proj.bias))
+    # up projection gradient with act' fused (relu' from its output; gelu'(z1) was stored by the
+    # forward epilogue: a multiply)
+    dz1 = linear_dgrad(dz2, w(fc.down_proj.weight), act_bwd=ACT_MUL if act == ACT_GELU else act, aux_in=zup,
+                       out_dtype=cdt, colsum=g(fc.up_proj.bias))
     side.run(lambda: linear_wgrad(dz1, h2, out=g(fc.up_proj.weight)), dz1, h2)
     dh2 = linear_dgrad(dz1, w(fc.up_proj.weight), out_dtype=_dh_dtype(cdt))
     # LN2 backward with the attention output projection's bias/dropout backward fused in:

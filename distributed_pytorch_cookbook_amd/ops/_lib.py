@@ -38,6 +38,7 @@ class GemmArgs(ctypes.Structure):
         ("aux_f32", c_int),  # dpc_gemm_f32: f32 aux_in / aux_out (else bf16)
         ("ws", P), ("ws_bytes", LL),  # split-K workspace (v7 slab split instead of atomics)
         ("nt_store", c_int),  # dispatcher-owned (pass 0): non-temporal epilogue stores
+        ("aux_deriv", c_int),  # aux_out = bf16(act'(v)) instead of the pre-activation (GELU only)
     ]
 
 

@@ -63,10 +63,6 @@ def hipcc() -> str:
 FILE_FLAGS = {"attention.hip": ["-fno-honor-nans", "-fno-slp-vectorize"], "attention_f32.hip": ["-fno-honor-nans"]}
 
 
-def _newest(paths) -> float:
-    return max(p.stat().st_mtime for p in paths)
-
-
 HASH_PATH = LIB_PATH.with_suffix(".so.srchash")
 
 
@@ -108,6 +104,18 @@ def _deps(name: str, seen=None) -> set:
     return seen
 
 
+def _obj_hash(name: str) -> str:
+    """Content hash of one object's inputs: its source, the local headers it includes
+    (transitively), the compiler and the flags it is built with (CFLAGS + its FILE_FLAGS)."""
+    import hashlib
+
+    h = hashlib.sha256((" ".join(CFLAGS + FILE_FLAGS.get(name, [])) + "\0" + hipcc()).encode())
+    for dep in [name] + sorted(_deps(name)):
+        h.update(dep.encode() + b"\0")
+        h.update((CSRC / dep).read_bytes())
+    return h.hexdigest()
+
+
 def build(force: bool = False, jobs: int = 8, verbose: bool = False) -> Path:
     if not force and not needs_build():
         return LIB_PATH
@@ -117,13 +125,23 @@ def build(force: bool = False, jobs: int = 8, verbose: bool = False) -> Path:
     for s in SOURCES:
         src, obj = CSRC / s, BUILD_DIR / (Path(s).stem + ".o")
         objs.append(obj)
-        newest = _newest([src] + [CSRC / h for h in _deps(s)])
-        if force or not obj.exists() or obj.stat().st_mtime < newest:
-            todo.append((src, obj))
+        # rebuilt when the recorded input hash differs (mtimes do not survive snapshot copies, and
+        # a flags-only change leaves every mtime alone)
+        stamp = obj.with_suffix(".o.hash")
+        want = _obj_hash(s)
+        if force or not obj.exists() or not stamp.exists() or stamp.read_text().strip() != want:
+            todo.append((src, obj, stamp, want))
     # the longest compiles first (the GEMM parts), so the pool's tail is short
     todo.sort(key=lambda so: 0 if "gemm7" in so[0].name else 1)
+
+    def one(item):
+        src, obj, stamp, want = item
+        stamp.unlink(missing_ok=True)
+        _compile(src, obj, verbose)
+        stamp.write_text(want + "\n")
+
     with ThreadPoolExecutor(max_workers=max(1, jobs)) as ex:
-        list(ex.map(lambda so: _compile(so[0], so[1], verbose), todo))
+        list(ex.map(one, todo))
     tmp = LIB_PATH.with_suffix(".so.tmp")
     cmd = [hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", *map(str, objs), "-o", str(tmp)]
     if verbose:

@@ -87,23 +87,24 @@ __device__ __forceinline__ int toff(int row, int chunk) {
 // ---- LDS-DMA from inline asm (buffer_load ... lds; M0 = the wave's LDS destination).
 // Issued from asm so that the compiler does not wait for it before every LDS read: the
 // kernels wait with explicit counted s_waitcnt at the ring boundary.
-// M0 is written without saving / restoring it: the compiler uses M0 for nothing in this file's
-// kernels (their gfx950 asm has no M0 access but these; check with
-// `hipcc -S attention.hip && grep m0`), and the save / restore pair was 2 of the ~13 scalar
-// instructions per MFMA the forward issues (rocprofv3 SQ_INSTS_SALU, profiles/r5_attn/pmc_final.txt).
+// M0 is declared clobbered rather than saved / restored around each piece: the save / restore pair
+// was 2 of the ~13 scalar instructions per MFMA the forward issues (rocprofv3 SQ_INSTS_SALU,
+// profiles/r5_attn/pmc_final.txt), and with the clobber the compiler itself keeps any value of its
+// own out of M0 across the DMA (today it uses M0 for nothing in these kernels, so the clobber
+// costs no instruction: the gfx950 asm is identical with and without it).
 __device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t rs, int voff, const void* lds) {
   const unsigned la = (unsigned)(uintptr_t)(lds_void_t)lds;
   asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tbuffer_load_dwordx4 %0, %1, 0 offen lds"
                :
                : "v"(voff), "s"(rs), "s"(la)
-               : "memory");
+               : "memory", "m0");
 }
 __device__ __forceinline__ void dma4(__amdgpu_buffer_rsrc_t rs, int voff, const void* lds) {
   const unsigned la = (unsigned)(uintptr_t)(lds_void_t)lds;
   asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tbuffer_load_dword %0, %1, 0 offen lds"
                :
                : "v"(voff), "s"(rs), "s"(la)
-               : "memory");
+               : "memory", "m0");
 }
 template <int N>
 __device__ __forceinline__ void vm_wait() {

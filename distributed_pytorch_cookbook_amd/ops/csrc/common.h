@@ -156,7 +156,26 @@ __device__ __forceinline__ dpc_f2_t gelu_tanh2(dpc_f2_t x) {
   return x * s;
 }
 
-enum Act { ACT_NONE = 0, ACT_RELU = 1, ACT_GELU = 2 };
+// GELU and its derivative at once (packed f32): the forward epilogue of the FFN up-projection
+// stores bf16 GELU'(z) as its second output, so the input-gradient epilogue of the backward is a
+// plain multiply (ACT_MUL) instead of a second exp / rcp per element.  Same s = sigmoid(2u) for
+// both: GELU = x s, GELU' = s + x s (1 - s) 2 k0 (1 + 3 k1 x^2).
+__device__ __forceinline__ dpc_f2_t gelu_tanh_fg2(dpc_f2_t x, dpc_f2_t& d) {
+  const float k0 = 0.7978845608028654f, k1 = 0.044715f, L2E = 1.4426950408889634f;
+  const dpc_f2_t x2 = x * x;
+  const dpc_f2_t u = x * (x2 * (-2.f * k0 * k1 * L2E) + (-2.f * k0 * L2E));
+  dpc_f2_t s;
+  s.x = __builtin_amdgcn_rcpf(1.f + __builtin_amdgcn_exp2f(u.x));
+  s.y = __builtin_amdgcn_rcpf(1.f + __builtin_amdgcn_exp2f(u.y));
+  const dpc_f2_t xs = x * s;
+  const dpc_f2_t t = x2 * (6.f * k0 * k1) + 2.f * k0;
+  d = (xs - xs * s) * t + s;
+  return xs;
+}
+
+// ACT_MUL (input-gradient epilogues only): the act' operand already holds act'(z) -- written by
+// a forward epilogue with GemmArgs::aux_deriv -- and is multiplied in as is
+enum Act { ACT_NONE = 0, ACT_RELU = 1, ACT_GELU = 2, ACT_MUL = 3 };
 
 __device__ __forceinline__ float act_fwd(float v, int act) {
   if (act == ACT_RELU) return fmaxf(v, 0.f);
@@ -168,6 +187,7 @@ __device__ __forceinline__ float act_fwd(float v, int act) {
 __device__ __forceinline__ float act_grad(float z, int act) {
   if (act == ACT_RELU) return z > 0.f ? 1.f : 0.f;
   if (act == ACT_GELU) return gelu_tanh_grad(z);
+  if (act == ACT_MUL) return z;
   return 1.f;
 }
 

@@ -46,6 +46,10 @@ struct GemmArgs {
   // v9 runs the GPT-2 QKV / up / LM-head forward 947 / 964 / 1031 -> 1151 / 1150 / 1163 TF/s
   // and 8192^3 1327 -> 1448 (bench/g7lab epi set, profiles/r4_gemm/lab_epi_nt.log)
   int nt_store;
+  // forward epilogues with aux_out and act == ACT_GELU: aux_out = bf16(act'(v)) instead of the
+  // pre-activation bf16(v), for an input gradient with act_bwd = ACT_MUL (models/fused.py: the
+  // FFN up-projection)
+  int aux_deriv;
 };
 
 // 16-B epilogue stores, plain or non-temporal (GemmArgs::nt_store; the flag is a kernel
@@ -61,6 +65,11 @@ __device__ __forceinline__ void st16(void* ptr, uint4 v, bool nt) {
 // outputs' scope (bits 2-3).  (f32 outputs -- the residual stream, split-K slabs -- are re-read
 // soon by the next kernel; A/B of a separate scope for them)
 // With bit 6: 0 = plain stores (-1 here), 1 sc0 nt, 2 sc1 nt, 3 sc0 sc1 nt.
+// the default bf16 store policy (DPC_GEMM_NT's default 77: bits 2-3 = 3, sc0 sc1 nt), which the
+// fused epilogues specialised at compile time assume; the dispatcher sends a product to them only
+// when its nt_store carries that policy (g_sp_default)
+constexpr int G_SP_DEFAULT = 3;
+__host__ __device__ __forceinline__ bool g_sp_default(int nt_store) { return ((nt_store >> 2) & 3) == G_SP_DEFAULT; }
 __device__ __forceinline__ int g_f32_pol(int nt_store) {
   if (!(nt_store & 64)) return (nt_store >> 2) & 3;
   const int v = (nt_store >> 4) & 3;

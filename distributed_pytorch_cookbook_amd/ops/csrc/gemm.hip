@@ -191,10 +191,15 @@ __device__ __forceinline__ void epi_tile(const GemmArgs& p, floatx4 (&acc)[FM][4
       }
 #pragma unroll
       for (int q = 0; q < 4; ++q) cs[q] += v[q];
-      if (aux_out) {
+      if (aux_out) {  // the pre-activation, or act'(v) (aux_deriv)
         uint2 w;
-        w.x = pack2bf(v[0], v[1]);
-        w.y = pack2bf(v[2], v[3]);
+        if (p.aux_deriv) {
+          w.x = pack2bf(act_grad(v[0], p.act), act_grad(v[1], p.act));
+          w.y = pack2bf(act_grad(v[2], p.act), act_grad(v[3], p.act));
+        } else {
+          w.x = pack2bf(v[0], v[1]);
+          w.y = pack2bf(v[2], v[3]);
+        }
         st8(aux_out + (long long)m * p.ld_aux_out + n, w, p.nt_store & 1);
       }
       if (p.act == ACT_GELU) {  // packed-f32 math (common.h:gelu_tanh2)
@@ -357,7 +362,7 @@ __global__ __launch_bounds__(NT, 2) void gemm_kernel(GemmArgs p) {
         float v = acc[i][j][r] * alpha + bn;
         if (p.act_bwd) v *= act_grad(bf2f(aux_in[(long long)m * p.ld_aux_in + n]), p.act_bwd);
         csum += v;
-        if (aux_out) aux_out[(long long)m * p.ld_aux_out + n] = f2bf(v);
+        if (aux_out) aux_out[(long long)m * p.ld_aux_out + n] = f2bf(p.aux_deriv ? act_grad(v, p.act) : v);
         v = act_fwd(v, p.act);
         if (p.residual) v += p.residual[(long long)m * p.ldr + n];
         const long long ci = (long long)m * p.ldc + n;
@@ -721,6 +726,9 @@ static int gemm_nt_mode() {
 
 DPC_API int dpc_gemm(const GemmArgs* a, hipStream_t stream) {
   if (a->M <= 0 || a->N <= 0) return 0;
+  // aux_deriv: GELU' as the second output (v9 / v7 / v7-generic / v2 / v3 epilogues; v7d and the
+  // LDS-staged residual epilogue are skipped by gemm7.hip)
+  if (a->aux_deriv && (!a->aux_out || a->act != ACT_GELU)) return -1;
   const int tiles = ((a->M + BM - 1) / BM) * ((a->N + BN - 1) / BN);
   dim3 grid(tiles), block(NT);
   // v2 requirements: a k-major operand must hold exactly K (% 64) columns (its k-tail is not

@@ -245,18 +245,20 @@ DPC_API int dpc_gemm7(const GemmArgs* a, int persistent, int sched, int splits, 
     static int env = -1;
     if (env < 0) env = getenv("DPC_G7_ACTLDS") ? atoi(getenv("DPC_G7_ACTLDS")) : 1;
     const int on = g7_act_lds >= 0 ? g7_act_lds : env;
+    // (ACT_MUL: EPI 10, compiled for the default store policy only -- another policy takes EPI 3)
     act_lds = on && !v8 && s == 1 && a->act_bwd && a->aux_in && !a->out_f32 && a->ld_aux_in % 8 == 0 &&
+              (a->act_bwd != ACT_MUL || g_sp_default(a->nt_store)) &&
               ((uintptr_t)a->aux_in % 16) == 0 && a->ld_aux_in <= (1 << 20);
   }
   // v7d: sched 5 (impl 24) takes the GELU / GELU' fused epilogues of full-depth products
   // (nk >= 18: at least 16 slices to spread a tile's deferred chunks over)
   if (sched == 5 && !v8 && s == 1 && pl.nk >= 18) {
     auto a16 = [](const void* q) { return ((uintptr_t)q % 16) == 0; };
-    const bool dfwd = a->act == ACT_GELU && a->aux_out && !a->residual && !a->accumulate && !a->out_f32 &&
+    const bool dfwd = a->act == ACT_GELU && a->aux_out && !a->aux_deriv && !a->residual && !a->accumulate && !a->out_f32 &&
                       !a->act_bwd && !a->colsum && a->ld_aux_out % 8 == 0 && a16(a->aux_out);
     const bool dbwd = a->act_bwd == ACT_GELU && a->aux_in && !a->out_f32 && !a->accumulate && !a->bias && !a->act &&
                       !a->aux_out && !a->residual && a->ld_aux_in % 8 == 0 && a16(a->aux_in);
-    const bool ddown = a->act == ACT_GELU && a->aux_out && a->residual && !a->accumulate && a->out_f32 &&
+    const bool ddown = a->act == ACT_GELU && a->aux_out && !a->aux_deriv && a->residual && !a->accumulate && a->out_f32 &&
                        !a->act_bwd && !a->colsum && a->ld_aux_out % 8 == 0 && a16(a->aux_out) && a->ldr % 4 == 0 &&
                        a16(a->residual);  // (residual may alias C: a chunk is read, then written, by one lane)
     if (dfwd && g7d_launch<5>(a, pl, stream, ab, bb)) return (int)hipGetLastError();
@@ -386,7 +388,7 @@ DPC_API int dpc_gemm7(const GemmArgs* a, int persistent, int sched, int splits, 
     // (g7_epilogue_res_lds; DPC_G7_RESLDS=0 or dpc_gemm7_set_res_lds(0) keeps the per-lane reads)
     static int res_env = -1;
     if (res_env < 0) res_env = getenv("DPC_G7_RESLDS") ? atoi(getenv("DPC_G7_RESLDS")) : 1;
-    const bool res_lds = (g7_res_lds >= 0 ? g7_res_lds : res_env) && s == 1 && a->residual && a->out_f32 &&
+    const bool res_lds = (g7_res_lds >= 0 ? g7_res_lds : res_env) && s == 1 && a->residual && a->out_f32 && !a->aux_deriv &&
                          !a->accumulate && a->ldr % 4 == 0 && ((uintptr_t)a->residual % 16) == 0 &&
                          a->ldr <= (1 << 20);
     if (res_lds) g7_launch_s<9>(a, pl, stream, ab, bb);
@@ -399,7 +401,9 @@ DPC_API int dpc_gemm7(const GemmArgs* a, int persistent, int sched, int splits, 
                        a->N % 4 == 0 && ((uintptr_t)a->colsum % 16) == 0;
     GemmArgs q = *a;
     if (!cs_ws) q.ws = nullptr;
-    g7_launch_s<8>(&q, pl, stream, ab, bb);
+    // (EPI 10: ACT_MUL with the default store policy compiled in)
+    if (a->act_bwd == ACT_MUL) g7_launch_s<10>(&q, pl, stream, ab, bb);
+    else g7_launch_s<8>(&q, pl, stream, ab, bb);
     if (cs_ws)
       hipLaunchKernelGGL(g7_colsum_reduce, dim3((unsigned)((a->N / 4 + 255) / 256), (unsigned)((rows + 15) / 16)),
                          dim3(256), 0, stream, a->colsum, static_cast<const float*>(a->ws), (int)rows, a->N);

@@ -172,7 +172,13 @@ __device__ __forceinline__ float g7_ror8(float v) { return __uint_as_float(g7_ro
 // round-5 asm of the v9 forward epilogue showed every element group wrapped in ~10 scalar
 // branches (the runtime activation switch, the m / n guards of each store): the bias-only form
 // ran 57 us over the plain product of the GPT-2 up-projection (bench/epi_decomp.py).
-template <int MODE, int NJ, bool PK = false, bool NOLD = false, int FA = -1, bool FULL = false>
+// AD (MODE 1, FA == ACT_GELU only): aux_out takes GELU'(v) (GemmArgs::aux_deriv known at compile
+// time); the generic copy (FA < 0) reads p.aux_deriv instead
+// SP (MODE 1): the bf16 stores' cache policy at compile time (st16p pol; -1 = GemmArgs::nt_store at
+// run time).  The run-time policy is a 4-way switch in front of EVERY store of the unrolled
+// epilogue -- ~2 scalar branches per 16-B store in the round-6 asm of the v9 forward epilogue.
+template <int MODE, int NJ, bool PK = false, bool NOLD = false, int FA = -1, bool FULL = false, bool AD = false,
+          int SP = -1>
 __device__ __forceinline__ void g7_epilogue(const GemmArgs& p, floatx4 (&acc)[8][NJ], int mw, int nw, int lane,
                                             int dbg = 0, const float* lbias = nullptr) {
   static_assert(!FULL || MODE == 1, "full-tile fast path: forward epilogues");
@@ -326,14 +332,26 @@ __device__ __forceinline__ void g7_epilogue(const GemmArgs& p, floatx4 (&acc)[8]
         for (int r = 0; r < 4; ++r) w[r] = acc[i][jj][r] * alpha;
         if constexpr (FWD) {
           w[0] += bias4[jj].x; w[1] += bias4[jj].y; w[2] += bias4[jj].z; w[3] += bias4[jj].w;
-          pa[h][0] = pack2bf(w[0], w[1]);  // the pre-activation (aux_out)
-          pa[h][1] = pack2bf(w[2], w[3]);
-          if (PK && fact == ACT_GELU) {
-            const dpc_f2_t g01 = gelu_tanh2(dpc_f2_t{w[0], w[1]}), g23 = gelu_tanh2(dpc_f2_t{w[2], w[3]});
+          if constexpr (AD) {  // GELU + GELU' (aux_out) from one sigmoid
+            dpc_f2_t d01, d23;
+            const dpc_f2_t g01 = gelu_tanh_fg2(dpc_f2_t{w[0], w[1]}, d01), g23 = gelu_tanh_fg2(dpc_f2_t{w[2], w[3]}, d23);
+            pa[h][0] = pack2bf(d01.x, d01.y);
+            pa[h][1] = pack2bf(d23.x, d23.y);
             w[0] = g01.x; w[1] = g01.y; w[2] = g23.x; w[3] = g23.y;
-          } else if (FA != 0) {
+          } else {
+            pa[h][0] = pack2bf(w[0], w[1]);  // the pre-activation (aux_out)
+            pa[h][1] = pack2bf(w[2], w[3]);
+            if (FA < 0 && p.aux_deriv) {  // (generic copy: act'(v) instead)
+              pa[h][0] = pack2bf(act_grad(w[0], fact), act_grad(w[1], fact));
+              pa[h][1] = pack2bf(act_grad(w[2], fact), act_grad(w[3], fact));
+            }
+            if (PK && fact == ACT_GELU) {
+              const dpc_f2_t g01 = gelu_tanh2(dpc_f2_t{w[0], w[1]}), g23 = gelu_tanh2(dpc_f2_t{w[2], w[3]});
+              w[0] = g01.x; w[1] = g01.y; w[2] = g23.x; w[3] = g23.y;
+            } else if (FA != 0) {
 #pragma unroll
-            for (int r = 0; r < 4; ++r) w[r] = act_fwd(w[r], fact);
+              for (int r = 0; r < 4; ++r) w[r] = act_fwd(w[r], fact);
+            }
           }
           if (fsrc) {
             w[0] += __uint_as_float(cur.x); w[1] += __uint_as_float(cur.y);
@@ -375,15 +393,15 @@ __device__ __forceinline__ void g7_epilogue(const GemmArgs& p, floatx4 (&acc)[8]
         const auto s0 = __builtin_amdgcn_permlane16_swap(pa[0][0], pa[1][0], false, false);
         const auto s1 = __builtin_amdgcn_permlane16_swap(pa[0][1], pa[1][1], false, false);
         if (ok8)
-          st16p(aux_out + (long long)m * p.ld_aux_out + n8, make_uint4(s0[0], s1[0], s0[1], s1[1]), p.nt_store & 1,
-                (p.nt_store >> 2) & 3);
+          st16p(aux_out + (long long)m * p.ld_aux_out + n8, make_uint4(s0[0], s1[0], s0[1], s1[1]),
+                SP >= 0 ? false : (p.nt_store & 1), SP >= 0 ? SP : (p.nt_store >> 2) & 3);
       }
       if (FULL || !p.out_f32) {
         const auto s0 = __builtin_amdgcn_permlane16_swap(pc[0][0], pc[1][0], false, false);
         const auto s1 = __builtin_amdgcn_permlane16_swap(pc[0][1], pc[1][1], false, false);
         if (ok8)
           st16p(static_cast<bf16_t*>(p.C) + (long long)m * p.ldc + n8, make_uint4(s0[0], s1[0], s0[1], s1[1]),
-                p.nt_store & 1, (p.nt_store >> 2) & 3);
+                SP >= 0 ? false : (p.nt_store & 1), SP >= 0 ? SP : (p.nt_store >> 2) & 3);
       }
     });
   });
@@ -430,7 +448,10 @@ __device__ __forceinline__ void g7_epilogue(const GemmArgs& p, floatx4 (&acc)[8]
 // waits for everything but the next DMA).
 // (round 5: act' by a select, the next column pair's operand read ahead, bounded buffer stores --
 // no branch inside the element loop; ONE copy per kernel, see the call site)
-template <int NJ>
+// MUL: the operand holds act'(z) already (act_bwd == ACT_MUL, written by the forward epilogue
+// with aux_deriv): a plain multiply, no GELU' math (EPI 10, which also fixes the bf16 store policy
+// at compile time -- SP, as in g7_epilogue -- instead of a run-time switch per store)
+template <int NJ, bool MUL = false, int SP = -1>
 __device__ __forceinline__ void g7_epilogue_act_lds(const GemmArgs& p, floatx4 (&acc)[8][NJ], int m0, int n0,
                                                     int wid, int lane_in, bf16_t* buf0, bf16_t* buf1) {
   static_assert(NJ == 8, "v7 tiles");
@@ -473,7 +494,7 @@ __device__ __forceinline__ void g7_epilogue_act_lds(const GemmArgs& p, floatx4 (
   const __amdgpu_buffer_rsrc_t rc =
       __builtin_amdgcn_make_buffer_rsrc((void*)(static_cast<bf16_t*>(p.C) + corg), 0, cnrec, 0x00020000);
   const bool gelu = fab == ACT_GELU;  // (else ReLU: act_lds is taken only with an act')
-  const int spol = (p.nt_store >> 2) & 3;
+  const int spol = SP >= 0 ? SP : (p.nt_store >> 2) & 3;
   auto proc = [&](auto Q, const bf16_t* buf) G7_AI {
     constexpr int q = decltype(Q)::value;
     sfor<2>([&](auto II) G7_AI {
@@ -508,11 +529,15 @@ __device__ __forceinline__ void g7_epilogue_act_lds(const GemmArgs& p, floatx4 (
           const float z2 = __uint_as_float(z.y << 16), z3 = __uint_as_float(z.y & 0xffff0000u);
           // GELU' in packed f32 (half the VALU issue of the scalar form), or ReLU' -- a select,
           // not a branch
-          const dpc_f2_t g01 = gelu_tanh_grad2(dpc_f2_t{z0, z1}), g23 = gelu_tanh_grad2(dpc_f2_t{z2, z3});
-          w[0] *= gelu ? g01.x : (z0 > 0.f ? 1.f : 0.f);
-          w[1] *= gelu ? g01.y : (z1 > 0.f ? 1.f : 0.f);
-          w[2] *= gelu ? g23.x : (z2 > 0.f ? 1.f : 0.f);
-          w[3] *= gelu ? g23.y : (z3 > 0.f ? 1.f : 0.f);
+          if constexpr (MUL) {
+            w[0] *= z0; w[1] *= z1; w[2] *= z2; w[3] *= z3;
+          } else {
+            const dpc_f2_t g01 = gelu_tanh_grad2(dpc_f2_t{z0, z1}), g23 = gelu_tanh_grad2(dpc_f2_t{z2, z3});
+            w[0] *= gelu ? g01.x : (z0 > 0.f ? 1.f : 0.f);
+            w[1] *= gelu ? g01.y : (z1 > 0.f ? 1.f : 0.f);
+            w[2] *= gelu ? g23.x : (z2 > 0.f ? 1.f : 0.f);
+            w[3] *= gelu ? g23.y : (z3 > 0.f ? 1.f : 0.f);
+          }
           // (rows past M: an M-major A reads the next k-row's data into acc there, and the act'
           // operand's LDS rows were never written by the DMA; columns past N may read the next
           // row's data: both are kept out of the column sums by a select)
@@ -780,7 +805,8 @@ __device__ __forceinline__ void g7_epilogue_atomic(const GemmArgs& p, floatx4 (&
 // EPI: 0 = plain products (bf16 / f32 C), 1 = forward fused epilogues, 2 = split-K f32 atomics,
 // 3 = input-gradient fused epilogues (act', column sums), 4 = split-K partial tiles stored to
 // the workspace slab of their k-range (plain 16-B stores; g7_splitk_reduce sums the slabs),
-// 8 = EPI 3 with an act' operand staged through LDS (v7 only; g7_epilogue_act_lds), 9 = EPI 1
+// 8 = EPI 3 with an act' operand staged through LDS (v7 only; g7_epilogue_act_lds; 10 = the same
+// with act' precomputed, ACT_MUL), 9 = EPI 1
 // with an f32 residual and output, the residual staged through LDS (v7 only; g7_epilogue_res_lds).
 // WN: output columns per wave.  128 = v7 (a 256 x 256 tile, one workgroup per CU); 64 = v8 (a
 // 256 x 128 tile, 128 accumulator registers, TWO workgroups per CU, each with a 3-slot ring:
@@ -1069,11 +1095,11 @@ __global__ __launch_bounds__(256, WN == 128 ? 1 : 2) void gemm7_kernel(GemmArgs 
       // down-projection 369 -> 568 us, act' input gradient 535 -> 749 us, round 5)
       g7_epilogue_res_lds<NJ>(p, acc, m0, n0, wid, lane, smem + ((rd_slot + 3) % NS) * SLOT,
                               smem + ((rd_slot + 4) % NS) * SLOT);
-    } else if constexpr (EPI == 8) {
+    } else if constexpr (EPI == 8 || EPI == 10) {
       // (its own instantiation: beside g7_epilogue<3> in one kernel the register allocator
-      // spilled ~120 registers, alone it spills 2)
+      // spilled ~120 registers, alone it spills 2; EPI 10 = the ACT_MUL form, another kernel)
       static_assert(WN == 128, "v7 only");
-      g7_epilogue_act_lds<NJ>(p, acc, m0, n0, wid, lane, smem + ((rd_slot + 3) % NS) * SLOT,
+      g7_epilogue_act_lds<NJ, EPI == 10, EPI == 10 ? G_SP_DEFAULT : -1>(p, acc, m0, n0, wid, lane, smem + ((rd_slot + 3) % NS) * SLOT,
                               smem + ((rd_slot + 4) % NS) * SLOT);
     } else {
       // packed-f32 GELU: v8 with a k-major A, and the v7 forward epilogues (measured: the act'

@@ -358,10 +358,14 @@ __global__ __launch_bounds__(256, 1) void gemm9_kernel(GemmArgs p, unsigned long
       // trading a chunk so one store writes 8 rows x 128 B -- was SLOWER here than these 16-row
       // x 64-B stores, 448.6 vs 405.5 us on the GPT-2 up-projection, bench/epi_decomp.py)
       const float* lb = sbias + ((u & 1) * 4 + wid) * 256 + bc;
-      if (m0 + 256 <= p.M && n0 + 256 <= p.N && !p.out_f32) {  // full tile, bf16 output: check-free
-        if (p.act == ACT_GELU) g7_epilogue<1, NJ, true, true, ACT_GELU, true>(p, acc, m0 + ar, n0 + bc, elane, 0, lb);
-        else if (p.act == ACT_RELU) g7_epilogue<1, NJ, true, true, ACT_RELU, true>(p, acc, m0 + ar, n0 + bc, elane, 0, lb);
-        else g7_epilogue<1, NJ, true, true, 0, true>(p, acc, m0 + ar, n0 + bc, elane, 0, lb);
+      // full tile, bf16 output, the default store policy: check-free, branch-free stores
+      constexpr int SP = G_SP_DEFAULT;
+      if (m0 + 256 <= p.M && n0 + 256 <= p.N && !p.out_f32 && g_sp_default(p.nt_store)) {
+        if (p.act == ACT_GELU && p.aux_deriv)  // (the FFN up-projection of training: GELU' as aux_out)
+          g7_epilogue<1, NJ, true, true, ACT_GELU, true, true, SP>(p, acc, m0 + ar, n0 + bc, elane, 0, lb);
+        else if (p.act == ACT_GELU) g7_epilogue<1, NJ, true, true, ACT_GELU, true, false, SP>(p, acc, m0 + ar, n0 + bc, elane, 0, lb);
+        else if (p.act == ACT_RELU) g7_epilogue<1, NJ, true, true, ACT_RELU, true, false, SP>(p, acc, m0 + ar, n0 + bc, elane, 0, lb);
+        else g7_epilogue<1, NJ, true, true, 0, true, false, SP>(p, acc, m0 + ar, n0 + bc, elane, 0, lb);
       } else {
         g7_epilogue<1, NJ, true, true>(p, acc, m0 + ar, n0 + bc, elane, 0, lb);
       }

@@ -154,8 +154,9 @@ __global__ __launch_bounds__(256, 2) void gemm_f32_kernel(GemmArgs p) {
         cs += v;
         if (p.aux_out) {
           const long long ai = (long long)m * p.ld_aux_out + n;
-          if (aux_f32) static_cast<float*>(p.aux_out)[ai] = v;
-          else static_cast<bf16_t*>(p.aux_out)[ai] = f2bf(v);
+          const float av = p.aux_deriv ? act_grad(v, p.act) : v;  // (act'(v): aux_deriv)
+          if (aux_f32) static_cast<float*>(p.aux_out)[ai] = av;
+          else static_cast<bf16_t*>(p.aux_out)[ai] = f2bf(av);
         }
         v = act_fwd(v, p.act);
         if (p.residual) v += p.residual[(long long)m * p.ldr + n];

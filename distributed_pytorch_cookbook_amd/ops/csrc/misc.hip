@@ -238,7 +238,9 @@ __global__ __launch_bounds__(CE_NT) void ce_kernel2(CEArgs p) {
         for (int j = 0; j < 8; ++j) f[j] = j < tail ? f[j] : -INFINITY;
       }
       const float cm = fmaxf(fmaxf(fmaxf(f[0], f[1]), fmaxf(f[2], f[3])), fmaxf(fmaxf(f[4], f[5]), fmaxf(f[6], f[7])));
-      const float cml = cm * L2E;
+      // (a chunk of eight -inf logits: cm = -inf would make every exponent -inf + inf = NaN; with
+      // 0 they are exp2(-inf) = 0 and the chunk adds nothing -- ms_combine skips an all -inf max)
+      const float cml = cm == -INFINITY ? 0.f : cm * L2E;
       float cs = 0.f;
 #pragma unroll
       for (int j = 0; j < 8; ++j) cs += __builtin_amdgcn_exp2f(fmaf(f[j], L2E, -cml));

@@ -9,8 +9,9 @@ copies (reference: ``/root/reference/models/gpt.py:29-30,60-64,219`` -- every Li
 Epilogue order (identical in the HIP kernel and the torch reference below)::
 
     v = acc * alpha (* alpha_t) + bias[n]
-    v = v * act'(aux_in)            if act_bwd
-    aux_out = bf16(v)               if aux_out (pre-activation saved for backward)
+    v = v * act'(aux_in)            if act_bwd (ACT_MUL: v * aux_in -- act' precomputed)
+    aux_out = bf16(v)               if aux_out (pre-activation saved for backward;
+                                    bf16(act'(v)) with aux_deriv, for a later ACT_MUL)
     v = act(v)                      if act
     v = v + residual                if residual
     C = C + v                       if accumulate (f32 C only)
@@ -32,6 +33,9 @@ import torch.nn.functional as F
 from . import _lib
 
 ACT_NONE, ACT_RELU, ACT_GELU = 0, 1, 2
+# input-gradient epilogues only: the act' operand holds act'(z) already (written by a forward
+# epilogue with aux_deriv=True), multiplied in as is (csrc/common.h:Act)
+ACT_MUL = 3
 ACTS = {None: ACT_NONE, "none": ACT_NONE, "relu": ACT_RELU, "gelu": ACT_GELU}
 
 
@@ -58,6 +62,8 @@ def act_grad_ref(z: torch.Tensor, act: int) -> torch.Tensor:
         u = k0 * (z + k1 * z * z * z)
         t = torch.tanh(u)
         return 0.5 * (1 + t) + 0.5 * z * (1 - t * t) * k0 * (1 + 3 * k1 * z * z)
+    if act == ACT_MUL:
+        return z
     return torch.ones_like(z)
 
 
@@ -184,6 +190,8 @@ def _sig(M, N, K, a_kmaj, b_kmaj, out_f32, bias, act, act_bwd, aux_out, residual
     flags = "".join(c for c, on in (("b", bias is not None), ("x", aux_out is not None),
                                      ("r", residual is not None), ("c", colsum is not None),
                                      ("a", accumulate)) if on)
+    # (ACT_MUL keys as GELU': same product and epilogue traffic, one table entry for both)
+    act_bwd = ACT_GELU if act_bwd == ACT_MUL else act_bwd
     return (f"{M}x{N}x{K}:{'k' if a_kmaj else 'm'}{'k' if b_kmaj else 'm'}:"
             f"{'f' if out_f32 else 'h'}:{act}{act_bwd}:{flags}")
 
@@ -257,8 +265,11 @@ def gemm(
     alpha_t: torch.Tensor | None = None,
     accumulate: bool = False,
     colsum: torch.Tensor | None = None,
+    aux_deriv: bool = False,
 ) -> torch.Tensor:
     act, act_bwd = act_code(act), act_code(act_bwd)
+    if aux_deriv and (aux_out is None or act != ACT_GELU):
+        raise ValueError("gemm: aux_deriv needs aux_out and act='gelu'")
     Ma, Ka = (a.shape[0], a.shape[1]) if a_kmaj else (a.shape[1], a.shape[0])
     Nb, Kb = (b.shape[0], b.shape[1]) if b_kmaj else (b.shape[1], b.shape[0])
     # logical sizes; an operand may be stored smaller than them (rows / k-rows beyond its
@@ -308,6 +319,7 @@ def gemm(
             a_kmaj=int(a_kmaj), b_kmaj=int(b_kmaj),
             a_r=a.shape[0], a_c=a.shape[1], b_r=b.shape[0], b_c=b.shape[1],
             ws=_lib.ptr(ws), ws_bytes=0 if ws is None else ws.numel() * 4,
+            aux_deriv=int(aux_deriv),
         )
         if (_table or _TUNE) and _lib.forced_gemm_impl < 0:
             key = _sig(M, N, K, a_kmaj, b_kmaj, out.dtype == torch.float32, bias, act, act_bwd,
@@ -324,13 +336,13 @@ def gemm(
         return out
     if a.is_cuda and a.dtype == torch.float32 and b.dtype == torch.float32 and out.dtype == torch.float32:
         return _gemm_f32(a, b, a_kmaj, b_kmaj, out, M, N, K, bias, act, act_bwd, aux_in, aux_out,
-                         residual, alpha, alpha_t, accumulate, colsum)
+                         residual, alpha, alpha_t, accumulate, colsum, aux_deriv)
     return _gemm_ref(a, b, a_kmaj, b_kmaj, out, bias, act, act_bwd, aux_in, aux_out, residual,
-                     alpha, alpha_t, accumulate, colsum)
+                     alpha, alpha_t, accumulate, colsum, aux_deriv)
 
 
 def _gemm_f32(a, b, a_kmaj, b_kmaj, out, M, N, K, bias, act, act_bwd, aux_in, aux_out, residual,
-              alpha, alpha_t, accumulate, colsum):
+              alpha, alpha_t, accumulate, colsum, aux_deriv=False):
     """f32 operands (the --disable_amp path): ``dpc_gemm_f32`` on the f32 matrix cores
     (csrc/gemm_f32.hip), same fused epilogue as the bf16 kernels."""
     for t, nm in ((a, "A"), (b, "B"), (out, "out")):
@@ -355,6 +367,7 @@ def _gemm_f32(a, b, a_kmaj, b_kmaj, out, M, N, K, bias, act, act_bwd, aux_in, au
         M=M, N=N, K=K, alpha=float(alpha), act=act, act_bwd=act_bwd, out_f32=1,
         accumulate=int(accumulate), a_kmaj=int(a_kmaj), b_kmaj=int(b_kmaj),
         a_r=a.shape[0], a_c=a.shape[1], b_r=b.shape[0], b_c=b.shape[1], aux_f32=int(aux_f32),
+        aux_deriv=int(aux_deriv),
     )
     _lib.call("dpc_gemm_f32", args, a.device)
     return out
@@ -369,7 +382,7 @@ def _pad_to(x: torch.Tensor, rows: int, cols: int) -> torch.Tensor:
 
 
 def _gemm_ref(a, b, a_kmaj, b_kmaj, out, bias, act, act_bwd, aux_in, aux_out, residual,
-              alpha, alpha_t, accumulate, colsum=None):
+              alpha, alpha_t, accumulate, colsum=None, aux_deriv=False):
     am = (a if a_kmaj else a.t()).float()
     bm = (b if b_kmaj else b.t()).float()
     M, N = out.shape
@@ -385,7 +398,7 @@ def _gemm_ref(a, b, a_kmaj, b_kmaj, out, bias, act, act_bwd, aux_in, aux_out, re
     if colsum is not None:
         colsum.add_(v.sum(0))
     if aux_out is not None:
-        aux_out.copy_(v)
+        aux_out.copy_(act_grad_ref(v, act) if aux_deriv else v)
     v = act_fwd_ref(v, act)
     if residual is not None:
         v = v + residual.float()
@@ -398,13 +411,14 @@ def _gemm_ref(a, b, a_kmaj, b_kmaj, out, bias, act, act_bwd, aux_in, aux_out, re
 
 # ---------------------------------------------------------------- Linear-shaped helpers
 def linear_fwd(x, w, *, bias=None, act=None, residual=None, aux_out=None, out=None,
-               out_dtype=torch.bfloat16):
-    """y = act(x @ w^T + bias) (+ residual); x [M, K], w [N, K] (nn.Linear layout)."""
+               out_dtype=torch.bfloat16, aux_deriv=False):
+    """y = act(x @ w^T + bias) (+ residual); x [M, K], w [N, K] (nn.Linear layout).
+    ``aux_out`` receives the pre-activation, or act'(pre-activation) with ``aux_deriv``."""
     if (x.is_cuda and x.shape[0] <= _GEMV_ROWS and aux_out is None and x.dtype == torch.bfloat16
             and w.dtype == torch.bfloat16):
         return _linear_fwd_few_rows(x, w, bias, act_code(act), residual, out, out_dtype)
     return gemm(x, w, a_kmaj=True, b_kmaj=True, bias=bias, act=act, residual=residual,
-                aux_out=aux_out, out=out, out_dtype=out_dtype)
+                aux_out=aux_out, out=out, out_dtype=out_dtype, aux_deriv=aux_deriv)
 
 
 # decode-shaped products (a handful of rows): the MFMA tile kernels would launch N / 256

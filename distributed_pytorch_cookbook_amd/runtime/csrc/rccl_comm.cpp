@@ -233,6 +233,9 @@ struct Watchdog {
   std::deque<Pending> q;
   std::vector<hipEvent_t> pool;  // completed events, re-recorded instead of re-created
   std::vector<ncclComm_t> comms;
+  // set (under mu) by wd_fire when it aborts its copy of `comms`: a destroy that starts after it
+  // parks instead of freeing a communicator that copy may still be aborting (wd_destroy_locked)
+  bool aborting = false;
   std::thread th;
   std::atomic<bool> running{false};
   std::atomic<int> paused{0};
@@ -260,6 +263,7 @@ Watchdog& wd = *new Watchdog;
   {
     std::lock_guard<std::mutex> lk(wd.mu);
     comms = wd.comms;
+    wd.aborting = true;  // (no later destroy touches a communicator of this copy)
   }  // (`life`, when taken, stays held: this thread ends the process)
   if (!owned) {
     fprintf(stderr, "[dpc watchdog] rank %d: a communicator destroy is stuck; aborting the other %zu\n", wd.rank,
@@ -388,6 +392,15 @@ DPC_API void dpc_wd_unregister(void* comm) {
 
 int wd_destroy_locked(void* comm) {
   std::lock_guard<std::timed_mutex> life(wd.life);
+  bool aborting;
+  {
+    std::lock_guard<std::mutex> lk(wd.mu);
+    aborting = wd.aborting;
+  }
+  // the watchdog took its copy while an earlier destroy was stuck (it could not take `life`) and
+  // may be aborting this very communicator now: never destroy it concurrently -- park until the
+  // watchdog's _exit (at most ~10 s away)
+  while (aborting) std::this_thread::sleep_for(std::chrono::seconds(1));
   dpc_wd_unregister(comm);
   return check(g.comm_destroy(static_cast<ncclComm_t>(comm)), "ncclCommDestroy");
 }

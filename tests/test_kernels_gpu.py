@@ -193,16 +193,18 @@ def test_gemm_v9_forward_epilogue(M, N, K, with_bias, act, out_f32):
     assert _lib.is_loaded()
 
 
+@pytest.mark.parametrize("act_bwd", [2, 3])
 @pytest.mark.parametrize("act_lds", [0, 1])
 @pytest.mark.parametrize("use_ws", [False, True])
 @pytest.mark.parametrize("a_kmaj,b_kmaj", [(True, False), (True, True), (False, False)])
 @pytest.mark.parametrize("M,N,K", [(1023, 768, 768), (4096, 4352, 256), (300, 264, 96), (2048, 3072, 512)])
-def test_gemm_v7_act_grad_epilogue_paths(monkeypatch, act_lds, use_ws, a_kmaj, b_kmaj, M, N, K):
+def test_gemm_v7_act_grad_epilogue_paths(monkeypatch, act_bwd, act_lds, use_ws, a_kmaj, b_kmaj, M, N, K):
     """The v7 input-gradient epilogue (act' of a bf16 operand + bias-gradient column sums) on
     both paths: the act' operand staged through LDS in quarters (gemm7_kern.h
-    g7_epilogue_act_lds, EPI 8; column sums as per-tile partials in the workspace + a reduction,
-    or f32 atomics without one) and the per-lane operand reads (DPC_G7_ACTLDS=0) -- ragged edge
-    tiles, and more tiles than CUs (4096 x 4352: a workgroup streams two through its ring)."""
+    g7_epilogue_act_lds, EPI 8; EPI 10 for ACT_MUL = 3, the operand already act'(z); column sums
+    as per-tile partials in the workspace + a reduction, or f32 atomics without one) and the
+    per-lane operand reads (DPC_G7_ACTLDS=0) -- ragged edge tiles, and more tiles than CUs
+    (4096 x 4352: a workgroup streams two through its ring)."""
     from distributed_pytorch_cookbook_amd.ops import gemm as G
 
     if not use_ws:
@@ -217,19 +219,55 @@ def test_gemm_v7_act_grad_epilogue_paths(monkeypatch, act_lds, use_ws, a_kmaj, b
     lib.dpc_gemm7_set_act_lds(act_lds)
     try:
         cs = torch.full((N,), 0.25, device=dev)
-        od = gemm(A, B, a_kmaj=a_kmaj, b_kmaj=b_kmaj, act_bwd=2, aux_in=z, colsum=cs)
-        of = gemm(A, B, a_kmaj=a_kmaj, b_kmaj=b_kmaj, act_bwd=2, aux_in=z, out_dtype=torch.float32, alpha=0.5)
+        od = gemm(A, B, a_kmaj=a_kmaj, b_kmaj=b_kmaj, act_bwd=act_bwd, aux_in=z, colsum=cs)
+        ran = _lib.gemm_last_kernel()
+        of = gemm(A, B, a_kmaj=a_kmaj, b_kmaj=b_kmaj, act_bwd=act_bwd, aux_in=z, out_dtype=torch.float32, alpha=0.5)
     finally:
         _lib.set_gemm_impl(-1)
         lib.dpc_gemm7_set_act_lds(-1)
+    if act_lds and a_kmaj:  # the LDS-staged epilogue itself ran (EPI 8, or EPI 10 for ACT_MUL)
+        assert ran == (710 if act_bwd == 3 else 708), ran
     od_r = torch.empty(M, N, device=dev)
     cs_r = torch.full((N,), 0.25, device=dev)
-    _gemm_ref(a, b, True, True, od_r, None, 0, 2, z, None, None, 1.0, None, False, cs_r)
+    _gemm_ref(a, b, True, True, od_r, None, 0, act_bwd, z, None, None, 1.0, None, False, cs_r)
     assert rel_err(od, od_r) < 1e-2
     assert rel_err(cs, cs_r) < 2e-3
     of_r = torch.empty(M, N, device=dev)
-    _gemm_ref(a, b, True, True, of_r, None, 0, 2, z, None, None, 0.5, None, False)
+    _gemm_ref(a, b, True, True, of_r, None, 0, act_bwd, z, None, None, 0.5, None, False)
     assert rel_err(of, of_r) < 2e-3
+
+
+@pytest.mark.parametrize("impl", [26, 25, 21, 10, 2])
+@pytest.mark.parametrize("M,N,K", [(1023, 768, 768), (4096, 4352, 256), (300, 264, 192), (2048, 3072, 768)])
+def test_gemm_aux_deriv_then_mul(impl, M, N, K):
+    """The FFN pair of models/fused.py: the up-projection forward stores GELU'(z) as its second
+    output (aux_deriv: v9 full-tile and edge copies, v7 / v8 generic MODE 1, v3 / v2 epi_tile) and
+    the input gradient multiplies it in (ACT_MUL); against f32 PyTorch of the z-form chain
+    (gelu'(z) evaluated from the f32 pre-activation)."""
+    torch.manual_seed(7)
+    a = torch.randn(M, K, device=dev).bfloat16() * 0.5
+    b = torch.randn(N, K, device=dev).bfloat16() * 0.1
+    bias = torch.randn(N, device=dev)
+    A, B = _store(a, True), _store(b, True)
+    g1 = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+    dy = torch.randn(M, K, device=dev).bfloat16()
+    Bn = _store(b, False)  # dz1 = (dy @ W) * g1: W stored [N, K] -> mn-major operand [K, N]
+    _lib.set_gemm_impl(impl)
+    try:
+        u = gemm(A, B, bias=bias, act=2, aux_out=g1, aux_deriv=True)
+        cs = torch.zeros(N, device=dev)
+        dz = gemm(dy, Bn, a_kmaj=True, b_kmaj=False, act_bwd=3, aux_in=g1, colsum=cs)
+    finally:
+        _lib.set_gemm_impl(-1)
+    z = a.float() @ b.float().t() + bias
+    from distributed_pytorch_cookbook_amd.ops.gemm import act_grad_ref
+
+    gd = act_grad_ref(z, 2)
+    assert rel_err(g1, gd) < 1e-2
+    assert rel_err(u, torch.nn.functional.gelu(z, approximate="tanh")) < 1e-2
+    dz_r = (dy.float() @ b.float().t()) * gd
+    assert rel_err(dz, dz_r) < 1.5e-2
+    assert rel_err(cs, dz_r.sum(0)) < 1e-2
 
 
 @pytest.mark.parametrize("res_lds", [0, 1])
@@ -622,6 +660,29 @@ def test_cross_entropy(V, mode):
     valid = tg != -100
     rc = (lf.argmax(-1) == tg)[valid].sum().item()
     assert abs(correct.item() - rc) <= 1
+
+
+@pytest.mark.parametrize("V", [50257, 1000])
+def test_cross_entropy_minus_inf_chunks(V):
+    """Rows holding whole 8-aligned chunks of -inf logits (e.g. a masked vocabulary range): the
+    chunk adds nothing to the row's sum-exp (no NaN from -inf - -inf), as in torch."""
+    torch.manual_seed(8)
+    T = 64
+    ld = (V + 63) // 64 * 64
+    buf = torch.zeros(T, ld, device=dev, dtype=torch.bfloat16)
+    buf[:, :V] = torch.randn(T, V, device=dev).bfloat16()
+    buf[::2, 16:40] = float("-inf")           # three whole chunks (16..39) on even rows
+    buf[1::4, 8 * 37:8 * 40] = float("-inf")  # and three more on every fourth row
+    logits = buf.clone()
+    tg = torch.randint(40, V, (T,), device=dev)
+    loss, n, correct = cross_entropy_fused(buf, tg, V, write_grad=True, want_correct=True)
+    lf = logits[:, :V].float().requires_grad_(True)
+    lr = torch.nn.functional.cross_entropy(lf, tg)
+    lr.backward()
+    assert torch.isfinite(loss).item()
+    assert abs(loss.item() - lr.item()) < 1e-3 * abs(lr.item())
+    assert torch.isfinite(buf[:, :V].float()).all()
+    assert rel_err(buf[:, :V], lf.grad) < 1e-2
 
 
 def test_gemm_autotune_leaves_outputs_intact():
