@@ -441,3 +441,34 @@ def worker_fake_rccl_semantics(rank, world, fake, fake_dir):
     assert got.tolist() == [float(lo + (1 - rank % 2)), 7.0]
     sub.destroy()
     c.destroy()
+
+
+def worker_fake_rccl_p2p_completion(rank, world, fake, fake_dir):
+    """RCCL's point-to-point completion rule in the fake (tests/fakes/fake_rccl_hip.cpp): a send
+    completes only once the peer has received it.  Two ranks that each send, ungrouped, before
+    they receive deadlock on xGMI; here that exchange must fail (time out) instead of passing,
+    while the same exchange as one group (the pipeline engine's only form) completes."""
+    import os
+
+    os.makedirs(fake_dir, exist_ok=True)
+    _use_fake(fake)
+    os.environ["FAKE_DIR"] = fake_dir
+    os.environ["FAKE_TIMEOUT_S"] = "4"
+    from distributed_pytorch_cookbook_amd.parallel import comm
+    from distributed_pytorch_cookbook_amd.parallel.native_comm import NativeComm
+
+    comm.init_dist(force_cpu=True)
+    c = NativeComm(None, device="cpu")
+    peer = 1 - rank
+    tx, rx = torch.full((4,), float(rank)), torch.empty(4)
+    with c.grouped():  # the deadlock-free form
+        c.send(tx, peer)
+        c.recv(rx, peer)
+    assert rx.tolist() == [float(peer)] * 4
+    try:  # both ranks send first, ungrouped: each send waits for a receive that never comes
+        c.send(tx, peer)
+        c.recv(rx, peer)
+    except RuntimeError as e:
+        assert "failed" in str(e), e
+    else:
+        raise AssertionError("a mis-ordered ungrouped exchange completed: the fake does not model RCCL's blocking sends")

@@ -15,9 +15,16 @@
 //                    that differs between ranks (op, count, dtype or root) fails the call:
 //                    the fake doubles as a collective-matching checker.  Send / recv post into
 //                    per-pair mailboxes K_p_<src>_<dst>_<n> (the n-th message from src to dst);
-//                    a receive blocks until its message is there.  Inside ncclGroupStart /
-//                    ncclGroupEnd every send is posted first, then the rest in issue order,
-//                    as RCCL's fused group progresses them concurrently.  ncclCommSplit is a
+//                    a receive blocks until its message is there, consumes it and leaves an
+//                    acknowledgement (<message>.ack).  A send COMPLETES only when that
+//                    acknowledgement is there -- RCCL's rule: ncclSend blocks the stream until the
+//                    peer's matching ncclRecv runs, and a group ends only when every operation of
+//                    it has completed -- so an ungrouped send waits for its ack at the call, and
+//                    inside ncclGroupStart / ncclGroupEnd every send is posted first, then the rest
+//                    run in issue order (RCCL's fused group progresses them concurrently), then
+//                    the group waits for the acks of all its sends.  An exchange whose order would
+//                    deadlock on xGMI (each rank's send waiting for a receive the peer posts only
+//                    after its own send completes) times out here instead of passing.  ncclCommSplit is a
 //                    rendezvous on the parent that exchanges (color, key) and derives the
 //                    child's key, rank (by key, then parent rank) and size.
 // Other switches:
@@ -276,6 +283,27 @@ enum Op : uint32_t { OP_AR = 1, OP_RS, OP_AG, OP_BC, OP_SPLIT };
 
 int g_group = 0;
 std::vector<std::function<ncclResult_t()>> g_sends, g_rest;
+std::vector<std::pair<std::string, int>> g_acks;  // (message path, peer) of the open group's sends
+
+// a send completes when its receiver has consumed the message (the .ack the receive leaves)
+ncclResult_t wait_ack(const std::string& msg, int peer) {
+  const std::string ack = msg + ".ack";
+  const double t0 = now_s(), lim = timeout_s();
+  struct stat st;
+  int spin = 0;
+  while (stat(ack.c_str(), &st) != 0) {
+    if (now_s() - t0 > lim) {
+      fprintf(stderr,
+              "[fake rccl] send to rank %d never completed: no matching receive consumed %s within %.0f s "
+              "(an unmatched send, or an exchange ordered so that it deadlocks under RCCL's blocking sends)\n",
+              peer, msg.c_str(), lim);
+      return kSystemError;
+    }
+    usleep(spin++ < 100 ? 50 : 1000);
+  }
+  unlink(ack.c_str());
+  return 0;
+}
 
 ncclResult_t run_or_queue(bool is_send, std::function<ncclResult_t()> fn) {
   if (g_group > 0) {
@@ -436,13 +464,18 @@ ncclResult_t ncclSend(const void* buf, size_t count, int dt, int peer, void* com
   if (peer < 0 || peer >= c->nranks) return kInvalidUsage;
   // (the bytes are taken at the call, as the fake runs the group's sends first at its end:
   // callers keep send buffers alive and unchanged until the group completes, as RCCL needs)
+  const bool grouped = g_group > 0;
   return run_or_queue(true, [=]() -> ncclResult_t {
     const uint64_t n = c->sent[peer]++;
     Header h{kMagic, 100, count, dt, 0, c->rank, 0};
-    return post(path_of("%016llx_p_%d_%d_%llu", (unsigned long long)c->key, c->rank, peer, (unsigned long long)n), h,
-                buf, count * dsize(dt))
-               ? 0
-               : kSystemError;
+    const std::string msg =
+        path_of("%016llx_p_%d_%d_%llu", (unsigned long long)c->key, c->rank, peer, (unsigned long long)n);
+    if (!post(msg, h, buf, count * dsize(dt))) return kSystemError;
+    if (grouped) {  // completed at ncclGroupEnd, with the rest of the group
+      g_acks.push_back({msg, peer});
+      return 0;
+    }
+    return wait_ack(msg, peer);
   });
 }
 ncclResult_t ncclRecv(void* buf, size_t count, int dt, int peer, void* comm, void*) {
@@ -458,6 +491,11 @@ ncclResult_t ncclRecv(void* buf, size_t count, int dt, int peer, void* comm, voi
     std::vector<char> data;
     if (!fetch(p, h, data)) return kSystemError;
     unlink(p.c_str());
+    {  // the acknowledgement the sender's completion waits for
+      FILE* f = fopen((p + ".ack").c_str(), "wb");
+      if (!f) return kSystemError;
+      fclose(f);
+    }
     if (h.count != count || h.dtype != dt) {
       fprintf(stderr, "[fake rccl] recv #%llu from %d: expected (count %zu, dtype %d), the send carried (%llu, %d)\n",
               (unsigned long long)n, peer, count, dt, (unsigned long long)h.count, h.dtype);
@@ -479,8 +517,11 @@ ncclResult_t ncclGroupEnd() {
     if (!err) err = f();
   for (auto& f : g_rest)
     if (!err) err = f();
+  for (auto& a : g_acks)  // the group ends when every send of it has been received
+    if (!err) err = wait_ack(a.first, a.second);
   g_sends.clear();
   g_rest.clear();
+  g_acks.clear();
   return err;
 }
 

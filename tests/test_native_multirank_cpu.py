@@ -80,11 +80,20 @@ CASES = [
     ("main-fsdp.py", 2, 4, ["--reduce_dtype", "bf16"], {"all_gather", "reduce_scatter"}, False),
     ("main-pipe.py", 2, 8, ["--num_microbatches", "4", "--schedule", "1f1b"], {"send", "recv"}, True),
     ("main-pipe-ddp.py", 4, 4, ["--num_microbatches", "2"], {"send", "recv", "all_reduce"}, True),
+    # the north-star topologies at full rank count (BASELINE.json: PP = 8 1F1B, PP 2 x DP 4) and
+    # the other schedule / precision at 4 ranks
+    ("main-pipe.py", 8, 16, ["--num_microbatches", "16", "--schedule", "1f1b", "--num_layers", "8"],
+     {"send", "recv"}, True),
+    ("main-pipe.py", 4, 8, ["--num_microbatches", "8", "--schedule", "gpipe"], {"send", "recv"}, True),
+    # (4 f32 gradients summed in another order than gloo's ring: equal to f32 rounding, not bitwise)
+    ("main-pipe-ddp.py", 8, 4, ["--num_microbatches", "2", "--dp_size", "4"], {"send", "recv", "all_reduce"}, "f32"),
+    ("main-fsdp.py", 4, 4, ["--reduce_dtype", "bf16"], {"all_gather", "reduce_scatter"}, False),
 ]
 
 
 @pytest.mark.parametrize("script,nproc,batch,extra,ops,exact", CASES,
-                         ids=["ddp2", "fsdp2", "fsdp2_bf16", "pipe2_1f1b", "pipe2xdp2"])
+                         ids=["ddp2", "fsdp2", "fsdp2_bf16", "pipe2_1f1b", "pipe2xdp2", "pipe8_1f1b", "pipe4_gpipe",
+                              "pipe2xdp4", "fsdp4_bf16"])
 def test_native_transport_multirank_matches_gloo(tmp_path, fake_lib, script, nproc, batch, extra, ops, exact):
     args = [*COMMON, "--batch_size", str(batch), *extra]
     ref_dir, nat_dir, fake_dir = tmp_path / "gloo", tmp_path / "native", tmp_path / "fake"
@@ -102,7 +111,9 @@ def test_native_transport_multirank_matches_gloo(tmp_path, fake_lib, script, npr
     a, b = _final(nat_dir / "ck"), _final(ref_dir / "ck")
     assert list(a) == list(b)
     for k in a:
-        if exact:
+        if exact == "f32":
+            torch.testing.assert_close(a[k], b[k], atol=1e-5, rtol=1e-5)
+        elif exact:
             assert torch.equal(a[k], b[k]), (k, (a[k] - b[k]).abs().max().item())
         else:
             torch.testing.assert_close(a[k], b[k], atol=2e-3, rtol=2e-2)
@@ -116,3 +127,13 @@ def test_fake_rccl_moves_data_and_splits(fake_lib, tmp_path):
     from dist_workers import worker_fake_rccl_semantics
 
     run_workers(worker_fake_rccl_semantics, 4, fake_lib, str(tmp_path / "fake"))
+
+
+def test_fake_rccl_blocking_send_rule(fake_lib, tmp_path):
+    """Negative test of the fake itself: an exchange ordered so that it deadlocks under RCCL's
+    blocking sends (both ranks send first, ungrouped) must fail, not pass -- so the recipe tests
+    above would catch a cross-group ordering that hangs on xGMI."""
+    from dist_helpers import run_workers
+    from dist_workers import worker_fake_rccl_p2p_completion
+
+    run_workers(worker_fake_rccl_p2p_completion, 2, fake_lib, str(tmp_path / "fake"))
