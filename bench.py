@@ -94,7 +94,7 @@ def main():
     ap.add_argument("--pp_comm_dtype", default="fp32", choices=["fp32", "bf16"],
                     help="pipe / pipe_ddp: wire dtype of the stage-boundary activations and gradients")
     ap.add_argument("--num_microbatches", type=int, default=0)
-    ap.add_argument("--schedule", default="1f1b", choices=["1f1b", "gpipe"])
+    ap.add_argument("--schedule", default="1f1b", choices=["1f1b", "gpipe", "zb"])
     ap.add_argument("--dp_size", type=int, default=0)
     ap.add_argument("--prefetch", type=int, default=None, help="FSDP: units all-gathered ahead")
     ap.add_argument("--no_graph", action="store_true", help="eager steps (no HIP-graph capture)")

@@ -5,7 +5,8 @@ Reference: ``/root/reference/main-pipe.py:85-221`` (GPipe via torch Pipe, chunks
 stages, single process) and ``main-pipe-ddp.py`` (an empty stub).  Here: one process per
 GPU on a (pp, dp) mesh -- rank = stage * dp + replica -- each stage owning a contiguous,
 cost-balanced run of units (``parallel/pipeline.py``), micro-batches (default 4 x stages)
-executed in exactly the order ``schedule_1f1b`` (default) or ``schedule_gpipe`` gives,
+executed in exactly the order ``schedule_1f1b`` (default), ``schedule_gpipe`` or the zero-bubble
+``schedule_zb`` (backward split into B and deferred W passes: ``models/fused.py:defer_weight_grads``) gives,
 activations exchanged by asynchronous grouped RCCL send/recv between neighbouring stages
 (``run_schedule``; optional bf16 wire format), and, for dp > 1, each stage's gradients
 all-reduced across its replicas with the bucketed DDP store once the last micro-batch's
@@ -17,15 +18,18 @@ weighted by their share of valid targets (computed on device, no sync).
 """
 from __future__ import annotations
 
+from contextlib import nullcontext as _nullcontext
+
 import torch
 import torch.distributed as dist
 
-from ..models.fused import run_embeddings, run_head, run_layers
+from ..models.fused import defer_weight_grads, run_embeddings, run_head, run_layers
 from ..ops.optim import FlatAdamW
 from ..parallel import comm
 from ..parallel.ddp import DDPStore
 from ..parallel.fsdp import _placeholder
-from ..parallel.pipeline import P2P, partition, run_schedule, schedule_1f1b, schedule_gpipe, unit_costs
+from ..parallel.pipeline import (P2P, partition, run_schedule, schedule_1f1b, schedule_gpipe, schedule_zb,
+                                 stage_costs, unit_costs)
 from ..parallel.store import LocalStore
 from ..parallel.transport import TorchTransport, make_mesh_transports
 from ..parallel.transport import check_drained
@@ -118,6 +122,7 @@ class PipelineEngine(Engine):
         self.graph = graph and self.device.type == "cuda" and (
             world == 1 or (self.pp_tp.capturable() and (dp == 1 or self.dp_tp.capturable())))
         self._stepper = GraphedStep(self, [self.opt])
+        self._cost_cache = {}
 
     # ------------------------------------------------------------------ pieces
     def _micro_count(self, N: int) -> int:
@@ -191,23 +196,44 @@ class PipelineEngine(Engine):
             outputs[m] = out
             return out
 
+        zb = self.schedule == "zb"
+        wq = {}  # zero-bubble: micro-batch -> its deferred weight-gradient closures
+
         def backward(m, g):
             y = outputs.pop(m)
             with mark(f"bwd mb{m}"):
-                if self.last:
-                    self._scaled(y).backward()
-                else:
-                    torch.autograd.backward(y, g)
+                with defer_weight_grads(wq.setdefault(m, [])) if zb else _nullcontext():
+                    if self.last:
+                        self._scaled(y).backward()
+                    else:
+                        torch.autograd.backward(y, g)
             x = inputs.pop(m)
             return None if x is None else x.grad
 
-        order = (schedule_gpipe if self.schedule == "gpipe" else schedule_1f1b)(self.n_micro, self.stage, self.pp)
-        run_schedule(order, self.first, self.last, forward, backward, self.p2p, shape)
+        def wgrad(m):
+            with mark(f"wgrad mb{m}"):
+                for fn in wq.pop(m):
+                    fn()
+
+        if zb:
+            order = schedule_zb(self.n_micro, self.stage, self.pp, costs=self._zb_costs(S))
+        else:
+            order = (schedule_gpipe if self.schedule == "gpipe" else schedule_1f1b)(self.n_micro, self.stage, self.pp)
+        run_schedule(order, self.first, self.last, forward, backward, self.p2p, shape, wgrad=wgrad)
+        assert not wq, "zero-bubble schedule left weight gradients unrun"
         if isinstance(st, DDPStore):
             with mark("comm:finish_grads"):
                 st.finish_grads()
         with mark("optim"):
             return self._optim(acc)
+
+    def _zb_costs(self, S):
+        """Per-stage (F, B, W) costs of the zero-bubble simulation: the same on every rank (model
+        configuration, sequence length and partition only)."""
+        key = ("zb", S)
+        if self._cost_cache.get(key) is None:
+            self._cost_cache[key] = tuple(stage_costs(self.model, S, self.groups))
+        return self._cost_cache[key]
 
     def _optim(self, acc):
         if self.scaler is not None:

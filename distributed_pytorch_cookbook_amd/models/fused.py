@@ -97,6 +97,39 @@ def _qkv_grad(store, attn):
     return buf, (gq, gk, gv)
 
 
+# ---- zero-bubble pipeline schedule (parallel/pipeline.py:schedule_zb): inside
+# ``defer_weight_grads(buf)`` a backward runs only its input-gradient chain (B); every
+# weight-gradient GEMM, the embedding scatter and the store's post_backward hook of each unit
+# (which launches a DDP bucket once the unit's gradients are final) are appended to ``buf`` as
+# closures, in issue order, for the engine to run later as the W pass.  The closures hold their
+# operands (dY, X) alive; the other saved activations are released with the autograd graph.
+_W_DEFER: Optional[list] = None
+
+
+class defer_weight_grads:
+    def __init__(self, buf: list):
+        self.buf = buf
+        self.prev = None
+
+    def __enter__(self):
+        global _W_DEFER
+        self.prev, _W_DEFER = _W_DEFER, self.buf
+        return self.buf
+
+    def __exit__(self, *exc):
+        global _W_DEFER
+        _W_DEFER = self.prev
+        return False
+
+
+def _w(fn) -> None:
+    """Run a weight-gradient step now, or queue it for the W pass."""
+    if _W_DEFER is not None:
+        _W_DEFER.append(fn)
+    else:
+        fn()
+
+
 class _EmbedFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, anchor, ids, pos, mod, store, training):
@@ -115,9 +148,14 @@ class _EmbedFn(torch.autograd.Function):
         mod, store = ctx.mod, ctx.store
         u = mod._unit_id
         store.pre_backward(u, need_weights=False)
-        embedding_bwd(dx.contiguous(), ids, pos, store.grad(mod.input_embeddings.weight),
-                      store.grad(mod.position_embeddings.weight))
-        store.post_backward(u)
+        dxc = dx.contiguous()
+
+        def scatter():  # (a W-pass op: nothing upstream waits for it)
+            embedding_bwd(dxc, ids, pos, store.grad(mod.input_embeddings.weight),
+                          store.grad(mod.position_embeddings.weight))
+            store.post_backward(u)
+
+        _w(scatter)
         return None, None, None, None, None, None
 
 
@@ -250,7 +288,8 @@ class _LayerFn(torch.autograd.Function):
             _, saved = _layer_forward(x, mask, layer, store, N, S, act, True, ctx.drops)
         dx = _layer_backward(dx3, x, mask, saved, layer, store, N, S, H, hd, act, ctx.drops,
                              ctx.prev_tail, ctx.tail)
-        store.post_backward(layer._unit_id)
+        u = layer._unit_id
+        _w(lambda: store.post_backward(u))  # (after the unit's deferred weight gradients)
         return dx, None, None, None, None, None, None, None, None, None, None, None
 
 
@@ -279,6 +318,9 @@ class _SideWork:
             self.stream = _side_streams[key]
 
     def run(self, fn, *tensors):
+        if _W_DEFER is not None:  # zero-bubble schedule: the W pass runs it later
+            _W_DEFER.append(fn)
+            return
         if not self.on:
             fn()
             return
@@ -399,7 +441,7 @@ class _HeadFn(torch.autograd.Function):
         w, g = store.weight, store.grad
         dl = dlogits[:, :V]
         scale = dloss.reshape(()).float().contiguous()
-        linear_wgrad(dl, hf, out=g(head.weight), alpha_t=scale)
+        _w(lambda: linear_wgrad(dl, hf, out=g(head.weight), alpha_t=scale))
         # K = padded vocab: the CE kernel zeroed dlogits' pad columns, W_lm rows >= V read as 0
         dhf = linear_dgrad(dlogits, _head_weight_padded(store, head, dlogits.shape[1]),
                            out_dtype=_dh_dtype(store.compute_dtype), alpha_t=scale)
@@ -408,7 +450,7 @@ class _HeadFn(torch.autograd.Function):
         if ctx.prev_tail is not None:  # the last layer's down-projection bias / act / dropout backward
             ctx.prev_tail.consume(kw, x.shape[0], x.shape[1], x.device, store.compute_dtype)
         layernorm_bwd(dhf, x, mu, rs, w(norm.weight), dx, g(norm.weight), g(norm.bias), dx_set=True, **kw)
-        store.post_backward(unit)
+        _w(lambda: store.post_backward(unit))
         return dx, None, None, None, None, None, None, None, None
 
 

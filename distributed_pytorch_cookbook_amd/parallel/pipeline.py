@@ -16,10 +16,23 @@ gradients move with RCCL send/recv over the direct xGMI link between the two GPU
 asynchronously on the transport's comm stream; paired send+recv are one grouped operation
 (ncclGroupStart/End) so the 1F1B steady state cannot deadlock, and compute waits on a
 receive only where it consumes it; the executed order is exactly ``schedule_1f1b`` /
-``schedule_gpipe`` (``run_schedule``); the key-padding mask and targets are NOT sent --
-every stage of a replica reads the same batch from its own loader.
+``schedule_gpipe`` / ``schedule_zb`` (``run_schedule``); the key-padding mask and targets are
+NOT sent -- every stage of a replica reads the same batch from its own loader.
+
+Zero-bubble schedule (``schedule_zb``, Qi et al. 2023 "Zero Bubble Pipeline Parallelism",
+the H1 family): a micro-batch's backward is split into B -- the input-gradient chain, what the
+previous stage waits for -- and W -- the weight-gradient GEMMs (and the embedding scatter),
+which nothing downstream needs.  W passes are deferred into the slots where 1F1B idles (an
+early stage waiting for gradients to come back), so the cooldown bubble is filled with work
+the step has to do anyway.  The per-stage orders come from an event simulation of every stage
+under a per-stage cost model (``simulate_orders``), identical on all ranks; the F / B
+relative order is 1F1B's.  HBM is plentiful on MI355X (288 GB), so a stage may hold up to
+``wmax`` deferred W passes (their dY / X operands) beside 1F1B's in-flight activations.
 """
 from __future__ import annotations
+
+import functools
+import heapq
 
 import torch
 
@@ -157,9 +170,10 @@ class Recv:
         return self.buf if self.buf.dtype == self.dtype else self.buf.to(self.dtype)
 
 
-def run_schedule(order, first: bool, last: bool, forward, backward, p2p: "P2P", shape):
+def run_schedule(order, first: bool, last: bool, forward, backward, p2p: "P2P", shape, wgrad=None):
     """Execute a stage's schedule -- a list of ('F', m) / ('B', m) from ``schedule_1f1b`` or
-    ``schedule_gpipe`` -- with asynchronous grouped p2p.
+    ``schedule_gpipe``, plus ('W', m) from ``schedule_zb`` (``wgrad(m)``: the deferred weight
+    gradients of micro-batch m; no communication) -- with asynchronous grouped p2p.
 
     Rule: before the first op its receive is posted; after every op ONE grouped exchange is
     posted holding that op's send (y_m to the next stage, dx_m to the previous) and the
@@ -174,6 +188,8 @@ def run_schedule(order, first: bool, last: bool, forward, backward, p2p: "P2P", 
         kind, _ = op
         if kind == "F":
             return (shape, None) if not first else (None, None)
+        if kind == "W":
+            return (None, None)
         return (None, shape) if not last else (None, None)
 
     pending = None  # the Recv the next op consumes
@@ -182,7 +198,10 @@ def run_schedule(order, first: bool, last: bool, forward, backward, p2p: "P2P", 
         a, b = p2p.post(recv_prev_shape=rp, recv_next_shape=rn)
         pending = a or b
     for i, (kind, m) in enumerate(order):
-        if kind == "F":
+        if kind == "W":
+            wgrad(m)
+            send_next = send_prev = None
+        elif kind == "F":
             x = pending.get() if (pending is not None and not first) else None
             out = forward(m, x)
             send_next, send_prev = (out if not last else None), None
@@ -190,10 +209,17 @@ def run_schedule(order, first: bool, last: bool, forward, backward, p2p: "P2P", 
             g = pending.get() if (pending is not None and not last) else None
             dx = backward(m, g)
             send_next, send_prev = None, (dx if not first else None)
-        pending = None
+        if kind != "W":  # (a W consumes nothing: a receive posted before it stays pending)
+            pending = None
         rp = rn = None
-        if i + 1 < len(order):
-            rp, rn = need(order[i + 1])
+        # the receive of the next op that communicates goes into THIS op's group, W passes in
+        # between or not: a send-only group followed by a receive-only group on both sides of a
+        # link deadlocks under RCCL's blocking sends (p2p_deadlock_free)
+        j = i + 1
+        while j < len(order) and order[j][0] == "W":
+            j += 1
+        if j < len(order) and pending is None:
+            rp, rn = need(order[j])
         if send_next is not None or send_prev is not None or rp is not None or rn is not None:
             a, b = p2p.post(send_next=send_next, send_prev=send_prev, recv_prev_shape=rp,
                             recv_next_shape=rn)
@@ -219,3 +245,209 @@ def schedule_1f1b(n_micro: int, stage: int, n_stages: int):
 
 def schedule_gpipe(n_micro: int, stage: int, n_stages: int):
     return [("F", m) for m in range(n_micro)] + [("B", m) for m in range(n_micro)]
+
+
+# ---------------------------------------------------------------- zero-bubble (B / W split)
+def stage_costs(model, seq_len: int, groups) -> list[tuple[float, float, float]]:
+    """(F, B, W) seconds per token of each stage's units under the ``unit_costs`` rates: B is the
+    input-gradient chain (dgrad GEMMs, the attention backward ~2.5 x its forward, the memory
+    passes), W the weight-gradient GEMMs (the LM head's included: the largest single product of
+    the last stage) and the embedding scatter."""
+    D = model.dim
+    hd = model.heads * model.head_dim
+    V = model.vocab_size
+    S = seq_len
+    g = 2 * (3 * D * hd + hd * D + 2 * 4 * D * D) / _GEMM_RATE
+    a = 2 * S * hd / _ATTN_RATE
+    mem = (32 * D + 4 * 4 * D) / _MEM_RATE
+    per_unit = {}
+    L = model.num_layers
+    for u in range(L + 2):
+        if u == 0:
+            per_unit[u] = (4 * D / _MEM_RATE, 0.0, (8 * D + 64) / _MEM_RATE)
+        elif u == L + 1:
+            hg = 2 * D * V / _GEMM_RATE
+            per_unit[u] = (hg + 2 * V / _MEM_RATE, hg + (2 * V + 16 * D) / _MEM_RATE, hg)
+        else:
+            per_unit[u] = (g + a + 0.4 * mem, g + 2.5 * a + 0.6 * mem, g)
+    return [tuple(sum(per_unit[u][k] for u in grp) for k in range(3)) for grp in groups]
+
+
+def simulate_orders(n_micro: int, costs, wmax=None, comm: float = 0.0, split_w: bool = True, fmax=None):
+    """Event simulation of a pipeline step: per-stage op orders and finish times.
+
+    ``costs[s] = (F, B, W)`` per micro-batch on stage s.  A stage, whenever it is free, runs (in
+    this priority): the next B if its gradient has arrived; a W if it already holds more than
+    ``wmax[s]`` deferred ones; the next F if its input has arrived and fewer than (stages - s)
+    micro-batches are between F and B (1F1B's activation memory); any deferred W; else it idles
+    until the next arrival.  ``split_w=False`` runs W right after its B (= 1F1B with B + W as one
+    backward).  Returns (orders, makespan, busy per stage).  Deterministic: every rank derives
+    the same orders."""
+    p = len(costs)
+    if wmax is None:
+        wmax = [p] * p
+    if fmax is None:
+        fmax = [p - s for s in range(p)]
+    INF = float("inf")
+    t = [0.0] * p
+    nf, nb = [0] * p, [0] * p
+    wq = [[] for _ in range(p)]
+    fin_f, fin_b = {}, {}
+    orders = [[] for _ in range(p)]
+    busy = [0.0] * p
+    total = 3 * n_micro
+
+    def done(s):
+        return len(orders[s]) == total
+
+    def dep_time(s, kind):
+        """Arrival time of the next F / B input of stage s (INF: not scheduled yet)."""
+        if kind == "F":
+            m = nf[s]
+            if m >= n_micro:
+                return INF
+            return 0.0 if s == 0 else fin_f.get((s - 1, m), INF) + comm
+        m = nb[s]
+        if m >= n_micro or m >= nf[s]:
+            return INF
+        return fin_f[(s, m)] if s == p - 1 else fin_b.get((s + 1, m), INF) + comm
+
+    def run(s, kind, m, c):
+        orders[s].append((kind, m))
+        t[s] += c
+        busy[s] += c
+
+    while not all(done(s) for s in range(p)):
+        # the stage that can act earliest (time-ordered, so every dependency that finishes
+        # before that time is already known)
+        best = None
+        for s in range(p):
+            if done(s):
+                continue
+            if wq[s]:
+                start = t[s]
+            else:
+                fb = dep_time(s, "B")
+                ff = dep_time(s, "F") if nf[s] - nb[s] < fmax[s] else INF
+                start = max(t[s], min(fb, ff))
+            if start < INF and (best is None or start < best[0]):
+                best = (start, s)
+        if best is None:
+            raise RuntimeError("pipeline simulation stalled")
+        start, s = best
+        t[s] = start
+        F, B, W = costs[s]
+        if dep_time(s, "B") <= t[s]:
+            m = nb[s]
+            nb[s] += 1
+            run(s, "B", m, B)
+            fin_b[(s, m)] = t[s]
+            if split_w:
+                wq[s].append(m)
+            else:
+                run(s, "W", m, W)
+        elif wq[s] and len(wq[s]) > wmax[s]:
+            run(s, "W", wq[s].pop(0), W)
+        elif nf[s] - nb[s] < fmax[s] and dep_time(s, "F") <= t[s]:
+            m = nf[s]
+            nf[s] += 1
+            run(s, "F", m, F)
+            fin_f[(s, m)] = t[s]
+        elif wq[s]:
+            run(s, "W", wq[s].pop(0), W)
+        else:  # nothing arrived yet: wait (re-evaluated in time order)
+            nxt = min(dep_time(s, "B"), dep_time(s, "F") if nf[s] - nb[s] < fmax[s] else INF)
+            t[s] = nxt
+    return orders, max(t), busy
+
+
+@functools.lru_cache(maxsize=64)
+def _zb_orders(n_micro: int, costs: tuple, wmax: tuple | None):
+    orders, _, _ = simulate_orders(n_micro, list(costs), list(wmax) if wmax else None)
+    return tuple(tuple(o) for o in orders)
+
+
+def schedule_zb(n_micro: int, stage: int, n_stages: int, costs=None, wmax=None):
+    """('F', m) / ('B', m) / ('W', m) in execution order for one stage: the zero-bubble (H1)
+    schedule of ``simulate_orders`` (``costs``: per-stage (F, B, W), default equal thirds)."""
+    c = tuple(tuple(x) for x in costs) if costs is not None else ((1.0, 1.0, 1.0),) * n_stages
+    if len(c) != n_stages:
+        raise ValueError("schedule_zb: one (F, B, W) cost triple per stage")
+    return list(_zb_orders(n_micro, c, tuple(wmax) if wmax is not None else None)[stage])
+
+
+def bubble_factor(n_micro: int, costs, schedule: str = "zb", comm: float = 0.0) -> float:
+    """Modelled step time over the busiest stage's work (1.0 = no bubble) for 1F1B (B + W as one
+    backward) or the zero-bubble orders, under the cost model -- the proxy's bubble term."""
+    _, span, busy = simulate_orders(n_micro, costs, comm=comm, split_w=schedule != "1f1b")
+    return span / max(busy)
+
+
+def p2p_deadlock_free(orders) -> bool:
+    """Check a set of per-stage orders against RCCL's point-to-point semantics as
+    ``run_schedule`` issues them: after op i one group holding op i's send and the receive the
+    next communicating op consumes (the first op's receive alone before it); a group completes only when every
+    send in it has been matched by the peer's receive in the peer's CURRENT group and every
+    receive by the peer's send.  True when every stage runs to the end."""
+    p = len(orders)
+    groups = []
+    for s, order in enumerate(orders):
+        first, last = s == 0, s == p - 1
+
+        def need(op):
+            if op[0] == "F":
+                return None if first else ("recv", s - 1, ("F", op[1]))
+            if op[0] == "B":
+                return None if last else ("recv", s + 1, ("B", op[1]))
+            return None
+
+        gs = []
+        pend = need(order[0]) if order else None  # (a schedule never starts with a W)
+        if pend:
+            gs.append([pend])
+        for i, op in enumerate(order):
+            g = []
+            if op[0] == "F" and not last:
+                g.append(("send", s + 1, ("F", op[1])))
+            if op[0] == "B" and not first:
+                g.append(("send", s - 1, ("B", op[1])))
+            if op[0] != "W":
+                pend = None
+            j = i + 1
+            while j < len(order) and order[j][0] == "W":
+                j += 1
+            if j < len(order) and pend is None:
+                pend = need(order[j])
+                if pend:
+                    g.append(pend)
+            if g:
+                gs.append(g)
+        groups.append(gs)
+    cur = [0] * p
+    left = [set(range(len(groups[s][0]))) if groups[s] else set() for s in range(p)]
+    progress = True
+    while progress:
+        progress = False
+        for s in range(p):
+            if cur[s] >= len(groups[s]):
+                continue
+            g = groups[s][cur[s]]
+            for j in list(left[s]):
+                kind, peer, msg = g[j]
+                if cur[peer] >= len(groups[peer]):
+                    continue
+                pg = groups[peer][cur[peer]]
+                want = ("recv" if kind == "send" else "send", s, msg)
+                for k in list(left[peer]):
+                    if pg[k] == want:
+                        left[s].discard(j)
+                        left[peer].discard(k)
+                        progress = True
+                        break
+            for q in (s,) + tuple(x for x in (s - 1, s + 1) if 0 <= x < p):
+                while cur[q] < len(groups[q]) and not left[q]:
+                    cur[q] += 1
+                    if cur[q] < len(groups[q]):
+                        left[q] = set(range(len(groups[q][cur[q]])))
+                    progress = True
+    return all(cur[s] >= len(groups[s]) for s in range(p))
