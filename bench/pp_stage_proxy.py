@@ -10,7 +10,10 @@ forward / autograd backward per micro-batch in the exact 1F1B order of that stag
 ``--pp_comm_dtype fp32`` carries them, or bf16), then one fused AdamW step.  Reports per-token
 time against the same layers run as ONE micro-batch of ``--full`` sequences (the pp1 step shape),
 so the difference is what the micro-batching itself costs (launches, small-M GEMM tiles,
-per-micro-batch allocations), eager and as a replayed HIP graph.
+per-micro-batch allocations), eager and as a replayed HIP graph.  ``--schedule zb`` runs the
+zero-bubble order (B / W split, deferred weight gradients); the per-op costs it measures feed the
+pipeline simulation (``parallel/pipeline.py:simulate_orders``) for the modelled bubble and stage
+efficiency of both schedules.
 
 Reference: ``/root/reference/main-pipe.py:78-83`` (Pipe with chunks = stages).
 """
@@ -26,10 +29,11 @@ import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from distributed_pytorch_cookbook_amd.config import PRESETS  # noqa: E402
-from distributed_pytorch_cookbook_amd.models.fused import run_layers  # noqa: E402
+from distributed_pytorch_cookbook_amd.models.fused import defer_weight_grads, run_layers  # noqa: E402
 from distributed_pytorch_cookbook_amd.models.gpt import TransformerDecoderLM  # noqa: E402
 from distributed_pytorch_cookbook_amd.ops.optim import FlatAdamW  # noqa: E402
-from distributed_pytorch_cookbook_amd.parallel.pipeline import partition, schedule_1f1b, unit_costs  # noqa: E402
+from distributed_pytorch_cookbook_amd.parallel.pipeline import (bubble_factor, partition, schedule_1f1b,  # noqa: E402
+                                                                schedule_zb, stage_costs, unit_costs)
 from distributed_pytorch_cookbook_amd.parallel.store import LocalStore  # noqa: E402
 
 
@@ -48,6 +52,8 @@ def main():
     ap.add_argument("--graph", action="store_true", help="also time the step as a replayed HIP graph")
     ap.add_argument("--only", default="both", choices=["both", "micro", "full"],
                     help="run one of the two steps (a kernel profile of each on its own)")
+    ap.add_argument("--schedule", default="1f1b", choices=["1f1b", "zb"],
+                    help="zb: the zero-bubble order (B / W split, parallel/pipeline.py:schedule_zb)")
     ap.add_argument("--json", default=None)
     a = ap.parse_args()
     dev = torch.device("cuda" if torch.cuda.is_available() else "cpu")
@@ -82,21 +88,37 @@ def main():
         T = mb * (S - 1)
         xs = [torch.randn(T, D, device=dev).to(wdt) for _ in range(n_micro)]
         gs = [torch.randn(T, D, device=dev).to(wdt) * 1e-3 for _ in range(n_micro)]
-        order = schedule_1f1b(n_micro, stage if n_micro > 1 else 0, a.pp if n_micro > 1 else 1)
+        zb = a.schedule == "zb" and n_micro > 1
+        if zb:
+            order = schedule_zb(n_micro, stage, a.pp, costs=stage_costs(model, S, groups))
+        else:
+            order = schedule_1f1b(n_micro, stage if n_micro > 1 else 0, a.pp if n_micro > 1 else 1)
         store.accum_steps = n_micro
 
-        def body():
+        def body(ev=None):
             store.zero_grad()
-            live = {}
+            live, wq = {}, {}
             for kind, m in order:
+                if ev is not None:
+                    ev.append((kind, torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)))
+                    ev[-1][1].record()
                 if kind == "F":
                     x = xs[m].float().requires_grad_(True)  # the received boundary tensor
                     y = run_layers(model, store, x, None, mb, S - 1, layers, True)
                     live[m] = (x, y.to(wdt))  # the tensor that would be sent on
-                else:
+                elif kind == "B":
                     x, y = live.pop(m)
-                    torch.autograd.backward(y, gs[m])
+                    if zb:
+                        with defer_weight_grads(wq.setdefault(m, [])):
+                            torch.autograd.backward(y, gs[m])
+                    else:
+                        torch.autograd.backward(y, gs[m])
                     _ = x.grad.to(wdt)  # the gradient that would be sent back
+                else:
+                    for fn in wq.pop(m):
+                        fn()
+                if ev is not None:
+                    ev[-1][2].record()
             opt.step(grad_scale=1.0)
         return body, n_micro * T
 
@@ -141,6 +163,31 @@ def main():
     for k in list(out):
         if ref and k.endswith("_us_per_ktok") and k != "full_eager_us_per_ktok":
             out[k.replace("_us_per_ktok", "_vs_full")] = round(out[k] / ref, 3)
+    # per-op costs of the micro-batched step (one more eager step, events around every op) and the
+    # modelled pipeline: bubble = simulated step time / busiest stage's work (every stage costed as
+    # this one), 1F1B (B + W as one backward) against the zero-bubble order; efficiency = 1 / (tax
+    # x bubble) with tax = the micro-batched step's per-token time over the one-batch step's
+    if a.only in ("both", "micro") and dev.type == "cuda":
+        body = steps[0][1]
+        ev = []
+        body(ev)
+        torch.cuda.synchronize()
+        tot = {"F": 0.0, "B": 0.0, "W": 0.0}
+        for kind, e0, e1 in ev:
+            tot[kind] += e0.elapsed_time(e1)
+        cF, cB, cW = (tot[k] / a.micro for k in "FBW")
+        if a.schedule != "zb":  # (1F1B's B holds its W: split by the cost model's share)
+            sc = stage_costs(model, S, groups)[stage]
+            cW = cB * sc[2] / (sc[1] + sc[2])
+            cB -= cW
+        out["op_ms"] = {"F": round(cF, 3), "B": round(cB, 3), "W": round(cW, 3)}
+        costs = [(cF, cB, cW)] * a.pp
+        b1, bz = bubble_factor(a.micro, costs, "1f1b"), bubble_factor(a.micro, costs, "zb")
+        out["bubble_1f1b"], out["bubble_zb"] = round(b1, 3), round(bz, 3)
+        tax = out.get("micro_eager_vs_full")
+        if tax:
+            out["eff_1f1b"] = round(1.0 / (tax * b1), 3)
+            out["eff_zb"] = round(1.0 / (tax * bz), 3)
     line = json.dumps(out)
     print(line, flush=True)
     if a.json:

@@ -221,6 +221,20 @@ class PipelineEngine(Engine):
             order = (schedule_gpipe if self.schedule == "gpipe" else schedule_1f1b)(self.n_micro, self.stage, self.pp)
         run_schedule(order, self.first, self.last, forward, backward, self.p2p, shape, wgrad=wgrad)
         assert not wq, "zero-bubble schedule left weight gradients unrun"
+        if isinstance(st, DDPStore) and st.tp.active and self.scaler is None:
+            # bucket by bucket, as the DDP engine does: AdamW of the buckets whose replica
+            # all-reduce has landed runs while the later ones are still on the links (a stage's
+            # buckets launch from its last micro-batch's backward -- or W -- passes, unit by unit)
+            with mark("optim"):
+                st.launch_all()
+                self.opt.begin_step()
+                for bi in range(len(st.buckets)):
+                    with mark("comm:wait_bucket"):
+                        st.wait_bucket(bi)
+                    lo, hi = st.bucket_range(bi)
+                    self.opt.update(lo, hi, grad_scale=1.0 / self.dp)
+                st.reset_buckets()
+            return acc.get("loss")
         if isinstance(st, DDPStore):
             with mark("comm:finish_grads"):
                 st.finish_grads()
