@@ -492,10 +492,13 @@ def run_layers(model, store, x, mask, N, S, layers, training, dropout_seed=None)
     use_drop = model.training and model.dropout > 0
     if use_drop and dropout_seed is None:
         dropout_seed = model.next_dropout_seed()
+        drawn = True
+    else:
+        drawn = False
     recompute = bool(getattr(model, "recompute", False)) and training
     prev = None
     for layer in layers:
-        drops = model.dropout_specs(layer, dropout_seed) if use_drop else (None, None)
+        drops = model.dropout_specs(layer, dropout_seed, drawn) if use_drop else (None, None)
         tail = _FfnTail() if training else None
         x = _LayerFn.apply(x, mask, layer, store, N, S, act, training, drops, recompute, prev, tail)
         prev = tail

@@ -226,7 +226,8 @@ class TransformerDecoderLM(nn.Module):
                 return v - (1 << 32) if v >= (1 << 31) else v
 
             base = i32(self.dropout_seed_base)
-            if self._seed_dev is None or self._seed_dev_base != base:
+            # (re)created on a new base or after the model moved to another device (model.to)
+            if self._seed_dev is None or self._seed_dev_base != base or self._seed_dev.device != dev:
                 self._seed_dev = torch.tensor([i32(seed), base], dtype=torch.int32, device=dev)
                 self._seed_dev_base = base
             snap = self._seed_dev.clone()
@@ -236,12 +237,15 @@ class TransformerDecoderLM(nn.Module):
                 self._seed_snaps.pop(next(iter(self._seed_snaps)))
         return seed
 
-    def dropout_specs(self, layer, seed):
-        """(attention-output, FFN-output) :class:`DropSpec` of ``layer`` for ``seed``."""
+    def dropout_specs(self, layer, seed, drawn: bool = False):
+        """(attention-output, FFN-output) :class:`DropSpec` of ``layer`` for ``seed``.
+        ``drawn``: the seed came from ``next_dropout_seed`` -- only then do the kernels read its
+        device snapshot (after graph replays the device counter runs ahead of the host one, so
+        an explicit ``dropout_seed`` equal to an old drawn value must keep its host key)."""
         from ..ops.dropout import DropSpec
 
         i = layer._layer_index
-        snap = self._seed_snaps.get(seed)
+        snap = self._seed_snaps.get(seed) if drawn else None
         return (DropSpec.make(self.dropout, seed, 2 * i, snap),
                 DropSpec.make(self.dropout, seed, 2 * i + 1, snap))
 

@@ -78,14 +78,15 @@ __device__ __forceinline__ int g_f32_pol(int nt_store) {
 __device__ __forceinline__ void st16p(void* ptr, uint4 v, bool nt, int pol) {
   typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
   const u32x4 w{v.x, v.y, v.z, v.w};
-  // (the trailing s_nop: gfx9's VMEM store-data hazard -- a VALU write to the data VGPRs of a
-  // dwordx3 / x4 store in the very next cycle corrupts the stored data.  The compiler inserts that
-  // wait state for its own stores but cannot see inside asm: with a compile-time policy (no
-  // branch after the store) 87 of the 896 stores of the v9 forward epilogue were followed at once
-  // by a VALU write of their data registers -- NaNs in test_gemm_v7_v8_v9, round 6)
-  if (pol == 1) asm volatile("global_store_dwordx4 %0, %1, off sc0 nt\n\ts_nop 0" ::"v"(ptr), "v"(w) : "memory");
-  else if (pol == 2) asm volatile("global_store_dwordx4 %0, %1, off sc1 nt\n\ts_nop 0" ::"v"(ptr), "v"(w) : "memory");
-  else if (pol == 3) asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1 nt\n\ts_nop 0" ::"v"(ptr), "v"(w) : "memory");
+  // (the trailing s_nop 1: gfx950's VMEM store-data hazard -- a VALU write to the data VGPRs of a
+  // dwordx3 / x4 store within 2 cycles corrupts the stored data.  The compiler puts exactly this
+  // s_nop 1 after its own stores (checked in a gfx950 listing) but cannot see inside asm: with a
+  // compile-time policy there is no branch after the store to absorb it, and 87 of the 896 stores
+  // of the v9 forward epilogue were followed at once by a VALU write of their data registers --
+  // scattered NaNs in test_gemm_v7_v8_v9, round 6)
+  if (pol == 1) asm volatile("global_store_dwordx4 %0, %1, off sc0 nt\n\ts_nop 1" ::"v"(ptr), "v"(w) : "memory");
+  else if (pol == 2) asm volatile("global_store_dwordx4 %0, %1, off sc1 nt\n\ts_nop 1" ::"v"(ptr), "v"(w) : "memory");
+  else if (pol == 3) asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1 nt\n\ts_nop 1" ::"v"(ptr), "v"(w) : "memory");
   else if (nt) __builtin_nontemporal_store(w, reinterpret_cast<u32x4*>(ptr));
   else *reinterpret_cast<uint4*>(ptr) = v;
 }

@@ -837,7 +837,7 @@ def test_layernorm_fwd_fused_residual_add(D, p_drop):
     assert rel_err(mu, xs_r.mean(-1)) < 1e-5
 
 
-@pytest.mark.parametrize("hd", [64, 32])
+@pytest.mark.parametrize("hd", [64, 32, 128, 96, 256])
 @pytest.mark.parametrize("pos", [0, 37, 299])
 def test_decode_attention(hd, pos):
     """Single-query KV-cache attention kernel (appends the new K/V at the device length) vs

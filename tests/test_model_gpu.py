@@ -209,7 +209,7 @@ def test_side_stream_wgrad_matches_single_stream(monkeypatch):
     assert ((grads[0] - grads[1]).norm() / grads[0].norm()).item() < 1e-5
 
 
-@pytest.mark.parametrize("hd", [64, 32])
+@pytest.mark.parametrize("hd", [64, 32, 128])
 def test_kv_cache_decode_gpu(hd):
     """KV-cache decode on the GPU kernels (flash-attention prefill, 1-row GEMMs) vs re-running
     the whole sequence through the fused forward."""
@@ -231,15 +231,17 @@ def test_kv_cache_decode_gpu(hd):
     assert _lib.is_loaded()
 
 
-def test_graph_decoder_matches_eager_decode():
+@pytest.mark.parametrize("hd", [64, 128])
+def test_graph_decoder_matches_eager_decode(hd):
     """The HIP-graph one-token decode step (static shapes over the cache capacity) gives the
-    same logits as the eager cached decode and the full forward; greedy text is unchanged."""
+    same logits as the eager cached decode and the full forward; greedy text is unchanged --
+    at GPT-2's head size and at 128 (the decode kernel takes any multiple of 8 up to 256)."""
     from distributed_pytorch_cookbook_amd.utils.batch import generate
     from distributed_pytorch_cookbook_amd.utils.tokenizer import ByteTokenizer
 
     torch.manual_seed(0)
     with torch.device("cuda"):
-        m = TransformerDecoderLM(256, 64, 4, 2, 50257, 128, activation="gelu")
+        m = TransformerDecoderLM(256, hd, 256 // hd, 2, 50257, 128, activation="gelu")
     m.eval()
     ids = torch.randint(0, 50257, (1, 30), device="cuda")
     with torch.no_grad():
