@@ -94,7 +94,10 @@ def main():
     ap.add_argument("--pp_comm_dtype", default="fp32", choices=["fp32", "bf16"],
                     help="pipe / pipe_ddp: wire dtype of the stage-boundary activations and gradients")
     ap.add_argument("--num_microbatches", type=int, default=0)
-    ap.add_argument("--schedule", default="1f1b", choices=["1f1b", "gpipe", "zb"])
+    ap.add_argument("--schedule", default=None, choices=["1f1b", "gpipe", "zb", "zb2"],
+                    help="pipeline schedule; default: zb2 for pipe (the PP=8 north star: modelled stage "
+                         "efficiency 0.848 against 1F1B's 0.764, profiles/r6_pp/), zb for pipe_ddp (its W "
+                         "passes stay spread, so the replica all-reduce still overlaps)")
     ap.add_argument("--dp_size", type=int, default=0)
     ap.add_argument("--prefetch", type=int, default=None, help="FSDP: units all-gathered ahead")
     ap.add_argument("--no_graph", action="store_true", help="eager steps (no HIP-graph capture)")
@@ -128,6 +131,8 @@ def main():
     rec = "pipe_ddp" if a.recipe == "pipe_ddp" else a.recipe
     argv = ["--model", model_name, "--batch_size", str(a.batch_size), "--bucket_mb", str(a.bucket_mb),
             "--reduce_dtype", a.reduce_dtype, "--synthetic_data"]
+    if a.schedule is None:
+        a.schedule = "zb2" if rec == "pipe" else "zb"
     if rec in ("pipe", "pipe_ddp"):
         argv += ["--schedule", a.schedule, "--num_microbatches", str(a.num_microbatches),
                  "--pp_comm_dtype", a.pp_comm_dtype]
@@ -231,6 +236,7 @@ def main():
                    "peak_mem_gib": round(float(peak.item()), 1),
                    "force_dist_path": bool(a.force_dist_path),
                    "reduce_dtype": a.reduce_dtype, "pp_comm_dtype": a.pp_comm_dtype,
+                   "schedule": a.schedule if a.recipe in ("pipe", "pipe_ddp") else None,
                    "mfu_per_gpu": round(mfu(value / n, train_flops_per_token(
                        args.dim, args.heads, args.head_dim, args.num_layers, vocab, S)), 4),
                    "baseline": ("stock PyTorch reference-default recipe (manual attention + torch.compile)"

@@ -52,7 +52,7 @@ def main():
     ap.add_argument("--graph", action="store_true", help="also time the step as a replayed HIP graph")
     ap.add_argument("--only", default="both", choices=["both", "micro", "full"],
                     help="run one of the two steps (a kernel profile of each on its own)")
-    ap.add_argument("--schedule", default="1f1b", choices=["1f1b", "zb"],
+    ap.add_argument("--schedule", default="1f1b", choices=["1f1b", "zb", "zb2"],
                     help="zb: the zero-bubble order (B / W split, parallel/pipeline.py:schedule_zb)")
     ap.add_argument("--json", default=None)
     a = ap.parse_args()
@@ -88,9 +88,10 @@ def main():
         T = mb * (S - 1)
         xs = [torch.randn(T, D, device=dev).to(wdt) for _ in range(n_micro)]
         gs = [torch.randn(T, D, device=dev).to(wdt) * 1e-3 for _ in range(n_micro)]
-        zb = a.schedule == "zb" and n_micro > 1
+        zb = a.schedule in ("zb", "zb2") and n_micro > 1
         if zb:
-            order = schedule_zb(n_micro, stage, a.pp, costs=stage_costs(model, S, groups))
+            order = schedule_zb(n_micro, stage, a.pp, costs=stage_costs(model, S, groups),
+                                mem=2 if a.schedule == "zb2" else 1)
         else:
             order = schedule_1f1b(n_micro, stage if n_micro > 1 else 0, a.pp if n_micro > 1 else 1)
         store.accum_steps = n_micro
@@ -176,18 +177,18 @@ def main():
         for kind, e0, e1 in ev:
             tot[kind] += e0.elapsed_time(e1)
         cF, cB, cW = (tot[k] / a.micro for k in "FBW")
-        if a.schedule != "zb":  # (1F1B's B holds its W: split by the cost model's share)
+        if a.schedule == "1f1b":  # (1F1B's B holds its W: split by the cost model's share)
             sc = stage_costs(model, S, groups)[stage]
             cW = cB * sc[2] / (sc[1] + sc[2])
             cB -= cW
         out["op_ms"] = {"F": round(cF, 3), "B": round(cB, 3), "W": round(cW, 3)}
         costs = [(cF, cB, cW)] * a.pp
-        b1, bz = bubble_factor(a.micro, costs, "1f1b"), bubble_factor(a.micro, costs, "zb")
-        out["bubble_1f1b"], out["bubble_zb"] = round(b1, 3), round(bz, 3)
         tax = out.get("micro_eager_vs_full")
-        if tax:
-            out["eff_1f1b"] = round(1.0 / (tax * b1), 3)
-            out["eff_zb"] = round(1.0 / (tax * bz), 3)
+        for sch in ("1f1b", "zb", "zb2"):
+            bf = bubble_factor(a.micro, costs, sch)
+            out["bubble_" + sch] = round(bf, 3)
+            if tax:
+                out["eff_" + sch] = round(1.0 / (tax * bf), 3)
     line = json.dumps(out)
     print(line, flush=True)
     if a.json:

@@ -85,9 +85,10 @@ def build_parser(recipe: str = "single") -> argparse.ArgumentParser:
     if recipe in ("pipe", "pipe_ddp"):
         p.add_argument("--pp_size", type=int, default=0, help="pipeline stages (0 = world size / dp)")
         p.add_argument("--num_microbatches", type=int, default=0, help="0 = 4 x stages (1 for a single stage)")
-        p.add_argument("--schedule", type=str, default="1f1b", choices=["1f1b", "gpipe", "zb"],
+        p.add_argument("--schedule", type=str, default="1f1b", choices=["1f1b", "gpipe", "zb", "zb2"],
                        help="micro-batch schedule: 1F1B (PipeDream-flush), GPipe, or zero-bubble (1F1B with the "
-                            "weight-gradient passes deferred into the pipeline bubbles)")
+                            "weight-gradient passes deferred into the pipeline bubbles; zb2: twice the forwards in "
+                            "flight and every W deferrable -- less bubble, more HBM)")
         p.add_argument("--pp_comm_dtype", type=str, default="fp32", choices=["fp32", "bf16"],
                        help="wire format of the stage-boundary activations and their gradients")
     if recipe == "pipe_ddp":

@@ -84,8 +84,11 @@ class PipelineEngine(Engine):
         # num_stages, /root/reference/main-pipe.py:83).  The batch size is known at the first
         # step (_micro_count).
         self.n_micro_req = num_microbatches
-        self.n_micro = max(1, num_microbatches or (4 * pp if pp > 1 else 1))
         self.schedule = schedule
+        # (the zero-bubble schedules leave less bubble to amortise: 2 x stages micro-batches --
+        # larger ones, a smaller per-micro-batch tax; bench/pp_stage_proxy.py, profiles/r6_pp/)
+        self._mfac = 2 if schedule in ("zb", "zb2") else 4
+        self.n_micro = max(1, num_microbatches or (self._mfac * pp if pp > 1 else 1))
         S = seq_len or model.max_position_embeddings
         groups = partition(unit_costs(model, S), pp)
         self.groups = groups
@@ -130,7 +133,8 @@ class PipelineEngine(Engine):
             return self.n_micro_req
         if self.pp == 1:
             return 1
-        return max(d for d in range(1, min(N, 4 * self.pp) + 1) if N % d == 0)
+        mfac = getattr(self, "_mfac", 4)
+        return max(d for d in range(1, min(N, mfac * self.pp) + 1) if N % d == 0)
 
     def _split(self, batch, targets):
         N = batch["input_ids"].shape[0]
@@ -196,7 +200,7 @@ class PipelineEngine(Engine):
             outputs[m] = out
             return out
 
-        zb = self.schedule == "zb"
+        zb = self.schedule in ("zb", "zb2")
         wq = {}  # zero-bubble: micro-batch -> its deferred weight-gradient closures
 
         def backward(m, g):
@@ -216,7 +220,8 @@ class PipelineEngine(Engine):
                     fn()
 
         if zb:
-            order = schedule_zb(self.n_micro, self.stage, self.pp, costs=self._zb_costs(S))
+            order = schedule_zb(self.n_micro, self.stage, self.pp, costs=self._zb_costs(S),
+                                mem=2 if self.schedule == "zb2" else 1)
         else:
             order = (schedule_gpipe if self.schedule == "gpipe" else schedule_1f1b)(self.n_micro, self.stage, self.pp)
         run_schedule(order, self.first, self.last, forward, backward, self.p2p, shape, wgrad=wgrad)

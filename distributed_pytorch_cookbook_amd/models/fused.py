@@ -163,12 +163,17 @@ class _EmbedFn(torch.autograd.Function):
 _FUSE_OUT_LN = os.environ.get("DPC_FUSE_OUT_LN", "1") == "1"
 
 
-def _layer_forward(x, mask, layer, store, N, S, act, training, drops, attend=None):
+def _layer_forward(x, mask, layer, store, N, S, act, training, drops, attend=None, pre=None, fuse_out=None):
     """Decoder-layer forward on the store's compute weights (no store hooks).
 
     Returns ``(x3, saved)``; ``saved`` holds what the backward needs when ``training``.
     ``attend(qkv) -> (o, lse)`` replaces the causal self-attention over these S tokens
     (the KV-cache decode attends over the cached keys instead).
+    ``pre``: the previous layer's FFN output not yet added to the residual stream,
+    ``(x2, z2, drop, act)`` -- x is then an unwritten buffer that LN1 fills with
+    ``x2 + drop(act(z2))`` as it normalises (``_ResidualHandoff``).  ``fuse_out``: a
+    ``_ResidualHandoff`` to leave this layer's own FFN output in, for the next layer's LN1
+    (the returned x3 is then the buffer that LN1 will fill).
     """
     drop_attn, drop_ffn = drops
     attn, fc = layer.attn, layer.fc
@@ -176,7 +181,12 @@ def _layer_forward(x, mask, layer, store, N, S, act, training, drops, attend=Non
     w = store.weight
     T, D = x.shape
     cdt = store.compute_dtype
-    h1, mu1, rs1 = layernorm_fwd(x, w(layer.norm1.weight), w(layer.norm1.bias), LN_EPS, cdt)
+    if pre is not None:  # the previous layer's down projection: residual add + act + dropout here
+        x2p, z2p, dropp, actp = pre
+        h1, mu1, rs1 = layernorm_fwd(x2p, w(layer.norm1.weight), w(layer.norm1.bias), LN_EPS, cdt,
+                                     add=(z2p, None, dropp, actp), x_out=x)
+    else:
+        h1, mu1, rs1 = layernorm_fwd(x, w(layer.norm1.weight), w(layer.norm1.bias), LN_EPS, cdt)
     qkv = linear_fwd(h1, _qkv_weight(store, attn), out_dtype=cdt)
     o, lse = attention_fwd(qkv, N, S, H, hd, mask, causal=True) if attend is None else attend(qkv)
     if x.is_cuda and cdt == torch.bfloat16 and _FUSE_OUT_LN:
@@ -203,6 +213,18 @@ def _layer_forward(x, mask, layer, store, N, S, act, training, drops, attend=Non
     g1 = torch.empty(T, F4, device=x.device, dtype=cdt) if (training and act == ACT_GELU) else None
     uact = linear_fwd(h2, w(fc.up_proj.weight), bias=w(fc.up_proj.bias), act=act, aux_out=g1,
                       out_dtype=cdt, aux_deriv=g1 is not None)
+    if fuse_out is not None:
+        # x3 = x2 + drop(act(z2)) is formed by the NEXT layer's LN1 (one f32 read of x2 and one
+        # write of x3 there, beside its own reads) instead of this GEMM's epilogue (f32 residual
+        # read, f32 x3 + bf16 z2 writes under the MFMA tail: gemm7 EPI 9): the down projection
+        # is a plain product with a bias, bf16 out -- z2 itself, kept for the backward
+        z2 = linear_fwd(uact, w(fc.down_proj.weight), bias=w(fc.down_proj.bias), out_dtype=cdt)
+        fuse_out.pending = (x2, z2, drop_ffn, act)
+        x3 = torch.empty(T, D, device=x.device, dtype=torch.float32)
+        saved = None
+        if training:
+            saved = (h1, mu1, rs1, qkv, o, lse, x2, h2, mu2, rs2, g1 if g1 is not None else uact, uact, z2)
+        return x3, saved
     z2 = torch.empty(T, D, device=x.device, dtype=cdt) if training else None
     if drop_ffn is None:
         x3 = linear_fwd(uact, w(fc.down_proj.weight), bias=w(fc.down_proj.bias), act=act,
@@ -229,10 +251,14 @@ class _FfnTail:
     backward then starts from dz2.  Filled in the forward only when the layer keeps its
     activations (no recompute: z2 must exist when the consumer's backward runs)."""
 
-    __slots__ = ("z2", "act", "drop", "dz2", "bias_grad")
+    __slots__ = ("z2", "act", "drop", "dz2", "bias_grad", "fuse_next", "pending")
 
-    def __init__(self):
+    def __init__(self, fuse_next: bool = False):
         self.z2 = self.act = self.drop = self.dz2 = self.bias_grad = None
+        # forward: this layer's FFN output is added to the residual stream by the next layer's
+        # LN1 (``pending`` = (x2, z2, drop, act) until it has been)
+        self.fuse_next = fuse_next
+        self.pending = None
 
     def consume(self, ln_bwd_kwargs, T, D, device, cdt):
         """Extend a LayerNorm backward call with this tail's fused consumer (if it has one)."""
@@ -247,6 +273,9 @@ class _FfnTail:
 
 # the fused consumer needs a bf16 operand on the GPU (the kernel's gout); off: DPC_FUSE_FFN_TAIL=0
 _FUSE_TAIL = os.environ.get("DPC_FUSE_FFN_TAIL", "1") == "1"
+# the FFN down projection's residual add / act / dropout in the next layer's LN1 forward (a plain
+# bias GEMM then writes z2); off: DPC_FUSE_FFN_LN=0 (the gemm7 EPI 9 epilogue does it)
+_FUSE_FFN_LN = os.environ.get("DPC_FUSE_FFN_LN", "1") == "1"
 
 
 def _tail_ok(x, cdt):
@@ -264,7 +293,12 @@ class _LayerFn(torch.autograd.Function):
                 prev_tail=None, tail=None):
         u = layer._unit_id
         store.pre_forward(u)
-        x3, saved = _layer_forward(x, mask, layer, store, N, S, act, training and not recompute, drops)
+        pre = None
+        if prev_tail is not None and prev_tail.pending is not None:
+            pre, prev_tail.pending = prev_tail.pending, None
+        fuse = tail if (tail is not None and tail.fuse_next) else None
+        x3, saved = _layer_forward(x, mask, layer, store, N, S, act, training and not recompute, drops,
+                                   pre=pre, fuse_out=fuse)
         store.post_forward(u, training)
         if training:
             ctx.save_for_backward(x, mask, *(saved or ()))
@@ -497,12 +531,14 @@ def run_layers(model, store, x, mask, N, S, layers, training, dropout_seed=None)
         drawn = False
     recompute = bool(getattr(model, "recompute", False)) and training
     prev = None
-    for layer in layers:
+    fuse_ok = _FUSE_FFN_LN and (store.compute_dtype == torch.bfloat16 or not x.is_cuda)
+    for i, layer in enumerate(layers):
         drops = model.dropout_specs(layer, dropout_seed, drawn) if use_drop else (None, None)
-        tail = _FfnTail() if training else None
+        # the last layer of the run materialises its output (a stage boundary / the head)
+        tail = _FfnTail(fuse_next=fuse_ok and i + 1 < len(layers))
         x = _LayerFn.apply(x, mask, layer, store, N, S, act, training, drops, recompute, prev, tail)
         prev = tail
-    if prev is not None:
+    if prev is not None and training:
         x._dpc_ffn_tail = prev  # (run_head's final norm consumes the last layer's output)
     return x
 

@@ -70,6 +70,7 @@ class LNArgs(ctypes.Structure):
         ("drop_seed", P), ("drop_site", c_uint),
         ("gz", P), ("ld_gz", LL), ("gact", c_int),
         ("dx_set", c_int),
+        ("add_act", c_int),  # fwd fused add: xs = x + keep * act(add_y + add_bias)
     ]
 
 

@@ -753,6 +753,14 @@ DPC_API int dpc_gemm(const GemmArgs* a, hipStream_t stream) {
     // 8-wave / 128-wide kernels (bench/gemm_ab.py, profiles/r2_gemm/)
     impl = 20;
   }
+  // forward epilogues that read nothing per element (bias / activation / aux_out: the FFN
+  // products, whose table entries all name v9) default to v9's load-free epilogue when no table
+  // entry covers the shape -- e.g. the down projection as a bias-only product since round 6 (its
+  // residual add moved into the next LayerNorm), which the older policy sent to the 128 x 128
+  // kernel at 366 us against ~280
+  const bool fwd_epi = a->a_kmaj && a->b_kmaj && !plain_any && !a->residual && !a->accumulate && !a->aux_in &&
+                       !a->colsum && !a->act_bwd && a->K % 64 == 0 && a->K >= 192;
+  if (impl < 0 && fwd_epi && policy_impl(a) <= 0 && dpc_gemm7_ok(a)) impl = 26;
   if (impl < 0) {
     // Default per operand layout and depth, from the GPT-2 shape sweep on MI355X
     // (bench/kernels.py, profiles/kernels_r1_*.json): forward products with a short K

@@ -58,6 +58,9 @@ struct LNArgs {
   long long ld_gz;
   int gact;
   int dx_set;  // bwd: dx = LN'(dy) (dx not read) instead of dx += LN'(dy)
+  // fwd, the fused producer with an activation: xs = x + keep * act(add_y + add_bias) (Act; the
+  // FFN down projection of the previous layer, whose GEMM then writes a plain bf16 z2)
+  int add_act;
 };
 
 // Every load of the row (x, the fused add's y and bias, gamma, beta) is issued up front and
@@ -65,7 +68,9 @@ struct LNArgs {
 // the row end re-reads the last chunk and is zeroed before the sums, and the add's operands read
 // gamma (row stride 0, L1-resident) when the add has no bias.  ADD: the launch has the fused add
 // (a template parameter: the plain form loads nothing of it).
-template <int NV, bool ADD>
+// AACT (with ADD): the activation applied to the added term (Act; a template parameter so the
+// element loop stays branch-free)
+template <int NV, bool ADD, int AACT = 0>
 __global__ __launch_bounds__(256) void ln_fwd_kernel(LNArgs p) {
   const uint32_t dkey = p.drop_scale != 0.f ? drop_key_of(p.drop_seed, p.drop_site, p.drop_key) : 0u;
   const int lane = threadIdx.x & 63;
@@ -105,6 +110,13 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(LNArgs p) {
     if constexpr (ADD) {  // the fused residual add (no loads in here)
       float a[4] = {__uint_as_float(yv[i].x << 16) + ab[i].x * bsc, __uint_as_float(yv[i].x & 0xffff0000u) + ab[i].y * bsc,
                     __uint_as_float(yv[i].y << 16) + ab[i].z * bsc, __uint_as_float(yv[i].y & 0xffff0000u) + ab[i].w * bsc};
+      if constexpr (AACT == ACT_GELU) {
+        const dpc_f2_t g01 = gelu_tanh2(dpc_f2_t{a[0], a[1]}), g23 = gelu_tanh2(dpc_f2_t{a[2], a[3]});
+        a[0] = g01.x; a[1] = g01.y; a[2] = g23.x; a[3] = g23.y;
+      } else if constexpr (AACT == ACT_RELU) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) a[e] = fmaxf(a[e], 0.f);
+      }
       if (p.drop_scale != 0.f) {
         const uint32_t idx = (uint32_t)(row * p.D + 4 * c);
 #pragma unroll
@@ -348,13 +360,15 @@ using namespace dpc;
 
 template <int NV>
 static void ln_fwd_nv(const LNArgs* a, dim3 grid, hipStream_t stream) {
-  if (a->add_y) hipLaunchKernelGGL((ln_fwd_kernel<NV, true>), grid, dim3(256), 0, stream, *a);
+  if (a->add_y && a->add_act == ACT_GELU) hipLaunchKernelGGL((ln_fwd_kernel<NV, true, ACT_GELU>), grid, dim3(256), 0, stream, *a);
+  else if (a->add_y && a->add_act == ACT_RELU) hipLaunchKernelGGL((ln_fwd_kernel<NV, true, ACT_RELU>), grid, dim3(256), 0, stream, *a);
+  else if (a->add_y) hipLaunchKernelGGL((ln_fwd_kernel<NV, true>), grid, dim3(256), 0, stream, *a);
   else hipLaunchKernelGGL((ln_fwd_kernel<NV, false>), grid, dim3(256), 0, stream, *a);
 }
 
 DPC_API int dpc_layernorm_fwd(const LNArgs* a, hipStream_t stream) {
   if (a->T <= 0) return 0;
-  if (a->D % 4) return (int)hipErrorInvalidValue;
+  if (a->D % 4 || a->add_act < 0 || a->add_act > ACT_GELU) return (int)hipErrorInvalidValue;
   dim3 grid((unsigned)((a->T + 3) / 4));
   switch ((a->D + 255) / 256) {
     case 1: ln_fwd_nv<1>(a, grid, stream); break;

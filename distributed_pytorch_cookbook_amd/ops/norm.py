@@ -25,18 +25,23 @@ def layernorm_fwd(x: torch.Tensor, gamma: torch.Tensor, beta: torch.Tensor, eps:
                   add=None, x_out: torch.Tensor | None = None):
     """x [T, D] f32 -> (y [T, D] out_dtype, mean [T], rstd [T]).
 
-    ``add=(y, bias, drop)`` fuses the residual add of the projection that feeds this
-    LayerNorm: the row normalised is ``xs = x + drop(y + bias)`` (y the plain GEMM output,
-    bf16 on the HIP path; drop a ``dropout.Drop`` or None), and ``xs`` is written to
-    ``x_out`` (f32 [T, D]) -- the new residual stream, read once and written once instead of
-    the GEMM epilogue writing it and this kernel reading it back."""
+    ``add=(y, bias, drop[, act])`` fuses the residual add of the projection that feeds this
+    LayerNorm: the row normalised is ``xs = x + drop(act(y + bias))`` (y the plain GEMM output,
+    bf16 on the HIP path; drop a ``dropout.Drop`` or None; act an activation code, default none
+    -- the FFN down projection's GELU / ReLU), and ``xs`` is written to ``x_out`` (f32 [T, D]) --
+    the new residual stream, read once and written once instead of the GEMM epilogue writing it
+    and this kernel reading it back."""
     T, D = x.shape
     if add is not None and x_out is None:
         raise ValueError("layernorm_fwd: add= needs x_out")
     if not _use_hip(x, out_dtype, add):
         if add is not None:
-            y_add, b_add, drop = add
+            y_add, b_add, drop, act = (tuple(add) + (0,))[:4]
             a = y_add.float() + (b_add.float() if b_add is not None else 0.0)
+            if act:
+                from .gemm import act_fwd_ref
+
+                a = act_fwd_ref(a, act)
             if drop is not None:
                 a = a * keep_mask(drop, T, D, x.device)
             x_out.copy_(x.float() + a)
@@ -64,7 +69,7 @@ def layernorm_fwd(x: torch.Tensor, gamma: torch.Tensor, beta: torch.Tensor, eps:
         T=T, D=D, eps=float(eps), y_f32=int(out.dtype == torch.float32),
     )
     if add is not None:
-        y_add, b_add, drop = add
+        y_add, b_add, drop, act = (tuple(add) + (0,))[:4]
         if (y_add.dtype != torch.bfloat16 or y_add.stride(1) != 1 or y_add.stride(0) % 4
                 or x_out.dtype != torch.float32 or x_out.stride(1) != 1 or x_out.stride(0) % 4
                 or tuple(y_add.shape) != (T, D) or tuple(x_out.shape) != (T, D)
@@ -72,6 +77,7 @@ def layernorm_fwd(x: torch.Tensor, gamma: torch.Tensor, beta: torch.Tensor, eps:
             raise ValueError("layernorm_fwd: add= needs bf16 y [T, D], f32 bias [D], f32 x_out [T, D]")
         args.add_y, args.add_bias, args.x_out = y_add.data_ptr(), _lib.ptr(b_add), x_out.data_ptr()
         args.ld_add, args.ld_xout = y_add.stride(0), x_out.stride(0)
+        args.add_act = int(act or 0)
         if drop is not None:
             if T * D >= 2 ** 32:
                 raise ValueError("layernorm_fwd: dropout needs T * D < 2^32")

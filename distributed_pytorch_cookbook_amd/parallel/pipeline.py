@@ -273,113 +273,136 @@ def stage_costs(model, seq_len: int, groups) -> list[tuple[float, float, float]]
     return [tuple(sum(per_unit[u][k] for u in grp) for k in range(3)) for grp in groups]
 
 
-def simulate_orders(n_micro: int, costs, wmax=None, comm: float = 0.0, split_w: bool = True, fmax=None):
+def fb_order(n_micro: int, stage: int, n_stages: int, warm: int | None = None):
+    """1F1B's F / B order for one stage with ``warm`` forwards before the first backward (default
+    stages - stage - 1, PipeDream-flush)."""
+    w = n_stages - stage - 1 if warm is None else warm
+    return [op for op in schedule_1f1b_w(n_micro, min(max(w, 0), n_micro))]
+
+
+def schedule_1f1b_w(n_micro: int, warm: int):
+    order = [("F", m) for m in range(warm)]
+    f, b = warm, 0
+    while f < n_micro:
+        order.append(("F", f))
+        f += 1
+        order.append(("B", b))
+        b += 1
+    while b < n_micro:
+        order.append(("B", b))
+        b += 1
+    return order
+
+
+def simulate_orders(n_micro: int, costs, wmax=None, comm: float = 0.0, split_w: bool = True, warm=None):
     """Event simulation of a pipeline step: per-stage op orders and finish times.
 
-    ``costs[s] = (F, B, W)`` per micro-batch on stage s.  A stage, whenever it is free, runs (in
-    this priority): the next B if its gradient has arrived; a W if it already holds more than
-    ``wmax[s]`` deferred ones; the next F if its input has arrived and fewer than (stages - s)
-    micro-batches are between F and B (1F1B's activation memory); any deferred W; else it idles
-    until the next arrival.  ``split_w=False`` runs W right after its B (= 1F1B with B + W as one
-    backward).  Returns (orders, makespan, busy per stage).  Deterministic: every rank derives
-    the same orders."""
+    ``costs[s] = (F, B, W)`` per micro-batch on stage s.  Every stage runs 1F1B's F / B order
+    (``warm[s]`` forwards before its first backward, default stages - s - 1) -- the order whose
+    grouped p2p is deadlock-free under RCCL's blocking sends (``p2p_deadlock_free``; W passes do
+    not communicate, so where they sit cannot change that) -- and places the W passes: whenever
+    its next F / B has not received its input yet, a stage runs its oldest deferred W; it also
+    runs one first when it already holds more than ``wmax[s]`` (default stages) deferred W
+    passes (their dY / X operands stay resident); the rest run after its last B.
+    ``split_w=False`` runs each W right after its B (= 1F1B with B + W as one backward).
+    Returns (orders, makespan, busy per stage).  Deterministic: every rank derives the same
+    orders."""
     p = len(costs)
     if wmax is None:
         wmax = [p] * p
-    if fmax is None:
-        fmax = [p - s for s in range(p)]
+    fbs = [fb_order(n_micro, s, p, None if warm is None else warm[s]) for s in range(p)]
     INF = float("inf")
     t = [0.0] * p
-    nf, nb = [0] * p, [0] * p
+    nxt = [0] * p  # index of the stage's next F / B op
     wq = [[] for _ in range(p)]
-    fin_f, fin_b = {}, {}
+    fin = {}  # (kind, stage, m) -> finish time
     orders = [[] for _ in range(p)]
     busy = [0.0] * p
-    total = 3 * n_micro
 
-    def done(s):
-        return len(orders[s]) == total
-
-    def dep_time(s, kind):
-        """Arrival time of the next F / B input of stage s (INF: not scheduled yet)."""
-        if kind == "F":
-            m = nf[s]
-            if m >= n_micro:
-                return INF
-            return 0.0 if s == 0 else fin_f.get((s - 1, m), INF) + comm
-        m = nb[s]
-        if m >= n_micro or m >= nf[s]:
+    def ready_at(s):
+        """Arrival time of the input of stage s's next F / B (INF: not scheduled yet)."""
+        if nxt[s] >= len(fbs[s]):
             return INF
-        return fin_f[(s, m)] if s == p - 1 else fin_b.get((s + 1, m), INF) + comm
+        kind, m = fbs[s][nxt[s]]
+        if kind == "F":
+            return 0.0 if s == 0 else fin.get(("F", s - 1, m), INF) + comm
+        if s == p - 1:
+            return fin.get(("F", s, m), INF)
+        return fin.get(("B", s + 1, m), INF) + comm
 
     def run(s, kind, m, c):
         orders[s].append((kind, m))
         t[s] += c
         busy[s] += c
+        fin[(kind, s, m)] = t[s]
 
-    while not all(done(s) for s in range(p)):
-        # the stage that can act earliest (time-ordered, so every dependency that finishes
-        # before that time is already known)
+    while True:
         best = None
         for s in range(p):
-            if done(s):
+            if nxt[s] >= len(fbs[s]) and not wq[s]:
                 continue
-            if wq[s]:
-                start = t[s]
-            else:
-                fb = dep_time(s, "B")
-                ff = dep_time(s, "F") if nf[s] - nb[s] < fmax[s] else INF
-                start = max(t[s], min(fb, ff))
+            start = t[s] if wq[s] else max(t[s], ready_at(s))
             if start < INF and (best is None or start < best[0]):
                 best = (start, s)
         if best is None:
-            raise RuntimeError("pipeline simulation stalled")
+            if any(nxt[s] < len(fbs[s]) or wq[s] for s in range(p)):
+                raise RuntimeError("pipeline simulation stalled")
+            break
         start, s = best
         t[s] = start
         F, B, W = costs[s]
-        if dep_time(s, "B") <= t[s]:
-            m = nb[s]
-            nb[s] += 1
-            run(s, "B", m, B)
-            fin_b[(s, m)] = t[s]
+        if wq[s] and (len(wq[s]) > wmax[s] or ready_at(s) > t[s]):
+            run(s, "W", wq[s].pop(0), W)
+            continue
+        kind, m = fbs[s][nxt[s]]
+        nxt[s] += 1
+        run(s, kind, m, F if kind == "F" else B)
+        if kind == "B":
             if split_w:
                 wq[s].append(m)
             else:
                 run(s, "W", m, W)
-        elif wq[s] and len(wq[s]) > wmax[s]:
-            run(s, "W", wq[s].pop(0), W)
-        elif nf[s] - nb[s] < fmax[s] and dep_time(s, "F") <= t[s]:
-            m = nf[s]
-            nf[s] += 1
-            run(s, "F", m, F)
-            fin_f[(s, m)] = t[s]
-        elif wq[s]:
-            run(s, "W", wq[s].pop(0), W)
-        else:  # nothing arrived yet: wait (re-evaluated in time order)
-            nxt = min(dep_time(s, "B"), dep_time(s, "F") if nf[s] - nb[s] < fmax[s] else INF)
-            t[s] = nxt
     return orders, max(t), busy
 
 
+def zb_limits(n_micro: int, n_stages: int, mem: int = 1):
+    """(wmax, warm) per stage of the zero-bubble policies: mem 1 = H1 (1F1B's warm-up, at most
+    ``stages`` deferred W passes); mem 2 = H2-like (twice 1F1B's forwards in flight -- warm-up
+    2 (stages - s) - 1, still deadlock-free, p2p_deadlock_free; 3x is not -- and every W deferrable:
+    the early stages run most of their W passes after their last B, so the later stages'
+    start-up bubble is not repeated at the end; more HBM, which MI355X has)."""
+    p = n_stages
+    if mem == 1:
+        return [p] * p, [p - s - 1 for s in range(p)]
+    return [n_micro] * p, [2 * (p - s) - 1 for s in range(p)]
+
+
 @functools.lru_cache(maxsize=64)
-def _zb_orders(n_micro: int, costs: tuple, wmax: tuple | None):
-    orders, _, _ = simulate_orders(n_micro, list(costs), list(wmax) if wmax else None)
+def _zb_orders(n_micro: int, costs: tuple, wmax: tuple | None, mem: int = 1):
+    wm, warm = zb_limits(n_micro, len(costs), mem)
+    orders, _, _ = simulate_orders(n_micro, list(costs), list(wmax) if wmax else wm, warm=warm)
     return tuple(tuple(o) for o in orders)
 
 
-def schedule_zb(n_micro: int, stage: int, n_stages: int, costs=None, wmax=None):
-    """('F', m) / ('B', m) / ('W', m) in execution order for one stage: the zero-bubble (H1)
-    schedule of ``simulate_orders`` (``costs``: per-stage (F, B, W), default equal thirds)."""
+def schedule_zb(n_micro: int, stage: int, n_stages: int, costs=None, wmax=None, mem: int = 1):
+    """('F', m) / ('B', m) / ('W', m) in execution order for one stage: the zero-bubble schedule
+    of ``simulate_orders`` (``costs``: per-stage (F, B, W), default equal thirds; ``mem``: the
+    memory policy of ``zb_limits``)."""
     c = tuple(tuple(x) for x in costs) if costs is not None else ((1.0, 1.0, 1.0),) * n_stages
     if len(c) != n_stages:
         raise ValueError("schedule_zb: one (F, B, W) cost triple per stage")
-    return list(_zb_orders(n_micro, c, tuple(wmax) if wmax is not None else None)[stage])
+    return list(_zb_orders(n_micro, c, tuple(wmax) if wmax is not None else None, mem)[stage])
 
 
 def bubble_factor(n_micro: int, costs, schedule: str = "zb", comm: float = 0.0) -> float:
     """Modelled step time over the busiest stage's work (1.0 = no bubble) for 1F1B (B + W as one
-    backward) or the zero-bubble orders, under the cost model -- the proxy's bubble term."""
-    _, span, busy = simulate_orders(n_micro, costs, comm=comm, split_w=schedule != "1f1b")
+    backward) or the zero-bubble orders ("zb" / "zb2"), under the cost model -- the proxy's
+    bubble term."""
+    if schedule == "1f1b":
+        _, span, busy = simulate_orders(n_micro, costs, comm=comm, split_w=False)
+    else:
+        wm, warm = zb_limits(n_micro, len(costs), 2 if schedule == "zb2" else 1)
+        _, span, busy = simulate_orders(n_micro, costs, wmax=wm, comm=comm, warm=warm)
     return span / max(busy)
 
 

@@ -1,30 +1,23 @@
 #!/bin/bash
-# round 6 job 3: stock PyTorch-ROCm yardsticks for the FSDP XL / pipe medium / PP x DP large
-# configs at N = 1, 64 sequences per GPU: the reference math
-# (manual attention) + torch.compile with gradient accumulation where one 64-sequence batch of
-# scores does not fit, and SDPA + compile on the whole batch; torch FSDP-wrapped for XL
+# round 6 job 3: the FFN down projection's residual add / act / dropout moved into the next
+# layer's LN1 (plain bias GEMM for z2): LN / GEMM / model GPU tests, DDP A/B against the round-start
+# tree, the other recipes, the step's kernel table; then the stock PyTorch yardsticks
 mkdir -p gpurun_out
 export HSA_ENABLE_IPC_MODE_LEGACY=0
-# (heartbeat: torch.compile of a 48-layer model prints nothing for minutes)
 (while sleep 45; do date >> gpurun_out/r6_hb.txt; done) &
 HB=$!
 trap "kill $HB 2>/dev/null" EXIT
-out=gpurun_out/r6_stock.jsonl
-: > $out
-run() {  # <limit> <args...>
-  local lim=$1; shift
-  echo "== $*"
-  timeout -k 10 $lim python -u bench/baseline_torch.py --steps 5 --warmup 3 "$@" > gpurun_out/r6_stock_last.log 2>&1
-  local rc=$?
-  grep '^{' gpurun_out/r6_stock_last.log | tee -a $out
-  [ $rc -eq 0 ] || { tail -5 gpurun_out/r6_stock_last.log; }
-  if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
-  return 0
-}
-run 500 --model gpt2-medium --batch_size 64 --sdpa --compile
-run 500 --model gpt2-medium --batch_size 16 --accum 4 --compile
-run 600 --model gpt2-large --batch_size 64 --sdpa --compile
-run 600 --model gpt2-large --batch_size 16 --accum 4 --compile
-run 700 --model gpt2-xl --batch_size 64 --sdpa --compile
-run 700 --model gpt2-xl --batch_size 8 --accum 8 --compile
-run 700 --model gpt2-xl --batch_size 64 --sdpa --compile --fsdp
+timeout -k 10 400 python -u -m pytest tests/test_kernels_gpu.py tests/test_model_gpu.py -x -q --timeout 120 --timeout-method thread \
+  -k "layernorm or aux_deriv or act_grad_epilogue or v9_forward or decode or model or recipe or gpt2 or graph or kv" \
+  > gpurun_out/r6j3_tests.log 2>&1 || { tail -30 gpurun_out/r6j3_tests.log; exit 3; }
+tail -2 gpurun_out/r6j3_tests.log
+for r in 1 2; do
+  echo "== new"; timeout -k 10 200 python -u bench.py || exit $?
+  echo "== old"; (cd ab_old && timeout -k 10 200 python -u bench.py) || exit $?
+done > gpurun_out/r6_bench3.log 2>&1
+grep -v amdgpu.ids gpurun_out/r6_bench3.log | sed 's/"unit".*//'
+scripts/prof_bench.sh r6s3 || exit $?
+for rc in fsdp pipe pipe_ddp; do
+  timeout -k 10 300 python -u bench.py --recipe $rc --steps 6 --warmup 2 > gpurun_out/r6_b_$rc.log 2>&1 || exit $?
+  grep '^{' gpurun_out/r6_b_$rc.log | cut -c1-170
+done

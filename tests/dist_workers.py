@@ -303,8 +303,9 @@ class _FailingCapture:
     def __enter__(self):
         st = self.eng.store
         tgt = st if hasattr(st, "finish_grads") and getattr(st, "tp", None) is not None else self.eng.p2p
-        # FSDP's unit-wise path (finish_grads_and_update) fails at the same point
-        names = ["finish_grads", "finish_grads_and_update"] if tgt is st else ["drain"]
+        # FSDP's unit-wise path (finish_grads_and_update) and the bucket-by-bucket AdamW of DDP /
+        # PP x DP (wait_bucket) fail at the same point
+        names = ["finish_grads", "finish_grads_and_update", "wait_bucket"] if tgt is st else ["drain"]
         for name in names:
             if hasattr(tgt, name):
                 self.saved.append((tgt, name))

@@ -157,6 +157,8 @@ def test_pipeline_default_microbatches_divide_the_batch():
 
     f = PipelineEngine._micro_count
     assert f(SimpleNamespace(n_micro_req=0, pp=3), 64) == 8
+    # the zero-bubble schedules: at most 2 x stages (profiles/r6_pp/)
+    assert f(SimpleNamespace(n_micro_req=0, pp=8, _mfac=2), 512) == 16
     assert f(SimpleNamespace(n_micro_req=0, pp=8), 512) == 32
     assert f(SimpleNamespace(n_micro_req=0, pp=2), 128) == 8
     assert f(SimpleNamespace(n_micro_req=0, pp=5), 36) == 18

@@ -814,10 +814,13 @@ def test_dropout_kernels_match_torch_twin():
 
 
 @pytest.mark.parametrize("D,p_drop", [(768, 0.0), (1600, 0.0), (768, 0.1)])
-def test_layernorm_fwd_fused_residual_add(D, p_drop):
-    """LN forward with the projection's bias + dropout + residual add fused in:
-    xs = x + keep * (y + b) written to x_out, LN(xs) vs the torch expression."""
+@pytest.mark.parametrize("act", [0, 1, 2])
+def test_layernorm_fwd_fused_residual_add(D, p_drop, act):
+    """LN forward with the projection's bias + activation + dropout + residual add fused in:
+    xs = x + keep * act(y + b) written to x_out, LN(xs) vs the torch expression (act: the FFN
+    down projection's ReLU / GELU, whose residual add the next layer's LN1 now does)."""
     from distributed_pytorch_cookbook_amd.ops.dropout import DropSpec, keep_mask
+    from distributed_pytorch_cookbook_amd.ops.gemm import act_fwd_ref
     torch.manual_seed(13)
     T = 1000
     x = torch.randn(T, D, device=dev)
@@ -826,12 +829,12 @@ def test_layernorm_fwd_fused_residual_add(D, p_drop):
     g, be = torch.randn(D, device=dev), torch.randn(D, device=dev)
     drop = DropSpec.make(p_drop, seed=5, site=3) if p_drop else None
     xs = torch.empty(T, D, device=dev)
-    h, mu, rs = layernorm_fwd(x, g, be, 1e-5, torch.bfloat16, add=(y, b, drop), x_out=xs)
-    a = y.float() + b
+    h, mu, rs = layernorm_fwd(x, g, be, 1e-5, torch.bfloat16, add=(y, b, drop, act), x_out=xs)
+    a = act_fwd_ref(y.float() + b, act)
     if drop is not None:
         a = a * keep_mask(drop, T, D, dev)
     xs_r = x + a
-    assert rel_err(xs, xs_r) < 1e-6
+    assert rel_err(xs, xs_r) < (1e-6 if act != 2 else 1e-5)
     h_r = torch.nn.functional.layer_norm(xs_r, (D,), g, be, 1e-5)
     assert rel_err(h, h_r) < 1e-2
     assert rel_err(mu, xs_r.mean(-1)) < 1e-5

@@ -90,13 +90,15 @@ CASES = [
     ("main-fsdp.py", 4, 4, ["--reduce_dtype", "bf16"], {"all_gather", "reduce_scatter"}, False),
     # the zero-bubble schedule (deferred W passes; its DP buckets launch from them)
     ("main-pipe.py", 4, 8, ["--num_microbatches", "8", "--schedule", "zb"], {"send", "recv"}, True),
+    ("main-pipe.py", 8, 16, ["--num_microbatches", "16", "--schedule", "zb2", "--num_layers", "8"], {"send", "recv"},
+     True),
     ("main-pipe-ddp.py", 4, 4, ["--num_microbatches", "4", "--schedule", "zb"], {"send", "recv", "all_reduce"}, True),
 ]
 
 
 @pytest.mark.parametrize("script,nproc,batch,extra,ops,exact", CASES,
                          ids=["ddp2", "fsdp2", "fsdp2_bf16", "pipe2_1f1b", "pipe2xdp2", "pipe8_1f1b", "pipe4_gpipe",
-                              "pipe2xdp4", "fsdp4_bf16", "pipe4_zb", "pipe2xdp2_zb"])
+                              "pipe2xdp4", "fsdp4_bf16", "pipe4_zb", "pipe8_zb2", "pipe2xdp2_zb"])
 def test_native_transport_multirank_matches_gloo(tmp_path, fake_lib, script, nproc, batch, extra, ops, exact):
     args = [*COMMON, "--batch_size", str(batch), *extra]
     ref_dir, nat_dir, fake_dir = tmp_path / "gloo", tmp_path / "native", tmp_path / "fake"

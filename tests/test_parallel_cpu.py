@@ -1,5 +1,6 @@
 """DDP / FSDP / pipeline / pipeline x DDP engines on CPU (gloo, multi-process) must produce
 the same parameters as the single-process engine on the same global batch."""
+import itertools
 import os
 
 import pytest
@@ -219,14 +220,14 @@ def test_fsdp_forced_sharded_path_matches_fast_path():
     assert_close_sd(res[0], res[1], atol=1e-6)
 
 
-@pytest.mark.parametrize("pp,dp,micro", [(2, 1, 4), (4, 1, 8), (2, 2, 4)])
-def test_zero_bubble_equals_1f1b_exactly(tmp_path, pp, dp, micro):
+@pytest.mark.parametrize("pp,dp,micro,sched", [(2, 1, 4, "zb"), (4, 1, 8, "zb"), (2, 2, 4, "zb"), (4, 1, 8, "zb2")])
+def test_zero_bubble_equals_1f1b_exactly(tmp_path, pp, dp, micro, sched):
     """The zero-bubble schedule (B / W split, W passes deferred) reorders work, not arithmetic:
     the weight gradients of a unit are still accumulated micro-batch by micro-batch in order, so
     the trained parameters equal 1F1B's bit for bit (gloo, 2 / 4 stages, and a 2 x 2 mesh whose
     DP buckets launch from the deferred W passes)."""
     a, b = tmp_path / "zb.pt", tmp_path / "1f1b.pt"
-    run_workers(worker_pipe, pp * dp, str(a), 2, pp, dp, micro, "zb")
+    run_workers(worker_pipe, pp * dp, str(a), 2, pp, dp, micro, sched)
     run_workers(worker_pipe, pp * dp, str(b), 2, pp, dp, micro, "1f1b")
     za, zb_ = torch.load(a, weights_only=True)["sd"], torch.load(b, weights_only=True)["sd"]
     assert list(za) == list(zb_)
@@ -235,17 +236,19 @@ def test_zero_bubble_equals_1f1b_exactly(tmp_path, pp, dp, micro):
 
 
 def test_zero_bubble_orders():
-    """schedule_zb: every F / B / W of every micro-batch exactly once, B after F, W after B, at most
-    1F1B's activations in flight (and 1F1B's F / B order at equal costs); deadlock-free under RCCL's blocking p2p as run_schedule issues
+    """schedule_zb: every F / B / W of every micro-batch exactly once, B after F, W after B, 1F1B's
+    F / B order (mem 2: twice its warm-up) and so at most (mem x) 1F1B's activations in flight;
+    deadlock-free under RCCL's blocking p2p as run_schedule issues
     it (p2p_deadlock_free, which 1F1B / GPipe also pass); and a smaller modelled bubble than
     1F1B under the cost model -- at PP = 8, M = 32 within 10 % of the bubble-free time."""
-    from distributed_pytorch_cookbook_amd.parallel.pipeline import (bubble_factor, p2p_deadlock_free, schedule_gpipe,
-                                                                    schedule_zb)
+    from distributed_pytorch_cookbook_amd.parallel.pipeline import (bubble_factor, fb_order, p2p_deadlock_free,
+                                                                    schedule_gpipe, schedule_zb)
 
-    for p in (2, 3, 4, 8):
-        for M in (1, 2, p, 2 * p, 4 * p):
-            for c in ((1.0, 1.0, 1.0), (1.0, 1.4, 1.0), (0.5, 2.0, 1.5)):
-                orders = [schedule_zb(M, s, p, costs=[c] * p) for s in range(p)]
+    for p, M, c, mem in itertools.product((2, 3, 4, 8), (1, 2, 3, 8, 16), ((1.0, 1.0, 1.0), (1.0, 1.4, 1.0), (0.5, 2.0, 1.5)),
+                                          (1, 2)):
+        if True:
+            if True:
+                orders = [schedule_zb(M, s, p, costs=[c] * p, mem=mem) for s in range(p)]
                 for s, o in enumerate(orders):
                     for kind in "FBW":
                         assert [m for k, m in o if k == kind] == list(range(M)), (p, M, s, kind)
@@ -256,19 +259,24 @@ def test_zero_bubble_orders():
                     for k, _ in o:
                         inflight += 1 if k == "F" else (-1 if k == "B" else 0)
                         mx = max(mx, inflight)
-                    assert mx <= p - s, (p, M, s, mx)
-                    if c == (1.0, 1.0, 1.0):  # equal costs: exactly 1F1B's F / B order
-                        assert [op for op in o if op[0] != "W"] == schedule_1f1b(M, s, p), (p, M, s)
-                assert p2p_deadlock_free(orders), (p, M, c)
-            assert p2p_deadlock_free([schedule_1f1b(M, s, p) for s in range(p)])
-            assert p2p_deadlock_free([schedule_gpipe(M, s, p) for s in range(p)])
+                    assert mx <= mem * (p - s), (p, M, s, mx)
+                    # the F / B order is 1F1B's (mem 2: with twice the warm-up forwards)
+                    want = schedule_1f1b(M, s, p) if mem == 1 else fb_order(M, s, p, 2 * (p - s) - 1)
+                    assert [op for op in o if op[0] != "W"] == want, (p, M, s, mem)
+                assert p2p_deadlock_free(orders), (p, M, c, mem)
+                assert p2p_deadlock_free([schedule_1f1b(M, s, p) for s in range(p)])
+                assert p2p_deadlock_free([schedule_gpipe(M, s, p) for s in range(p)])
+    # 1F1B with three times the warm-up forwards is NOT deadlock-free under grouped blocking p2p
+    assert not p2p_deadlock_free([fb_order(8, s, 4, 3 * (4 - s) - 1) for s in range(4)])
     # the checker does catch a mis-ordered exchange: stage 0 expects B1 before B0
     bad = [[("F", 0), ("F", 1), ("B", 1), ("B", 0)], [("F", 0), ("B", 0), ("F", 1), ("B", 1)]]
     assert not p2p_deadlock_free(bad)
-    for p, M in ((8, 32), (2, 8)):
+    for p, M in ((8, 32), (2, 8), (8, 16)):
         costs = [(1.0, 1.2, 1.0)] * p
-        assert bubble_factor(M, costs, "zb") < bubble_factor(M, costs, "1f1b")
+        assert bubble_factor(M, costs, "zb2") <= bubble_factor(M, costs, "zb") < bubble_factor(M, costs, "1f1b")
     assert bubble_factor(32, [(1.0, 1.0, 1.0)] * 8, "zb") < 1.10
+    # the measured GPT-2 medium PP=8 stage costs (F, B, W ms, profiles/r6_pp/): zb2 at M = 16
+    assert bubble_factor(16, [(4.30, 5.19, 2.96)] * 8, "zb2") < 1.16
 
 
 def test_run_schedule_executes_zero_bubble_order():
