@@ -41,8 +41,14 @@ METRIC = "tokens/sec (node) GPT-2 training per recipe (DDP/FSDP/PP) at 1/2/4/8 M
 # bf16 autocast, fused AdamW) measured on one MI355X at the same per-GPU batch x 1024 tokens
 # (bench/baseline_torch.py --compile; profiles/r1_stock_pytorch_baselines.jsonl), scaled
 # linearly with the GPU count.
+# The other recipes (round 6, profiles/r6_stock/stock.jsonl): the same reference math + compile on one
+# MI355X at 64 sequences per GPU -- gradient accumulation where one 64-sequence batch of
+# materialised scores does not fit (medium / large 16 x 4, XL 8 x 8: the same optimizer step).
 BASELINE_TOKS_PER_GPU = {("ddp", "gpt2-small", 32, 1024): 276672.6,
-                         ("ddp", "gpt2-small", 64, 1024): 300633.0}
+                         ("ddp", "gpt2-small", 64, 1024): 300633.0,
+                         ("fsdp", "gpt2-xl", 64, 1024): 32427.5,
+                         ("pipe", "gpt2-medium", 64, 1024): 114526.6,
+                         ("pipe_ddp", "gpt2-large", 64, 1024): 57297.5}
 # Per-GPU batch (sequences) per recipe when --batch_size is not given: every recipe runs the
 # reference's own default per-rank batch (--batch_size 64, main-*.py argparse).
 # On one MI355X that is also the fastest measured (profiles/r2_recipes/batch_sweep_s4.txt):
@@ -215,7 +221,7 @@ def main():
     n = info.world_size
     par = {"ddp": f"dp{n}", "fsdp": f"fsdp{n}", "pipe": f"pp{n}",
            "pipe_ddp": f"pp{n // max(engine.dp_world, 1)}xdp{engine.dp_world}"}[a.recipe]
-    base = BASELINE_TOKS_PER_GPU.get((a.recipe, model_name, B, S))
+    base = BASELINE_TOKS_PER_GPU.get((a.recipe, model_name, a.batch_size, S))
     base = base * n if base else None
     out = {
         "metric": METRIC,
@@ -240,7 +246,7 @@ def main():
                    "mfu_per_gpu": round(mfu(value / n, train_flops_per_token(
                        args.dim, args.heads, args.head_dim, args.num_layers, vocab, S)), 4),
                    "baseline": ("stock PyTorch reference-default recipe (manual attention + torch.compile)"
-                                " x n_gpus" if base else None)},
+                                " per GPU x n_gpus" if base else None)},
     }
     if info.is_main:
         line = json.dumps(out)
