@@ -161,7 +161,7 @@ class PipelineEngine(Engine):
             x = run_embeddings(self.model, st, ids, pos, training)
         else:
             x = x_in
-        x = run_layers(self.model, st, x, mask, mb, S, self.layers, training)
+        x = run_layers(self.model, st, x, mask, mb, S, self.layers, training, head_next=self.last)
         if self.last:
             return run_head(self.model, st, x, tg, training, want_correct)
         return x
@@ -297,7 +297,7 @@ class PipelineEngine(Engine):
             st = eng.store
             if eng.first:
                 x = run_embeddings(eng.model, st, input_ids, position_ids, False)
-            x = run_layers(eng.model, st, x, None, N, S, eng.layers, False)
+            x = run_layers(eng.model, st, x, None, N, S, eng.layers, False)  # (output formed here)
             V = eng.model.vocab_size
             tok = torch.zeros(1, dtype=torch.int64, device=eng.device)
             if eng.last:

@@ -304,6 +304,7 @@ class _LayerFn(torch.autograd.Function):
             ctx.save_for_backward(x, mask, *(saved or ()))
             ctx.layer, ctx.store, ctx.dims, ctx.act = layer, store, (N, S), act
             ctx.drops, ctx.recompute = drops, recompute
+            ctx.fused_out = fuse is not None  # (the recompute re-runs the same down-projection form)
             ctx.prev_tail, ctx.tail = prev_tail, tail
             if tail is not None and saved is not None and _tail_ok(x, store.compute_dtype):
                 tail.z2, tail.act, tail.drop = saved[-1], act, drops[1]
@@ -319,7 +320,8 @@ class _LayerFn(torch.autograd.Function):
         H, hd = layer.attn.heads, layer.attn.head_dim
         store.pre_backward(layer._unit_id)
         if ctx.recompute:
-            _, saved = _layer_forward(x, mask, layer, store, N, S, act, True, ctx.drops)
+            _, saved = _layer_forward(x, mask, layer, store, N, S, act, True, ctx.drops,
+                                      fuse_out=_FfnTail() if ctx.fused_out else None)
         dx = _layer_backward(dx3, x, mask, saved, layer, store, N, S, H, hd, act, ctx.drops,
                              ctx.prev_tail, ctx.tail)
         u = layer._unit_id
@@ -421,6 +423,35 @@ def _layer_backward(dx3, x, mask, saved, layer, store, N, S, H, hd, act, drops, 
     return dx
 
 
+def _ln_in(x, pending, gamma, beta, cdt):
+    """LayerNorm of x -- or, with the previous layer's FFN output still pending (x an unwritten
+    buffer), of x2 + drop(act(z2)), written into x on the way (``_FfnTail.pending``)."""
+    if pending is None:
+        return layernorm_fwd(x, gamma, beta, LN_EPS, cdt)
+    x2p, z2p, dropp, actp = pending
+    return layernorm_fwd(x2p, gamma, beta, LN_EPS, cdt, add=(z2p, None, dropp, actp), x_out=x)
+
+
+_unit_ln = {}
+
+
+def materialize_pending(x, tail) -> None:
+    """Form a run's output x3 = x2 + drop(act(z2)) in place when no LayerNorm consumes it in the
+    same pass (a pipeline stage boundary, the last-row decode head): through the same fused
+    LayerNorm kernel (its normalised output discarded), so x3 has the same bits whichever way it is
+    formed -- a layer's position in a run never changes the math."""
+    if tail is None or tail.pending is None:
+        return
+    pending, tail.pending = tail.pending, None
+    D = x.shape[1]
+    key = (x.device, D)
+    if key not in _unit_ln:
+        _unit_ln[key] = (torch.ones(D, device=x.device), torch.zeros(D, device=x.device))
+    g, b = _unit_ln[key]
+    with torch.no_grad():
+        _ln_in(x, pending, g, b, pending[1].dtype)
+
+
 class _HeadFn(torch.autograd.Function):
     """norm_out -> lm_head -> fused cross-entropy (reference gpt.py:229-231 + main-*.py loss)."""
 
@@ -431,7 +462,10 @@ class _HeadFn(torch.autograd.Function):
         cdt = store.compute_dtype
         V = w(head.weight).shape[0]
         T = x.shape[0]
-        hf, mu, rs = layernorm_fwd(x, w(norm.weight), w(norm.bias), LN_EPS, cdt)
+        pending = None
+        if prev_tail is not None and prev_tail.pending is not None:  # the last layer's FFN output
+            pending, prev_tail.pending = prev_tail.pending, None
+        hf, mu, rs = _ln_in(x, pending, w(norm.weight), w(norm.bias), cdt)
         ld = vocab_ld(V) if x.is_cuda else V
         buf = torch.empty(T, ld, device=x.device, dtype=cdt)
         # padded columns come out 0 (B rows >= V are the layout's zero rows / read as 0)
@@ -488,14 +522,17 @@ class _HeadFn(torch.autograd.Function):
         return dx, None, None, None, None, None, None, None, None
 
 
-def head_logits(model, x, store):
-    """Inference head: logits [T, V] (view of a row-padded buffer), no loss."""
+def head_logits(model, x, store, tail=None):
+    """Inference head: logits [T, V] (view of a row-padded buffer), no loss.  ``tail``: the last
+    layer's, whose FFN output the final norm adds to the residual stream (x then unwritten)."""
     w = store.weight
     unit = model._head_unit_id
     store.pre_forward(unit)
     V = w(model.lm_head.weight).shape[0]
-    hf, _, _ = layernorm_fwd(x, w(model.norm_out.weight), w(model.norm_out.bias), LN_EPS,
-                             store.compute_dtype)
+    pending = None
+    if tail is not None and tail.pending is not None:
+        pending, tail.pending = tail.pending, None
+    hf, _, _ = _ln_in(x, pending, w(model.norm_out.weight), w(model.norm_out.bias), store.compute_dtype)
     ld = vocab_ld(V) if x.is_cuda else V
     buf = torch.empty(x.shape[0], ld, device=x.device, dtype=store.compute_dtype)
     linear_fwd(hf, w(model.lm_head.weight), out=buf)
@@ -519,9 +556,12 @@ def run_embeddings(model, store, input_ids, position_ids, training):
                           model.embeddings, store, training)
 
 
-def run_layers(model, store, x, mask, N, S, layers, training, dropout_seed=None):
+def run_layers(model, store, x, mask, N, S, layers, training, dropout_seed=None, head_next=False):
     """``training``: keep activations for the backward.  Dropout follows the module mode
-    (``model.train()`` / ``model.eval()``) like ``nn.Dropout``."""
+    (``model.train()`` / ``model.eval()``) like ``nn.Dropout``.  ``head_next``: the model's final
+    norm consumes the output in this pass (``run_head`` / ``head_logits`` with the returned
+    tensor's ``_dpc_tail``), so the last layer's residual add is left to it as every other
+    layer's is left to the next layer's LN1; otherwise the output is formed here."""
     act = act_code(model.activation)
     use_drop = model.training and model.dropout > 0
     if use_drop and dropout_seed is None:
@@ -534,18 +574,24 @@ def run_layers(model, store, x, mask, N, S, layers, training, dropout_seed=None)
     fuse_ok = _FUSE_FFN_LN and (store.compute_dtype == torch.bfloat16 or not x.is_cuda)
     for i, layer in enumerate(layers):
         drops = model.dropout_specs(layer, dropout_seed, drawn) if use_drop else (None, None)
-        # the last layer of the run materialises its output (a stage boundary / the head)
-        tail = _FfnTail(fuse_next=fuse_ok and i + 1 < len(layers))
+        # every layer hands its FFN output to the next LayerNorm (the last one to the final norm,
+        # or to materialize_pending below): one formula for x3 whatever the layer's position
+        tail = _FfnTail(fuse_next=fuse_ok)
         x = _LayerFn.apply(x, mask, layer, store, N, S, act, training, drops, recompute, prev, tail)
         prev = tail
-    if prev is not None and training:
-        x._dpc_ffn_tail = prev  # (run_head's final norm consumes the last layer's output)
+    if prev is not None:
+        if head_next:
+            x._dpc_tail = prev  # (the final norm consumes the last layer's output -- forward and backward)
+        else:
+            materialize_pending(x, prev)
+            if training:
+                x._dpc_tail = prev  # (backward only: the head's LN bwd, if any, takes dz2)
     return x
 
 
 def run_head(model, store, x, targets, training, want_correct):
     return _HeadFn.apply(x, targets.reshape(-1), model.norm_out, model.lm_head, store,
-                         model._head_unit_id, training, want_correct, getattr(x, "_dpc_ffn_tail", None))
+                         model._head_unit_id, training, want_correct, getattr(x, "_dpc_tail", None))
 
 
 def last_rows(x, N, S):
@@ -561,11 +607,12 @@ def fused_lm_forward(model, input_ids, position_ids, mask=None, targets=None, wa
     if mask is not None:
         mask = mask.to(device=input_ids.device, dtype=torch.bool).contiguous()
     x = run_embeddings(model, store, input_ids, position_ids, training)
-    x = run_layers(model, store, x, mask, N, S, model.decoder.layers, training, dropout_seed)
+    x = run_layers(model, store, x, mask, N, S, model.decoder.layers, training, dropout_seed,
+                   head_next=not (targets is None and last_only))
     if targets is None:
         if last_only:  # decode: LM head on the last position only ([N, 1, V]; T x fewer FLOPs)
             return head_logits(model, last_rows(x, N, S), store).reshape(N, 1, -1)
-        return head_logits(model, x, store).reshape(N, S, -1)
+        return head_logits(model, x, store, getattr(x, "_dpc_tail", None)).reshape(N, S, -1)
     loss, n_valid, n_correct = run_head(model, store, x, targets, training, want_correct)
     return LMOutput(loss, n_valid, n_correct if want_correct else None)
 
