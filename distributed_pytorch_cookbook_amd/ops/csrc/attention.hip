@@ -532,7 +532,10 @@ struct PairItem {
   int bh, blk0, blk1, len0, len;
 };
 
-template <int HD, int OCC, bool LMFMA>
+// LAZY: the running max moves only when a tile max exceeds it by > 2^8 (a wave-uniform branch; the
+// default); false: rescale O every tile (no branch, no join copies of the accumulators -- variants
+// 9 / 10 of DPC_ATTN_VAR, round-6 A/B)
+template <int HD, int OCC, bool LMFMA, bool LAZY = true>
 __global__ __launch_bounds__(256, OCC) void attn_fwd2_kernel(AttnArgs p, int nitems) {
   using A = AT<HD>;
   __shared__ __attribute__((aligned(16))) bf16_t smem[NSLOT * 2 * A::TILE];  // [slot][K|V] or [slot][Q lo|Q hi]
@@ -725,7 +728,7 @@ __global__ __launch_bounds__(256, OCC) void attn_fwd2_kernel(AttnArgs p, int nit
       mx = fmaxf(__uint_as_float(sw[0]), __uint_as_float(sw[1])) * c;  // scaled log2 units (c > 0)
     }
     // lazy rescale: the running max only moves when the tile max exceeds it by > 2^8
-    if (__ballot(mx > m + 8.f)) {
+    if (!LAZY || __ballot(mx > m + 8.f)) {
       const float mn = fmaxf(m, mx);
       const float alpha = (m == -INFINITY) ? 1.f : fast_exp2(m - mn);
       m = mn;
@@ -1185,7 +1188,7 @@ __global__ __launch_bounds__(256, OCC) void attn_bwd_dq_kernel(AttnArgs p) {
 // 0 = software-pipelined, 2 workgroups / CU; 1 = plain order, 2 / CU; 2 = plain, 3 / CU;
 // 3 = pipelined, 3 / CU; 4 (forward only) = pipelined + fragments up front + pinned interleave;
 // forward only: 5 / 6 = pair stream (attn_fwd2_kernel) with / without the MFMA row sum,
-// 7 / 8 = the same on a persistent grid.
+// 7 / 8 = the same on a persistent grid, 9 / 10 = 6 / 5 with the O rescale on every tile.
 // Defaults per head size (GPT-2 small shape, B=64 S=1023 H=12, profiles/r2_attn/):
 //   hd 64: forward 6, backward 1;  hd 32: forward 2, backward 2.
 static int g_attn_env[2] = {-2, -2};
@@ -1227,11 +1230,14 @@ template <int HD>
 static int launch_fwd(const AttnArgs* a, hipStream_t stream) {
   const int var = attn_var(HD, 0);
   dim3 grid((unsigned)(((a->S + QB - 1) / QB) * a->N * a->H));  // 1-D: xcd_work() maps it
-  if (var >= 5 && var <= 8) {  // pair stream (attn_fwd2_kernel); 7, 8: persistent grid
+  if (var >= 5 && var <= 10) {  // pair stream (attn_fwd2_kernel); 7, 8: persistent grid; 9, 10: = 6, 5
+    // with the O rescale on every tile (no lazy-rescale branch)
     const int nqb = (a->S + QB - 1) / QB;
     const int nitems = ((nqb + 1) / 2) * a->N * a->H;
-    dim3 g2((unsigned)((var >= 7 && nitems > 512) ? 512 : nitems));
-    if (var == 5 || var == 8) hipLaunchKernelGGL((attn_fwd2_kernel<HD, 2, true>), g2, dim3(256), 0, stream, *a, nitems);
+    dim3 g2((unsigned)((var == 7 || var == 8) && nitems > 512 ? 512 : nitems));
+    if (var == 9) hipLaunchKernelGGL((attn_fwd2_kernel<HD, 2, false, false>), g2, dim3(256), 0, stream, *a, nitems);
+    else if (var == 10) hipLaunchKernelGGL((attn_fwd2_kernel<HD, 2, true, false>), g2, dim3(256), 0, stream, *a, nitems);
+    else if (var == 5 || var == 8) hipLaunchKernelGGL((attn_fwd2_kernel<HD, 2, true>), g2, dim3(256), 0, stream, *a, nitems);
     else hipLaunchKernelGGL((attn_fwd2_kernel<HD, 2, false>), g2, dim3(256), 0, stream, *a, nitems);
   } else if (var == 4) hipLaunchKernelGGL((attn_fwd_kernel<HD, 2, 2>), grid, dim3(256), 0, stream, *a);
   else DPC_ATTN_SWITCH(var, attn_fwd_kernel, grid, dim3(256), 0, stream, *a);
