@@ -151,4 +151,7 @@ def test_dropout_step_graph_replays_fresh_masks():
     assert graphed._stepper.graph is not None, "the dropout step was not captured"
     for a, b in zip(le, lg):
         assert abs(a - b) < 1e-3, (le, lg)
-    close(sdg, sde, tol=1e-3, steps=4)
+    # the LayerNorm backward sums dgamma / dbeta across workgroups with atomics, so the two runs
+    # are not bitwise equal and Adam's ~lr step on a near-zero bias gradient can flip; measured
+    # 1.1e-3 on a bias.  Stale masks on 10 % of the elements part the weights by O(0.1).
+    close(sdg, sde, tol=5e-3, steps=4)
