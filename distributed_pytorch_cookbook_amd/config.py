@@ -39,8 +39,8 @@ def build_parser(recipe: str = "single") -> argparse.ArgumentParser:
                    help="architecture preset (overrides dim/head_dim/heads/num_layers/sequence_length)")
     p.add_argument("--activation", type=str, default=None, choices=["relu", "gelu"])
     p.add_argument("--graph", action="store_true",
-                   help="capture the step into a HIP graph also at N > 1 (RCCL collectives inside the "
-                        "graph); by default only a one-rank run is captured, N > 1 runs eager steps")
+                   help="(kept for old command lines: the step is captured into a HIP graph on every "
+                        "rank by default, RCCL collectives inside; --disable_compile runs eager steps)")
     p.add_argument("--grad_scaler", action="store_true",
                    help="dynamic loss scaling as the reference's GradScaler (fused non-finite check, "
                         "skip + back-off on device); unnecessary for bf16, off by default")

@@ -36,6 +36,7 @@
 
 #include <cstdio>
 #include <cstdlib>
+#include <type_traits>
 
 namespace dpc {
 
@@ -252,6 +253,63 @@ __device__ __forceinline__ void zero_if_gt(floatx16& x, int r, int v) {
                : "n"(K), "v"(v)
                : "vcc");
 }
+
+// x *= a when `up` (a wave ballot, SGPR pair) is non-zero.  The branch sits INSIDE the asm statement, so the
+// compiler sees straight-line code and has no join after which to copy the accumulator (a C++
+// branch around scale16 gave both O accumulators new registers and a copy back on the path that
+// did not rescale: 16 v_mov_b64 on most tiles, round-6 listing of attn_fwd2_kernel).  The s_nops
+// keep the MFMA-result -> VALU and VALU -> MFMA-SrcC distances on the (rare) taken path, which the
+// hazard recognizer cannot see inside asm.
+#define DPC_RS_MUL(i) "v_mul_f32 %" #i ", %" #i ", %16\n\t"
+__device__ __forceinline__ void scale16_if(floatx16& x, float a, unsigned long long up) {
+  asm volatile(
+      "s_cmp_eq_u64 %17, 0\n\t"
+      "s_cbranch_scc1 .Ldpc_rs%=\n\t"
+      "s_nop 7\n\ts_nop 7\n\t"
+      DPC_RS_MUL(0) DPC_RS_MUL(1) DPC_RS_MUL(2) DPC_RS_MUL(3) DPC_RS_MUL(4) DPC_RS_MUL(5) DPC_RS_MUL(6)
+      DPC_RS_MUL(7) DPC_RS_MUL(8) DPC_RS_MUL(9) DPC_RS_MUL(10) DPC_RS_MUL(11) DPC_RS_MUL(12)
+      DPC_RS_MUL(13) DPC_RS_MUL(14) DPC_RS_MUL(15)
+      "s_nop 7\n"
+      ".Ldpc_rs%=:"
+      : "+v"(x[0]), "+v"(x[1]), "+v"(x[2]), "+v"(x[3]), "+v"(x[4]), "+v"(x[5]), "+v"(x[6]), "+v"(x[7]),
+        "+v"(x[8]), "+v"(x[9]), "+v"(x[10]), "+v"(x[11]), "+v"(x[12]), "+v"(x[13]), "+v"(x[14]), "+v"(x[15])
+      : "v"(a), "s"(up)
+      : "scc");
+}
+#undef DPC_RS_MUL
+
+// The plain tile's whole lazy-rescale update, when the ballot `up` is non-zero: mn = max(m, mx), alpha = 2^(m - mn),
+// m = mn, l *= alpha, x *= alpha (the first O accumulator); alpha is returned for the others
+// (scale16_if).  Nothing of it runs on the tiles that keep the running max (most of them): fwd2
+// formed alpha and selected m / l on every tile.  m = -inf (a block's first tile) gives alpha = 0
+// on zero accumulators; up is never set with mx = -inf.  s_nop 0 after v_exp: gfx950's
+// transcendental-result wait state; v_swap_b32 leaves m = mn and alpha in a (one temporary).
+#define DPC_RS_MUL(i) "v_mul_f32 %" #i ", %" #i ", %17\n\t"
+__device__ __forceinline__ float rescale16_if(floatx16& x, float& m, float& l, float mx, unsigned long long up) {
+  float a;
+  asm volatile(
+      "s_cmp_eq_u64 %20, 0\n\t"
+      "s_cbranch_scc1 .Ldpc_ru%=\n\t"
+      "s_nop 7\n\ts_nop 7\n\t"
+      "v_max_f32 %17, %16, %19\n\t"
+      "v_sub_f32 %16, %16, %17\n\t"
+      "v_exp_f32 %16, %16\n\t"
+      "s_nop 0\n\t"
+      "v_swap_b32 %16, %17\n\t"
+      "v_mul_f32 %18, %18, %17\n\t"
+      DPC_RS_MUL(0) DPC_RS_MUL(1) DPC_RS_MUL(2) DPC_RS_MUL(3) DPC_RS_MUL(4) DPC_RS_MUL(5) DPC_RS_MUL(6)
+      DPC_RS_MUL(7) DPC_RS_MUL(8) DPC_RS_MUL(9) DPC_RS_MUL(10) DPC_RS_MUL(11) DPC_RS_MUL(12)
+      DPC_RS_MUL(13) DPC_RS_MUL(14) DPC_RS_MUL(15)
+      "s_nop 7\n"
+      ".Ldpc_ru%=:"
+      : "+v"(x[0]), "+v"(x[1]), "+v"(x[2]), "+v"(x[3]), "+v"(x[4]), "+v"(x[5]), "+v"(x[6]), "+v"(x[7]),
+        "+v"(x[8]), "+v"(x[9]), "+v"(x[10]), "+v"(x[11]), "+v"(x[12]), "+v"(x[13]), "+v"(x[14]), "+v"(x[15]),
+        "+v"(m), "=&v"(a), "+v"(l)
+      : "v"(mx), "s"(up)
+      : "scc");
+  return a;
+}
+#undef DPC_RS_MUL
 
 __device__ __forceinline__ void zero16(floatx16& x) {
 #pragma unroll
@@ -532,10 +590,7 @@ struct PairItem {
   int bh, blk0, blk1, len0, len;
 };
 
-// LAZY: the running max moves only when a tile max exceeds it by > 2^8 (a wave-uniform branch; the
-// default); false: rescale O every tile (no branch, no join copies of the accumulators -- variants
-// 9 / 10 of DPC_ATTN_VAR, round-6 A/B)
-template <int HD, int OCC, bool LMFMA, bool LAZY = true>
+template <int HD, int OCC, bool LMFMA>
 __global__ __launch_bounds__(256, OCC) void attn_fwd2_kernel(AttnArgs p, int nitems) {
   using A = AT<HD>;
   __shared__ __attribute__((aligned(16))) bf16_t smem[NSLOT * 2 * A::TILE];  // [slot][K|V] or [slot][Q lo|Q hi]
@@ -728,7 +783,7 @@ __global__ __launch_bounds__(256, OCC) void attn_fwd2_kernel(AttnArgs p, int nit
       mx = fmaxf(__uint_as_float(sw[0]), __uint_as_float(sw[1])) * c;  // scaled log2 units (c > 0)
     }
     // lazy rescale: the running max only moves when the tile max exceeds it by > 2^8
-    if (!LAZY || __ballot(mx > m + 8.f)) {
+    if (__ballot(mx > m + 8.f)) {
       const float mn = fmaxf(m, mx);
       const float alpha = (m == -INFINITY) ? 1.f : fast_exp2(m - mn);
       m = mn;
@@ -766,6 +821,283 @@ __global__ __launch_bounds__(256, OCC) void attn_fwd2_kernel(AttnArgs p, int nit
   for (int e = 0; e < total; e += 2) {
     step(e, s0, s1);
     if (e + 1 < total) step(e + 1, s1, s0);
+  }
+  finish();
+  vm_wait<0>();  // the pieces issued past the end (empty descriptors) drained
+}
+
+// Forward, round 6 (DPC_ATTN_VAR 9 / 10): attn_fwd2_kernel's pair stream, DMA ring and math with
+// the consume side split by tile kind.  fwd2 ran ONE step body for every element (block start,
+// masked tile, skipped tile, plain tile), and at its joins the compiler copied the score and O
+// accumulators: 48 v_mov_b64 per plain tile in its gfx950 listing, ~1/4 of the tile's VALU.  Here,
+// per block and wave, the leading tiles that need no mask and have a successor tile run in a
+// two-tile unrolled loop of straight-line code (no mask, no skip, the next tile's scores always
+// formed, the lazy rescale's branch inside asm: scale16_if); the block's other tiles -- the
+// causal diagonal, past the end, padded, or skipped by this wave -- take the general body one
+// at a time, with one explicit copy of the next scores each.
+template <int HD, int OCC, bool LMFMA>
+__global__ __launch_bounds__(256, OCC) void attn_fwd3_kernel(AttnArgs p, int nitems) {
+  using A = AT<HD>;
+  __shared__ __attribute__((aligned(16))) bf16_t smem[NSLOT * 2 * A::TILE];  // [slot][K|V] or [slot][Q lo|Q hi]
+  const int S = p.S, H = p.H;
+  const int nqb = (S + QB - 1) / QB;
+  const int npr = (nqb + 1) / 2;
+  const int grid = gridDim.x;
+  const int local = g7_local_attn(blockIdx.x, grid);
+  const int lane = threadIdx.x & 63, hh = lane >> 5;
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  auto ntiles_of = [&](int qb) {
+    const int kend = p.causal ? min(S, qb * QB + QB) : S;
+    return (kend + KT - 1) / KT;
+  };
+  auto item = [&](int k) {  // k-th item of this workgroup
+    PairItem it;
+    const int id = local + k * grid;
+    it.bh = id / npr;
+    const int pr = id - it.bh * npr;
+    it.blk0 = nqb - 1 - pr;
+    it.blk1 = pr;
+    it.len0 = 1 + ntiles_of(it.blk0);
+    it.len = it.len0 + (it.blk1 != it.blk0 ? 1 + ntiles_of(it.blk1) : 0);
+    return it;
+  };
+  const int nmine = local < nitems ? (nitems - local + grid - 1) / grid : 0;
+  if (nmine == 0) return;
+
+  int dv[A::NPW];
+  dma_voff<HD>(dv, p.ld_qkv, wid, lane);
+  // ---- issue cursor (as attn_fwd2_kernel): element e+3 is issued while element e is consumed
+  int is_k = 0, is_off = 0;
+  PairItem is_it = item(0);
+  long long is_hoff = 0;
+  auto enter = [&]() {
+    const int n = is_it.bh / H, h = is_it.bh - n * H;
+    is_hoff = (long long)n * S * p.ld_qkv + h * HD;
+  };
+  enter();
+  auto issue_next = [&](int e) {
+    bf16_t* st = smem + (e % NSLOT) * 2 * A::TILE;
+    const bool valid = is_k < nmine;
+    const bool second = is_off >= is_it.len0;
+    const int i = is_off - (second ? is_it.len0 : 0);
+    if (i == 0 || !valid) {
+      const bf16_t* base = static_cast<const bf16_t*>(p.q) + is_hoff;
+      const int r0 = (second ? is_it.blk1 : is_it.blk0) * QB;
+      tile_dma<HD>(base, p.ld_qkv, r0, S, valid, dv, st, wid);
+      tile_dma<HD>(base, p.ld_qkv, r0 + KT, S, valid, dv, st + A::TILE, wid);
+    } else {
+      const bf16_t* K = static_cast<const bf16_t*>(p.k) + is_hoff;
+      const bf16_t* V = static_cast<const bf16_t*>(p.v) + is_hoff;
+      tile_dma<HD>(K, p.ld_qkv, (i - 1) * KT, S, true, dv, st, wid);
+      tile_dma<HD>(V, p.ld_qkv, (i - 1) * KT, S, true, dv, st + A::TILE, wid);
+    }
+    if (valid && ++is_off == is_it.len) {
+      is_off = 0;
+      if (++is_k < nmine) {
+        is_it = item(is_k);
+        enter();
+      }
+    }
+  };
+  auto sync = [&](int e) {
+    vm_wait<2 * A::NPW>();  // this wave's pieces of element e+1 landed (e+2 may fly)
+    ring_barrier();         // ... every wave's; every wave is done with element e-1's slot
+    issue_next(e + 3);
+  };
+  auto slot = [&](int e) -> const bf16_t* { return smem + (e % NSLOT) * 2 * A::TILE; };
+
+  const float c = p.scale * LOG2E;
+  bf16x8 qf[A::NST];
+  float m = -INFINITY, l = 0.f;
+  constexpr int NO = A::NDT + (LMFMA ? 1 : 0);  // O^T blocks (+ the row-sum block)
+  floatx16 o[NO];
+  int q0 = 0, q = 0, last_w = 0;
+  int bh = 0, h = 0, n = 0;
+  const unsigned char* pad = nullptr;
+  bf16x8 ones;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) ones[i] = (__bf16)1.0f;
+
+  auto qk = [&](floatx16 (&s)[2], const bf16_t* lk) {
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb) {
+      zero16(s[kb]);
+#pragma unroll
+      for (int st = 0; st < A::NST; ++st) s[kb] = MFMA32(row_frag<HD>(lk, kb * 32, st, lane), qf[st], s[kb]);
+    }
+  };
+  auto finish = [&]() {  // the block's O and lse
+    if constexpr (LMFMA) l = o[A::NDT][0];
+    else l += __shfl_xor(l, 32, 64);
+    if (q < S) {
+      const float inv = l > 0.f ? __builtin_amdgcn_rcpf(l) : 0.f;
+      bf16_t* O = static_cast<bf16_t*>(p.o) + (long long)n * S * p.ld_o + h * HD + q * (int)p.ld_o;
+#pragma unroll
+      for (int d = 0; d < A::NDT; ++d)
+#pragma unroll
+        for (int g = 0; g < 4; g += 2) {
+          uint2 wa, wb;
+          wa.x = pack2bf(o[d][4 * g + 0] * inv, o[d][4 * g + 1] * inv);
+          wa.y = pack2bf(o[d][4 * g + 2] * inv, o[d][4 * g + 3] * inv);
+          wb.x = pack2bf(o[d][4 * g + 4] * inv, o[d][4 * g + 5] * inv);
+          wb.y = pack2bf(o[d][4 * g + 6] * inv, o[d][4 * g + 7] * inv);
+          store_pair16(O + d * 32, g, hh, wa, wb);
+        }
+      if (hh == 0) p.lse[(long long)bh * S + q] = (l > 0.f) ? (m + log2f(l)) / LOG2E : INFINITY;
+    }
+  };
+  // one KV tile (element e, tile t of the block): sc = this tile's raw scores -> P, O += V^T P^T,
+  // and the next tile's scores into sn.  GEN: the general body (mask, C++ lazy branch, the next
+  // scores only if this wave needs that tile); otherwise the plain straight-line body.
+  auto tile = [&](auto gen, int e, int t, floatx16 (&sc)[2], floatx16 (&sn)[2]) {
+    constexpr bool GEN = decltype(gen)::value;
+    const bf16_t* ls = slot(e);
+    const bf16_t* lv = ls + A::TILE;
+    const int kt0 = t * KT;
+    if constexpr (GEN) {
+      const bool need_mask = (p.causal && kt0 + KT - 1 > q0) || (kt0 + KT > S) || pad;  // wave-uniform
+      if (need_mask) {
+        const int limh = (p.causal ? min(q, S - 1) : S - 1) - kt0 - 4 * hh;
+        const unsigned long long pm = pad_bits(pad, kt0, S, lane) >> (4 * hh);
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb) {
+          const unsigned pk = (unsigned)(pm >> (32 * kb));
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const int kc = kb * 32 + (r & 3) + 8 * (r >> 2);
+            const bool masked = (kc > limh) || ((pk >> ((r & 3) + 8 * (r >> 2))) & 1u);
+            if (masked) sc[kb][r] = -INFINITY;
+          }
+        }
+      }
+    }
+    float mq[4];
+#pragma unroll
+    for (int q4 = 0; q4 < 4; ++q4) {
+      const floatx16& sq = sc[q4 >> 1];
+      const int r0 = (q4 & 1) * 8;
+      float v = max3f(sq[r0], sq[r0 + 1], sq[r0 + 2]);
+      v = max3f(v, sq[r0 + 3], sq[r0 + 4]);
+      v = max3f(v, sq[r0 + 5], sq[r0 + 6]);
+      mq[q4] = fmaxf(v, sq[r0 + 7]);
+    }
+    float mx = fmaxf(max3f(mq[0], mq[1], mq[2]), mq[3]);
+    {
+      const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(mx), __float_as_uint(mx), false, false);
+      mx = fmaxf(__uint_as_float(sw[0]), __uint_as_float(sw[1])) * c;  // scaled log2 units (c > 0)
+    }
+    // lazy rescale: the running max only moves when the tile max exceeds it by > 2^8
+    if constexpr (GEN) {
+      if (__ballot(mx > m + 8.f)) {
+        const float mn = fmaxf(m, mx);
+        const float alpha = (m == -INFINITY) ? 1.f : fast_exp2(m - mn);
+        m = mn;
+        if constexpr (!LMFMA) l *= alpha;
+#pragma unroll
+        for (int d = 0; d < NO; ++d) scale16(o[d], alpha);
+      }
+    } else {
+      static_assert(!LMFMA, "plain tiles: the row sum in l");
+      const unsigned long long up = __ballot(mx > m + 8.f);
+      const float alpha = rescale16_if(o[0], m, l, mx, up);
+#pragma unroll
+      for (int d = 1; d < NO; ++d) scale16_if(o[d], alpha, up);
+    }
+    // (a plain tile has no masked score, so m is finite after its update)
+    const float nmu = (!GEN || m != -INFINITY) ? -m : 0.f;
+    if constexpr (GEN) {
+      if (t + 1 <= last_w) qk(sn, slot(e + 1));
+    } else {
+      qk(sn, slot(e + 1));  // next tile's scores beside this tile's exponentials
+    }
+    float lq[4] = {0.f, 0.f, 0.f, 0.f};
+    bf16x8 pb[2][2];
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const float ex = fast_exp2(fmaf(sc[kb][r], c, nmu));
+        sc[kb][r] = ex;
+        if constexpr (!LMFMA) lq[r & 3] += ex;
+      }
+      pb[kb][0] = acc_frag(sc[kb], 0);
+      pb[kb][1] = acc_frag(sc[kb], 1);
+    }
+    if constexpr (!LMFMA) l += (lq[0] + lq[1]) + (lq[2] + lq[3]);
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+      for (int ss = 0; ss < 2; ++ss) {
+#pragma unroll
+        for (int d = 0; d < A::NDT; ++d)
+          o[d] = MFMA32(tr_frag<HD>(lv, kb * 32, ss, d * 32, lane), pb[kb][ss], o[d]);
+        if constexpr (LMFMA) o[A::NDT] = MFMA32(ones, pb[kb][ss], o[A::NDT]);
+      }
+  };
+  using Plain = std::integral_constant<bool, false>;
+  using General = std::integral_constant<bool, true>;
+
+  issue_next(0);
+  issue_next(1);
+  issue_next(2);
+  floatx16 sA[2], sB[2];
+  int e = 0;
+  for (int k = 0; k < nmine; ++k) {
+    const PairItem it = item(k);
+    for (int half = 0; half < 2; ++half) {
+      if (half == 1 && it.blk1 == it.blk0) break;
+      const int blk = half ? it.blk1 : it.blk0;
+      // ---- block start: the previous block's O, then this block's Q and first scores
+      sync(e);
+      const bf16_t* ls = slot(e);
+      if (e > 0) finish();
+      if (half == 0) {
+        bh = it.bh;
+        n = bh / H;
+        h = bh - n * H;
+        pad = p.pad ? p.pad + (long long)n * S : nullptr;
+      }
+      q0 = blk * QB + wid * 32;
+      q = q0 + (lane & 31);
+      const int nt = ntiles_of(blk);
+      last_w = p.causal ? min(nt - 1, max(0, min(q0 + 31, S - 1)) / KT) : nt - 1;
+#pragma unroll
+      for (int st = 0; st < A::NST; ++st) qf[st] = row_frag<HD>(ls + (wid >> 1) * A::TILE, 32 * (wid & 1), st, lane);
+      m = -INFINITY;
+      l = 0.f;
+#pragma unroll
+      for (int d = 0; d < NO; ++d) zero16(o[d]);
+      qk(sA, slot(e + 1));
+      ++e;
+      // ---- plain tiles: no mask (inside S, no padding, wholly at or below the wave's first
+      // query) and followed by another tile of this wave
+      int nf = pad ? 0 : min(last_w, S / KT);
+      if (p.causal) nf = min(nf, (q0 + 1) / KT);
+      int t = 0;
+      for (; t + 2 <= nf; t += 2, e += 2) {
+        sync(e);
+        tile(Plain(), e, t, sA, sB);
+        sync(e + 1);
+        tile(Plain(), e + 1, t + 1, sB, sA);
+      }
+      if (t < nf) {
+        sync(e);
+        tile(Plain(), e, t, sA, sB);
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb) sA[kb] = sB[kb];
+        ++e;
+        ++t;
+      }
+      // ---- the rest of the block's tiles: masked, the wave's last, or skipped by this wave
+      for (; t < nt; ++t, ++e) {
+        sync(e);
+        if (t <= last_w) {  // wave-uniform
+          tile(General(), e, t, sA, sB);
+#pragma unroll
+          for (int kb = 0; kb < 2; ++kb) sA[kb] = sB[kb];
+        }
+      }
+    }
   }
   finish();
   vm_wait<0>();  // the pieces issued past the end (empty descriptors) drained
@@ -1188,9 +1520,10 @@ __global__ __launch_bounds__(256, OCC) void attn_bwd_dq_kernel(AttnArgs p) {
 // 0 = software-pipelined, 2 workgroups / CU; 1 = plain order, 2 / CU; 2 = plain, 3 / CU;
 // 3 = pipelined, 3 / CU; 4 (forward only) = pipelined + fragments up front + pinned interleave;
 // forward only: 5 / 6 = pair stream (attn_fwd2_kernel) with / without the MFMA row sum,
-// 7 / 8 = the same on a persistent grid, 9 / 10 = 6 / 5 with the O rescale on every tile.
-// Defaults per head size (GPT-2 small shape, B=64 S=1023 H=12, profiles/r2_attn/):
-//   hd 64: forward 6, backward 1;  hd 32: forward 2, backward 2.
+// 7 / 8 = the same on a persistent grid, 9 = 6 with the tile loop split by kind (attn_fwd3_kernel;
+// its MFMA-row-sum form spilled 80 registers and ran 272 us, so it is not built).
+// Defaults per head size (GPT-2 small shape, B=64 S=1023 H=12, profiles/r2_attn/, round 6:
+// profiles/r6_attn/):  hd 64: forward 9, backward 1;  hd 32: forward 2, backward 2.
 static int g_attn_env[2] = {-2, -2};
 static int attn_var(int hd, int bwd) {
   if (g_attn_env[0] == -2) {
@@ -1199,7 +1532,7 @@ static int attn_var(int hd, int bwd) {
   }
   if (g_attn_env[bwd] >= 0) return g_attn_env[bwd];
   if (hd == 32) return 2;
-  return bwd ? 1 : 6;
+  return bwd ? 1 : 9;
 }
 
 #define DPC_ATTN_SWITCH(var, KERNEL, ...)                                                   \
@@ -1230,13 +1563,12 @@ template <int HD>
 static int launch_fwd(const AttnArgs* a, hipStream_t stream) {
   const int var = attn_var(HD, 0);
   dim3 grid((unsigned)(((a->S + QB - 1) / QB) * a->N * a->H));  // 1-D: xcd_work() maps it
-  if (var >= 5 && var <= 10) {  // pair stream (attn_fwd2_kernel); 7, 8: persistent grid; 9, 10: = 6, 5
-    // with the O rescale on every tile (no lazy-rescale branch)
+  if (var >= 5 && var <= 9) {  // pair stream (attn_fwd2_kernel); 7, 8: persistent grid; 9: = 6 with
+    // the tile loop split by kind (attn_fwd3_kernel)
     const int nqb = (a->S + QB - 1) / QB;
     const int nitems = ((nqb + 1) / 2) * a->N * a->H;
     dim3 g2((unsigned)((var == 7 || var == 8) && nitems > 512 ? 512 : nitems));
-    if (var == 9) hipLaunchKernelGGL((attn_fwd2_kernel<HD, 2, false, false>), g2, dim3(256), 0, stream, *a, nitems);
-    else if (var == 10) hipLaunchKernelGGL((attn_fwd2_kernel<HD, 2, true, false>), g2, dim3(256), 0, stream, *a, nitems);
+    if (var == 9) hipLaunchKernelGGL((attn_fwd3_kernel<HD, 2, false>), g2, dim3(256), 0, stream, *a, nitems);
     else if (var == 5 || var == 8) hipLaunchKernelGGL((attn_fwd2_kernel<HD, 2, true>), g2, dim3(256), 0, stream, *a, nitems);
     else hipLaunchKernelGGL((attn_fwd2_kernel<HD, 2, false>), g2, dim3(256), 0, stream, *a, nitems);
   } else if (var == 4) hipLaunchKernelGGL((attn_fwd_kernel<HD, 2, 2>), grid, dim3(256), 0, stream, *a);

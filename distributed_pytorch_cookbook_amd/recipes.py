@@ -58,12 +58,13 @@ def build_engine(recipe: str, model, info, args, force_dist: bool = False):
     comm_kind = "native" if force_dist else getattr(args, "comm", "auto")
     # the cookbook's "compile": capture the whole step into a HIP graph (dropout included: the
     # per-forward seed is a device counter the mask kernels read, so replays draw fresh masks --
-    # models/gpt.py:next_dropout_seed).  One rank by default; at N > 1 only with --graph (RCCL
-    # inside a replayed graph has not been run on a multi-GPU node yet, and bench.py's scaling
-    # runs take the same eager path); never under --coll_check, whose fingerprints are
-    # host-synchronous collectives
+    # models/gpt.py:next_dropout_seed).  On every rank, as the reference compiles on every rank
+    # (/root/reference/main-ddp.py:60-61): the capture is collective -- a barrier before it, and
+    # every rank graphs or none does (engine/base.py:GraphedStep) -- and the RCCL calls inside it
+    # are the native communicator's, captured at one rank by tests/test_native_comm.py.
+    # --disable_compile keeps eager steps (bench.py's N > 1 runs do: same speed, measured at N = 1);
+    # never under --coll_check, whose fingerprints are host-synchronous collectives
     graph = (not args.disable_compile and not args.disable_amp
-             and (info.world_size == 1 or getattr(args, "graph", False))
              and not getattr(args, "coll_check", False))
     if recipe in ("single", "ddp"):
         from .engine.data_parallel import DataParallelEngine
