@@ -66,9 +66,10 @@ def build_parser(recipe: str = "single") -> argparse.ArgumentParser:
     p.add_argument("--bucket_mb", type=float, default=128.0, help="DDP gradient bucket size")
     p.add_argument("--reduce_dtype", type=str, default="fp32", choices=["fp32", "bf16"])
     p.add_argument("--no_overlap", action="store_true", help="all-reduce after backward instead of during")
-    p.add_argument("--comm", default=os.environ.get("DPC_COMM", "auto"), choices=["auto", "torch", "native"],
+    p.add_argument("--comm", default=os.environ.get("DPC_COMM", "auto"), choices=["auto", "torch", "native", "ipc"],
                    help="collective transport of every engine (parallel/transport.py): the native C++ RCCL "
-                        "communicator on its own HIP stream (auto = on a GPU), or torch.distributed")
+                        "communicator on its own HIP stream (auto = on a GPU), torch.distributed, or ipc -- "
+                        "direct peer-access collectives over xGMI (parallel/ipc_comm.py; DDP / FSDP)")
     p.add_argument("--profile", type=str, default=None, help="write a torch.profiler trace here")
     p.add_argument("--log_jsonl", type=str, default=None, help="append step metrics as JSON lines")
     p.add_argument("--cpu", action="store_true", help="force CPU (gloo) even if a GPU is present")

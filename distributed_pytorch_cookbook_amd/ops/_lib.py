@@ -42,6 +42,19 @@ class GemmArgs(ctypes.Structure):
     ]
 
 
+IPC_MAXW = 8
+
+
+class IpcCollArgs(ctypes.Structure):
+    """``ipc_coll.hip:IpcCollArgs``."""
+    _fields_ = [
+        ("slot", P * IPC_MAXW), ("flags", P * IPC_MAXW), ("ep", P), ("error", P),
+        ("inp", P), ("out", P),
+        ("n", LL), ("half_bytes", LL), ("spin_limit", LL),
+        ("op", c_int), ("bf16", c_int), ("rank", c_int), ("world", c_int), ("root", c_int),
+    ]
+
+
 class AttnArgs(ctypes.Structure):
     _fields_ = [
         ("q", P), ("k", P), ("v", P), ("o", P), ("lse", P), ("pad", P), ("dout", P),
@@ -232,6 +245,16 @@ def lib() -> ctypes.CDLL:
             handle.dpc_occupy.restype = c_int
             handle.dpc_embedding_bwd_ws.argtypes = [c_int, c_int]
             handle.dpc_embedding_bwd_ws.restype = ctypes.c_ulonglong
+            # intra-node peer-access collectives (ipc_coll.hip, parallel/ipc_comm.py)
+            handle.dpc_ipc_alloc.argtypes = [ctypes.c_longlong, c_int, ctypes.POINTER(c_void_p)]
+            handle.dpc_ipc_free.argtypes = [c_void_p]
+            handle.dpc_ipc_handle.argtypes = [c_void_p, c_void_p]
+            handle.dpc_ipc_open.argtypes = [c_void_p, ctypes.POINTER(c_void_p)]
+            handle.dpc_ipc_close.argtypes = [c_void_p]
+            handle.dpc_ipc_coll.argtypes = [ctypes.POINTER(IpcCollArgs), c_void_p]
+            for f in ("dpc_ipc_alloc", "dpc_ipc_free", "dpc_ipc_handle", "dpc_ipc_open", "dpc_ipc_close",
+                      "dpc_ipc_coll", "dpc_ipc_handle_size", "dpc_ipc_max_world", "dpc_ipc_groups"):
+                getattr(handle, f).restype = c_int
             _lib = handle
     return _lib
 

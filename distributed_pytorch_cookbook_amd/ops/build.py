@@ -31,7 +31,7 @@ ARCH = os.environ.get("DPC_OFFLOAD_ARCH", "gfx950")
 # gemm7_part*.hip: the persistent GEMM kernels' instantiations, dealt over several files that
 # compile in parallel (ops/gen_gemm_parts.py; gemm7.hip itself is the host-side dispatcher)
 SOURCES = ["gemm.hip", "gemm7.hip", "gemm_f32.hip", "attention.hip", "attention_f32.hip", "layernorm.hip", "misc.hip",
-           "decode.hip", "embed_bwd.hip"] + sorted(p.name for p in CSRC.glob("gemm7_part*.hip"))
+           "decode.hip", "embed_bwd.hip", "ipc_coll.hip"] + sorted(p.name for p in CSRC.glob("gemm7_part*.hip"))
 HEADERS = ["common.h", "gemm.h", "gemm7_kern.h", "gemm9_kern.h", "gemm7_extern.inc"]
 
 # code-object v5 keeps the library loadable by torch's bundled ROCm 7.0 runtime as

@@ -369,6 +369,11 @@ class FSDPStore(ParamStore):
             sh = self.shard(flat_shards, u).to(self.device).contiguous()
             if not self.sharded:
                 full = sh
+            elif not getattr(self.tp, "p2p", True):  # (a transport without point-to-point: all-gather)
+                full = torch.empty(self.unit_len[u], dtype=sh.dtype, device=self.device)
+                self.tp.all_gather(full, sh)
+                if self.rank != dst_rank:
+                    continue
             elif self.rank == dst_rank:
                 # gathered to dst_rank ONLY (grouped point-to-point): the reference's
                 # FULL_STATE_DICT all-gathers every unit onto every rank (main-fsdp.py:193-194),

@@ -1,0 +1,204 @@
+"""Intra-node collectives by direct peer access (``ops/csrc/ipc_coll.hip``), SURVEY.md §5.8.
+
+Every rank allocates a staging buffer (two halves, used alternately) and an uncached flag
+array, exports both through HIP IPC, and maps every other rank's; the handles travel over
+the bootstrap process group (``all_gather_object``).  A collective is then ONE kernel on the
+caller's stream: the two-shot all-reduce reads each shard straight out of the peers' HBM over
+their xGMI links (reduce-scatter, then all-gather of the summed shards), so all 7 links of an
+8-GPU node carry traffic at once instead of a ring's one.  No host synchronisation and no
+per-call host state (the epoch counters live in device memory), so a HIP graph captures the
+collectives of a step and every replay runs them afresh.
+
+It is also what lets ONE GPU rehearse the N > 1 step graph: RCCL refuses two ranks on one
+device ("Duplicate GPU detected"), HIP IPC does not, so ``IpcTransport`` runs DDP / FSDP at
+world 2 on one MI355X with the step captured on both ranks (``tests/test_ipc_gpu.py``).
+
+Results are bitwise identical on every rank (each shard is summed once, in rank order, by its
+owner).  Collectives larger than a staging half are chunked.  A wait that never completes --
+a peer that crashed or took another code path -- sets the error word after ``spin_limit``
+polls instead of hanging the GPU; ``check()`` raises on it.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import torch
+import torch.distributed as dist
+
+ALLREDUCE, REDUCE_SCATTER, ALLGATHER, BROADCAST = 0, 1, 2, 3
+_ALIGN = 64  # elements (ipc_coll.hip: IPC_ALIGN)
+
+
+def _lib():
+    from ..ops import _lib as L
+
+    return L.lib()
+
+
+def _rc(rc: int, what: str) -> None:
+    if rc != 0:
+        raise RuntimeError(f"{what} failed: hipError {rc}")
+
+
+class IpcComm:
+    """Peer-access communicator over the ranks of ``group`` (all on one node, ``world <= 8``).
+
+    ``slot_mb``: one staging half in MiB (DPC_IPC_SLOT_MB, default 64); the buffer holds two."""
+
+    def __init__(self, group=None, device=None, slot_mb: float | None = None, spin_limit: int | None = None):
+        from ..ops import _lib as L
+
+        self.group = group
+        self.rank = dist.get_rank(group) if dist.is_initialized() else 0
+        self.size = dist.get_world_size(group) if dist.is_initialized() else 1
+        if self.size > L.IPC_MAXW:
+            raise ValueError(f"IpcComm: {self.size} ranks, at most {L.IPC_MAXW} (one node)")
+        self.device = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+        slot_mb = float(os.environ.get("DPC_IPC_SLOT_MB", "64")) if slot_mb is None else slot_mb
+        self.half_bytes = max(256, int(slot_mb * 2**20) // 256 * 256)
+        # ~2^26 polls with a short sleep each: tens of seconds before a wait gives up
+        self.spin_limit = int(os.environ.get("DPC_IPC_SPIN", str(1 << 26))) if spin_limit is None else spin_limit
+        lib = _lib()
+        self.groups = lib.dpc_ipc_groups()
+        hsize = lib.dpc_ipc_handle_size()
+        with torch.cuda.device(self.device):
+            slot, flags = ctypes.c_void_p(), ctypes.c_void_p()
+            _rc(lib.dpc_ipc_alloc(2 * self.half_bytes, 0, ctypes.byref(slot)), "staging buffer allocation")
+            _rc(lib.dpc_ipc_alloc(L.IPC_MAXW * self.groups * 4, 1, ctypes.byref(flags)), "flag allocation")
+            self._own = (slot.value, flags.value)
+            hs, hf = ctypes.create_string_buffer(hsize), ctypes.create_string_buffer(hsize)
+            _rc(lib.dpc_ipc_handle(slot, hs), "hipIpcGetMemHandle (staging)")
+            _rc(lib.dpc_ipc_handle(flags, hf), "hipIpcGetMemHandle (flags)")
+            torch.cuda.synchronize(self.device)  # (the allocations' zero fill done before any peer maps them)
+            handles = [None] * self.size
+            if self.size > 1:
+                dist.all_gather_object(handles, (hs.raw, hf.raw), group=group)
+            else:
+                handles[0] = (hs.raw, hf.raw)
+            self.slots = [0] * L.IPC_MAXW
+            self.flags = [0] * L.IPC_MAXW
+            self._opened = []
+            for p in range(self.size):
+                if p == self.rank:
+                    self.slots[p], self.flags[p] = self._own
+                    continue
+                for i, raw in enumerate(handles[p]):
+                    out = ctypes.c_void_p()
+                    _rc(lib.dpc_ipc_open(ctypes.create_string_buffer(raw, hsize), ctypes.byref(out)),
+                        f"hipIpcOpenMemHandle (rank {p})")
+                    self._opened.append(out.value)
+                    (self.slots if i == 0 else self.flags)[p] = out.value
+            self.ep = torch.zeros(self.groups, dtype=torch.int32, device=self.device)
+            self.error = torch.zeros(1, dtype=torch.int32, device=self.device)
+        if self.size > 1:
+            dist.barrier(group=group)  # every rank mapped every buffer before any collective
+
+    # ------------------------------------------------------------------ collectives
+    def _launch(self, op, inp, out, n, bf16, root=0, stream=None):
+        from ..ops import _lib as L
+
+        a = L.IpcCollArgs()
+        for p in range(L.IPC_MAXW):
+            a.slot[p] = self.slots[p] or None
+            a.flags[p] = self.flags[p] or None
+        a.ep, a.error = self.ep.data_ptr(), self.error.data_ptr()
+        a.inp, a.out = inp, out
+        a.n, a.half_bytes, a.spin_limit = int(n), self.half_bytes, self.spin_limit
+        a.op, a.bf16, a.rank, a.world, a.root = op, int(bf16), self.rank, self.size, int(root)
+        s = (stream or torch.cuda.current_stream(self.device)).cuda_stream
+        _rc(_lib().dpc_ipc_coll(ctypes.byref(a), s), "dpc_ipc_coll")
+
+    def _cap(self, op, es):
+        """Elements per chunk that fit one staging half."""
+        W = self.size
+        per = self.half_bytes // es
+        if op == ALLREDUCE:  # n <= W x (largest padded shard that fits)
+            return W * (per // W // _ALIGN * _ALIGN)
+        if op == REDUCE_SCATTER:
+            return per // W // _ALIGN * _ALIGN
+        return per // _ALIGN * _ALIGN
+
+    @staticmethod
+    def _kind(t):
+        if t.dtype == torch.float32:
+            return False, 4
+        if t.dtype == torch.bfloat16:
+            return True, 2
+        raise TypeError(f"IpcComm: {t.dtype} (f32 and bf16 only)")
+
+    def all_reduce(self, t, stream=None):
+        """Sum over the ranks, in place."""
+        bf, es = self._kind(t)
+        flat = t.view(-1)
+        n, cap = flat.numel(), self._cap(ALLREDUCE, es)
+        for c0 in range(0, n, cap):
+            c1 = min(n, c0 + cap)
+            p = flat[c0:c1].data_ptr()
+            self._launch(ALLREDUCE, p, p, c1 - c0, bf, stream=stream)
+
+    def reduce_scatter(self, out, inp, stream=None):
+        """out = sum over ranks of inp[rank * n : (rank + 1) * n], n = out.numel()."""
+        bf, es = self._kind(out)
+        n, W = out.numel(), self.size
+        if inp.numel() != W * n or inp.dtype != out.dtype:
+            raise ValueError("reduce_scatter: inp must hold world x out elements of out's dtype")
+        cap = self._cap(REDUCE_SCATTER, es)
+        if n <= cap:
+            self._launch(REDUCE_SCATTER, inp.data_ptr(), out.data_ptr(), n, bf, stream=stream)
+            return
+        # chunked: shard s of chunk k = inp[s n + k cap ...]: gather those pieces per chunk
+        iv = inp.view(W, n)
+        for c0 in range(0, n, cap):
+            c1 = min(n, c0 + cap)
+            piece = iv[:, c0:c1].contiguous()
+            self._launch(REDUCE_SCATTER, piece.data_ptr(), out.view(-1)[c0:c1].data_ptr(), c1 - c0, bf, stream=stream)
+            piece.record_stream(stream or torch.cuda.current_stream(self.device))
+
+    def all_gather(self, out, inp, stream=None):
+        """out[rank * n : (rank + 1) * n] = inp of every rank, n = inp.numel()."""
+        bf, es = self._kind(inp)
+        n, W = inp.numel(), self.size
+        if out.numel() != W * n or inp.dtype != out.dtype:
+            raise ValueError("all_gather: out must hold world x inp elements of inp's dtype")
+        cap = self._cap(ALLGATHER, es)
+        if n <= cap:
+            self._launch(ALLGATHER, inp.data_ptr(), out.data_ptr(), n, bf, stream=stream)
+            return
+        ov = out.view(W, n)
+        for c0 in range(0, n, cap):
+            c1 = min(n, c0 + cap)
+            piece = torch.empty((W, c1 - c0), dtype=out.dtype, device=out.device)
+            self._launch(ALLGATHER, inp.view(-1)[c0:c1].data_ptr(), piece.data_ptr(), c1 - c0, bf, stream=stream)
+            ov[:, c0:c1].copy_(piece)
+
+    def broadcast(self, t, src: int = 0, stream=None):
+        bf, es = self._kind(t)
+        flat = t.view(-1)
+        n, cap = flat.numel(), self._cap(BROADCAST, es)
+        for c0 in range(0, n, cap):
+            c1 = min(n, c0 + cap)
+            p = flat[c0:c1].data_ptr()
+            self._launch(BROADCAST, p, p, c1 - c0, bf, root=src, stream=stream)
+
+    # ------------------------------------------------------------------ health / teardown
+    def check(self) -> None:
+        """Raise if a peer wait timed out (the data of that collective is not valid)."""
+        if int(self.error.item()) != 0:
+            raise RuntimeError("IpcComm: a peer never reached a collective's barrier (timed out)")
+
+    check_async = check  # (transport.check_drained polls every communicator through this name)
+
+    def destroy(self) -> None:
+        if not self._own:
+            return
+        torch.cuda.synchronize(self.device)
+        if self.size > 1 and dist.is_initialized():
+            dist.barrier(group=self.group)  # no peer still reads this rank's buffers
+        lib = _lib()
+        for p in self._opened:
+            lib.dpc_ipc_close(ctypes.c_void_p(p))
+        self._opened = []
+        for p in self._own:
+            lib.dpc_ipc_free(ctypes.c_void_p(p))
+        self._own = ()

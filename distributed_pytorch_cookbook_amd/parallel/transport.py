@@ -460,6 +460,31 @@ class NativeTransport(Transport):
         return NativeTransport(group, self.device, native=self.nc.split(color, key))
 
 
+class IpcTransport(NativeTransport):
+    """Intra-node collectives by direct peer access (``parallel/ipc_comm.py``, ``--comm ipc``):
+    the same side-stream / event / watchdog plumbing as the RCCL transport, the kernels of
+    ``ops/csrc/ipc_coll.hip`` instead of RCCL's.  All-reduce, reduce-scatter, all-gather and
+    broadcast (DDP and FSDP); no point-to-point, so the pipeline recipes keep RCCL / torch.
+    Bootstraps over any process group -- gloo included -- so two ranks may share one GPU."""
+
+    kind = "ipc"
+    p2p = False  # (FSDP's rank-0 checkpoint gather all-gathers instead)
+
+    def __init__(self, group=None, device=None):
+        from .ipc_comm import IpcComm
+
+        dev = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+        if dev.type == "cuda" and dev.index is None:
+            dev = torch.device("cuda", torch.cuda.current_device())
+        super().__init__(group, dev, native=IpcComm(group, dev))
+
+    def sendrecv(self, sends=(), recvs=(), async_op=False):
+        raise NotImplementedError("IpcTransport: no point-to-point (pipeline recipes: --comm native / torch)")
+
+    def split(self, color: int, key: int, group=None):
+        raise NotImplementedError("IpcTransport: no sub-communicators")
+
+
 def _want_native(kind: str, device) -> bool:
     if kind == "torch":
         return False
@@ -477,6 +502,8 @@ def make_transport(group=None, device=None, kind: str | None = None) -> Transpor
     nccl backend, torch otherwise) | native | torch.  Falls back to torch -- before any
     collective -- if the native communicator cannot be built."""
     kind = kind or os.environ.get("DPC_COMM", "auto")
+    if kind == "ipc" and torch.device(device if device is not None else "cpu").type == "cuda" and dist.is_initialized():
+        return IpcTransport(group, device)  # (no fallback: asked for by name)
     if (comm.world_size(group) > 1 or kind == "native") and _want_native(kind, device):
         try:
             return NativeTransport(group, device)
@@ -491,6 +518,8 @@ def make_mesh_transports(pp_group, dp_group, stage: int, replica: int, device=No
     ONE world communicator split twice with ncclCommSplit (color = replica -> the pipeline of
     this replica, color = stage -> the replicas of this stage)."""
     kind = kind or os.environ.get("DPC_COMM", "auto")
+    if kind == "ipc":  # (no point-to-point over IPC: the mesh takes the automatic choice)
+        kind = "auto"
     if comm.world_size() > 1 and _want_native(kind, device):
         built = []
         try:

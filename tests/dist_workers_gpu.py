@@ -74,3 +74,107 @@ def worker(rank, world, out, kind, steps, opts):
     sd = eng.full_state_dict()  # gathered to rank 0 (None elsewhere for FSDP / pipeline)
     if rank == 0:
         torch.save({k: v.float().cpu() for k, v in sd.items()}, out)
+
+
+# ---------------------------------------------------------------- peer-access collectives
+def _ipc_input(p, n, dtype, salt=0):
+    """Rank p's deterministic input of n elements (every rank can form every rank's)."""
+    g = torch.Generator().manual_seed(1000 * p + 17 * n + salt)
+    return torch.randn(n, generator=g).to(dtype).cuda()
+
+
+def ipc_collectives_worker(rank, world, out):
+    """Every collective of IpcComm on two ranks sharing cuda:0: exact against the rank-order f32
+    sums, aligned and unaligned buffers, chunked (a small staging half) and not, f32 and bf16,
+    and replayed from a HIP graph (the per-workgroup epochs advance on the device)."""
+    _init()
+    from distributed_pytorch_cookbook_amd.parallel.ipc_comm import IpcComm
+
+    c = IpcComm(slot_mb=0.25, spin_limit=1 << 22)
+    W = world
+
+    def ref_sum(n, dtype, salt=0):
+        acc = torch.zeros(n, device="cuda")
+        for p in range(W):
+            acc = acc + _ipc_input(p, n, dtype, salt).float()
+        return acc.to(dtype)
+
+    checked = 0
+    for dtype in (torch.float32, torch.bfloat16):
+        for n in (1, 63, 64, 1000, 4099, 300001):  # 300001 f32 > one 0.25 MiB half: chunked
+            t = _ipc_input(rank, n, dtype)
+            c.all_reduce(t)
+            assert torch.equal(t, ref_sum(n, dtype)), ("all_reduce", dtype, n)
+            # unaligned view (element-wise edges)
+            big = torch.zeros(n + 1, dtype=dtype, device="cuda")
+            big[1:] = _ipc_input(rank, n, dtype)
+            c.all_reduce(big[1:])
+            assert torch.equal(big[1:], ref_sum(n, dtype)), ("all_reduce unaligned", dtype, n)
+            checked += 2
+        for n in (1, 1000, 50000):
+            full = [_ipc_input(p, W * n, dtype, 1) for p in range(W)]
+            outp = torch.empty(n, dtype=dtype, device="cuda")
+            c.reduce_scatter(outp, full[rank])
+            exp = sum(f.float() for f in full).to(dtype)[rank * n:(rank + 1) * n]
+            assert torch.equal(outp, exp), ("reduce_scatter", dtype, n)
+            mine = _ipc_input(rank, n, dtype, 2)
+            gath = torch.empty(W * n, dtype=dtype, device="cuda")
+            c.all_gather(gath, mine)
+            assert torch.equal(gath, torch.cat([_ipc_input(p, n, dtype, 2) for p in range(W)])), ("all_gather", dtype, n)
+            b = _ipc_input(rank, n, dtype, 3)
+            c.broadcast(b, src=1)
+            assert torch.equal(b, _ipc_input(1, n, dtype, 3)), ("broadcast", dtype, n)
+            checked += 3
+    # captured: two all-reduces per replay, new inputs each replay
+    x = torch.empty(5000, device="cuda")
+    y = torch.empty(777, dtype=torch.bfloat16, device="cuda")
+    torch.cuda.synchronize()
+    import torch.distributed as dist
+
+    dist.barrier()
+    g = torch.cuda.CUDAGraph()
+    s = torch.cuda.Stream()
+    with torch.cuda.stream(s):
+        with torch.cuda.graph(g, stream=s):
+            c.all_reduce(x)
+            c.all_reduce(y)
+    for it in range(3):
+        x.copy_(_ipc_input(rank, 5000, torch.float32, 10 + it))
+        y.copy_(_ipc_input(rank, 777, torch.bfloat16, 20 + it))
+        g.replay()
+        torch.cuda.synchronize()
+        assert torch.equal(x, ref_sum(5000, torch.float32, 10 + it)), ("graph f32", it)
+        assert torch.equal(y, ref_sum(777, torch.bfloat16, 20 + it)), ("graph bf16", it)
+        checked += 2
+    c.check()
+    c.destroy()
+    if rank == 0:
+        torch.save({"checked": checked}, out)
+
+
+def ipc_engine_worker(rank, world, out, kind, steps, graph):
+    """DDP / FSDP over the peer-access transport, two ranks on cuda:0, the step captured into a
+    HIP graph on both ranks when ``graph``: the N > 1 capture path (collective capture decision,
+    collectives recorded into the step graph, replays) run for real on one GPU."""
+    info = _init()
+    assert info.device.type == "cuda"
+    from distributed_pytorch_cookbook_amd.engine.data_parallel import DataParallelEngine
+    from distributed_pytorch_cookbook_amd.engine.fsdp import FSDPEngine
+
+    m = make_model()
+    if kind == "ddp":
+        eng = DataParallelEngine(m, "cuda", lr=LR, bucket_mb=0.2, graph=graph, comm_kind="ipc")
+        assert len(eng.store.buckets) >= 2
+    else:
+        eng = FSDPEngine(m, "cuda", lr=LR, prefetch=1, graph=graph, comm_kind="ipc")
+    assert eng.store.tp.kind == "ipc", eng.store.tp.kind
+    for s in range(steps):
+        eng.train_step(*shard(*full_batch(step=s), rank, world))
+    torch.cuda.synchronize()
+    if graph:
+        assert eng._stepper.graph is not None, "the two-rank step was not captured"
+    eng.store.tp.nc.check()
+    # the replicas / shards agree bit for bit across the ranks (each shard summed once, by its owner)
+    sd = eng.full_state_dict()
+    if rank == 0:
+        torch.save({k: v.float().cpu() for k, v in sd.items()}, out)

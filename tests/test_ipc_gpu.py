@@ -1,0 +1,40 @@
+"""Peer-access collectives (ops/csrc/ipc_coll.hip, parallel/ipc_comm.py) with two ranks sharing
+the one GPU of a test box: HIP IPC maps a buffer of another process on the same device, which
+RCCL refuses ("Duplicate GPU detected") -- so these are also the only tests in which an N > 1
+step graph, collectives inside, is captured and replayed for real."""
+import pytest
+import torch
+
+from dist_helpers import run_workers
+from dist_workers_gpu import ipc_collectives_worker, ipc_engine_worker, reference_state
+
+pytestmark = pytest.mark.gpu
+
+
+def test_ipc_collectives_two_ranks_one_gpu(tmp_path):
+    out = tmp_path / "ipc.pt"
+    run_workers(ipc_collectives_worker, 2, str(out), timeout=110)
+    assert torch.load(out, weights_only=True)["checked"] == 48
+
+
+@pytest.fixture(scope="module")
+def ref():
+    return reference_state(steps=3)
+
+
+def close(sd_a, sd_b, tol=5e-2, lr=1e-3, steps=3):
+    assert list(sd_a) == list(sd_b)
+    bad = {}
+    for k in sd_b:
+        scale = max(sd_b[k].norm().item(), lr * steps * sd_b[k].numel() ** 0.5)
+        e = (sd_a[k] - sd_b[k]).norm().item() / scale
+        if e >= tol:
+            bad[k] = round(e, 4)
+    assert not bad, bad
+
+
+@pytest.mark.parametrize("kind,graph", [("ddp", True), ("ddp", False), ("fsdp", True)])
+def test_ipc_transport_engines_two_ranks_one_gpu(tmp_path, ref, kind, graph):
+    out = tmp_path / f"{kind}.pt"
+    run_workers(ipc_engine_worker, 2, str(out), kind, 3, graph, timeout=110)
+    close(torch.load(out, weights_only=True), ref[0])
