@@ -113,6 +113,9 @@ def main():
                     help="one rank on the engines' N > 1 code path over a native 1-rank RCCL communicator "
                          "(bucketed DDP store / sharded FSDP store / replica DDP store): profiles that path "
                          "on one GPU; the result is not the headline number")
+    ap.add_argument("--comm", default=os.environ.get("DPC_COMM", "auto"), choices=["auto", "torch", "native", "ipc"],
+                    help="collective transport (default auto: the native RCCL communicator at N > 1); ipc = the "
+                         "peer-access collectives of parallel/ipc_comm.py (DDP / FSDP)")
     ap.add_argument("--json", default=None, help="also write the result line to this file")
     a = ap.parse_args()
 
@@ -136,7 +139,7 @@ def main():
     model_name = a.model or default_model
     rec = "pipe_ddp" if a.recipe == "pipe_ddp" else a.recipe
     argv = ["--model", model_name, "--batch_size", str(a.batch_size), "--bucket_mb", str(a.bucket_mb),
-            "--reduce_dtype", a.reduce_dtype, "--synthetic_data"]
+            "--reduce_dtype", a.reduce_dtype, "--synthetic_data", "--comm", a.comm]
     if a.schedule is None:
         a.schedule = "zb2" if rec == "pipe" else "zb"
     if rec in ("pipe", "pipe_ddp"):
