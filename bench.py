@@ -246,6 +246,9 @@ def main():
                    "force_dist_path": bool(a.force_dist_path),
                    "reduce_dtype": a.reduce_dtype, "pp_comm_dtype": a.pp_comm_dtype,
                    "schedule": a.schedule if a.recipe in ("pipe", "pipe_ddp") else None,
+                   "comm": getattr(getattr(engine, "store", None), "tp", None).kind
+                   if getattr(getattr(engine, "store", None), "tp", None) is not None else None,
+                   "step_graph": getattr(getattr(engine, "_stepper", None), "graph", None) is not None,
                    "mfu_per_gpu": round(mfu(value / n, train_flops_per_token(
                        args.dim, args.heads, args.head_dim, args.num_layers, vocab, S)), 4),
                    "baseline": ("stock PyTorch reference-default recipe (manual attention + torch.compile)"

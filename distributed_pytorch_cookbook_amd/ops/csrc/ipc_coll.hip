@@ -36,7 +36,14 @@ namespace dpc {
 typedef unsigned v4u32_t __attribute__((ext_vector_type(4)));
 
 constexpr int IPC_MAXW = 8;
-constexpr int IPC_G = 64;      // workgroups per collective (flag columns)
+// workgroups per collective (flag columns).  Few on purpose: a waiting workgroup holds a slot on
+// its CU, and a persistent GEMM launched beside it (one 512-register wave per SIMD) cannot place
+// its workgroup on that CU until the wait ends.  Across GPUs that only delays this GPU's own GEMM
+// until the peer arrives; with two ranks sharing ONE GPU (the tests' rehearsal) the other rank's
+// GEMM may be the one the waiting workgroups stall, and it must still find CUs free: 64 workgroups
+// passed every rehearsal, 256 deadlocked the two-rank DDP step (round-6 job 14).  64 workgroups
+// moved 180 GB/s on one GPU (profiles/r6_ipc/).
+constexpr int IPC_G = 64;
 constexpr int IPC_ALIGN = 64;  // elements: shard / sub-slice granularity
 
 struct IpcCollArgs {
@@ -218,7 +225,7 @@ __device__ void ipc_barrier(const IpcCollArgs& a, int g, unsigned v) {
         __hip_atomic_store(a.error, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         break;
       }
-      __builtin_amdgcn_s_sleep(2);
+      __builtin_amdgcn_s_sleep(1);
     }
   }
   __syncthreads();
