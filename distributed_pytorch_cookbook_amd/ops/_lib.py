@@ -55,6 +55,21 @@ class IpcCollArgs(ctypes.Structure):
     ]
 
 
+IPC_P2P_MAX = 8
+
+
+class IpcP2PArgs(ctypes.Structure):
+    """``ipc_coll.hip:IpcP2PArgs``."""
+    _fields_ = [
+        ("slot", P * IPC_MAXW), ("flags", P * IPC_MAXW), ("cnt", P), ("error", P),
+        ("send_ptr", P * IPC_P2P_MAX), ("recv_ptr", P * IPC_P2P_MAX),
+        ("send_n", LL * IPC_P2P_MAX), ("recv_n", LL * IPC_P2P_MAX),
+        ("send_peer", c_int * IPC_P2P_MAX), ("recv_peer", c_int * IPC_P2P_MAX),
+        ("region_bytes", LL), ("spin_limit", LL),
+        ("nsend", c_int), ("nrecv", c_int), ("rank", c_int), ("world", c_int),
+    ]
+
+
 class AttnArgs(ctypes.Structure):
     _fields_ = [
         ("q", P), ("k", P), ("v", P), ("o", P), ("lse", P), ("pad", P), ("dout", P),
@@ -252,8 +267,9 @@ def lib() -> ctypes.CDLL:
             handle.dpc_ipc_open.argtypes = [c_void_p, ctypes.POINTER(c_void_p)]
             handle.dpc_ipc_close.argtypes = [c_void_p]
             handle.dpc_ipc_coll.argtypes = [ctypes.POINTER(IpcCollArgs), c_void_p]
+            handle.dpc_ipc_p2p.argtypes = [ctypes.POINTER(IpcP2PArgs), c_void_p]
             for f in ("dpc_ipc_alloc", "dpc_ipc_free", "dpc_ipc_handle", "dpc_ipc_open", "dpc_ipc_close",
-                      "dpc_ipc_coll", "dpc_ipc_handle_size", "dpc_ipc_max_world", "dpc_ipc_groups"):
+                      "dpc_ipc_coll", "dpc_ipc_p2p", "dpc_ipc_handle_size", "dpc_ipc_max_world", "dpc_ipc_groups"):
                 getattr(handle, f).restype = c_int
             _lib = handle
     return _lib

@@ -48,7 +48,7 @@ constexpr int IPC_ALIGN = 64;  // elements: shard / sub-slice granularity
 
 struct IpcCollArgs {
   void* slot[IPC_MAXW];        // every rank's staging buffer (two halves of half_bytes), this rank's at [rank]
-  unsigned* flags[IPC_MAXW];   // every rank's flag array [IPC_MAXW][IPC_G] (uncached)
+  unsigned* flags[IPC_MAXW];   // every rank's flag arrays [3][IPC_MAXW][IPC_G] (uncached; [0]: barriers)
   unsigned* ep;                // this rank's per-workgroup collective counters [IPC_G]
   int* error;                  // set to 1 by a wait that timed out
   const void* in;
@@ -301,6 +301,87 @@ __global__ __launch_bounds__(256) void ipc_coll_kernel(IpcCollArgs a) {
   if (threadIdx.x == 0) a.ep[g] = e + 1u;
 }
 
+// ---------------------------------------------------------------- point-to-point
+// A grouped exchange (the pipeline's activations / gradients): per ordered pair (p -> q) a channel
+// of two buffered messages in p's p2p staging buffer (half = message parity, region q of the half)
+// and two monotonic counters per workgroup: READY (raised by p in q's flag array after a message's
+// bytes are in place) and ACK (raised by q in p's array after it copied them out).  Workgroup g
+// moves sub-slice g of every message and meets only workgroup g of the peer, as the collectives
+// do.  A send waits only when its channel already holds two unconsumed messages, so a schedule
+// that is deadlock-free under RCCL's blocking sends (parallel/pipeline.py:p2p_deadlock_free) is
+// deadlock-free here; every wait is bounded like the barriers'.
+constexpr int IPC_P2P_MAX = 8;
+
+struct IpcP2PArgs {
+  void* slot[IPC_MAXW];       // every rank's p2p staging buffer: 2 halves x world regions of region_bytes
+  unsigned* flags[IPC_MAXW];  // every rank's flag arrays: [0] barriers, [1] READY, [2] ACK
+  unsigned* cnt;              // this rank's counters [2][IPC_MAXW][IPC_G]: messages sent to / received from
+  int* error;
+  const void* send_ptr[IPC_P2P_MAX];
+  void* recv_ptr[IPC_P2P_MAX];
+  long long send_n[IPC_P2P_MAX];  // 2-byte units
+  long long recv_n[IPC_P2P_MAX];
+  int send_peer[IPC_P2P_MAX];
+  int recv_peer[IPC_P2P_MAX];
+  long long region_bytes, spin_limit;
+  int nsend, nrecv, rank, world;
+};
+
+__device__ void ipc_wait(const unsigned* f, unsigned v, long long limit, int* error) {
+  long long n = 0;
+  while ((int)(__hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) - v) < 0) {
+    if (++n > limit) {
+      __hip_atomic_store(error, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      return;
+    }
+    __builtin_amdgcn_s_sleep(1);
+  }
+}
+
+__global__ __launch_bounds__(256) void ipc_p2p_kernel(IpcP2PArgs a) {
+  const int g = blockIdx.x, r = a.rank;
+  constexpr int FL = IPC_MAXW * IPC_G;  // one flag array
+  unsigned* sent = a.cnt;
+  unsigned* rcvd = a.cnt + FL;
+  long long lo, hi;
+  for (int i = 0; i < a.nsend; ++i) {
+    const int q = a.send_peer[i];
+    const unsigned c = sent[q * IPC_G + g];
+    if (c >= 2) {  // the message two back on this channel copied out by q (its half is free again)
+      if (threadIdx.x == 0) ipc_wait(a.flags[r] + 2 * FL + q * IPC_G + g, c - 1, a.spin_limit, a.error);
+      __syncthreads();
+    }
+    const long long n = a.send_n[i];
+    ipc_sub((n + IPC_ALIGN - 1) / IPC_ALIGN * IPC_ALIGN, g, lo, hi);
+    hi = min(hi, n);
+    char* dst = static_cast<char*>(a.slot[r]) + (long long)(c & 1u) * a.world * a.region_bytes + q * a.region_bytes;
+    if (hi > lo) ipc_copy(a.send_ptr[i], 0, false, dst, 0, true, lo, hi, true);
+    __threadfence_system();
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      __hip_atomic_store(a.flags[q] + FL + r * IPC_G + g, c + 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+      sent[q * IPC_G + g] = c + 1u;
+    }
+  }
+  for (int i = 0; i < a.nrecv; ++i) {
+    const int p = a.recv_peer[i];
+    const unsigned c = rcvd[p * IPC_G + g];
+    if (threadIdx.x == 0) ipc_wait(a.flags[r] + FL + p * IPC_G + g, c + 1u, a.spin_limit, a.error);
+    __syncthreads();
+    const long long n = a.recv_n[i];
+    ipc_sub((n + IPC_ALIGN - 1) / IPC_ALIGN * IPC_ALIGN, g, lo, hi);
+    hi = min(hi, n);
+    const char* src = static_cast<const char*>(a.slot[p]) + (long long)(c & 1u) * a.world * a.region_bytes + r * a.region_bytes;
+    if (hi > lo) ipc_copy(src, 0, true, a.recv_ptr[i], 0, false, lo, hi, true);
+    __threadfence_system();  // (this workgroup's reads of the message done before the ACK)
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      __hip_atomic_store(a.flags[p] + 2 * FL + r * IPC_G + g, c + 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+      rcvd[p * IPC_G + g] = c + 1u;
+    }
+  }
+}
+
 }  // namespace dpc
 
 using namespace dpc;
@@ -361,5 +442,26 @@ DPC_API int dpc_ipc_coll(const IpcCollArgs* a, hipStream_t stream) {
   return (int)hipGetLastError();
 }
 
+DPC_API int dpc_ipc_p2p(const IpcP2PArgs* a, hipStream_t stream) {
+  if (a->world < 1 || a->world > IPC_MAXW || a->rank < 0 || a->rank >= a->world) return (int)hipErrorInvalidValue;
+  if (a->nsend < 0 || a->nsend > IPC_P2P_MAX || a->nrecv < 0 || a->nrecv > IPC_P2P_MAX) return (int)hipErrorInvalidValue;
+  if (a->nsend + a->nrecv == 0) return 0;
+  if (!a->cnt || !a->error || a->spin_limit <= 0 || a->region_bytes % 256) return (int)hipErrorInvalidValue;
+  if (!a->slot[a->rank] || !a->flags[a->rank]) return (int)hipErrorInvalidValue;
+  for (int i = 0; i < a->nsend; ++i) {
+    const int q = a->send_peer[i];
+    if (q < 0 || q >= a->world || q == a->rank || !a->flags[q] || !a->send_ptr[i]) return (int)hipErrorInvalidValue;
+    if (a->send_n[i] < 0 || a->send_n[i] * 2 > a->region_bytes) return (int)hipErrorInvalidValue;
+  }
+  for (int i = 0; i < a->nrecv; ++i) {
+    const int p = a->recv_peer[i];
+    if (p < 0 || p >= a->world || p == a->rank || !a->slot[p] || !a->flags[p] || !a->recv_ptr[i]) return (int)hipErrorInvalidValue;
+    if (a->recv_n[i] < 0 || a->recv_n[i] * 2 > a->region_bytes) return (int)hipErrorInvalidValue;
+  }
+  hipLaunchKernelGGL(ipc_p2p_kernel, dim3(IPC_G), dim3(256), 0, stream, *a);
+  return (int)hipGetLastError();
+}
+
 DPC_API int dpc_ipc_max_world() { return IPC_MAXW; }
+DPC_API int dpc_ipc_p2p_max() { return IPC_P2P_MAX; }
 DPC_API int dpc_ipc_groups() { return IPC_G; }

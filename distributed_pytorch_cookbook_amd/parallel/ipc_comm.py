@@ -44,9 +44,12 @@ def _rc(rc: int, what: str) -> None:
 class IpcComm:
     """Peer-access communicator over the ranks of ``group`` (all on one node, ``world <= 8``).
 
-    ``slot_mb``: one staging half in MiB (DPC_IPC_SLOT_MB, default 64); the buffer holds two."""
+    ``slot_mb``: one staging half in MiB (DPC_IPC_SLOT_MB, default 64); the buffer holds two.
+    ``p2p_mb``: one point-to-point channel buffer in MiB (DPC_IPC_P2P_MB, default 16; 2 x world
+    of them per rank, 0 = no point-to-point)."""
 
-    def __init__(self, group=None, device=None, slot_mb: float | None = None, spin_limit: int | None = None):
+    def __init__(self, group=None, device=None, slot_mb: float | None = None, spin_limit: int | None = None,
+                 p2p_mb: float | None = None):
         from ..ops import _lib as L
 
         self.group = group
@@ -57,39 +60,51 @@ class IpcComm:
         self.device = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
         slot_mb = float(os.environ.get("DPC_IPC_SLOT_MB", "64")) if slot_mb is None else slot_mb
         self.half_bytes = max(256, int(slot_mb * 2**20) // 256 * 256)
+        p2p_mb = float(os.environ.get("DPC_IPC_P2P_MB", "16")) if p2p_mb is None else p2p_mb
+        self.region_bytes = int(p2p_mb * 2**20) // 256 * 256 if self.size > 1 else 0
         # ~2^26 polls with a short sleep each: tens of seconds before a wait gives up
         self.spin_limit = int(os.environ.get("DPC_IPC_SPIN", str(1 << 26))) if spin_limit is None else spin_limit
         lib = _lib()
         self.groups = lib.dpc_ipc_groups()
         hsize = lib.dpc_ipc_handle_size()
         with torch.cuda.device(self.device):
-            slot, flags = ctypes.c_void_p(), ctypes.c_void_p()
-            _rc(lib.dpc_ipc_alloc(2 * self.half_bytes, 0, ctypes.byref(slot)), "staging buffer allocation")
-            _rc(lib.dpc_ipc_alloc(L.IPC_MAXW * self.groups * 4, 1, ctypes.byref(flags)), "flag allocation")
-            self._own = (slot.value, flags.value)
-            hs, hf = ctypes.create_string_buffer(hsize), ctypes.create_string_buffer(hsize)
-            _rc(lib.dpc_ipc_handle(slot, hs), "hipIpcGetMemHandle (staging)")
-            _rc(lib.dpc_ipc_handle(flags, hf), "hipIpcGetMemHandle (flags)")
+            # staging (collectives), flag arrays ([0] barriers, [1] p2p READY, [2] p2p ACK: uncached),
+            # p2p channel buffers (2 halves x world regions)
+            sizes = [(2 * self.half_bytes, 0), (3 * L.IPC_MAXW * self.groups * 4, 1)]
+            if self.region_bytes:
+                sizes.append((2 * self.size * self.region_bytes, 0))
+            own, raws = [], []
+            for nbytes, uncached in sizes:
+                ptr, h = ctypes.c_void_p(), ctypes.create_string_buffer(hsize)
+                _rc(lib.dpc_ipc_alloc(nbytes, uncached, ctypes.byref(ptr)), "IPC buffer allocation")
+                own.append(ptr.value)
+                _rc(lib.dpc_ipc_handle(ptr, h), "hipIpcGetMemHandle")
+                raws.append(h.raw)
+            self._own = tuple(own)
             torch.cuda.synchronize(self.device)  # (the allocations' zero fill done before any peer maps them)
             handles = [None] * self.size
             if self.size > 1:
-                dist.all_gather_object(handles, (hs.raw, hf.raw), group=group)
+                dist.all_gather_object(handles, tuple(raws), group=group)
             else:
-                handles[0] = (hs.raw, hf.raw)
+                handles[0] = tuple(raws)
             self.slots = [0] * L.IPC_MAXW
             self.flags = [0] * L.IPC_MAXW
+            self.p2p_slots = [0] * L.IPC_MAXW
+            tables = (self.slots, self.flags, self.p2p_slots)
             self._opened = []
             for p in range(self.size):
                 if p == self.rank:
-                    self.slots[p], self.flags[p] = self._own
+                    for tab, v in zip(tables, self._own):
+                        tab[p] = v
                     continue
-                for i, raw in enumerate(handles[p]):
+                for tab, raw in zip(tables, handles[p]):
                     out = ctypes.c_void_p()
                     _rc(lib.dpc_ipc_open(ctypes.create_string_buffer(raw, hsize), ctypes.byref(out)),
                         f"hipIpcOpenMemHandle (rank {p})")
                     self._opened.append(out.value)
-                    (self.slots if i == 0 else self.flags)[p] = out.value
+                    tab[p] = out.value
             self.ep = torch.zeros(self.groups, dtype=torch.int32, device=self.device)
+            self.p2p_cnt = torch.zeros(2 * L.IPC_MAXW * self.groups, dtype=torch.int32, device=self.device)
             self.error = torch.zeros(1, dtype=torch.int32, device=self.device)
         if self.size > 1:
             dist.barrier(group=group)  # every rank mapped every buffer before any collective
@@ -180,6 +195,50 @@ class IpcComm:
             c1 = min(n, c0 + cap)
             p = flat[c0:c1].data_ptr()
             self._launch(BROADCAST, p, p, c1 - c0, bf, root=src, stream=stream)
+
+    def sendrecv(self, sends=(), recvs=(), stream=None):
+        """One grouped exchange: ``sends`` / ``recvs`` are (tensor, peer group rank) pairs; messages
+        on one channel are received in the order they were sent.  Messages larger than a channel
+        buffer go in pieces, piece i of every message in the i-th kernel (both sides derive the
+        same split from the message sizes)."""
+        from ..ops import _lib as L
+
+        if not sends and not recvs:
+            return
+        if not self.region_bytes:
+            raise RuntimeError("IpcComm: point-to-point disabled (p2p_mb = 0) or a one-rank group")
+        units = self.region_bytes // 2
+
+        def pieces(t):
+            if not t.is_contiguous() or (t.numel() * t.element_size()) % 2:
+                raise ValueError("IpcComm.sendrecv: contiguous tensors of an even byte count")
+            n = t.numel() * t.element_size() // 2
+            base = t.data_ptr()
+            return [(base + 2 * u0, min(units, n - u0)) for u0 in range(0, n, units)] or [(base, 0)]
+
+        sp = [(pieces(t), q) for t, q in sends]
+        rp = [(pieces(t), q) for t, q in recvs]
+        nround = max([len(x) for x, _ in sp + rp])
+        s = (stream or torch.cuda.current_stream(self.device)).cuda_stream
+        for i in range(nround):
+            snd = [(x[i], q) for x, q in sp if i < len(x)]
+            rcv = [(x[i], q) for x, q in rp if i < len(x)]
+            while snd or rcv:
+                a = L.IpcP2PArgs()
+                for p in range(L.IPC_MAXW):
+                    a.slot[p] = self.p2p_slots[p] or None
+                    a.flags[p] = self.flags[p] or None
+                a.cnt, a.error = self.p2p_cnt.data_ptr(), self.error.data_ptr()
+                a.region_bytes, a.spin_limit = self.region_bytes, self.spin_limit
+                a.rank, a.world = self.rank, self.size
+                bs, snd = snd[:L.IPC_P2P_MAX], snd[L.IPC_P2P_MAX:]
+                br, rcv = rcv[:L.IPC_P2P_MAX], rcv[L.IPC_P2P_MAX:]
+                for j, ((ptr, n), q) in enumerate(bs):
+                    a.send_ptr[j], a.send_n[j], a.send_peer[j] = ptr, n, q
+                for j, ((ptr, n), q) in enumerate(br):
+                    a.recv_ptr[j], a.recv_n[j], a.recv_peer[j] = ptr, n, q
+                a.nsend, a.nrecv = len(bs), len(br)
+                _rc(_lib().dpc_ipc_p2p(ctypes.byref(a), s), "dpc_ipc_p2p")
 
     # ------------------------------------------------------------------ health / teardown
     def check(self) -> None:

@@ -463,12 +463,11 @@ class NativeTransport(Transport):
 class IpcTransport(NativeTransport):
     """Intra-node collectives by direct peer access (``parallel/ipc_comm.py``, ``--comm ipc``):
     the same side-stream / event / watchdog plumbing as the RCCL transport, the kernels of
-    ``ops/csrc/ipc_coll.hip`` instead of RCCL's.  All-reduce, reduce-scatter, all-gather and
-    broadcast (DDP and FSDP); no point-to-point, so the pipeline recipes keep RCCL / torch.
-    Bootstraps over any process group -- gloo included -- so two ranks may share one GPU."""
+    ``ops/csrc/ipc_coll.hip`` instead of RCCL's -- all-reduce, reduce-scatter, all-gather,
+    broadcast and grouped point-to-point, so every recipe runs on it.  Bootstraps over any process
+    group -- gloo included -- so several ranks may share one GPU."""
 
     kind = "ipc"
-    p2p = False  # (FSDP's rank-0 checkpoint gather all-gathers instead)
 
     def __init__(self, group=None, device=None):
         from .ipc_comm import IpcComm
@@ -479,10 +478,14 @@ class IpcTransport(NativeTransport):
         super().__init__(group, dev, native=IpcComm(group, dev))
 
     def sendrecv(self, sends=(), recvs=(), async_op=False):
-        raise NotImplementedError("IpcTransport: no point-to-point (pipeline recipes: --comm native / torch)")
+        if not sends and not recvs:
+            return _Done()
+        sends = [(t.detach().contiguous(), p) for t, p in sends]
+        return self._enqueue(lambda s: self.nc.sendrecv(sends, recvs, stream=s),
+                             [t for t, _ in sends] + [t for t, _ in recvs], async_op, "sendrecv")
 
     def split(self, color: int, key: int, group=None):
-        raise NotImplementedError("IpcTransport: no sub-communicators")
+        raise NotImplementedError("IpcTransport: no sub-communicators (make_mesh_transports builds one per group)")
 
 
 def _want_native(kind: str, device) -> bool:
@@ -518,8 +521,9 @@ def make_mesh_transports(pp_group, dp_group, stage: int, replica: int, device=No
     ONE world communicator split twice with ncclCommSplit (color = replica -> the pipeline of
     this replica, color = stage -> the replicas of this stage)."""
     kind = kind or os.environ.get("DPC_COMM", "auto")
-    if kind == "ipc":  # (no point-to-point over IPC: the mesh takes the automatic choice)
-        kind = "auto"
+    if kind == "ipc" and comm.world_size() > 1 and torch.device(device if device is not None else "cpu").type == "cuda":
+        # one peer-access communicator per group (they bootstrap over any torch group: no split)
+        return IpcTransport(pp_group, device), IpcTransport(dp_group, device)
     if comm.world_size() > 1 and _want_native(kind, device):
         built = []
         try:

@@ -146,6 +146,31 @@ def ipc_collectives_worker(rank, world, out):
         assert torch.equal(x, ref_sum(5000, torch.float32, 10 + it)), ("graph f32", it)
         assert torch.equal(y, ref_sum(777, torch.bfloat16, 20 + it)), ("graph bf16", it)
         checked += 2
+    # point-to-point: both directions in one group, two messages on one channel, a message larger
+    # than a channel buffer (pieces), f32 and bf16, then three groups in a row on a channel
+    cp = IpcComm(slot_mb=0.25, spin_limit=1 << 22, p2p_mb=0.0625)  # 64 KiB channels
+    peer = 1 - rank
+    for n, dtype in ((10, torch.float32), (100000, torch.float32), (77777, torch.bfloat16)):
+        s1, s2 = _ipc_input(rank, n, dtype, 30), _ipc_input(rank, n // 2 + 1, dtype, 31)
+        r1 = torch.empty(n, dtype=dtype, device="cuda")
+        r2 = torch.empty(n // 2 + 1, dtype=dtype, device="cuda")
+        cp.sendrecv(sends=[(s1, peer), (s2, peer)], recvs=[(r1, peer), (r2, peer)])
+        torch.cuda.synchronize()
+        assert torch.equal(r1, _ipc_input(peer, n, dtype, 30)) and torch.equal(r2, _ipc_input(peer, n // 2 + 1, dtype, 31)), ("p2p", n)
+        checked += 2
+    for it in range(3):  # one direction per group, alternating (the 1F1B pattern of two stages)
+        t = _ipc_input(rank, 5000, torch.float32, 40 + it)
+        r = torch.empty(5000, device="cuda")
+        if (rank + it) % 2 == 0:
+            cp.sendrecv(sends=[(t, peer)])
+        else:
+            cp.sendrecv(recvs=[(r, peer)])
+            torch.cuda.synchronize()
+            assert torch.equal(r, _ipc_input(peer, 5000, torch.float32, 40 + it)), ("p2p alternating", it)
+            checked += 1
+    torch.cuda.synchronize()
+    cp.check()
+    cp.destroy()
     c.check()
     c.destroy()
     if rank == 0:
@@ -161,19 +186,27 @@ def ipc_engine_worker(rank, world, out, kind, steps, graph):
     from distributed_pytorch_cookbook_amd.engine.data_parallel import DataParallelEngine
     from distributed_pytorch_cookbook_amd.engine.fsdp import FSDPEngine
 
+    from distributed_pytorch_cookbook_amd.engine.pipeline import PipelineEngine
+
     m = make_model()
     if kind == "ddp":
         eng = DataParallelEngine(m, "cuda", lr=LR, bucket_mb=0.2, graph=graph, comm_kind="ipc")
         assert len(eng.store.buckets) >= 2
-    else:
+        tp, dp, rep = eng.store.tp, world, rank
+    elif kind == "fsdp":
         eng = FSDPEngine(m, "cuda", lr=LR, prefetch=1, graph=graph, comm_kind="ipc")
-    assert eng.store.tp.kind == "ipc", eng.store.tp.kind
+        tp, dp, rep = eng.store.tp, world, rank
+    else:  # pipeline over the peer-access point-to-point: "pipe-<schedule>"
+        eng = PipelineEngine(m, "cuda", lr=LR, pp=world, dp=1, num_microbatches=4, schedule=kind.split("-")[1],
+                             bucket_mb=0.2, seq_len=S - 1, graph=graph, comm_kind="ipc")
+        tp, dp, rep = eng.pp_tp, 1, 0
+    assert tp.kind == "ipc", tp.kind
     for s in range(steps):
-        eng.train_step(*shard(*full_batch(step=s), rank, world))
+        eng.train_step(*shard(*full_batch(step=s), rep, dp))
     torch.cuda.synchronize()
     if graph:
         assert eng._stepper.graph is not None, "the two-rank step was not captured"
-    eng.store.tp.nc.check()
+    tp.nc.check()
     # the replicas / shards agree bit for bit across the ranks (each shard summed once, by its owner)
     sd = eng.full_state_dict()
     if rank == 0:

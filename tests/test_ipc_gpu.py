@@ -14,7 +14,7 @@ pytestmark = pytest.mark.gpu
 def test_ipc_collectives_two_ranks_one_gpu(tmp_path):
     out = tmp_path / "ipc.pt"
     run_workers(ipc_collectives_worker, 2, str(out), timeout=110)
-    assert torch.load(out, weights_only=True)["checked"] == 48
+    assert torch.load(out, weights_only=True)["checked"] == 48 + 6 + 1
 
 
 @pytest.fixture(scope="module")
@@ -33,7 +33,8 @@ def close(sd_a, sd_b, tol=5e-2, lr=1e-3, steps=3):
     assert not bad, bad
 
 
-@pytest.mark.parametrize("kind,graph", [("ddp", True), ("ddp", False), ("fsdp", True)])
+@pytest.mark.parametrize("kind,graph", [("ddp", True), ("ddp", False), ("fsdp", True), ("pipe-1f1b", True),
+                                        ("pipe-zb2", True), ("pipe-1f1b", False)])
 def test_ipc_transport_engines_two_ranks_one_gpu(tmp_path, ref, kind, graph):
     out = tmp_path / f"{kind}.pt"
     run_workers(ipc_engine_worker, 2, str(out), kind, 3, graph, timeout=110)
