@@ -21,6 +21,7 @@ import time
 import torch
 from torch.utils.data import DataLoader, Sampler
 
+from ..parallel.transport import check_peer_comms
 from ..parallel import comm
 from ..utils.batch import generate, prepare_batch
 from ..utils.checkpoint import (latest_checkpoint, load_model_state, load_train_state, rng_state,
@@ -229,6 +230,7 @@ class Trainer:
                 avg = (window / max(nwin, 1)).item() if window is not None else float("nan")
                 if self.device.type == "cuda":
                     torch.cuda.synchronize()
+                    check_peer_comms()  # (a peer-access wait that gave up would leave wrong data)
                 dt = time.perf_counter() - t0
                 tps = tokens / dt if dt > 0 else 0.0
                 util = mfu(tps / max(comm.world_size(), 1), self.flops_per_token)

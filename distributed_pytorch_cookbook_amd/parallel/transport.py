@@ -337,6 +337,16 @@ def _capturing() -> bool:
     return torch.cuda.is_available() and torch.cuda.is_current_stream_capturing()
 
 
+def check_peer_comms() -> None:
+    """Raise if a peer-access (IPC) communicator's wait gave up since the last check: its data is
+    not valid.  Host-synchronous (one read of each error word): called at the trainer's progress
+    points and at shutdown."""
+    for nc in _native_comms:
+        chk = getattr(nc, "check", None)
+        if chk is not None and getattr(nc, "_own", None):
+            chk()
+
+
 def shutdown_native() -> None:
     """Destroy every native communicator (splits first) and stop the watchdog: the native
     half of the reference's ``destroy_process_group`` (``/root/reference/main-ddp.py:34-35``).
@@ -347,6 +357,10 @@ def shutdown_native() -> None:
 
     if torch.cuda.is_available():
         torch.cuda.synchronize()
+    try:
+        check_peer_comms()
+    except RuntimeError as exc:  # (teardown goes on; the run already produced its output)
+        print(f"[comm] {exc}")
     native_comm.watchdog_stop()
     while _native_comms:
         nc = _native_comms.pop()
