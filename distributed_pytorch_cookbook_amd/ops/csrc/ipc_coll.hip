@@ -14,8 +14,10 @@
 //   * epoch: each workgroup keeps its own collective counter in device memory (ep[g]), read at its
 //     start and advanced at its end, so a replayed graph runs a new collective every time.  The
 //     staging buffer has two halves used alternately (epoch parity): a rank rewrites a half only
-//     after the barrier of the NEXT collective, which every peer enters after finishing its reads
-//     of that half.
+//     after the barrier of the NEXT collective, and a peer workgroup at that barrier means the
+//     peer's previous collective kernel -- every workgroup of it, whatever sub-slices they read --
+//     has finished (its kernels run in stream order).  (Point-to-point has no such ordering: a
+//     sender waits for the ACKs of all of the receiver's workgroups before it reuses a half.)
 //   * barrier value of phase k in epoch e: 2 e + k (k = 1, 2), so flags never need resetting.
 //   * every wait is bounded (spin_limit polls): a peer that never arrives sets *error and the
 //     kernel finishes -- the host raises on the error word (IpcComm.check) instead of hanging.
@@ -347,8 +349,12 @@ __global__ __launch_bounds__(256) void ipc_p2p_kernel(IpcP2PArgs a) {
   for (int i = 0; i < a.nsend; ++i) {
     const int q = a.send_peer[i];
     const unsigned c = sent[q * IPC_G + g];
-    if (c >= 2) {  // the message two back on this channel copied out by q (its half is free again)
-      if (threadIdx.x == 0) ipc_wait(a.flags[r] + 2 * FL + q * IPC_G + g, c - 1, a.spin_limit, a.error);
+    if (c >= 2) {
+      // the message two back on this channel copied out of its half by EVERY workgroup of q: two
+      // messages of different sizes split into different sub-slices, so this workgroup's part of
+      // the new message may overlap another workgroup's part of the old one (one ACK per
+      // workgroup of q, all in this rank's array)
+      if (threadIdx.x < IPC_G) ipc_wait(a.flags[r] + 2 * FL + q * IPC_G + threadIdx.x, c - 1, a.spin_limit, a.error);
       __syncthreads();
     }
     const long long n = a.send_n[i];
@@ -362,6 +368,7 @@ __global__ __launch_bounds__(256) void ipc_p2p_kernel(IpcP2PArgs a) {
       __hip_atomic_store(a.flags[q] + FL + r * IPC_G + g, c + 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
       sent[q * IPC_G + g] = c + 1u;
     }
+    __syncthreads();  // (the next message to q reads the advanced counter)
   }
   for (int i = 0; i < a.nrecv; ++i) {
     const int p = a.recv_peer[i];
@@ -379,6 +386,7 @@ __global__ __launch_bounds__(256) void ipc_p2p_kernel(IpcP2PArgs a) {
       __hip_atomic_store(a.flags[p] + 2 * FL + r * IPC_G + g, c + 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
       rcvd[p * IPC_G + g] = c + 1u;
     }
+    __syncthreads();
   }
 }
 

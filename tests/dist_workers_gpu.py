@@ -168,6 +168,20 @@ def ipc_collectives_worker(rank, world, out):
             torch.cuda.synchronize()
             assert torch.equal(r, _ipc_input(peer, 5000, torch.float32, 40 + it)), ("p2p alternating", it)
             checked += 1
+    # a stream of messages of different sizes on one channel (rank 1 -> 0): every half is reused with
+    # a different split into workgroup sub-slices than its previous message (the FSDP checkpoint
+    # gather's pattern), and the sender runs ahead of the receiver by up to two messages
+    sizes = [200000, 1000, 150000, 70, 99999, 64, 180000, 3000, 120000, 5]
+    if rank == 1:
+        for k, n in enumerate(sizes):
+            cp.sendrecv(sends=[(_ipc_input(1, n, torch.float32, 50 + k), 0)])
+    else:
+        for k, n in enumerate(sizes):
+            r = torch.empty(n, device="cuda")
+            cp.sendrecv(recvs=[(r, 1)])
+            torch.cuda.synchronize()
+            assert torch.equal(r, _ipc_input(1, n, torch.float32, 50 + k)), ("p2p stream", k, n)
+            checked += 1
     torch.cuda.synchronize()
     cp.check()
     cp.destroy()

@@ -14,7 +14,7 @@ pytestmark = pytest.mark.gpu
 def test_ipc_collectives_two_ranks_one_gpu(tmp_path):
     out = tmp_path / "ipc.pt"
     run_workers(ipc_collectives_worker, 2, str(out), timeout=110)
-    assert torch.load(out, weights_only=True)["checked"] == 48 + 6 + 1
+    assert torch.load(out, weights_only=True)["checked"] == 48 + 6 + 1 + 10
 
 
 @pytest.fixture(scope="module")
