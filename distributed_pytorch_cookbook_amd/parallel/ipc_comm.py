@@ -92,17 +92,28 @@ class IpcComm:
             self.p2p_slots = [0] * L.IPC_MAXW
             tables = (self.slots, self.flags, self.p2p_slots)
             self._opened = []
-            for p in range(self.size):
-                if p == self.rank:
-                    for tab, v in zip(tables, self._own):
-                        tab[p] = v
-                    continue
-                for tab, raw in zip(tables, handles[p]):
-                    out = ctypes.c_void_p()
-                    _rc(lib.dpc_ipc_open(ctypes.create_string_buffer(raw, hsize), ctypes.byref(out)),
-                        f"hipIpcOpenMemHandle (rank {p})")
-                    self._opened.append(out.value)
-                    tab[p] = out.value
+            err = None
+            try:
+                for p in range(self.size):
+                    if p == self.rank:
+                        for tab, v in zip(tables, self._own):
+                            tab[p] = v
+                        continue
+                    for tab, raw in zip(tables, handles[p]):
+                        out = ctypes.c_void_p()
+                        _rc(lib.dpc_ipc_open(ctypes.create_string_buffer(raw, hsize), ctypes.byref(out)),
+                            f"hipIpcOpenMemHandle (rank {p})")
+                        self._opened.append(out.value)
+                        tab[p] = out.value
+            except RuntimeError as exc:
+                err = exc
+            # every rank mapped every peer, or all of them give up together (no rank left waiting in
+            # a barrier for one that raised)
+            from .native_comm import _agree
+
+            if not _agree(err is None, group):
+                self._release_buffers()
+                raise RuntimeError(f"IpcComm: peer buffers could not be mapped on every rank ({err or 'another rank'})")
             self.ep = torch.zeros(self.groups, dtype=torch.int32, device=self.device)
             self.p2p_cnt = torch.zeros(2 * L.IPC_MAXW * self.groups, dtype=torch.int32, device=self.device)
             self.error = torch.zeros(1, dtype=torch.int32, device=self.device)
@@ -248,12 +259,7 @@ class IpcComm:
 
     check_async = check  # (transport.check_drained polls every communicator through this name)
 
-    def destroy(self) -> None:
-        if not self._own:
-            return
-        torch.cuda.synchronize(self.device)
-        if self.size > 1 and dist.is_initialized():
-            dist.barrier(group=self.group)  # no peer still reads this rank's buffers
+    def _release_buffers(self) -> None:
         lib = _lib()
         for p in self._opened:
             lib.dpc_ipc_close(ctypes.c_void_p(p))
@@ -261,3 +267,11 @@ class IpcComm:
         for p in self._own:
             lib.dpc_ipc_free(ctypes.c_void_p(p))
         self._own = ()
+
+    def destroy(self) -> None:
+        if not self._own:
+            return
+        torch.cuda.synchronize(self.device)
+        if self.size > 1 and dist.is_initialized():
+            dist.barrier(group=self.group)  # no peer still reads this rank's buffers
+        self._release_buffers()
