@@ -225,3 +225,26 @@ def ipc_engine_worker(rank, world, out, kind, steps, graph):
     sd = eng.full_state_dict()
     if rank == 0:
         torch.save({k: v.float().cpu() for k, v in sd.items()}, out)
+
+
+def ipc_timeout_worker(rank, world, out):
+    """A rank that never arrives: the peer's bounded waits give up, the kernel ends (no hung GPU),
+    and check() names the failure."""
+    _init()
+    import torch.distributed as dist
+
+    from distributed_pytorch_cookbook_amd.parallel.ipc_comm import IpcComm
+
+    c = IpcComm(slot_mb=0.25, spin_limit=1 << 14)
+    if rank == 0:
+        t = torch.ones(1000, device="cuda")
+        c.all_reduce(t)  # rank 1 never calls it
+        torch.cuda.synchronize()
+        try:
+            c.check()
+            raised = False
+        except RuntimeError:
+            raised = True
+        torch.save({"raised": raised}, out)
+    dist.barrier()
+    c.destroy()

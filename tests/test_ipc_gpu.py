@@ -39,3 +39,11 @@ def test_ipc_transport_engines_two_ranks_one_gpu(tmp_path, ref, kind, graph):
     out = tmp_path / f"{kind}.pt"
     run_workers(ipc_engine_worker, 2, str(out), kind, 3, graph, timeout=110)
     close(torch.load(out, weights_only=True), ref[0])
+
+
+def test_ipc_wait_gives_up_without_peer(tmp_path):
+    out = tmp_path / "timeout.pt"
+    from dist_workers_gpu import ipc_timeout_worker
+
+    run_workers(ipc_timeout_worker, 2, str(out), timeout=110)
+    assert torch.load(out, weights_only=True)["raised"]
