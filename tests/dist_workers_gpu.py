@@ -149,7 +149,7 @@ def ipc_collectives_worker(rank, world, out):
     # point-to-point: both directions in one group, two messages on one channel, a message larger
     # than a channel buffer (pieces), f32 and bf16, then three groups in a row on a channel
     cp = IpcComm(slot_mb=0.25, spin_limit=1 << 22, p2p_mb=0.0625)  # 64 KiB channels
-    peer = 1 - rank
+    peer = rank ^ 1  # (pairs 0-1, 2-3, ...)
     for n, dtype in ((10, torch.float32), (100000, torch.float32), (77777, torch.bfloat16)):
         s1, s2 = _ipc_input(rank, n, dtype, 30), _ipc_input(rank, n // 2 + 1, dtype, 31)
         r1 = torch.empty(n, dtype=dtype, device="cuda")
@@ -175,7 +175,7 @@ def ipc_collectives_worker(rank, world, out):
     if rank == 1:
         for k, n in enumerate(sizes):
             cp.sendrecv(sends=[(_ipc_input(1, n, torch.float32, 50 + k), 0)])
-    else:
+    elif rank == 0:
         for k, n in enumerate(sizes):
             r = torch.empty(n, device="cuda")
             cp.sendrecv(recvs=[(r, 1)])

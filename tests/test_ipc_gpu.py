@@ -11,9 +11,10 @@ from dist_workers_gpu import ipc_collectives_worker, ipc_engine_worker, referenc
 pytestmark = pytest.mark.gpu
 
 
-def test_ipc_collectives_two_ranks_one_gpu(tmp_path):
+@pytest.mark.parametrize("world", [2, 4])
+def test_ipc_collectives_two_ranks_one_gpu(tmp_path, world):
     out = tmp_path / "ipc.pt"
-    run_workers(ipc_collectives_worker, 2, str(out), timeout=110)
+    run_workers(ipc_collectives_worker, world, str(out), timeout=110)
     assert torch.load(out, weights_only=True)["checked"] == 48 + 6 + 1 + 10
 
 
@@ -33,11 +34,12 @@ def close(sd_a, sd_b, tol=5e-2, lr=1e-3, steps=3):
     assert not bad, bad
 
 
-@pytest.mark.parametrize("kind,graph", [("ddp", True), ("ddp", False), ("fsdp", True), ("pipe-1f1b", True),
-                                        ("pipe-zb2", True), ("pipe-1f1b", False)])
-def test_ipc_transport_engines_two_ranks_one_gpu(tmp_path, ref, kind, graph):
+@pytest.mark.parametrize("kind,graph,world", [("ddp", True, 2), ("ddp", False, 2), ("fsdp", True, 2),
+                                              ("pipe-1f1b", True, 2), ("pipe-zb2", True, 2), ("pipe-1f1b", False, 2),
+                                              ("ddp", True, 4), ("fsdp", True, 4)])
+def test_ipc_transport_engines_two_ranks_one_gpu(tmp_path, ref, kind, graph, world):
     out = tmp_path / f"{kind}.pt"
-    run_workers(ipc_engine_worker, 2, str(out), kind, 3, graph, timeout=110)
+    run_workers(ipc_engine_worker, world, str(out), kind, 3, graph, timeout=110)
     close(torch.load(out, weights_only=True), ref[0])
 
 
