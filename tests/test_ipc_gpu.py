@@ -1,4 +1,4 @@
-"""Peer-access collectives (ops/csrc/ipc_coll.hip, parallel/ipc_comm.py) with two ranks sharing
+"""Peer-access collectives (ops/csrc/ipc_coll.hip, parallel/ipc_comm.py) with 2, 4 or 8 ranks sharing
 the one GPU of a test box: HIP IPC maps a buffer of another process on the same device, which
 RCCL refuses ("Duplicate GPU detected") -- so these are also the only tests in which an N > 1
 step graph, collectives inside, is captured and replayed for real."""
@@ -11,8 +11,8 @@ from dist_workers_gpu import ipc_collectives_worker, ipc_engine_worker, referenc
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize("world", [2, 4])
-def test_ipc_collectives_two_ranks_one_gpu(tmp_path, world):
+@pytest.mark.parametrize("world", [2, 4, 8])
+def test_ipc_collectives_ranks_share_one_gpu(tmp_path, world):
     out = tmp_path / "ipc.pt"
     run_workers(ipc_collectives_worker, world, str(out), timeout=110)
     assert torch.load(out, weights_only=True)["checked"] == 48 + 6 + 1 + 10
@@ -36,8 +36,8 @@ def close(sd_a, sd_b, tol=5e-2, lr=1e-3, steps=3):
 
 @pytest.mark.parametrize("kind,graph,world", [("ddp", True, 2), ("ddp", False, 2), ("fsdp", True, 2),
                                               ("pipe-1f1b", True, 2), ("pipe-zb2", True, 2), ("pipe-1f1b", False, 2),
-                                              ("ddp", True, 4), ("fsdp", True, 4)])
-def test_ipc_transport_engines_two_ranks_one_gpu(tmp_path, ref, kind, graph, world):
+                                              ("ddp", True, 4), ("fsdp", True, 4), ("ddp", True, 8)])
+def test_ipc_transport_engines_ranks_share_one_gpu(tmp_path, ref, kind, graph, world):
     out = tmp_path / f"{kind}.pt"
     run_workers(ipc_engine_worker, world, str(out), kind, 3, graph, timeout=110)
     close(torch.load(out, weights_only=True), ref[0])
