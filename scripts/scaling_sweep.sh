@@ -5,7 +5,8 @@
 # reduce-scatter dtype at N = 8, then the pipeline recipes' boundary (p2p) dtype and the PP x DP
 # stage all-reduce dtype at N = 8, and the RCCL channel count against the GEMMs it shares CUs
 # with (a 16-CU collective-sized occupier cost DDP 3.6 % on one GPU,
-# profiles/r4_corun/; fewer channels = fewer co-resident CUs, at a lower ring bandwidth).  One
+# profiles/r4_corun/; fewer channels = fewer co-resident CUs, at a lower ring bandwidth), and the
+# peer-access transport (--comm ipc) and the N > 1 step graph against the RCCL defaults.  One
 # JSON line per run in gpurun_out/scaling_sweep.jsonl.
 #   bash scripts/scaling_sweep.sh [max_gpus]
 set -u
@@ -35,6 +36,13 @@ for r in pipe pipe_ddp; do
   for w in fp32 bf16; do run "$MAXG" --recipe $r --pp_comm_dtype $w || exit $?; done  # PP wire dtype
 done
 for dt in fp32 bf16; do run "$MAXG" --recipe pipe_ddp --reduce_dtype $dt || exit $?; done  # PP x DP AR dtype
+for n in 2 4 8; do  # the peer-access transport (parallel/ipc_comm.py: two-shot over all links) vs RCCL
+  [ "$n" -gt "$MAXG" ] && break
+  run $n --comm ipc || exit $?
+  run $n --comm ipc --graph || exit $?
+done
+run "$MAXG" --recipe fsdp --comm ipc || exit $?
+run "$MAXG" --graph || exit $?  # RCCL inside the captured step at N > 1
 for ch in 4 8 16 32; do  # RCCL channels (CUs a collective occupies) under the DDP / FSDP steps
   NCCL_MIN_NCHANNELS=$ch NCCL_MAX_NCHANNELS=$ch run "$MAXG" || exit $?
   NCCL_MIN_NCHANNELS=$ch NCCL_MAX_NCHANNELS=$ch run "$MAXG" --recipe fsdp || exit $?
