@@ -1523,15 +1523,18 @@ __global__ __launch_bounds__(256, OCC) void attn_bwd_dq_kernel(AttnArgs p) {
 // 7 / 8 = the same on a persistent grid, 9 = 6 with the tile loop split by kind (attn_fwd3_kernel;
 // its MFMA-row-sum form spilled 80 registers and ran 272 us, so it is not built).
 // Defaults per head size (GPT-2 small shape, B=64 S=1023 H=12, profiles/r2_attn/, round 6:
-// profiles/r6_attn/):  hd 64: forward 9, backward 1;  hd 32: forward 2, backward 2.
+// profiles/r6_attn/):  hd 64: forward 9, backward 1;  hd 32: forward 6 (S < 512) / 9, backward 2.
 static int g_attn_env[2] = {-2, -2};
-static int attn_var(int hd, int bwd) {
+static int attn_var(int hd, int bwd, int S = 0) {
   if (g_attn_env[0] == -2) {
     g_attn_env[0] = g_attn_env[1] = -1;
     if (const char* e = getenv("DPC_ATTN_VAR")) sscanf(e, "%d,%d", &g_attn_env[0], &g_attn_env[1]);
   }
   if (g_attn_env[bwd] >= 0) return g_attn_env[bwd];
-  if (hd == 32) return 2;
+  // hd 32 forward (round 6, profiles/r6_attn/hd32_fwd_variants.log): the pair streams beat the
+  // per-block kernel (2) -- fwd2 (6) at the reference CLI default S = 255 (16.9 vs 18.2 us),
+  // fwd3 (9) at S = 1023 (111.3 vs 120.5 us)
+  if (hd == 32) return bwd ? 2 : (S < 512 ? 6 : 9);
   return bwd ? 1 : 9;
 }
 
@@ -1561,7 +1564,7 @@ static int launch_bwd128(const AttnArgs* a, hipStream_t stream) {
 
 template <int HD>
 static int launch_fwd(const AttnArgs* a, hipStream_t stream) {
-  const int var = attn_var(HD, 0);
+  const int var = attn_var(HD, 0, a->S);
   dim3 grid((unsigned)(((a->S + QB - 1) / QB) * a->N * a->H));  // 1-D: xcd_work() maps it
   if (var >= 5 && var <= 9) {  // pair stream (attn_fwd2_kernel); 7, 8: persistent grid; 9: = 6 with
     // the tile loop split by kind (attn_fwd3_kernel)
