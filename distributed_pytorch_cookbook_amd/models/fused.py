@@ -47,6 +47,22 @@ def _dh_dtype(cdt):
     return torch.float32 if _DH_F32 else cdt
 
 
+# The LM-head input gradient dX = dlogits @ W_lm has K = the padded vocabulary (50304) and an
+# [T, D] output: at a small D it is a handful of 256 x 256 tiles (the reference CLI default model,
+# D = 256 at T = 16320: 64 tiles for 256 CUs), and a bf16 output cannot be split along K (the
+# split-K kernel sums f32 slabs).  Below half a chip of tiles the product is formed in f32, which
+# the persistent kernel splits along K to fill the chip; the final LayerNorm backward reads f32 dy
+# as it does under DPC_DH_F32.  DPC_HEAD_DGRAD_F32=0 / 1 forces either form.
+_HEAD_DGRAD_F32 = os.environ.get("DPC_HEAD_DGRAD_F32", "auto")
+
+
+def _head_dgrad_dtype(T, D, cdt):
+    if _HEAD_DGRAD_F32 in ("0", "1"):
+        return torch.float32 if _HEAD_DGRAD_F32 == "1" else _dh_dtype(cdt)
+    tiles = ((T + 255) // 256) * ((D + 255) // 256)
+    return torch.float32 if tiles < 128 else _dh_dtype(cdt)
+
+
 # rows per chunk of the logits GEMM + cross-entropy (0 = whole batch at once).  Off by
 # default: on GPT-2 small (B=32) chunks of 1024 / 2048 / 4096 rows ran 751K / 757K / 762K
 # tok/s against 775-781K unchunked -- the smaller logits GEMMs lose more than the
@@ -512,7 +528,8 @@ class _HeadFn(torch.autograd.Function):
         _w(lambda: linear_wgrad(dl, hf, out=g(head.weight), alpha_t=scale))
         # K = padded vocab: the CE kernel zeroed dlogits' pad columns, W_lm rows >= V read as 0
         dhf = linear_dgrad(dlogits, _head_weight_padded(store, head, dlogits.shape[1]),
-                           out_dtype=_dh_dtype(store.compute_dtype), alpha_t=scale)
+                           out_dtype=_head_dgrad_dtype(x.shape[0], x.shape[1], store.compute_dtype),
+                           alpha_t=scale)
         dx = torch.empty_like(x)  # (written, not accumulated: dx_set)
         kw = {}
         if ctx.prev_tail is not None:  # the last layer's down-projection bias / act / dropout backward
