@@ -52,7 +52,9 @@ def _dh_dtype(cdt):
 # D = 256 at T = 16320: 64 tiles for 256 CUs), and a bf16 output cannot be split along K (the
 # split-K kernel sums f32 slabs).  Below half a chip of tiles the product is formed in f32, which
 # the persistent kernel splits along K to fill the chip; the final LayerNorm backward reads f32 dy
-# as it does under DPC_DH_F32.  DPC_HEAD_DGRAD_F32=0 / 1 forces either form.
+# as it does under DPC_DH_F32.  DPC_HEAD_DGRAD_F32=0 / 1 forces either form.  (The same rule for
+# the layers' QKV / FFN-up input gradients, K = 3 D / 4 D, measured 1.7 % slower on that model --
+# too short a K to split: profiles/r6_final2/ref_default_ln_dgrad_negative.log.)
 _HEAD_DGRAD_F32 = os.environ.get("DPC_HEAD_DGRAD_F32", "auto")
 
 
