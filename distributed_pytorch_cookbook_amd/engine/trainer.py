@@ -227,7 +227,7 @@ class Trainer:
                 window = loss if window is None else window + loss
                 nwin += 1
             if (i + 1) % PRINT_FREQ == 0:
-                avg = (window / max(nwin, 1)).item() if window is not None else float("nan")
+                avg = self._window_loss(window, nwin)
                 if self.device.type == "cuda":
                     torch.cuda.synchronize()
                     check_peer_comms()  # (a peer-access wait that gave up would leave wrong data)
@@ -243,9 +243,24 @@ class Trainer:
                 self._jsonl(rec)
                 window, nwin, tokens, t0 = None, 0, 0, time.perf_counter()
         prof.close()
-        if window is not None and nwin:
-            avg = (window / nwin).item()
-            self.history.append({"epoch": ei + 1, "step": e.step_count, "loss": avg})
+        if self._pipelined() or (window is not None and nwin):  # (a collective for pipelines: every rank)
+            avg = self._window_loss(window, nwin)
+            if avg == avg:
+                self.history.append({"epoch": ei + 1, "step": e.step_count, "loss": avg})
+
+    def _pipelined(self) -> bool:
+        return getattr(self.engine, "pp", 1) > 1 and comm.world_size() > 1
+
+    def _window_loss(self, window, nwin) -> float:
+        """Mean training loss of the last window.  A pipeline's loss exists only on its last stage
+        (one per replica) while rank 0 -- the logger -- holds the first: the window sums and counts
+        are summed over the world (the other stages add zeros), one collective on every rank."""
+        if not self._pipelined():
+            return (window / max(nwin, 1)).item() if window is not None else float("nan")
+        ws = window if window is not None else torch.zeros((), device=self.device)
+        red = comm.all_reduce_scalars([ws, float(nwin if window is not None else 0)], self.device)
+        n = float(red[1])
+        return float(red[0]) / n if n > 0 else float("nan")
 
     @torch.no_grad()
     def validate(self, ei, loader):
