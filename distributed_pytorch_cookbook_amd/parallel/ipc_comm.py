@@ -151,7 +151,18 @@ class IpcComm:
             return False, 4
         if t.dtype == torch.bfloat16:
             return True, 2
-        raise TypeError(f"IpcComm: {t.dtype} (f32 and bf16 only)")
+        raise TypeError(f"IpcComm: {t.dtype} (sums in f32 and bf16 only)")
+
+    @staticmethod
+    def _raw(t):
+        """A tensor of any dtype as 2-byte units for the copy-only collectives (broadcast,
+        all-gather): the kernel moves their bits without arithmetic."""
+        if t.dtype in (torch.float32, torch.bfloat16):
+            return t
+        flat = t.reshape(-1)
+        if (flat.numel() * flat.element_size()) % 2:
+            raise TypeError(f"IpcComm: {t.dtype} x {flat.numel()} is an odd number of bytes")
+        return flat.view(torch.uint8).view(torch.bfloat16) if flat.element_size() == 1 else flat.view(torch.bfloat16)
 
     def all_reduce(self, t, stream=None):
         """Sum over the ranks, in place."""
@@ -182,7 +193,10 @@ class IpcComm:
             piece.record_stream(stream or torch.cuda.current_stream(self.device))
 
     def all_gather(self, out, inp, stream=None):
-        """out[rank * n : (rank + 1) * n] = inp of every rank, n = inp.numel()."""
+        """out[rank * n : (rank + 1) * n] = inp of every rank, n = inp.numel() (any dtype)."""
+        if out.dtype != inp.dtype:
+            raise ValueError("all_gather: out and inp dtypes differ")
+        out, inp = self._raw(out), self._raw(inp)
         bf, es = self._kind(inp)
         n, W = inp.numel(), self.size
         if out.numel() != W * n or inp.dtype != out.dtype:
@@ -199,6 +213,8 @@ class IpcComm:
             ov[:, c0:c1].copy_(piece)
 
     def broadcast(self, t, src: int = 0, stream=None):
+        """``t`` of rank ``src`` to every rank, in place (any dtype)."""
+        t = self._raw(t)
         bf, es = self._kind(t)
         flat = t.view(-1)
         n, cap = flat.numel(), self._cap(BROADCAST, es)

@@ -125,6 +125,14 @@ def ipc_collectives_worker(rank, world, out):
             c.broadcast(b, src=1)
             assert torch.equal(b, _ipc_input(1, n, dtype, 3)), ("broadcast", dtype, n)
             checked += 3
+    # copy-only collectives of any dtype (the pipeline's generation broadcasts int64 tokens)
+    tok = torch.tensor([1000 + rank, -7, 1 << 40], dtype=torch.int64, device="cuda")
+    c.broadcast(tok, src=1)
+    assert tok.tolist() == [1001, -7, 1 << 40], ("broadcast int64", tok.tolist())
+    g8 = torch.empty(W * 6, dtype=torch.uint8, device="cuda")
+    c.all_gather(g8, torch.full((6,), 10 + rank, dtype=torch.uint8, device="cuda"))
+    assert g8.tolist() == [10 + p for p in range(W) for _ in range(6)], ("all_gather uint8", g8.tolist())
+    checked += 2
     # captured: two all-reduces per replay, new inputs each replay
     x = torch.empty(5000, device="cuda")
     y = torch.empty(777, dtype=torch.bfloat16, device="cuda")
