@@ -19,10 +19,11 @@ ap.add_argument("--impls", type=int, nargs="+", default=[2, 4, 11])
 ap.add_argument("--splits", type=int, nargs="+", default=[0, 1, 2, 4, 8, 16])
 ap.add_argument("--T", type=int, default=32736)
 ap.add_argument("--xcd", type=int, nargs="+", default=[0])
+ap.add_argument("--vocab", type=int, default=50304)
 a = ap.parse_args()
 T = a.T
 r = lambda *s: torch.randn(*s, device="cuda").bfloat16()  # noqa: E731
-for M, N in [(2304, 768), (3072, 768), (768, 3072), (768, 768), (50257, 768)]:
+for M, N in [(2304, 768), (3072, 768), (768, 3072), (768, 768), (a.vocab, 768)]:
     fl = 2.0 * M * N * T
     out = torch.zeros(M, N, device="cuda")
     A, B = r(T, (M + 7) // 8 * 8)[:, :M], r(T, N)
