@@ -20,6 +20,7 @@ polls instead of hanging the GPU; ``check()`` raises on it.
 """
 from __future__ import annotations
 
+import contextlib
 import ctypes
 import os
 
@@ -146,6 +147,12 @@ class IpcComm:
         return per // _ALIGN * _ALIGN
 
     @staticmethod
+    def _on(stream):
+        """The collective's stream as the current one (the chunked paths' staging tensors are
+        allocated, filled and read there, in order with the kernels)."""
+        return torch.cuda.stream(stream) if stream is not None else contextlib.nullcontext()
+
+    @staticmethod
     def _kind(t):
         if t.dtype == torch.float32:
             return False, 4
@@ -184,13 +191,15 @@ class IpcComm:
         if n <= cap:
             self._launch(REDUCE_SCATTER, inp.data_ptr(), out.data_ptr(), n, bf, stream=stream)
             return
-        # chunked: shard s of chunk k = inp[s n + k cap ...]: gather those pieces per chunk
+        # chunked: shard s of chunk k = inp[s n + k cap ...]: gather those pieces per chunk (the
+        # staging copies on the collective's stream, ordered with its kernels)
         iv = inp.view(W, n)
-        for c0 in range(0, n, cap):
-            c1 = min(n, c0 + cap)
-            piece = iv[:, c0:c1].contiguous()
-            self._launch(REDUCE_SCATTER, piece.data_ptr(), out.view(-1)[c0:c1].data_ptr(), c1 - c0, bf, stream=stream)
-            piece.record_stream(stream or torch.cuda.current_stream(self.device))
+        with self._on(stream):
+            for c0 in range(0, n, cap):
+                c1 = min(n, c0 + cap)
+                piece = iv[:, c0:c1].contiguous()
+                self._launch(REDUCE_SCATTER, piece.data_ptr(), out.view(-1)[c0:c1].data_ptr(), c1 - c0, bf,
+                             stream=stream)
 
     def all_gather(self, out, inp, stream=None):
         """out[rank * n : (rank + 1) * n] = inp of every rank, n = inp.numel() (any dtype)."""
@@ -206,11 +215,12 @@ class IpcComm:
             self._launch(ALLGATHER, inp.data_ptr(), out.data_ptr(), n, bf, stream=stream)
             return
         ov = out.view(W, n)
-        for c0 in range(0, n, cap):
-            c1 = min(n, c0 + cap)
-            piece = torch.empty((W, c1 - c0), dtype=out.dtype, device=out.device)
-            self._launch(ALLGATHER, inp.view(-1)[c0:c1].data_ptr(), piece.data_ptr(), c1 - c0, bf, stream=stream)
-            ov[:, c0:c1].copy_(piece)
+        with self._on(stream):
+            for c0 in range(0, n, cap):
+                c1 = min(n, c0 + cap)
+                piece = torch.empty((W, c1 - c0), dtype=out.dtype, device=out.device)
+                self._launch(ALLGATHER, inp.view(-1)[c0:c1].data_ptr(), piece.data_ptr(), c1 - c0, bf, stream=stream)
+                ov[:, c0:c1].copy_(piece)
 
     def broadcast(self, t, src: int = 0, stream=None):
         """``t`` of rank ``src`` to every rank, in place (any dtype)."""
