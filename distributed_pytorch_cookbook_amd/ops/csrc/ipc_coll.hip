@@ -458,12 +458,14 @@ DPC_API int dpc_ipc_p2p(const IpcP2PArgs* a, hipStream_t stream) {
   if (!a->slot[a->rank] || !a->flags[a->rank]) return (int)hipErrorInvalidValue;
   for (int i = 0; i < a->nsend; ++i) {
     const int q = a->send_peer[i];
-    if (q < 0 || q >= a->world || q == a->rank || !a->flags[q] || !a->send_ptr[i]) return (int)hipErrorInvalidValue;
+    if (q < 0 || q >= a->world || q == a->rank || !a->flags[q] || (!a->send_ptr[i] && a->send_n[i] > 0))
+      return (int)hipErrorInvalidValue;  // (an empty message may carry no pointer)
     if (a->send_n[i] < 0 || a->send_n[i] * 2 > a->region_bytes) return (int)hipErrorInvalidValue;
   }
   for (int i = 0; i < a->nrecv; ++i) {
     const int p = a->recv_peer[i];
-    if (p < 0 || p >= a->world || p == a->rank || !a->slot[p] || !a->flags[p] || !a->recv_ptr[i]) return (int)hipErrorInvalidValue;
+    if (p < 0 || p >= a->world || p == a->rank || !a->slot[p] || !a->flags[p] || (!a->recv_ptr[i] && a->recv_n[i] > 0))
+      return (int)hipErrorInvalidValue;
     if (a->recv_n[i] < 0 || a->recv_n[i] * 2 > a->region_bytes) return (int)hipErrorInvalidValue;
   }
   hipLaunchKernelGGL(ipc_p2p_kernel, dim3(IPC_G), dim3(256), 0, stream, *a);

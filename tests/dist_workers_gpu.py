@@ -176,6 +176,14 @@ def ipc_collectives_worker(rank, world, out):
             torch.cuda.synchronize()
             assert torch.equal(r, _ipc_input(peer, 5000, torch.float32, 40 + it)), ("p2p alternating", it)
             checked += 1
+    # an empty message beside a non-empty one in one group (an empty tensor may have no pointer;
+    # both sides still count it, so the channel stays in step)
+    e_s, e_r = torch.empty(0, device="cuda"), torch.empty(0, device="cuda")
+    t, r = _ipc_input(rank, 33, torch.float32, 45), torch.empty(33, device="cuda")
+    cp.sendrecv(sends=[(e_s, peer), (t, peer)], recvs=[(e_r, peer), (r, peer)])
+    torch.cuda.synchronize()
+    assert torch.equal(r, _ipc_input(peer, 33, torch.float32, 45)), "p2p after an empty message"
+    checked += 1
     # a stream of messages of different sizes on one channel (rank 1 -> 0): every half is reused with
     # a different split into workgroup sub-slices than its previous message (the FSDP checkpoint
     # gather's pattern), and the sender runs ahead of the receiver by up to two messages

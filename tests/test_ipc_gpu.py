@@ -15,7 +15,7 @@ pytestmark = pytest.mark.gpu
 def test_ipc_collectives_ranks_share_one_gpu(tmp_path, world):
     out = tmp_path / "ipc.pt"
     run_workers(ipc_collectives_worker, world, str(out), timeout=110)
-    assert torch.load(out, weights_only=True)["checked"] == 48 + 2 + 6 + 1 + 10
+    assert torch.load(out, weights_only=True)["checked"] == 48 + 2 + 6 + 1 + 1 + 10
 
 
 @pytest.fixture(scope="module")
